@@ -1,0 +1,536 @@
+#!/usr/bin/env python3
+"""Extract the reference's table-driven unit-test cases into JSON golden fixtures.
+
+Run in the build container (where ``/root/reference`` exists):
+
+    python tests/golden/extract_golden.py
+
+It reads the reference ``*_test.go`` files AS TEXT with ``goliteral`` (a
+minimal Go literal reader), evaluates each test table with Python stand-ins for
+the test helpers (``makeCluster``, ``clusterWithTaints``, ...) and k8s
+constructors (``resource.NewMilliQuantity`` → ``"<n>m"``), and writes
+``tests/golden/*.json`` in this repo's object-model JSON (see
+``kubeadmiral_amd/types.py``). The fixtures hold only inputs and expected
+outputs — the data of the reference's tests — plus ``source`` = file:line of
+each case. SURVEY.md Appendix C lists the inventory.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from goliteral import Evaluator, Parser, find_func_body, tokenize  # noqa: E402
+
+REF = os.environ.get("KAD_REFERENCE", "/root/reference")
+SCHED = "pkg/controllers/scheduler"
+PLUG = SCHED + "/framework/plugins"
+
+CONSTS = {
+    "corev1.TaintEffectNoSchedule": "NoSchedule",
+    "corev1.TaintEffectPreferNoSchedule": "PreferNoSchedule",
+    "corev1.TaintEffectNoExecute": "NoExecute",
+    "corev1.TolerationOpEqual": "Equal",
+    "corev1.TolerationOpExists": "Exists",
+    "corev1.ResourceCPU": "cpu",
+    "corev1.ResourceMemory": "memory",
+    "corev1.ConditionTrue": "True",
+    "resource.DecimalSI": "DecimalSI",
+    "resource.BinarySI": "BinarySI",
+    "fedcorev1a1.ClusterSelectorOpIn": "In",
+    "fedcorev1a1.ClusterSelectorOpNotIn": "NotIn",
+    "fedcorev1a1.ClusterSelectorOpExists": "Exists",
+    "fedcorev1a1.ClusterSelectorOpDoesNotExist": "DoesNotExist",
+    "fedcorev1a1.ClusterSelectorOpGt": "Gt",
+    "fedcorev1a1.ClusterSelectorOpLt": "Lt",
+    "fedcorev1a1.SchedulingModeDuplicate": "Duplicate",
+    "fedcorev1a1.SchedulingModeDivide": "Divide",
+    "fedcorev1a1.ClusterJoined": "Joined",
+    "framework.MaxClusterScore": 100,
+    "framework.Success": "Success",
+    "framework.Unschedulable": "Unschedulable",
+    "framework.Error": "Error",
+    "ErrReason": "cluster(s) didn't match cluster selector",
+    "MaxClusterErrReason": "max cluster is less than 0",
+    # named container aliases
+    "framework.ClusterScoreList": ("slice", ("named", "framework.ClusterScore")),
+    "framework.ClusterReplicasList": ("slice", ("named", "framework.ClusterReplicas")),
+    "corev1.ResourceList": ("map", ("named", "corev1.ResourceName"), ("named", "resource.Quantity")),
+}
+
+
+def _qty_milli(v, _fmt=None):
+    return f"{v}m"
+
+
+def _qty(v, _fmt=None):
+    return str(v)
+
+
+BASE_FUNCS = {
+    "resource.NewMilliQuantity": _qty_milli,
+    "resource.NewQuantity": _qty,
+    "resource.MustParse": lambda s: s,
+    "strconv.Itoa": lambda v: str(v),
+    "pointer.Int64": lambda v: v,
+    "pointer.Int64Ptr": lambda v: v,
+    "int64": lambda v: v,
+    "int32": lambda v: v,
+    "corev1.ResourceName": lambda s: s,
+    "framework.NewResult": lambda code, *reasons: {"__result__": code, "reasons": list(reasons)},
+    "appsv1.SchemeGroupVersion.WithKind": lambda k: {"Group": "apps", "Version": "v1", "Kind": k},
+}
+
+
+def read(rel):
+    with open(os.path.join(REF, rel)) as f:
+        return f.read()
+
+
+def line_of(src, func_name, tok_pos):
+    import re
+    m = re.search(r"^func\s+" + func_name + r"\s*\(", src, re.M)
+    return src.count("\n", 0, m.start() + tok_pos) + 1
+
+
+# ------------------------------------------------------------------ converters
+def conv_cluster(d):
+    """Raw FederatedCluster literal → repo JSON (FederatedCluster.to_json shape)."""
+    if d is None:
+        return None
+    meta = d.get("ObjectMeta") or {}
+    spec = d.get("Spec") or {}
+    status = d.get("Status") or {}
+    res = status.get("Resources") or {}
+    out = {"metadata": {"name": meta.get("Name", "")}, "spec": {}, "status": {}}
+    if meta.get("Labels") is not None:
+        out["metadata"]["labels"] = dict(meta["Labels"])
+    if spec.get("Taints"):
+        out["spec"]["taints"] = [{"key": t.get("Key", ""), "value": t.get("Value", ""), "effect": t.get("Effect", "")}
+                                 for t in spec["Taints"]]
+    r = {}
+    if res.get("Allocatable") is not None:
+        r["allocatable"] = dict(res["Allocatable"])
+    if res.get("Available") is not None:
+        r["available"] = dict(res["Available"])
+    if r:
+        out["status"]["resources"] = r
+    if status.get("APIResourceTypes"):
+        out["status"]["apiResourceTypes"] = [{"group": a.get("Group", ""), "version": a.get("Version", ""),
+                                              "kind": a.get("Kind", "")} for a in status["APIResourceTypes"]]
+    return out
+
+
+def conv_reqs(lst):
+    if lst is None:
+        return None
+    return [{"key": r.get("Key", ""), "operator": r.get("Operator", ""), **({"values": r["Values"]} if "Values" in r else {})}
+            for r in lst]
+
+
+def conv_term(t):
+    out = {}
+    if "MatchExpressions" in t:
+        out["matchExpressions"] = conv_reqs(t["MatchExpressions"])
+    if "MatchFields" in t:
+        out["matchFields"] = conv_reqs(t["MatchFields"])
+    return out
+
+
+def conv_affinity(a):
+    if a is None:
+        return None
+    out = {}
+    ca = a.get("ClusterAffinity")
+    if ca is not None:
+        c = {}
+        req = ca.get("RequiredDuringSchedulingIgnoredDuringExecution")
+        if "RequiredDuringSchedulingIgnoredDuringExecution" in ca and req is not None:
+            terms = req.get("ClusterSelectorTerms")
+            c["requiredDuringSchedulingIgnoredDuringExecution"] = {
+                "clusterSelectorTerms": None if terms is None else [conv_term(t) for t in terms]}
+        pref = ca.get("PreferredDuringSchedulingIgnoredDuringExecution")
+        if pref is not None:
+            c["preferredDuringSchedulingIgnoredDuringExecution"] = [
+                {"weight": p.get("Weight", 0), "preference": conv_term(p.get("Preference") or {})} for p in pref]
+        out["clusterAffinity"] = c
+    return out
+
+
+def conv_su(d):
+    if d is None:
+        return None
+    out = {"Name": d.get("Name", ""), "Namespace": d.get("Namespace", "")}
+    gv = d.get("GroupVersion")
+    if gv:
+        out["GroupVersion"] = {"Group": gv.get("Group", ""), "Version": gv.get("Version", "")}
+    if "Kind" in d:
+        out["Kind"] = d["Kind"]
+    rr = d.get("ResourceRequest")
+    if rr:
+        r = {"millicpu": rr.get("MilliCPU", 0), "memory": rr.get("Memory", 0),
+             "ephemeralStorage": rr.get("EphemeralStorage", 0)}
+        if rr.get("ScalarResources") is not None:
+            r["scalarResources"] = dict(rr["ScalarResources"])
+        out["ResourceRequest"] = r
+    for k in ("ClusterSelector", "DesiredReplicas", "SchedulingMode", "StickyCluster", "AvoidDisruption",
+              "MaxClusters", "MinReplicas", "MaxReplicas", "Weights", "CurrentClusters"):
+        if k in d and d[k] is not None:
+            out[k] = d[k]
+    if d.get("ClusterNames") is not None:
+        out["ClusterNames"] = list(d["ClusterNames"].keys())
+    if d.get("Affinity") is not None:
+        out["Affinity"] = conv_affinity(d["Affinity"])
+    if d.get("Tolerations") is not None:
+        out["Tolerations"] = [{k.lower(): v for k, v in t.items() if k != "__type__"} for t in d["Tolerations"]]
+    return out
+
+
+def code_of(res):
+    if res is None:
+        return "Success"
+    return res["__result__"]
+
+
+# ------------------------------------------------------------------ table reader
+def read_table(src, func_name, env_funcs, var="tests", pre_env=None):
+    """Evaluate ``<var> := <composite>`` inside ``func_name`` → list of (line, case)."""
+    body = find_func_body(src, func_name)
+    ev = Evaluator(CONSTS, {**BASE_FUNCS, **env_funcs}, pre_env or {})
+    p = Parser(body)
+    cases = None
+    while p.peek().kind != "eof":
+        tok = p.peek()
+        if tok.kind == "ident" and p.peek(1).val == ":=" and p.peek(2).val != "range":
+            name = tok.val
+            p.next()
+            p.next()
+            start_tok = p.peek()
+            try:
+                node = p.parse_expr()
+            except SyntaxError:
+                continue
+            if node[0] == "funclit":
+                continue
+            if name == var:
+                elems = node[2]
+                cases = []
+                for (_, e), epos in zip(elems, node[3]):
+                    line = line_of(src, func_name, epos - body[0].pos + _body_off(body))
+                    cases.append((line, ev.eval(e, node[1][1] if node[1][0] == "slice" else None)))
+                break
+            try:
+                ev.env[name] = ev.eval(node)
+            except (KeyError, SyntaxError):
+                pass
+        else:
+            p.next()
+    if cases is None:
+        raise KeyError(f"no table {var} in {func_name}")
+    return cases
+
+
+def _body_off(body):
+    return body[0].pos
+
+
+def _first_pos(node, body):
+    # best-effort: find the position of the first literal token inside the element
+    def walk(n):
+        if isinstance(n, tuple):
+            for x in n:
+                r = walk(x)
+                if r is not None:
+                    return r
+        elif isinstance(n, list):
+            for x in n:
+                r = walk(x)
+                if r is not None:
+                    return r
+        return None
+    return None
+
+
+def read_calls(src, func_name, call_names, env_funcs):
+    """Evaluate every top-level call ``name(args...)`` in ``func_name`` whose name is in call_names."""
+    body = find_func_body(src, func_name)
+    ev = Evaluator(CONSTS, {**BASE_FUNCS, **env_funcs})
+    p = Parser(body)
+    out = []
+    while p.peek().kind != "eof":
+        tok = p.peek()
+        if tok.kind == "ident" and tok.val in call_names and p.peek(1).val == "(":
+            node = p.parse_expr()
+            args = []
+            for a in node[2][1:]:  # skip t
+                args.append(ev.eval(a))
+            out.append((line_of(src, func_name, tok.pos), tok.val, args))
+        else:
+            p.next()
+    return out
+
+
+# ------------------------------------------------------------------ extractors
+def mk_obj(name=None, labels=None):
+    meta = {"__type__": "metav1.ObjectMeta", "Name": name or ""}
+    if labels is not None:
+        meta["Labels"] = labels
+    return {"__type__": "fedcorev1a1.FederatedCluster", "ObjectMeta": meta}
+
+
+def res_cluster(name, am, amem, vm, vmem):
+    c = mk_obj(name)
+    c["Status"] = {"Resources": {"Allocatable": {"cpu": _qty_milli(am), "memory": _qty(amem)},
+                                 "Available": {"cpu": _qty_milli(vm), "memory": _qty(vmem)}}}
+    return c
+
+
+def res_su(name, cpu, mem):
+    return {"__type__": "framework.SchedulingUnit", "Name": name, "ResourceRequest": {"MilliCPU": cpu, "Memory": mem}}
+
+
+def extract_filters():
+    out = []
+    # ---- fit
+    rel = PLUG + "/clusterresources/fit_test.go"
+    src = read(rel)
+    funcs = {
+        "makeSchedulingUnit": res_su,
+        "makeCluster": res_cluster,
+        "makeClusterWithScalarResource": lambda n, a: {**mk_obj(n), "Status": {"Resources": {
+            "Allocatable": {"example.com/aaa": _qty(a)}, "Available": {"example.com/aaa": _qty(a)}}}},
+        "makeSchedulingUnitWithScalarResource": lambda n, a: {"__type__": "framework.SchedulingUnit", "Name": n,
+                                                              "ResourceRequest": {"ScalarResources": {"example.com/aaa": a}}},
+        "getErrReason": lambda rn: f"Insufficient {rn}",
+    }
+    pre = {"extendedResourceA": "example.com/aaa"}
+    for line, c in read_table(src, "TestEnoughRequests", funcs, "enoughschedulingUnitsTests", pre):
+        out.append({"plugin": "ClusterResourcesFit", "source": f"{rel}:{line}", "name": c["name"],
+                    "su": conv_su(c["su"]), "cluster": conv_cluster(c["cluster"]), "want": code_of(c["wantResult"])})
+    # ---- taint toleration filter
+    rel = PLUG + "/tainttoleration/taint_toleration_test.go"
+    src = read(rel)
+    funcs = {
+        "clusterWithTaints": lambda n, taints: {**mk_obj(n), "Spec": {"Taints": taints}},
+        "suWithTolerations": lambda n, tols: {"__type__": "framework.SchedulingUnit", "Name": n, "Tolerations": tols},
+    }
+    for line, c in read_table(src, "TestTaintTolerationFilter", funcs):
+        out.append({"plugin": "TaintToleration", "source": f"{rel}:{line}", "name": c["name"],
+                    "su": conv_su(c["su"]), "cluster": conv_cluster(c["cluster"]), "want": code_of(c["wantResult"])})
+    # ---- cluster affinity filter
+    rel = PLUG + "/clusteraffinity/cluster_affinity_test.go"
+    src = read(rel)
+    for line, c in read_table(src, "TestClusterAffinity", {}):
+        cl = mk_obj(c.get("clusterName", ""), c.get("labels"))
+        out.append({"plugin": "ClusterAffinity", "source": f"{rel}:{line}", "name": c["name"],
+                    "su": conv_su(c["su"]), "cluster": conv_cluster(cl), "want": code_of(c.get("wantResult"))})
+    # ---- api resources
+    rel = PLUG + "/apiresources/apiresources_test.go"
+    src = read(rel)
+    funcs = {
+        "clusterWithAPIResource": lambda n, rs: {**mk_obj(n), "Status": {"APIResourceTypes": rs}},
+        "suWithAPIResource": lambda n, gvk: {"__type__": "framework.SchedulingUnit", "Name": n,
+                                             "GroupVersion": {"Group": gvk["Group"], "Version": gvk["Version"]},
+                                             "Kind": gvk["Kind"]},
+    }
+    for line, c in read_table(src, "TestAPIResourcesFilter", funcs):
+        out.append({"plugin": "APIResources", "source": f"{rel}:{line}", "name": c["name"],
+                    "su": conv_su(c["su"]), "cluster": conv_cluster(c["cluster"]), "want": code_of(c["wantResult"])})
+    # ---- placement (the reference test only checks IsSuccess)
+    rel = PLUG + "/placement/filter_test.go"
+    src = read(rel)
+    funcs = {"makeCluster": lambda n: mk_obj(n)}
+    for line, c in read_table(src, "TestPlacementFilterPlugin", funcs):
+        want = code_of(c["expectedResult"])
+        out.append({"plugin": "PlacementFilter", "source": f"{rel}:{line}", "name": c["name"],
+                    "su": conv_su(c["su"]), "cluster": conv_cluster(c["cluster"]),
+                    "want": "Success" if want == "Success" else "NotSuccess"})
+    return out
+
+
+def extract_scores():
+    out = []
+    funcs_res = {"makeSchedulingUnit": res_su, "makeCluster": res_cluster}
+    for plugin, rel, fn in (
+        ("ClusterResourcesBalancedAllocation", PLUG + "/clusterresources/balanced_allocation_test.go",
+         "TestClusterResourcesBalancedAllocation"),
+        ("ClusterResourcesLeastAllocated", PLUG + "/clusterresources/least_allocated_test.go",
+         "TestClusterResourcesLeastAllocated"),
+        ("ClusterResourcesMostAllocated", PLUG + "/clusterresources/most_allocated_test.go",
+         "TestClusterResourcesMostAllocated"),
+    ):
+        src = read(rel)
+        for line, c in read_table(src, fn, funcs_res):
+            out.append({"plugin": plugin, "source": f"{rel}:{line}", "name": c["name"], "normalize": False,
+                        "su": conv_su(c["su"]), "clusters": [conv_cluster(x) for x in c["clusters"]],
+                        "want": [e["Score"] for e in c["expectedList"]]})
+    rel = PLUG + "/tainttoleration/taint_toleration_test.go"
+    src = read(rel)
+    funcs = {
+        "clusterWithTaints": lambda n, taints: {**mk_obj(n), "Spec": {"Taints": taints}},
+        "suWithTolerations": lambda n, tols: {"__type__": "framework.SchedulingUnit", "Name": n, "Tolerations": tols},
+    }
+    for line, c in read_table(src, "TestTaintTolerationScore", funcs):
+        out.append({"plugin": "TaintToleration", "source": f"{rel}:{line}", "name": c["name"], "normalize": True,
+                    "su": conv_su(c["su"]), "clusters": [conv_cluster(x) for x in c["clusters"]],
+                    "want": [e["Score"] for e in c["expectedList"]]})
+    rel = PLUG + "/clusteraffinity/cluster_affinity_test.go"
+    src = read(rel)
+    for line, c in read_table(src, "TestClusterAffinityPriority", {}):
+        out.append({"plugin": "ClusterAffinity", "source": f"{rel}:{line}", "name": c["name"], "normalize": True,
+                    "su": conv_su(c["su"]), "clusters": [conv_cluster(x) for x in c["clusters"]],
+                    "want": list(c["expectedList"])})
+    return out
+
+
+def extract_maxcluster():
+    rel = PLUG + "/maxcluster/max_cluster_test.go"
+    src = read(rel)
+    funcs = {"makeCluster": lambda n: mk_obj(n), "newIntP64": lambda v: v}
+    out = []
+    for line, c in read_table(src, "TestMaxClusterSelectClusters", funcs):
+        out.append({"source": f"{rel}:{line}", "name": c["name"], "su": conv_su(c["su"]),
+                    "scores": [[e["Cluster"]["ObjectMeta"]["Name"], e["Score"]] for e in (c.get("clusterScoreList") or [])],
+                    "want_clusters": list(c["expectedCluster"] or []), "want": code_of(c["expectedResult"])})
+    return out
+
+
+def extract_rsp():
+    rel = PLUG + "/rsp/rsp_test.go"
+    src = read(rel)
+
+    def cpu_cluster(name, alloc, avail):
+        c = mk_obj(name)
+        if alloc >= 0 and avail >= 0:
+            c["Status"] = {"Resources": {"Allocatable": {"cpu": str(alloc)}, "Available": {"cpu": str(avail)}}}
+        return c
+
+    def make_args(*clusters):
+        return {"__make_args__": [conv_cluster(c) for c in clusters]}
+
+    funcs = {"makeClusterWithCPU": cpu_cluster, "NewFederatedCluster": lambda n: mk_obj(n), "makeArgs": make_args,
+             "assert.NoError": None}
+    consts_extra = {"assert.NoError": "NoError", "assert.Error": "Error"}
+    CONSTS.update(consts_extra)
+    wl = []
+    for line, c in read_table(src, "TestCalcWeightLimit", funcs):
+        wl.append({"source": f"{rel}:{line}", "name": c["name"],
+                   "clusters": [conv_cluster(x) for x in c["args"]["clusters"]],
+                   "ratio": c["args"]["supplyLimitRatio"], "want": c["wantWeightLimit"]})
+    atp = []
+    for line, c in read_table(src, "TestAvailableToPercentage", funcs):
+        atp.append({"source": f"{rel}:{line}", "name": c["name"], "clusters": c["args"]["__make_args__"],
+                    "want": c["wantClusterWeights"]})
+    plug = []
+    for fn in ("TestClusterWeights", "TestMinReplicas", "TestMaxReplicas"):
+        for line, c in read_table(src, fn, funcs):
+            plug.append({"source": f"{rel}:{line}", "name": c["name"], "su": conv_su(c["schedulingUnit"]),
+                         "clusters": [conv_cluster(x) for x in c["clusters"]],
+                         "want": [[e["Cluster"]["ObjectMeta"]["Name"], e["Replicas"]]
+                                  for e in c["expectedReplicasList"]],
+                         "want_code": code_of(c["expectedResult"])})
+    return wl, atp, plug
+
+
+def extract_planner():
+    rel = "pkg/controllers/util/planner/planner_test.go"
+    src = read(rel)
+    out = []
+    combos = {
+        "doCheckWithoutExisting": [(False, False, 0), (False, True, 0), (True, False, 0), (True, True, 0)],
+        "doCheckWithExisting": [(False, False, 0), (False, True, 0), (True, False, 1), (True, True, 1)],
+        "doCheckWithExistingAndCapacity": [(False, False, 0), (False, True, 1), (True, False, 2), (True, True, 3)],
+    }
+    for fn in ("TestWithoutExisting", "TestWithExisting", "TestWithExistingAndCapacity"):
+        for line, call, args in read_calls(src, fn, set(combos), {}):
+            tc, expected = args[0], args[1]
+            if not isinstance(expected, list):
+                expected = [expected]
+            rsp = {}
+            for k, p in tc["rsp"].items():
+                rsp[k] = {"MinReplicas": p.get("MinReplicas", 0), "MaxReplicas": p.get("MaxReplicas"),
+                          "Weight": p.get("Weight", 0)}
+            for avoid, keep, idx in combos[call]:
+                e = expected[idx]
+                out.append({"source": f"{rel}:{line}", "rsp": rsp, "replicas": tc["replicas"],
+                            "clusters": list(tc["clusters"]), "existing": tc.get("existing"),
+                            "capacity": tc.get("capacity"), "avoidDisruption": avoid,
+                            "keepUnschedulableReplicas": keep,
+                            "want_plan": e.get("plan") or {}, "want_overflow": e.get("overflow") or {}})
+    return out
+
+
+def extract_profile():
+    rel = SCHED + "/profile_test.go"
+    src = read(rel)
+    base = {"__type__": "fedcore.EnabledPlugins", "FilterPlugins": ["a", "b", "c"], "ScorePlugins": ["a", "b", "c"],
+            "SelectPlugins": ["a", "b", "c"], "ReplicasPlugins": ["a", "b", "c"]}
+    funcs = {"getBase": lambda: json.loads(json.dumps(base))}
+    out = []
+    for line, c in read_table(src, "TestApplyProfile", funcs):
+        prof = c.get("profile")
+        plugins = None
+        if prof is not None:
+            pl = (prof.get("Spec") or {}).get("Plugins")
+            if pl is not None:
+                plugins = {}
+                for point, key in (("filter", "Filter"), ("score", "Score"), ("select", "Select")):
+                    ps = pl.get(key) or {}
+                    plugins[point] = {"enabled": [x["Name"] for x in (ps.get("Enabled") or [])],
+                                      "disabled": [x["Name"] for x in (ps.get("Disabled") or [])]}
+        exp = c["expectedResult"]
+        out.append({"source": f"{rel}:{line}", "name": c["name"],
+                    "base": {k: v for k, v in c["base"].items() if k != "__type__"},
+                    "plugins": plugins,
+                    "want": {k: (v or []) for k, v in exp.items() if k != "__type__"}})
+    return out
+
+
+def extract_core():
+    """core/generic_scheduler_test.go:64-196 — orchestrated with a naive replicas plugin (1 per cluster)."""
+    rel = SCHED + "/core/generic_scheduler_test.go"
+    clusters = [{"metadata": {"name": "cluster1"}, "spec": {}, "status": {}},
+                {"metadata": {"name": "cluster2"}, "spec": {}, "status": {}}]
+    return [
+        {"source": f"{rel}:80", "name": "Duplicate mode should skip replicas scheduling", "clusters": clusters,
+         "su": {"StickyCluster": True, "DesiredReplicas": 10, "SchedulingMode": "Duplicate"},
+         "want": {"cluster1": None, "cluster2": None}},
+        {"source": f"{rel}:98", "name": "Divide mode should do replicas scheduling", "clusters": clusters,
+         "su": {"StickyCluster": True, "DesiredReplicas": 10, "SchedulingMode": "Divide"},
+         "want": {"cluster1": 1, "cluster2": 1}},
+        {"source": f"{rel}:157", "name": "should schedule the first time", "clusters": clusters,
+         "su": {"StickyCluster": True, "DesiredReplicas": 10, "SchedulingMode": "Divide"},
+         "want": {"cluster1": 1, "cluster2": 1}},
+        {"source": f"{rel}:176", "name": "should not reschedule after first time", "clusters": clusters,
+         "su": {"StickyCluster": True, "DesiredReplicas": 10, "SchedulingMode": "Divide",
+                "CurrentClusters": {"cluster1": 60}},
+         "want": {"cluster1": 60}},
+    ]
+
+
+def main():
+    outdir = HERE
+    fixtures = {
+        "filters.json": extract_filters(),
+        "scores.json": extract_scores(),
+        "maxcluster.json": extract_maxcluster(),
+        "planner.json": extract_planner(),
+        "profile.json": extract_profile(),
+        "core.json": extract_core(),
+    }
+    wl, atp, plug = extract_rsp()
+    fixtures["rsp_weight_limit.json"] = wl
+    fixtures["rsp_available_to_percentage.json"] = atp
+    fixtures["rsp_plugin.json"] = plug
+    for name, data in fixtures.items():
+        with open(os.path.join(outdir, name), "w") as f:
+            json.dump({"generated_by": "tests/golden/extract_golden.py", "reference": "JackZxj/kubeadmiral @ /root/reference",
+                       "cases": data}, f, indent=1, sort_keys=False)
+        print(f"{name}: {len(data)} cases")
+
+
+if __name__ == "__main__":
+    main()
