@@ -1,0 +1,325 @@
+/*
+ * kad_sched.h — C ABI of the MI355X-native batch scheduler for KubeAdmiral's
+ * scheduling framework (libkad.so).
+ *
+ * Drop-in boundary. The reference runs, per SchedulingUnit and on one Go
+ * goroutine,
+ *
+ *   core.ScheduleAlgorithm.Schedule(ctx, framework.Framework,
+ *       framework.SchedulingUnit, []*FederatedCluster) (ScheduleResult, error)
+ *   (pkg/controllers/scheduler/core/generic_scheduler.go:37-44, installed at
+ *    pkg/controllers/scheduler/scheduler.go:208, called at scheduler.go:507).
+ *
+ * This library evaluates the same Filter → Score → Select → Replicas pipeline
+ * for a whole batch of SchedulingUnits against one cluster snapshot on the GPU.
+ * A cgo shim implements ScheduleAlgorithm on top of it:
+ *
+ *   kad_snapshot_upload   ← the []*FederatedCluster argument, packed once per
+ *                           snapshot version (clusters are read-only informer
+ *                           cache objects, generic_scheduler.go:96)
+ *   kad_batch_upload      ← a batch of framework.SchedulingUnit values
+ *                           (framework/types.go:33-69), packed
+ *   kad_schedule          ← genericScheduler.Schedule for every unit
+ *                           (generic_scheduler.go:92-150) under the plugin set
+ *                           of the framework (kad_profile ← EnabledPlugins,
+ *                           pkg/apis/core/types.go:21-43, built by
+ *                           scheduler/profile.go:84-113)
+ *   kad_results_download  ← ScheduleResult.SuggestedClusters per unit
+ *                           (generic_scheduler.go:48-53) + error class
+ *
+ * Conventions: every function returns 0 on success or a negative KAD_E* code;
+ * kad_last_error() gives the message. Inputs are caller-owned host buffers,
+ * read only during the call; the library owns all device memory and never
+ * keeps caller pointers. A kad_ctx is bound to one HIP device and one HIP
+ * stream and is internally serialised (a mutex), so concurrent worker
+ * goroutines (worker.go:132-134) may share it.
+ *
+ * Packed layouts: a snapshot blob and a batch blob are single contiguous byte
+ * buffers — a header followed by 256-byte aligned arrays located by byte
+ * offsets in the header — so one H2D copy (or one RCCL broadcast) moves them.
+ * The host-side packer is kubeadmiral_amd/pack.py; the layout below is the
+ * contract a Go packer would reproduce.
+ */
+#ifndef KAD_SCHED_H
+#define KAD_SCHED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KAD_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- errors */
+#define KAD_OK 0
+#define KAD_EINVAL -1       /* malformed blob / profile / argument          */
+#define KAD_EHIP -2         /* HIP runtime error (caller falls back)        */
+#define KAD_ENOMEM -3       /* device allocation failed                     */
+#define KAD_ESTATE -4       /* e.g. schedule before snapshot/batch upload   */
+#define KAD_EUNSUPPORTED -5 /* plugin not in the in-tree set (webhook)      */
+
+/* ------------------------------------------------------------- plugins
+ * In-tree plugin ids = bit positions in kad_profile masks.
+ * Names: pkg/controllers/scheduler/framework/plugins/names/names.go:19-30;
+ * registry: pkg/controllers/scheduler/profile.go:39-50.                    */
+enum kad_plugin {
+  KAD_PL_API_RESOURCES = 0,          /* APIResources                       */
+  KAD_PL_TAINT_TOLERATION = 1,       /* TaintToleration (filter + score)   */
+  KAD_PL_CLUSTER_RESOURCES_FIT = 2,  /* ClusterResourcesFit                */
+  KAD_PL_PLACEMENT_FILTER = 3,       /* PlacementFilter                    */
+  KAD_PL_CLUSTER_AFFINITY = 4,       /* ClusterAffinity (filter + score)   */
+  KAD_PL_BALANCED_ALLOCATION = 5,    /* ClusterResourcesBalancedAllocation */
+  KAD_PL_LEAST_ALLOCATED = 6,        /* ClusterResourcesLeastAllocated     */
+  KAD_PL_MOST_ALLOCATED = 7,         /* ClusterResourcesMostAllocated      */
+  KAD_PL_MAX_CLUSTER = 8,            /* MaxCluster (select)                */
+  KAD_PL_CLUSTER_CAPACITY_WEIGHT = 9 /* ClusterCapacityWeight (replicas)   */
+};
+
+/* kad_profile.flags */
+#define KAD_PROFILE_XORSHIFT_GO121 (1u << 0) /* pdqsort breakPatterns with the
+                                                 13/7/17 xorshift triple instead of go1.19's 13/17/5 */
+
+/* The framework: which in-tree plugin runs at which extension point.
+ * Filters are an AND (runtime/framework.go:114-126) and score sums are
+ * order-independent (core/generic_scheduler.go:182-190), so masks suffice;
+ * only the FIRST select / replicas plugin runs (framework.go:194-207,
+ * 234-247). Framework construction errors (unknown / duplicate / wrong-type
+ * plugin, framework.go:70-95) are raised by the host before this call.      */
+typedef struct kad_profile {
+  uint32_t filter_mask;    /* bits of KAD_PL_* filter plugins                  */
+  uint32_t score_mask;     /* bits of KAD_PL_* score plugins                   */
+  int32_t select_plugin;   /* -1 = none (all feasible selected), KAD_PL_MAX_CLUSTER */
+  int32_t replicas_plugin; /* -1 = none, KAD_PL_CLUSTER_CAPACITY_WEIGHT        */
+  uint32_t flags;          /* KAD_PROFILE_*                                    */
+  uint32_t reserved[3];
+} kad_profile;
+
+/* ------------------------------------------------------ snapshot blob
+ * C clusters in snapshot order (the order of the []*FederatedCluster slice;
+ * MaxCluster's tie behaviour is defined relative to it).
+ * Array element [i][c] is stored at i*C + c ("row-major by attribute"), so a
+ * wavefront reading 64 consecutive clusters is one coalesced access.        */
+#define KAD_SNAPSHOT_MAGIC 0x5344414Bu /* "KADS" */
+enum kad_snapshot_array {
+  KAD_S_ALLOC_CPU = 0, /* i64[C]  Allocatable cpu MilliValue (framework/util.go:106)      */
+  KAD_S_ALLOC_MEM,     /* i64[C]  Allocatable memory Value()                            */
+  KAD_S_USED_CPU,      /* i64[C]  (Allocatable − Available) cpu via Resource.Sub
+                                  (clusterresources/fit.go:140-147)                      */
+  KAD_S_USED_MEM,      /* i64[C]                                                         */
+  KAD_S_ALLOC_SCALAR,  /* i64[S][C] scalar resources (IsScalarResourceName) allocatable  */
+  KAD_S_USED_SCALAR,   /* i64[S][C] scalar resources used                                */
+  KAD_S_ALLOC_CORES,   /* i64[C]  Value() of (0 + Allocatable cpu) (rsp.go:305-325)      */
+  KAD_S_AVAIL_CORES,   /* i64[C]  Value() of (0 + Available cpu)   (rsp.go:286-304)      */
+  KAD_S_GVK,           /* u64[GW][C] bit g set ⇔ cluster lists APIResource g             */
+  KAD_S_TAINT_NSNE,    /* u64[TW][C] taints with effect NoSchedule|NoExecute             */
+  KAD_S_TAINT_NE,      /* u64[TW][C] taints with effect NoExecute                        */
+  KAD_S_TAINT_PNS,     /* u64[TW][C] PreferNoSchedule taints (one id per occurrence)     */
+  KAD_S_LABEL_VAL,     /* i32[K][C] value id of label key k (-1 = absent)                */
+  KAD_S_LABEL_INT,     /* i64[K][C] strconv.ParseInt(value,10,64)                        */
+  KAD_S_LABEL_INT_OK,  /* u8[K][C]  1 if the parse succeeded                             */
+  KAD_S_NAME_FNV,      /* u32[C]  FNV-1 32 state after the cluster name bytes
+                                  (util/planner/planner.go:185-195)                      */
+  KAD_S_CFLAGS,        /* u32[C]  bit0: Resource.Sub error (map-order dependent input)   */
+  KAD_S_NARRAYS
+};
+
+typedef struct kad_snapshot_header {
+  uint32_t magic;
+  uint32_t abi_version;
+  int32_t n_clusters;    /* C  */
+  int32_t n_gvk_words;   /* GW */
+  int32_t n_taint_words; /* TW */
+  int32_t n_label_keys;  /* K  */
+  int32_t n_scalar;      /* S  */
+  int32_t reserved0;
+  uint64_t total_bytes;
+  uint64_t fingerprint; /* batches carry it: packed against this snapshot  */
+  uint64_t off[KAD_S_NARRAYS];
+} kad_snapshot_header;
+
+/* --------------------------------------------------------- batch blob
+ * W scheduling units; CSR arrays are indexed by *_OFF[w] .. *_OFF[w+1].    */
+#define KAD_BATCH_MAGIC 0x4241444Bu /* "KADB" */
+
+/* per-unit flags (KAD_B_FLAGS) */
+#define KAD_W_DUPLICATE (1u << 0)         /* SchedulingMode == Duplicate (generic_scheduler.go:130)  */
+#define KAD_W_STICKY (1u << 1)            /* StickyCluster && len(CurrentClusters)>0 (:101-104)      */
+#define KAD_W_AVOID_DISRUPTION (1u << 2)  /* AvoidDisruption (planner.go:116-176)                   */
+#define KAD_W_KEEP_UNSCHED (1u << 3)      /* AutoMigration.KeepUnschedulableReplicas (rsp.go:128-139)*/
+#define KAD_W_HAS_DESIRED (1u << 4)       /* DesiredReplicas != nil                                  */
+#define KAD_W_HAS_MAX_CLUSTERS (1u << 5)  /* MaxClusters != nil (max_cluster.go:48-58)               */
+#define KAD_W_FIT_NONZERO (1u << 6)       /* fit.go:82-87 early return NOT taken                     */
+#define KAD_W_HAS_PLACEMENT (1u << 7)     /* len(ClusterNames) > 0 (placement/filter.go:47)          */
+#define KAD_W_SCORE_ERROR (1u << 8)       /* ClusterAffinity.Score errors (cluster_affinity.go:121)  */
+#define KAD_W_DYNAMIC_WEIGHTS (1u << 9)   /* len(Weights) == 0 (rsp.go:69)                           */
+#define KAD_W_HAS_CURRENT (1u << 10)      /* len(CurrentClusters) > 0                                */
+#define KAD_W_WIDE_SCORES (1u << 11)      /* affinity weights may exceed the narrow i32 path         */
+
+enum kad_batch_array {
+  KAD_B_FLAGS = 0,     /* u32[W]                                                          */
+  KAD_B_GVK,           /* i32[W]  snapshot GVK id of (GroupVersion, Kind); -1 = none has it */
+  KAD_B_REQ_CPU,       /* i64[W]  ResourceRequest.MilliCPU                                */
+  KAD_B_REQ_MEM,       /* i64[W]  ResourceRequest.Memory                                  */
+  KAD_B_DESIRED,       /* i64[W]  *DesiredReplicas (0 when nil)                           */
+  KAD_B_MAX_CLUSTERS,  /* i64[W]  *MaxClusters                                            */
+  KAD_B_TOLSET,        /* i32[W]  toleration-set id                                       */
+  KAD_B_TOL_ALL,       /* u64[NT][TW] taints tolerated by some toleration                 */
+  KAD_B_TOL_PNS,       /* u64[NT][TW] ... by a toleration with effect "" or PreferNoSchedule */
+  KAD_B_SREQ_OFF,      /* i32[W+1] scalar requests (ScalarResources map)                  */
+  KAD_B_SREQ_ID,       /* i32[]    snapshot scalar id (-1: no cluster has it)             */
+  KAD_B_SREQ_VAL,      /* i64[]    requested value                                        */
+  KAD_B_FPROG_OFF,     /* i32[W+1] ClusterAffinity filter program (see KAD_OP_*)          */
+  KAD_B_FPROG,         /* i32[]                                                           */
+  KAD_B_SPROG_OFF,     /* i32[W+1] ClusterAffinity score program                          */
+  KAD_B_SPROG,         /* i32[]                                                           */
+  KAD_B_PLACE_OFF,     /* i32[W+1] ClusterNames as snapshot cluster ids (sorted, unique)  */
+  KAD_B_PLACE,         /* i32[]                                                           */
+  KAD_B_CUR_OFF,       /* i32[W+1] CurrentClusters as snapshot ids (sorted)               */
+  KAD_B_CUR_ID,        /* i32[]                                                           */
+  KAD_B_CUR_REP,       /* i64[]    replicas (nil resolved to DesiredReplicas, rsp.go:119-126) */
+  KAD_B_PREF_OFF,      /* i32[W+1] per-cluster Weights/MinReplicas/MaxReplicas/EstimatedCapacity */
+  KAD_B_PREF_ID,       /* i32[]    snapshot cluster id (sorted)                           */
+  KAD_B_PREF_W,        /* i64[]    Weights[cluster]                                       */
+  KAD_B_PREF_MIN,      /* i64[]    MinReplicas[cluster]                                   */
+  KAD_B_PREF_MAX,      /* i64[]    MaxReplicas[cluster]                                   */
+  KAD_B_PREF_CAP,      /* i64[]    EstimatedCapacity[cluster] (only entries >= 0)         */
+  KAD_B_PREF_FLAGS,    /* u32[]    bit0 has weight, bit1 has max, bit2 has cap            */
+  KAD_B_KEY_OFF,       /* i32[W+1] su.Key() bytes (types.go:123-128)                      */
+  KAD_B_KEY,           /* u8[]                                                            */
+  KAD_B_OUT_OFF,       /* i64[W+1] output slot ranges (host-computed upper bounds)        */
+  KAD_B_NARRAYS
+};
+
+#define KAD_PREF_HAS_WEIGHT 1u
+#define KAD_PREF_HAS_MAX 2u
+#define KAD_PREF_HAS_CAP 4u
+
+typedef struct kad_batch_header {
+  uint32_t magic;
+  uint32_t abi_version;
+  int32_t n_units;       /* W                                        */
+  int32_t n_clusters;    /* must equal the snapshot's C              */
+  int32_t n_taint_words; /* must equal the snapshot's TW             */
+  int32_t n_tolsets;     /* NT                                       */
+  int64_t n_out_slots;   /* = OUT_OFF[W]                             */
+  int32_t max_row_slots; /* max_w OUT_OFF[w+1]-OUT_OFF[w]            */
+  uint32_t packed_filter_mask;  /* profile the output bounds were sized for:  */
+  int32_t packed_select_plugin; /* kad_schedule rejects any other profile     */
+  int32_t reserved1;
+  uint64_t total_bytes;
+  uint64_t snapshot_fingerprint;
+  uint64_t off[KAD_B_NARRAYS];
+} kad_batch_header;
+
+/* ------------------------------------------------ predicate programs
+ * A requirement is  [op | n_payload<<8, key, payload...]  (i32 words):
+ *   KAD_OP_IN / NOTIN / EQ : payload = value ids of that key (labels.Requirement
+ *                            In / NotIn / SelectorFromSet's Equals)
+ *   KAD_OP_EXISTS / DNE    : no payload
+ *   KAD_OP_GT / LT         : payload = int64 threshold as (lo, hi) words
+ *   KAD_OP_NAME_EQ / NE    : key = snapshot cluster id (-1: no such cluster);
+ *                            field selector on metadata.name
+ *                            (util/clusterselector/util.go:65-93)
+ *   KAD_OP_TRUE / FALSE    : folded on the host (key or value absent from
+ *                            every cluster, field keys other than metadata.name)
+ * Filter program (cluster_affinity.go:50-94, clusterselector/util.go:97-132):
+ *   n_sel, <n_sel requirements: ClusterSelector map>,
+ *   req_present, [n_terms, { tflags, n_expr, n_field, <exprs>, <fields> } ...]
+ *   tflags: bit0 has_expr, bit1 expr_valid, bit2 has_field, bit3 field_valid
+ *   (invalid parts carry no requirements; reaching one makes the whole
+ *    MatchClusterSelectorTerms return false, as the reference's error does).
+ * Score program (cluster_affinity.go:96-135): n_terms, { weight, n_expr, <exprs> } ...
+ *   (only valid, non-empty terms with weight != 0)                           */
+enum kad_op {
+  KAD_OP_IN = 1, KAD_OP_NOTIN = 2, KAD_OP_EXISTS = 3, KAD_OP_DNE = 4,
+  KAD_OP_GT = 5, KAD_OP_LT = 6, KAD_OP_EQ = 7, KAD_OP_TRUE = 8, KAD_OP_FALSE = 9,
+  KAD_OP_NAME_EQ = 10, KAD_OP_NAME_NE = 11
+};
+#define KAD_TERM_HAS_EXPR 1
+#define KAD_TERM_EXPR_VALID 2
+#define KAD_TERM_HAS_FIELD 4
+#define KAD_TERM_FIELD_VALID 8
+
+/* ------------------------------------------------------------ results
+ * Per unit: status, count and flags; pairs in the unit's output slot range
+ * [OUT_OFF[w], OUT_OFF[w] + count) in ascending cluster id.
+ *   Duplicate mode: replicas = -1 (the Go nil pointer).
+ *   Divide mode   : replicas > 0 (zero entries are dropped, rsp.go:170-179).
+ *   KAD_ST_STICKY : SuggestedClusters = CurrentClusters (host copies it).
+ *   KAD_ST_NO_FEASIBLE: SuggestedClusters = nil (generic_scheduler.go:112-114). */
+enum kad_status {
+  KAD_ST_OK = 0,
+  KAD_ST_STICKY = 1,
+  KAD_ST_NO_FEASIBLE = 2,
+  KAD_ST_ERR_SCORE = 3,    /* "failed to scoreClusters"      */
+  KAD_ST_ERR_SELECT = 4,   /* "failed to selectClusters"     */
+  KAD_ST_ERR_REPLICAS = 5  /* "failed to do replicaScheduling" */
+};
+/* result flags */
+#define KAD_RF_TIE_STRADDLE 1u  /* MaxCluster cut fell inside a run of equal scores: pdqsort emulated */
+#define KAD_RF_REMAINDER_TIE 2u /* AvailableToPercentage remainder had tied recipients (rsp.go:257-270) */
+#define KAD_RF_HASH_TIE 4u      /* planner (weight, FNV) tie: reference order is map-order dependent */
+
+typedef struct kad_result_view {
+  int32_t* status;      /* [W]           */
+  int32_t* count;       /* [W]           */
+  uint32_t* flags;      /* [W]           */
+  int32_t* cluster;     /* [n_out_slots] */
+  int64_t* replicas;    /* [n_out_slots] */
+} kad_result_view;
+
+/* ------------------------------------------------------------ context */
+typedef struct kad_ctx kad_ctx;
+
+int kad_ctx_create(int hip_device, kad_ctx** out);
+int kad_ctx_destroy(kad_ctx* ctx);
+const char* kad_last_error(kad_ctx* ctx);
+int kad_abi_version(void);
+
+/* snapshot / batch residency (H2D, or D2D from a device buffer e.g. after an
+ * RCCL broadcast of the snapshot blob). Allocation happens here, never in
+ * kad_schedule.                                                              */
+int kad_snapshot_upload(kad_ctx* ctx, const void* blob, size_t nbytes);
+int kad_snapshot_upload_device(kad_ctx* ctx, const void* dev_blob, size_t nbytes);
+int kad_batch_upload(kad_ctx* ctx, const void* blob, size_t nbytes);
+
+/* Run the pipeline for the resident batch; asynchronous on the ctx stream. */
+int kad_schedule(kad_ctx* ctx, const kad_profile* profile);
+int kad_sync(kad_ctx* ctx);
+/* Device time of the last kad_schedule, from HIP events on the ctx stream:
+ * ms[0] = whole pipeline, ms[1] = filter/score/select kernel, ms[2] = planner. */
+int kad_last_timing(kad_ctx* ctx, float ms[3]);
+int kad_results_download(kad_ctx* ctx, const kad_result_view* out);
+
+/* All in one: upload batch, schedule, download (blocking). */
+int kad_schedule_batch(kad_ctx* ctx, const kad_profile* profile, const void* batch_blob, size_t nbytes,
+                       const kad_result_view* out);
+
+/* ---------------------------------------------------- stage entry points
+ * The select and planner stages on caller-provided rows, for parity tests of
+ * each plugin in isolation (max_cluster_test.go, planner_test.go).          */
+/* MaxCluster over rows of scores in input order; out_sel gets, per row, the
+ * selected input positions (ascending) in [row_off[r], row_off[r]+out_count[r]). */
+int kad_select_rows(kad_ctx* ctx, int n_rows, const int32_t* row_off, const int64_t* scores,
+                    const int64_t* max_clusters /* <0: error, INT64_MAX: nil */, uint32_t profile_flags,
+                    int32_t* out_count, int32_t* out_sel, int32_t* out_status);
+
+/* planner.Plan over rows: per element name hash (FNV-1 of name‖key), weight,
+ * min, max (flags bit1), capacity (flags bit2), current; per row total
+ * replicas, avoid_disruption / keep_unschedulable (row_flags bit0 / bit1).
+ * Outputs per element plan and overflow.                                    */
+int kad_plan_rows(kad_ctx* ctx, int n_rows, const int32_t* row_off, const uint32_t* hash, const int64_t* weight,
+                  const int64_t* min_r, const int64_t* max_r, const int64_t* cap, const int64_t* current,
+                  const uint32_t* elem_flags, const int64_t* total, const uint32_t* row_flags,
+                  int64_t* out_plan, int64_t* out_overflow);
+
+/* Debug: per (unit, cluster) feasibility and total score of the last
+ * kad_schedule (feasible: u8[W*C]; total: i64[W*C], meaningful where feasible). */
+int kad_debug_scores(kad_ctx* ctx, const kad_profile* profile, uint8_t* feasible, int64_t* total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KAD_SCHED_H */

@@ -1,0 +1,89 @@
+"""The C restatement (oracle/kad_ref.c over packed blobs) == the pinned Python oracle (objects).
+
+This validates, at once, the host packer (kubeadmiral_amd/pack.py: interning,
+program compilation, resource conversion) and the C oracle that the GPU
+parity tests and the CPU baseline use at sizes the Python oracle cannot reach.
+"""
+
+import pytest
+
+from kubeadmiral_amd import pack, synth
+from kubeadmiral_amd import types as T
+from kubeadmiral_amd.results import to_schedule_result
+from oracle import kad_oracle as O
+from oracle import ref
+
+
+def oracle_fwk(fwk):
+    e = fwk.enabled
+    return O.Framework(O.EnabledPlugins(e.filter_plugins, e.score_plugins, e.select_plugins, e.replicas_plugins))
+
+
+def py_results(fwk, units, clusters):
+    ofw = oracle_fwk(fwk)
+    out = []
+    for su in units:
+        kind, val = O.schedule_or_error(ofw, su, clusters)
+        out.append(T.ScheduleError(val) if kind == "error" else val)
+    return out
+
+
+def same(a, b):
+    if isinstance(a, T.ScheduleError) or isinstance(b, T.ScheduleError):
+        return isinstance(a, T.ScheduleError) and isinstance(b, T.ScheduleError) and a.stage == b.stage
+    return a.suggested_clusters == b.suggested_clusters
+
+
+def compare(clusters, units, fwk, n_threads=1):
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, units)
+    res = ref.schedule(snap, batch, fwk, n_threads=n_threads)
+    want = py_results(fwk, units, clusters)
+    bad = []
+    for w, su in enumerate(units):
+        got = to_schedule_result(res, w, su, snap.names)
+        if not same(got, want[w]):
+            bad.append((w, su.name, got, want[w]))
+    return bad
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_c_oracle_matches_python_oracle_fuzz(seed):
+    clusters, units = synth.gen_fuzz(seed, W=50)
+    fwk = synth.fuzz_framework(seed)
+    bad = compare(clusters, units, fwk)
+    assert not bad, bad[:3]
+
+
+def test_c_oracle_matches_python_oracle_c1():
+    clusters, units, fwk = synth.make_config("c1", W=200)
+    assert not compare(clusters, units, fwk, n_threads=4)
+
+
+def test_c_oracle_matches_python_oracle_c2_small():
+    clusters, units, fwk = synth.make_config("c2", W=150, C=64)
+    assert not compare(clusters, units, fwk)
+
+
+def test_c_oracle_matches_python_oracle_c4_small():
+    clusters, units, fwk = synth.make_config("c4", W=120, C=80)
+    assert not compare(clusters, units, fwk)
+
+
+def test_c_oracle_matches_python_oracle_c5_small():
+    clusters, units, fwk = synth.make_config("c5", W=40, C=120)
+    assert not compare(clusters, units, fwk)
+
+
+def test_c_select_rows_match_python_sort():
+    import numpy as np
+    from oracle.gosem import go_sort_slice
+    rng = np.random.default_rng(7)
+    for _ in range(300):
+        n = int(rng.integers(0, 200))
+        scores = rng.integers(0, int(rng.integers(1, 12)), n).tolist()
+        k = int(rng.integers(0, n + 2))
+        items = [[i, s] for i, s in enumerate(scores)]
+        go_sort_slice(items, lambda a, b: a[1] > b[1])
+        want = [i for i, _ in items[:min(k, n)]]
+        assert ref.select_row(scores, k) == want
