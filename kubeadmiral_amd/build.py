@@ -1,0 +1,54 @@
+"""Build libkad.so (HIP, gfx950) in-tree, next to this file.
+
+    python -m kubeadmiral_amd.build [--force] [--verbose]
+
+hipcc cross-compiles for gfx950 without a GPU. ``-ffp-contract=off`` keeps
+BalancedAllocation's and rsp's float64 arithmetic bit-identical to Go (no FMA
+contraction, SURVEY.md §7 hard part 2).
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libkad.so")
+SOURCES = ["kad_kernels.hip", "kad_api.hip"]
+HEADERS = ["kad_device.h", "kad_wave.h", "kad_select.h", "kad_plan.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("KAD_OFFLOAD_ARCH", "gfx950")
+
+
+def _inputs():
+    return [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [
+        os.path.join(os.path.dirname(HERE), "include", "kad_sched.h")]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(p) <= t for p in _inputs())
+
+
+def build(force: bool = False, verbose: bool = False, extra=()) -> str:
+    if not force and up_to_date():
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+           "-fno-fast-math", "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"]
+    cmd += list(extra)
+    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True,
+          extra=["-Rpass-analysis=kernel-resource-usage"] if "--resource-usage" in sys.argv else [])
+    print(LIB)

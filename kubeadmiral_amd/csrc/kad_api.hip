@@ -1,0 +1,525 @@
+// C ABI of libkad.so (include/kad_sched.h): context, residency, launch, results.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kad_sched.h"
+#include "kad_device.h"
+
+using namespace kad;
+
+struct kad_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::mutex mu;
+  std::string err;
+  // snapshot
+  void* d_snap = nullptr;
+  size_t snap_bytes = 0;
+  kad_snapshot_header snap_hdr{};
+  SnapDev sd{};
+  // batch
+  void* d_batch = nullptr;
+  size_t batch_cap = 0;
+  kad_batch_header batch_hdr{};
+  BatchDev bd{};
+  std::vector<int32_t> plan_rows;
+  int32_t* d_plan_rows = nullptr;
+  size_t plan_rows_cap = 0;
+  // outputs
+  int32_t *d_status = nullptr, *d_count = nullptr, *d_cluster = nullptr;
+  uint32_t* d_flags = nullptr;
+  int64_t* d_replicas = nullptr;
+  size_t out_w_cap = 0, out_slot_cap = 0;
+  // scratch (per-wave slabs for rows that do not fit LDS)
+  void* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  bool have_snapshot = false, have_batch = false, ran = false;
+};
+
+static int fail(kad_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPCHK(ctx, x)                                                                             \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) return fail(ctx, KAD_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+static const T* at(const void* base, const uint64_t* off, int i) {
+  return reinterpret_cast<const T*>(static_cast<const char*>(base) + off[i]);
+}
+
+static int grow(kad_ctx* c, void** p, size_t* cap, size_t need) {
+  if (need <= *cap && *p) return 0;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (need == 0) need = 256;
+  hipError_t e = hipMalloc(p, need);
+  if (e != hipSuccess) return fail(c, KAD_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  *cap = need;
+  return 0;
+}
+
+template <class T>
+static int to_dev(kad_ctx* c, const T* h, size_t n, T** d, std::vector<void*>& owned) {
+  HIPCHK(c, hipMalloc((void**)d, (n ? n : 1) * sizeof(T)));
+  owned.push_back(*d);
+  if (n) HIPCHK(c, hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+extern "C" {
+
+int kad_abi_version(void) { return KAD_ABI_VERSION; }
+
+int kad_ctx_create(int hip_device, kad_ctx** out) {
+  if (!out) return KAD_EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return KAD_EHIP;
+  if (hip_device < 0 || hip_device >= n) return KAD_EINVAL;
+  auto* c = new kad_ctx();
+  c->device = hip_device;
+  if (hipSetDevice(hip_device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return KAD_EHIP;
+  }
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return KAD_EHIP;
+    }
+  *out = c;
+  return KAD_OK;
+}
+
+int kad_ctx_destroy(kad_ctx* c) {
+  if (!c) return KAD_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_status, (void*)c->d_count,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch})
+    if (p) (void)hipFree(p);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return KAD_OK;
+}
+
+const char* kad_last_error(kad_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+static int bind_snapshot(kad_ctx* c, const kad_snapshot_header& h) {
+  const char* base = static_cast<const char*>(c->d_snap);
+  SnapDev& s = c->sd;
+  s.C = h.n_clusters;
+  s.GW = h.n_gvk_words;
+  s.TW = h.n_taint_words;
+  s.K = h.n_label_keys;
+  s.S = h.n_scalar;
+  s.alloc_cpu = at<int64_t>(base, h.off, KAD_S_ALLOC_CPU);
+  s.alloc_mem = at<int64_t>(base, h.off, KAD_S_ALLOC_MEM);
+  s.used_cpu = at<int64_t>(base, h.off, KAD_S_USED_CPU);
+  s.used_mem = at<int64_t>(base, h.off, KAD_S_USED_MEM);
+  s.alloc_s = at<int64_t>(base, h.off, KAD_S_ALLOC_SCALAR);
+  s.used_s = at<int64_t>(base, h.off, KAD_S_USED_SCALAR);
+  s.alloc_cores = at<int64_t>(base, h.off, KAD_S_ALLOC_CORES);
+  s.avail_cores = at<int64_t>(base, h.off, KAD_S_AVAIL_CORES);
+  s.gvk = at<uint64_t>(base, h.off, KAD_S_GVK);
+  s.nsne = at<uint64_t>(base, h.off, KAD_S_TAINT_NSNE);
+  s.ne = at<uint64_t>(base, h.off, KAD_S_TAINT_NE);
+  s.pns = at<uint64_t>(base, h.off, KAD_S_TAINT_PNS);
+  s.lval = at<int32_t>(base, h.off, KAD_S_LABEL_VAL);
+  s.lint = at<int64_t>(base, h.off, KAD_S_LABEL_INT);
+  s.lok = at<uint8_t>(base, h.off, KAD_S_LABEL_INT_OK);
+  s.name_fnv = at<uint32_t>(base, h.off, KAD_S_NAME_FNV);
+  if (s.C < 0 || s.C > 65535) return fail(c, KAD_EINVAL, "n_clusters must be in [0, 65535]");
+  return 0;
+}
+
+static int check_snapshot_header(kad_ctx* c, const kad_snapshot_header& h, size_t nbytes) {
+  if (nbytes < sizeof(h) || h.magic != KAD_SNAPSHOT_MAGIC) return fail(c, KAD_EINVAL, "bad snapshot magic");
+  if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "snapshot ABI version mismatch");
+  if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "snapshot size mismatch");
+  for (int i = 0; i < KAD_S_NARRAYS; i++)
+    if (h.off[i] > nbytes || (h.off[i] & 7)) return fail(c, KAD_EINVAL, "bad snapshot array offset");
+  return 0;
+}
+
+int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
+  if (!c || !blob) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  kad_snapshot_header h;
+  std::memcpy(&h, blob, sizeof(h) < nbytes ? sizeof(h) : nbytes);
+  if (int r = check_snapshot_header(c, h, nbytes)) return r;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_snap, blob, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->snap_hdr = h;
+  if (int r = bind_snapshot(c, h)) return r;
+  c->have_snapshot = true;
+  c->have_batch = false;
+  return KAD_OK;
+}
+
+int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) {
+  if (!c || !dev_blob) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  kad_snapshot_header h;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpy(&h, dev_blob, sizeof(h), hipMemcpyDeviceToHost));
+  if (int r = check_snapshot_header(c, h, nbytes)) return r;
+  if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_snap, dev_blob, nbytes, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->snap_hdr = h;
+  if (int r = bind_snapshot(c, h)) return r;
+  c->have_snapshot = true;
+  c->have_batch = false;
+  return KAD_OK;
+}
+
+int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
+  if (!c || !blob) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot uploaded");
+  kad_batch_header h;
+  if (nbytes < sizeof(h)) return fail(c, KAD_EINVAL, "batch too small");
+  std::memcpy(&h, blob, sizeof(h));
+  if (h.magic != KAD_BATCH_MAGIC) return fail(c, KAD_EINVAL, "bad batch magic");
+  if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "batch ABI version mismatch");
+  if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "batch size mismatch");
+  if (h.snapshot_fingerprint != c->snap_hdr.fingerprint || h.n_clusters != c->snap_hdr.n_clusters ||
+      h.n_taint_words != c->snap_hdr.n_taint_words)
+    return fail(c, KAD_EINVAL, "batch was packed against a different snapshot");
+  for (int i = 0; i < KAD_B_NARRAYS; i++)
+    if (h.off[i] > nbytes || (h.off[i] & 7)) return fail(c, KAD_EINVAL, "bad batch array offset");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int r = grow(c, &c->d_batch, &c->batch_cap, nbytes)) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_batch, blob, nbytes, hipMemcpyHostToDevice, c->stream));
+  const int W = h.n_units;
+  // rows that need the replica planner: Divide mode, DesiredReplicas > 0, not sticky
+  const uint32_t* fl = at<uint32_t>(blob, h.off, KAD_B_FLAGS);
+  const int64_t* des = at<int64_t>(blob, h.off, KAD_B_DESIRED);
+  c->plan_rows.clear();
+  for (int w = 0; w < W; w++) {
+    const uint32_t f = fl[w];
+    if (!(f & KAD_W_DUPLICATE) && !(f & KAD_W_STICKY) && (f & KAD_W_HAS_DESIRED) && des[w] > 0) c->plan_rows.push_back(w);
+  }
+  if (int r = grow(c, (void**)&c->d_plan_rows, &c->plan_rows_cap, c->plan_rows.size() * 4)) return r;
+  if (!c->plan_rows.empty())
+    HIPCHK(c, hipMemcpyAsync(c->d_plan_rows, c->plan_rows.data(), c->plan_rows.size() * 4, hipMemcpyHostToDevice,
+                             c->stream));
+  // outputs
+  size_t wcap = c->out_w_cap, scap = c->out_slot_cap;
+  if ((size_t)W > c->out_w_cap || !c->d_status) {
+    if (c->d_status) { (void)hipFree(c->d_status); (void)hipFree(c->d_count); (void)hipFree(c->d_flags); }
+    c->d_status = c->d_count = nullptr;
+    c->d_flags = nullptr;
+    wcap = W > 0 ? W : 1;
+    HIPCHK(c, hipMalloc(&c->d_status, wcap * 4));
+    HIPCHK(c, hipMalloc(&c->d_count, wcap * 4));
+    HIPCHK(c, hipMalloc(&c->d_flags, wcap * 4));
+    c->out_w_cap = wcap;
+  }
+  const size_t slots = h.n_out_slots > 0 ? (size_t)h.n_out_slots : 1;
+  if (slots > scap || !c->d_cluster) {
+    if (c->d_cluster) { (void)hipFree(c->d_cluster); (void)hipFree(c->d_replicas); }
+    HIPCHK(c, hipMalloc(&c->d_cluster, slots * 4));
+    HIPCHK(c, hipMalloc(&c->d_replicas, slots * 8));
+    c->out_slot_cap = slots;
+  }
+  // scratch for rows whose state does not fit LDS
+  size_t need = 0;
+  const size_t sw = select_wave_bytes(c->sd.C);
+  if (sw > 64 * 1024) need = sw * (W < 8192 ? (W > 0 ? W : 1) : 8192);
+  const size_t pw = plan_wave_bytes(h.max_row_slots);
+  if (pw > 64 * 1024) {
+    size_t n2 = pw * (c->plan_rows.size() < 8192 ? (c->plan_rows.empty() ? 1 : c->plan_rows.size()) : 8192);
+    need = need > n2 ? need : n2;
+  }
+  if (need > c->scratch_bytes) {
+    if (c->d_scratch) (void)hipFree(c->d_scratch);
+    c->d_scratch = nullptr;
+    c->scratch_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_scratch, need));
+    c->scratch_bytes = need;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->batch_hdr = h;
+  const char* base = static_cast<const char*>(c->d_batch);
+  BatchDev& b = c->bd;
+  b.W = W;
+  b.NT = h.n_tolsets;
+  b.TW = h.n_taint_words;
+  b.flags = at<uint32_t>(base, h.off, KAD_B_FLAGS);
+  b.gvk = at<int32_t>(base, h.off, KAD_B_GVK);
+  b.req_cpu = at<int64_t>(base, h.off, KAD_B_REQ_CPU);
+  b.req_mem = at<int64_t>(base, h.off, KAD_B_REQ_MEM);
+  b.desired = at<int64_t>(base, h.off, KAD_B_DESIRED);
+  b.maxc = at<int64_t>(base, h.off, KAD_B_MAX_CLUSTERS);
+  b.tolset = at<int32_t>(base, h.off, KAD_B_TOLSET);
+  b.tol_all = at<uint64_t>(base, h.off, KAD_B_TOL_ALL);
+  b.tol_pns = at<uint64_t>(base, h.off, KAD_B_TOL_PNS);
+  b.sreq_off = at<int32_t>(base, h.off, KAD_B_SREQ_OFF);
+  b.sreq_id = at<int32_t>(base, h.off, KAD_B_SREQ_ID);
+  b.sreq_val = at<int64_t>(base, h.off, KAD_B_SREQ_VAL);
+  b.fprog_off = at<int32_t>(base, h.off, KAD_B_FPROG_OFF);
+  b.fprog = at<int32_t>(base, h.off, KAD_B_FPROG);
+  b.sprog_off = at<int32_t>(base, h.off, KAD_B_SPROG_OFF);
+  b.sprog = at<int32_t>(base, h.off, KAD_B_SPROG);
+  b.place_off = at<int32_t>(base, h.off, KAD_B_PLACE_OFF);
+  b.place = at<int32_t>(base, h.off, KAD_B_PLACE);
+  b.cur_off = at<int32_t>(base, h.off, KAD_B_CUR_OFF);
+  b.cur_id = at<int32_t>(base, h.off, KAD_B_CUR_ID);
+  b.cur_rep = at<int64_t>(base, h.off, KAD_B_CUR_REP);
+  b.pref_off = at<int32_t>(base, h.off, KAD_B_PREF_OFF);
+  b.pref_id = at<int32_t>(base, h.off, KAD_B_PREF_ID);
+  b.pref_w = at<int64_t>(base, h.off, KAD_B_PREF_W);
+  b.pref_min = at<int64_t>(base, h.off, KAD_B_PREF_MIN);
+  b.pref_max = at<int64_t>(base, h.off, KAD_B_PREF_MAX);
+  b.pref_cap = at<int64_t>(base, h.off, KAD_B_PREF_CAP);
+  b.pref_fl = at<uint32_t>(base, h.off, KAD_B_PREF_FLAGS);
+  b.key_off = at<int32_t>(base, h.off, KAD_B_KEY_OFF);
+  b.key = at<uint8_t>(base, h.off, KAD_B_KEY);
+  b.out_off = at<int64_t>(base, h.off, KAD_B_OUT_OFF);
+  c->have_batch = true;
+  c->ran = false;
+  return KAD_OK;
+}
+
+static int validate_profile(kad_ctx* c, const kad_profile* p) {
+  if (!p) return fail(c, KAD_EINVAL, "null profile");
+  const uint32_t filters = (1u << KAD_PL_API_RESOURCES) | (1u << KAD_PL_TAINT_TOLERATION) |
+                           (1u << KAD_PL_CLUSTER_RESOURCES_FIT) | (1u << KAD_PL_PLACEMENT_FILTER) |
+                           (1u << KAD_PL_CLUSTER_AFFINITY);
+  const uint32_t scores = (1u << KAD_PL_TAINT_TOLERATION) | (1u << KAD_PL_BALANCED_ALLOCATION) |
+                          (1u << KAD_PL_LEAST_ALLOCATED) | (1u << KAD_PL_MOST_ALLOCATED) |
+                          (1u << KAD_PL_CLUSTER_AFFINITY);
+  if (p->filter_mask & ~filters) return fail(c, KAD_EUNSUPPORTED, "filter plugin outside the in-tree set");
+  if (p->score_mask & ~scores) return fail(c, KAD_EUNSUPPORTED, "score plugin outside the in-tree set");
+  if (p->select_plugin != -1 && p->select_plugin != KAD_PL_MAX_CLUSTER)
+    return fail(c, KAD_EUNSUPPORTED, "select plugin outside the in-tree set");
+  if (p->replicas_plugin != -1 && p->replicas_plugin != KAD_PL_CLUSTER_CAPACITY_WEIGHT)
+    return fail(c, KAD_EUNSUPPORTED, "replicas plugin outside the in-tree set");
+  return 0;
+}
+
+static OutDev out_dev(kad_ctx* c) {
+  OutDev o{};
+  o.status = c->d_status;
+  o.count = c->d_count;
+  o.flags = c->d_flags;
+  o.cluster = c->d_cluster;
+  o.replicas = c->d_replicas;
+  return o;
+}
+
+static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, int64_t* dbg_total) {
+  if (!c->have_snapshot || !c->have_batch) return fail(c, KAD_ESTATE, "snapshot and batch must be uploaded first");
+  if (int r = validate_profile(c, p)) return r;
+  if (p->filter_mask != c->batch_hdr.packed_filter_mask || p->select_plugin != c->batch_hdr.packed_select_plugin)
+    return fail(c, KAD_EINVAL, "profile differs from the one the batch output bounds were packed for");
+  HIPCHK(c, hipSetDevice(c->device));
+  ProfDev pd{p->filter_mask, p->score_mask, p->select_plugin, p->replicas_plugin, p->flags};
+  OutDev o = out_dev(c);
+  o.dbg_feas = dbg_feas;
+  o.dbg_total = dbg_total;
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())
+    HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, c->d_plan_rows, (int)c->plan_rows.size(), c->batch_hdr.max_row_slots,
+                          c->d_scratch, c->scratch_bytes, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  c->ran = true;
+  return KAD_OK;
+}
+
+int kad_schedule(kad_ctx* c, const kad_profile* p) {
+  if (!c) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return schedule_locked(c, p, nullptr, nullptr);
+}
+
+int kad_sync(kad_ctx* c) {
+  if (!c) return KAD_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KAD_OK;
+}
+
+int kad_last_timing(kad_ctx* c, float ms[3]) {
+  if (!c || !ms) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
+  HIPCHK(c, hipEventSynchronize(c->ev[2]));
+  HIPCHK(c, hipEventElapsedTime(&ms[0], c->ev[0], c->ev[2]));
+  HIPCHK(c, hipEventElapsedTime(&ms[1], c->ev[0], c->ev[1]));
+  HIPCHK(c, hipEventElapsedTime(&ms[2], c->ev[1], c->ev[2]));
+  return KAD_OK;
+}
+
+int kad_results_download(kad_ctx* c, const kad_result_view* out) {
+  if (!c || !out) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t W = c->batch_hdr.n_units;
+  const size_t S = c->batch_hdr.n_out_slots;
+  if (W) {
+    HIPCHK(c, hipMemcpyAsync(out->status, c->d_status, W * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->count, c->d_count, W * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->flags, c->d_flags, W * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (S) {
+    HIPCHK(c, hipMemcpyAsync(out->cluster, c->d_cluster, S * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->replicas, c->d_replicas, S * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KAD_OK;
+}
+
+int kad_schedule_batch(kad_ctx* c, const kad_profile* p, const void* blob, size_t nbytes, const kad_result_view* out) {
+  if (int r = kad_batch_upload(c, blob, nbytes)) return r;
+  if (int r = kad_schedule(c, p)) return r;
+  return kad_results_download(c, out);
+}
+
+int kad_debug_scores(kad_ctx* c, const kad_profile* p, uint8_t* feasible, int64_t* total) {
+  if (!c || !feasible || !total) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  const size_t n = (size_t)c->batch_hdr.n_units * c->sd.C;
+  uint8_t* df = nullptr;
+  int64_t* dt = nullptr;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMalloc(&df, n ? n : 1));
+  HIPCHK(c, hipMalloc(&dt, (n ? n : 1) * 8));
+  HIPCHK(c, hipMemsetAsync(df, 0, n ? n : 1, c->stream));
+  HIPCHK(c, hipMemsetAsync(dt, 0, (n ? n : 1) * 8, c->stream));
+  int r = schedule_locked(c, p, df, dt);
+  if (r == 0 && n) {
+    HIPCHK(c, hipMemcpyAsync(feasible, df, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(total, dt, n * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(df);
+  (void)hipFree(dt);
+  return r;
+}
+
+
+int kad_select_rows(kad_ctx* c, int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,
+                    uint32_t pflags, int32_t* out_count, int32_t* out_sel, int32_t* out_status) {
+  if (!c || n_rows < 0) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t tot = row_off[n_rows];
+  int kmax = 1;
+  for (int r = 0; r < n_rows; r++) {
+    const int k = row_off[r + 1] - row_off[r];
+    if (k > 65535) return fail(c, KAD_EINVAL, "row longer than 65535");
+    kmax = k > kmax ? k : kmax;
+  }
+  std::vector<void*> owned;
+  int32_t *d_off, *d_cnt, *d_sel, *d_st;
+  int64_t *d_sc, *d_mc;
+  int r = 0;
+  if ((r = to_dev(c, row_off, n_rows + 1, &d_off, owned)) || (r = to_dev(c, scores, tot, &d_sc, owned)) ||
+      (r = to_dev(c, maxc, n_rows, &d_mc, owned)) || (r = to_dev<int32_t>(c, nullptr, n_rows, &d_cnt, owned)) ||
+      (r = to_dev<int32_t>(c, nullptr, tot, &d_sel, owned)) || (r = to_dev<int32_t>(c, nullptr, n_rows, &d_st, owned))) {
+    for (void* p : owned) (void)hipFree(p);
+    return r;
+  }
+  void* scr = nullptr;
+  size_t scr_bytes = 0;
+  const size_t wb = select_wave_bytes(kmax);
+  if (wb > 64 * 1024) {
+    scr_bytes = wb * (size_t)(n_rows < 4096 ? n_rows : 4096);
+    HIPCHK(c, hipMalloc(&scr, scr_bytes));
+    owned.push_back(scr);
+  }
+  hipError_t e = launch_select_rows(n_rows, d_off, d_sc, d_mc, pflags, kmax, d_cnt, d_sel, d_st, scr, scr_bytes, c->stream);
+  if (e == hipSuccess) {
+    (void)hipMemcpyAsync(out_count, d_cnt, n_rows * 4, hipMemcpyDeviceToHost, c->stream);
+    if (tot) (void)hipMemcpyAsync(out_sel, d_sel, tot * 4, hipMemcpyDeviceToHost, c->stream);
+    (void)hipMemcpyAsync(out_status, d_st, n_rows * 4, hipMemcpyDeviceToHost, c->stream);
+    e = hipStreamSynchronize(c->stream);
+  }
+  for (void* p : owned) (void)hipFree(p);
+  if (e != hipSuccess) return fail(c, KAD_EHIP, hipGetErrorString(e));
+  return KAD_OK;
+}
+
+int kad_plan_rows(kad_ctx* c, int n_rows, const int32_t* row_off, const uint32_t* hash, const int64_t* weight,
+                  const int64_t* min_r, const int64_t* max_r, const int64_t* cap, const int64_t* current,
+                  const uint32_t* elem_flags, const int64_t* total, const uint32_t* row_flags, int64_t* out_plan,
+                  int64_t* out_overflow) {
+  if (!c || n_rows < 0) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t tot = row_off[n_rows];
+  int kmax = 1;
+  for (int r = 0; r < n_rows; r++) {
+    const int k = row_off[r + 1] - row_off[r];
+    kmax = k > kmax ? k : kmax;
+  }
+  std::vector<void*> owned;
+  PlanRowsDev R{};
+  R.n_rows = n_rows;
+  int32_t* d_off;
+  uint32_t *d_hash, *d_ef, *d_rf;
+  int64_t *d_w, *d_mn, *d_mx, *d_cap, *d_cur, *d_tot, *d_plan, *d_over;
+  int r = 0;
+  if ((r = to_dev(c, row_off, n_rows + 1, &d_off, owned)) || (r = to_dev(c, hash, tot, &d_hash, owned)) ||
+      (r = to_dev(c, weight, tot, &d_w, owned)) || (r = to_dev(c, min_r, tot, &d_mn, owned)) ||
+      (r = to_dev(c, max_r, tot, &d_mx, owned)) || (r = to_dev(c, cap, tot, &d_cap, owned)) ||
+      (r = to_dev(c, current, tot, &d_cur, owned)) || (r = to_dev(c, elem_flags, tot, &d_ef, owned)) ||
+      (r = to_dev(c, total, n_rows, &d_tot, owned)) || (r = to_dev(c, row_flags, n_rows, &d_rf, owned)) ||
+      (r = to_dev<int64_t>(c, nullptr, tot, &d_plan, owned)) || (r = to_dev<int64_t>(c, nullptr, tot, &d_over, owned))) {
+    for (void* p : owned) (void)hipFree(p);
+    return r;
+  }
+  R.row_off = d_off;
+  R.hash = d_hash;
+  R.weight = d_w;
+  R.min_r = d_mn;
+  R.max_r = d_mx;
+  R.cap = d_cap;
+  R.current = d_cur;
+  R.elem_flags = d_ef;
+  R.total = d_tot;
+  R.row_flags = d_rf;
+  R.out_plan = d_plan;
+  R.out_overflow = d_over;
+  void* scr = nullptr;
+  size_t scr_bytes = 0;
+  const size_t wb = plan_wave_bytes(kmax);
+  if (wb > 64 * 1024) {
+    scr_bytes = wb * (size_t)(n_rows < 4096 ? n_rows : 4096);
+    HIPCHK(c, hipMalloc(&scr, scr_bytes));
+    owned.push_back(scr);
+  }
+  hipError_t e = launch_plan_rows(R, kmax, scr, scr_bytes, c->stream);
+  if (e == hipSuccess) {
+    if (tot) {
+      (void)hipMemcpyAsync(out_plan, d_plan, tot * 8, hipMemcpyDeviceToHost, c->stream);
+      (void)hipMemcpyAsync(out_overflow, d_over, tot * 8, hipMemcpyDeviceToHost, c->stream);
+    }
+    e = hipStreamSynchronize(c->stream);
+  }
+  for (void* p : owned) (void)hipFree(p);
+  if (e != hipSuccess) return fail(c, KAD_EHIP, hipGetErrorString(e));
+  return KAD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,747 @@
+// HIP kernels of libkad.so for gfx950 (MI355X, CDNA4).
+//
+// schedule_kernel — one 64-lane wavefront per SchedulingUnit:
+//   filters (ballot bitmask) → raw scores → per-row max → normalisation →
+//   totals → MaxCluster first-k set (radix select + restricted pdqsort replay)
+//   → ascending cluster-id output via ballot compaction.
+//   Reference: genericScheduler.Schedule, core/generic_scheduler.go:92-150.
+// plan_kernel — one wavefront per Divide-mode unit with ≥1 selected cluster:
+//   ClusterCapacityWeight (rsp.go:65-181) + planner.Plan (planner.go:83-366).
+//
+// Nothing here is a dense contraction (no MFMA). Cluster attributes are read
+// attribute-major (attr[i*C + c]) so each wave's 64 lanes read 64 consecutive
+// clusters: one coalesced 512-B access per i64 attribute. Per-row state lives
+// in LDS (per-wave region) when it fits, else in a per-wave global scratch slab.
+#include "kad_device.h"
+#include "kad_plan.h"
+#include "kad_select.h"
+#include "kad_wave.h"
+
+namespace kad {
+
+// ----------------------------------------------------------- per-wave layout
+struct RowLayout {
+  size_t tot, fx, idx, feas, sel, place, cur, hist, bytes;
+};
+__host__ __device__ inline RowLayout row_layout(int C) {
+  size_t Cp = (size_t)((C + 63) & ~63);
+  size_t nw = Cp / 64;
+  RowLayout L;
+  L.tot = 0;
+  L.fx = L.tot + 8 * Cp;
+  L.idx = L.fx + 4 * Cp;
+  L.feas = (L.idx + 2 * Cp + 15) & ~(size_t)15;
+  L.sel = L.feas + 8 * nw;
+  L.place = L.sel + 8 * nw;
+  L.cur = L.place + 8 * nw;
+  L.hist = L.cur + 8 * nw;
+  L.bytes = (L.hist + 4 * 256 + 15) & ~(size_t)15;
+  return L;
+}
+size_t select_wave_bytes(int C) { return row_layout(C).bytes; }
+
+// ---------------------------------------------------------- predicate programs
+__device__ __forceinline__ bool eval_req(const SnapDev& s, const int32_t* p, int c, int& used) {
+  const int w0 = p[0];
+  const int op = w0 & 0xff, n = w0 >> 8, key = p[1];
+  used = 2 + n;
+  switch (op) {
+    case KAD_OP_TRUE: return true;
+    case KAD_OP_FALSE: return false;
+    case KAD_OP_NAME_EQ: return c == key;
+    case KAD_OP_NAME_NE: return c != key;
+    default: break;
+  }
+  const size_t at = (size_t)key * s.C + c;
+  const int32_t v = s.lval[at];
+  switch (op) {
+    case KAD_OP_EXISTS: return v >= 0;
+    case KAD_OP_DNE: return v < 0;
+    case KAD_OP_EQ:
+    case KAD_OP_IN: {
+      bool hit = false;
+      for (int i = 0; i < n; i++) hit |= (p[2 + i] == v);
+      return v >= 0 && hit;
+    }
+    case KAD_OP_NOTIN: {
+      bool hit = false;
+      for (int i = 0; i < n; i++) hit |= (p[2 + i] == v);
+      return v < 0 || !hit;
+    }
+    case KAD_OP_GT:
+    case KAD_OP_LT: {
+      if (v < 0 || !s.lok[at]) return false;
+      const int64_t thr = (int64_t)(((uint64_t)(uint32_t)p[3] << 32) | (uint32_t)p[2]);
+      const int64_t lv = s.lint[at];
+      return op == KAD_OP_GT ? lv > thr : lv < thr;
+    }
+  }
+  return false;
+}
+
+// ClusterAffinity.Filter (cluster_affinity.go:50-94) with
+// clusterselector.MatchClusterSelectorTerms (clusterselector/util.go:97-132).
+__device__ bool filter_affinity(const SnapDev& s, const int32_t* p, int c) {
+  int used, pc = 0;
+  const int n_sel = p[pc++];
+  bool ok = true;
+  for (int i = 0; i < n_sel; i++) {
+    ok &= eval_req(s, p + pc, c, used);
+    pc += used;
+  }
+  if (!ok) return false;
+  if (!p[pc++]) return true;  // Required == nil
+  const int n_terms = p[pc++];
+  for (int t = 0; t < n_terms; t++) {
+    const int tf = p[pc], ne = p[pc + 1], nf = p[pc + 2];
+    pc += 3;
+    bool me = true;
+    for (int i = 0; i < ne; i++) {
+      me &= eval_req(s, p + pc, c, used);
+      pc += used;
+    }
+    bool mf = true;
+    for (int i = 0; i < nf; i++) {
+      mf &= eval_req(s, p + pc, c, used);
+      pc += used;
+    }
+    if (!(tf & (KAD_TERM_HAS_EXPR | KAD_TERM_HAS_FIELD))) continue;  // empty term: skipped
+    if (tf & KAD_TERM_HAS_EXPR) {
+      if (!(tf & KAD_TERM_EXPR_VALID)) return false;  // error when reached ⇒ false
+      if (!me) continue;
+    }
+    if (tf & KAD_TERM_HAS_FIELD) {
+      if (!(tf & KAD_TERM_FIELD_VALID)) return false;
+      if (!mf) continue;
+    }
+    return true;
+  }
+  return false;
+}
+
+// ClusterAffinity.Score raw (cluster_affinity.go:96-135)
+__device__ int64_t score_affinity(const SnapDev& s, const int32_t* p, int c) {
+  int used, pc = 0;
+  const int n_terms = p[pc++];
+  int64_t score = 0;
+  for (int t = 0; t < n_terms; t++) {
+    const int32_t wgt = p[pc], ne = p[pc + 1];
+    pc += 2;
+    bool m = true;
+    for (int i = 0; i < ne; i++) {
+      m &= eval_req(s, p + pc, c, used);
+      pc += used;
+    }
+    if (m) score = wadd(score, wgt);
+  }
+  return score;
+}
+
+// least_allocated.go:88-94 / most_allocated.go:90-97
+__device__ __forceinline__ int64_t least_requested(int64_t req, int64_t cap) {
+  if (cap == 0 || req > cap) return 0;
+  const int64_t num = wmul(wsub(cap, req), 100);
+  if (cap > 0 && req >= 0 && num >= 0) return small_quot(num, cap);
+  return go_div(num, cap);
+}
+__device__ __forceinline__ int64_t most_requested(int64_t req, int64_t cap) {
+  if (cap == 0 || req > cap) return 0;
+  const int64_t num = wmul(req, 100);
+  if (cap > 0 && req >= 0 && num >= 0) return small_quot(num, cap);
+  return go_div(num, cap);
+}
+// balanced_allocation.go:45-88 — IEEE float64, no contraction (-ffp-contract=off)
+__device__ __forceinline__ int64_t balanced(int64_t rc, int64_t cc, int64_t rm, int64_t cm) {
+  const double cf = cc == 0 ? 1.0 : (double)rc / (double)cc;
+  const double mf = cm == 0 ? 1.0 : (double)rm / (double)cm;
+  if (cf >= 1 || mf >= 1) return 0;
+  const double diff = fabs(cf - mf);
+  const double one_minus = 1 - diff;
+  return go_f2i(one_minus * 100.0);
+}
+
+constexpr uint32_t BIT(int pl) { return 1u << pl; }
+
+// ========================================================= schedule kernel
+template <bool GSCR>
+__global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, OutDev o, ProfDev p, char* gscratch,
+                                                       int wave_bytes, int waves_per_block, int w_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  const int gw = blockIdx.x * waves_per_block + wv;
+  char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem + (size_t)wv * wave_bytes;
+  const int C = s.C;
+  const RowLayout L = row_layout(C);
+  int64_t* tot = (int64_t*)(region + L.tot);
+  uint32_t* fx = (uint32_t*)(region + L.fx);
+  uint16_t* idxb = (uint16_t*)(region + L.idx);
+  uint64_t* feas = (uint64_t*)(region + L.feas);
+  uint64_t* selb = (uint64_t*)(region + L.sel);
+  uint64_t* plb = (uint64_t*)(region + L.place);
+  uint64_t* curb = (uint64_t*)(region + L.cur);
+  uint32_t* hist = (uint32_t*)(region + L.hist);
+  const int nch = (C + 63) >> 6;
+  const int TW = s.TW;
+  const uint32_t fm = p.filter_mask, sm = p.score_mask;
+  const int xs_b = (p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
+  const int xs_c = (p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+
+  for (int w = gw; w < b.W; w += w_stride) {
+    const uint32_t f = b.flags[w];
+    if (f & KAD_W_STICKY) {  // generic_scheduler.go:101-104
+      if (lane == 0) {
+        o.status[w] = KAD_ST_STICKY;
+        o.count[w] = 0;
+        o.flags[w] = 0;
+      }
+      continue;
+    }
+    const bool use_place = (fm & BIT(KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
+    const bool use_cur = (fm & BIT(KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
+    if (use_place || use_cur) {
+      for (int i = lane; i < nch; i += WAVE) {
+        plb[i] = 0;
+        curb[i] = 0;
+      }
+      wave_sync();
+      if (use_place)
+        for (int j = b.place_off[w] + lane; j < b.place_off[w + 1]; j += WAVE) {
+          const int c = b.place[j];
+          atomicOr((unsigned long long*)&plb[c >> 6], 1ull << (c & 63));
+        }
+      if (use_cur)
+        for (int j = b.cur_off[w] + lane; j < b.cur_off[w + 1]; j += WAVE) {
+          const int c = b.cur_id[j];
+          atomicOr((unsigned long long*)&curb[c >> 6], 1ull << (c & 63));
+        }
+      wave_sync();
+    }
+    const int gv = b.gvk[w];
+    const int ts = b.tolset[w];
+    const uint64_t* tolA = b.tol_all + (size_t)ts * TW;
+    const uint64_t* tolP = b.tol_pns + (size_t)ts * TW;
+    const int32_t* fp = b.fprog + b.fprog_off[w];
+    const int32_t* sp = b.sprog + b.sprog_off[w];
+    const int64_t rq_cpu = b.req_cpu[w], rq_mem = b.req_mem[w];
+    const bool fit_on = (fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO);
+    const int s0 = b.sreq_off[w], s1 = b.sreq_off[w + 1];
+
+    // ---------------- pass 1: filters + raw scores (findClustersThatFitWorkload)
+    int cnt = 0;
+    int64_t ttmax = 0, affmax = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int c = ch * WAVE + lane;
+      bool ok = c < C;
+      if (ok && (fm & BIT(KAD_PL_API_RESOURCES)))
+        ok = gv >= 0 && ((s.gvk[(size_t)(gv >> 6) * C + c] >> (gv & 63)) & 1);
+      if (ok && (fm & BIT(KAD_PL_TAINT_TOLERATION))) {
+        const bool sch = use_cur && ((curb[ch] >> lane) & 1);
+        const uint64_t* mt = sch ? s.ne : s.nsne;
+        for (int t = 0; t < TW; ++t) ok &= (mt[(size_t)t * C + c] & ~tolA[t]) == 0;
+      }
+      if (ok && fit_on) {
+        ok = s.alloc_cpu[c] >= wadd(rq_cpu, s.used_cpu[c]) && s.alloc_mem[c] >= wadd(rq_mem, s.used_mem[c]);
+        for (int j = s0; j < s1 && ok; ++j) {
+          const int sid = b.sreq_id[j];
+          const int64_t a = sid >= 0 ? s.alloc_s[(size_t)sid * C + c] : 0;
+          const int64_t u = sid >= 0 ? s.used_s[(size_t)sid * C + c] : 0;
+          ok = a >= wadd(b.sreq_val[j], u);
+        }
+      }
+      if (ok && use_place) ok = (plb[ch] >> lane) & 1;
+      if (ok && (fm & BIT(KAD_PL_CLUSTER_AFFINITY))) ok = filter_affinity(s, fp, c);
+      const uint64_t m = ballot(ok);
+      if (lane == 0) feas[ch] = m;
+      if (ok) {
+        const int64_t rc = wadd(s.used_cpu[c], rq_cpu), rm = wadd(s.used_mem[c], rq_mem);
+        const int64_t cc = s.alloc_cpu[c], cm = s.alloc_mem[c];
+        int64_t fixed = 0;
+        if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
+          fixed += go_div(wadd(least_requested(rm, cm), least_requested(rc, cc)), 2);
+        if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+          fixed += go_div(wadd(most_requested(rm, cm), most_requested(rc, cc)), 2);
+        if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) fixed += balanced(rc, cc, rm, cm);
+        int tt = 0;
+        if (sm & BIT(KAD_PL_TAINT_TOLERATION))
+          for (int t = 0; t < TW; ++t) tt += popc64(s.pns[(size_t)t * C + c] & ~tolP[t]);
+        int64_t aff = 0;
+        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) aff = score_affinity(s, sp, c);
+        fx[c] = (uint32_t)fixed | ((uint32_t)tt << 16);
+        tot[c] = aff;
+        ttmax = tt > ttmax ? tt : ttmax;
+        affmax = aff > affmax ? aff : affmax;
+        cnt++;
+      }
+    }
+    const int n = wave_sum_i32(cnt);
+    if (n == 0) {  // generic_scheduler.go:112-114
+      if (lane == 0) {
+        o.status[w] = KAD_ST_NO_FEASIBLE;
+        o.count[w] = 0;
+        o.flags[w] = 0;
+      }
+      continue;
+    }
+    if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && (f & KAD_W_SCORE_ERROR)) {  // framework.go:149-159
+      if (lane == 0) {
+        o.status[w] = KAD_ST_ERR_SCORE;
+        o.count[w] = 0;
+        o.flags[w] = 0;
+      }
+      continue;
+    }
+    ttmax = wave_max_i64(ttmax);
+    affmax = wave_max_i64(affmax);
+    wave_sync();
+
+    // ---------------- pass 2: DefaultNormalizeScore (framework/util.go:455-483) + sum
+    int64_t rmin = I64_MAX, rmax = I64_MIN;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int c = ch * WAVE + lane;
+      if (c < C && ((feas[ch] >> lane) & 1)) {
+        const uint32_t x = fx[c];
+        int64_t t = (int64_t)(x & 0xFFFF);
+        if (sm & BIT(KAD_PL_TAINT_TOLERATION)) {
+          const int64_t tt = (int64_t)(x >> 16);
+          t += ttmax == 0 ? 100 : 100 - (100 * tt) / ttmax;
+        }
+        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {
+          const int64_t a = tot[c];
+          t = wadd(t, affmax == 0 ? a : go_div(wmul(100, a), affmax));
+        }
+        tot[c] = t;
+        rmin = t < rmin ? t : rmin;
+        rmax = t > rmax ? t : rmax;
+        if (o.dbg_total) o.dbg_total[(size_t)w * C + c] = t;
+      }
+      if (o.dbg_feas && c < C) o.dbg_feas[(size_t)w * C + c] = (feas[ch] >> lane) & 1;
+    }
+    rmin = wave_min_i64(rmin);
+    rmax = wave_max_i64(rmax);
+    wave_sync();
+
+    // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
+    int64_t k = n;
+    if (p.select_plugin == KAD_PL_MAX_CLUSTER) {
+      const bool hm = f & KAD_W_HAS_MAX_CLUSTERS;
+      const int64_t mc = b.maxc[w];
+      if (hm && mc < 0) {
+        if (lane == 0) {
+          o.status[w] = KAD_ST_ERR_SELECT;
+          o.count[w] = 0;
+          o.flags[w] = 0;
+        }
+        continue;
+      }
+      if (hm && mc < k) k = mc;
+    }
+    SelWs ws{tot, feas, selb, idxb, hist};
+    const uint32_t rflags = select_topk(ws, C, n, k, rmin, rmax, xs_b, xs_c);
+
+    // ---------------- output: ascending cluster ids
+    const bool dup = f & KAD_W_DUPLICATE;
+    const bool replicas = !dup && p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (f & KAD_W_HAS_DESIRED) &&
+                          b.desired[w] > 0 && k > 0;
+    const int64_t off = b.out_off[w];
+    if (dup || replicas) {
+      int base = 0;
+      for (int ch = 0; ch < nch; ++ch) {
+        const uint64_t m = selb[ch];
+        if ((m >> lane) & 1) {
+          const int64_t at = off + base + mbcnt(m);
+          o.cluster[at] = ch * WAVE + lane;
+          o.replicas[at] = dup ? -1 : 0;
+        }
+        base += popc64(m);
+      }
+    }
+    if (lane == 0) {
+      o.status[w] = KAD_ST_OK;
+      o.count[w] = (dup || replicas) ? (int32_t)k : 0;  // Divide without replicas plugin: empty map
+      o.flags[w] = rflags;
+    }
+  }
+}
+
+// ============================================================ plan kernel
+struct PlanLayout {
+  size_t cid, hash, w, mn, mx, cap, cur, fl, plan, over, ofl, w2, mx2, adj, plan2, over2, ofl2, ord, act, act2, bytes;
+};
+__host__ __device__ inline PlanLayout plan_layout(int K) {
+  const size_t Kp = (size_t)((K + 63) & ~63);
+  PlanLayout L;
+  size_t o = 0;
+  auto take = [&](size_t n) {
+    size_t r = o;
+    o += (n + 15) & ~(size_t)15;
+    return r;
+  };
+  L.w = take(8 * Kp);
+  L.mn = take(8 * Kp);
+  L.mx = take(8 * Kp);
+  L.cap = take(8 * Kp);
+  L.cur = take(8 * Kp);
+  L.plan = take(8 * Kp);
+  L.over = take(8 * Kp);
+  L.w2 = take(8 * Kp);
+  L.mx2 = take(8 * Kp);
+  L.adj = take(8 * Kp);
+  L.plan2 = take(8 * Kp);
+  L.over2 = take(8 * Kp);
+  L.cid = take(4 * Kp);
+  L.hash = take(4 * Kp);
+  L.fl = take(4 * Kp);
+  L.ofl = take(4 * Kp);
+  L.ofl2 = take(4 * Kp);
+  L.ord = take(4 * Kp);
+  L.act = take(4 * Kp);
+  L.act2 = take(4 * Kp);
+  L.bytes = o;
+  return L;
+}
+size_t plan_wave_bytes(int K) { return plan_layout(K).bytes; }
+
+__device__ PlanWs plan_ws(char* region, int K) {
+  const PlanLayout L = plan_layout(K);
+  PlanWs ws;
+  ws.cid = (int32_t*)(region + L.cid);
+  ws.hash = (uint32_t*)(region + L.hash);
+  ws.w = (int64_t*)(region + L.w);
+  ws.mn = (int64_t*)(region + L.mn);
+  ws.mx = (int64_t*)(region + L.mx);
+  ws.cap = (int64_t*)(region + L.cap);
+  ws.cur = (int64_t*)(region + L.cur);
+  ws.fl = (uint32_t*)(region + L.fl);
+  ws.plan = (int64_t*)(region + L.plan);
+  ws.over = (int64_t*)(region + L.over);
+  ws.ofl = (uint32_t*)(region + L.ofl);
+  ws.w2 = (int64_t*)(region + L.w2);
+  ws.mx2 = (int64_t*)(region + L.mx2);
+  ws.adj = (int64_t*)(region + L.adj);
+  ws.plan2 = (int64_t*)(region + L.plan2);
+  ws.over2 = (int64_t*)(region + L.over2);
+  ws.ofl2 = (uint32_t*)(region + L.ofl2);
+  ws.ord = (int32_t*)(region + L.ord);
+  ws.act = (int32_t*)(region + L.act);
+  ws.act2 = (int32_t*)(region + L.act2);
+  return ws;
+}
+
+// binary search of cluster id c in a sorted CSR slice [lo, hi)
+__device__ __forceinline__ int find_sorted(const int32_t* a, int lo, int hi, int c) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const int v = a[mid];
+    if (v == c) return mid;
+    if (v < c)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return -1;
+}
+
+template <bool GSCR>
+__global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev o, const int32_t* rows, int n_rows,
+                                                  int kmax, char* gscratch, int wave_bytes, int r_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = lane_id();
+  const int gw = blockIdx.x;
+  char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem;
+  for (int r = gw; r < n_rows; r += r_stride) {
+    const int w = rows[r];
+    if (o.status[w] != KAD_ST_OK) continue;
+    const int K = o.count[w];
+    if (K <= 0) continue;
+    const uint32_t f = b.flags[w];
+    PlanWs ws = plan_ws(region, K);
+    const int64_t off = b.out_off[w];
+    const int p0 = b.pref_off[w], p1 = b.pref_off[w + 1];
+    const int c0 = b.cur_off[w], c1 = b.cur_off[w + 1];
+    const uint8_t* key = b.key + b.key_off[w];
+    const int klen = b.key_off[w + 1] - b.key_off[w];
+    const int64_t total = (f & KAD_W_HAS_DESIRED) ? b.desired[w] : 0;
+    // preferences (rsp.go:99-126)
+    for (int i = lane; i < K; i += WAVE) {
+      const int c = o.cluster[off + i];
+      ws.cid[i] = c;
+      ws.hash[i] = fnv_cont(s.name_fnv[c], key, klen);
+      const int pi = find_sorted(b.pref_id, p0, p1, c);
+      uint32_t fl = 0;
+      int64_t wt = 0, mn = 0, mx = 0, cp = 0;
+      if (pi >= 0) {
+        const uint32_t pf = b.pref_fl[pi];
+        if (pf & KAD_PREF_HAS_WEIGHT) wt = b.pref_w[pi];
+        mn = b.pref_min[pi];
+        if (pf & KAD_PREF_HAS_MAX) {
+          fl |= EF_HAS_MAX;
+          mx = b.pref_max[pi];
+        }
+        if (pf & KAD_PREF_HAS_CAP) {
+          fl |= EF_HAS_CAP;
+          cp = b.pref_cap[pi];
+        }
+      }
+      ws.w[i] = wt;
+      ws.mn[i] = mn;
+      ws.mx[i] = mx;
+      ws.cap[i] = cp;
+      ws.fl[i] = fl;
+      const int ci = find_sorted(b.cur_id, c0, c1, c);
+      ws.cur[i] = ci >= 0 ? b.cur_rep[ci] : 0;
+    }
+    wave_sync();
+    uint32_t rflags = o.flags[w];
+    if (f & KAD_W_DYNAMIC_WEIGHTS) {
+      // CalcWeightLimit (rsp.go:183-213) + AvailableToPercentage (rsp.go:215-272)
+      double sum = 0.0, suma = 0.0;
+      for (int i = lane; i < K; i += WAVE) {
+        const int c = ws.cid[i];
+        sum += (double)s.alloc_cores[c];
+        const int64_t av = s.avail_cores[c];
+        if (av > 0) suma += (double)av;
+      }
+      sum = wave_sum_f64(sum);
+      suma = wave_sum_f64(suma);
+      if (suma == 0) {
+        const int64_t even = go_f2i(round(1000.0 / (double)K));
+        for (int i = lane; i < K; i += WAVE) ws.w[i] = even;
+      } else {
+        int64_t sumtmp = 0;
+        for (int i = lane; i < K; i += WAVE) {
+          const int c = ws.cid[i];
+          const int64_t lim = sum == 0 ? go_f2i(round(1000.0 / (double)K))
+                                       : go_f2i(round((double)s.alloc_cores[c] / sum * 1000.0 * 1.4));
+          double v = (double)s.avail_cores[c];
+          if (v < 0.0) v = 0.0;
+          int64_t wt = go_f2i(round(v / suma * 1000.0));
+          if (wt > lim) wt = lim;
+          ws.w[i] = wt;
+          sumtmp = wadd(sumtmp, wt);
+        }
+        sumtmp = wave_sum_i64(sumtmp);
+        int64_t other = 0, maxw = 0;
+        for (int i = lane; i < K; i += WAVE) {
+          const int64_t wt = go_f2i(round((double)ws.w[i] / (double)sumtmp * 1000.0));
+          ws.w[i] = wt;
+          other = wadd(other, wt);
+          maxw = wt > maxw ? wt : maxw;
+        }
+        other = wave_sum_i64(other);
+        maxw = wave_max_i64(maxw);
+        wave_sync();
+        if (maxw > 0) {  // remainder → first strict maximum (lowest cluster id among ties)
+          int first = K, ties = 0;
+          for (int i = lane; i < K; i += WAVE) {
+            if (ws.w[i] == maxw) {
+              first = i < first ? i : first;
+              ties++;
+            }
+          }
+          for (int m = 32; m >= 1; m >>= 1) {
+            const int of = __shfl_xor(first, m);
+            first = of < first ? of : first;
+          }
+          ties = wave_sum_i32(ties);
+          if (ties > 1) rflags |= KAD_RF_REMAINDER_TIE;
+          if (lane == 0) ws.w[first] = wadd(ws.w[first], wsub(1000, other));
+        }
+      }
+      wave_sync();
+    }
+    const bool avoid = f & KAD_W_AVOID_DISRUPTION;
+    const bool keep = f & KAD_W_KEEP_UNSCHED;
+    rflags |= plan_row(ws, K, total, avoid, keep);
+    // result = plan + overflow, zeros dropped (rsp.go:162-179), ascending cluster id
+    int base = 0;
+    for (int i0 = 0; i0 < K; i0 += WAVE) {
+      const int i = i0 + lane;
+      int64_t r = 0;
+      if (i < K) r = wadd(ws.plan[i], (ws.ofl[i] & EF_HAS_OVER) ? ws.over[i] : 0);
+      const bool nz = i < K && r != 0;
+      const uint64_t m = ballot(nz);
+      if (nz) {
+        const int64_t at = off + base + mbcnt(m);
+        o.cluster[at] = ws.cid[i];
+        o.replicas[at] = r;
+      }
+      base += popc64(m);
+    }
+    if (lane == 0) {
+      o.count[w] = base;
+      o.flags[w] = rflags;
+    }
+    wave_sync();
+  }
+}
+
+// ============================================= stand-alone stage entry points
+template <bool GSCR>
+__global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32_t* row_off, const int64_t* scores,
+                                                         const int64_t* maxc, uint32_t pflags, int32_t* out_count,
+                                                         int32_t* out_sel, int32_t* out_status, char* gscratch,
+                                                         int wave_bytes, int kmax, int r_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = lane_id();
+  char* region = GSCR ? gscratch + (size_t)blockIdx.x * wave_bytes : smem;
+  const RowLayout L = row_layout(kmax);
+  int64_t* tot = (int64_t*)(region + L.tot);
+  uint16_t* idxb = (uint16_t*)(region + L.idx);
+  uint64_t* feas = (uint64_t*)(region + L.feas);
+  uint64_t* selb = (uint64_t*)(region + L.sel);
+  uint32_t* hist = (uint32_t*)(region + L.hist);
+  const int xs_b = (pflags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
+  const int xs_c = (pflags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+  for (int r = blockIdx.x; r < n_rows; r += r_stride) {
+    const int a = row_off[r], n = row_off[r + 1] - a;
+    const int64_t mc = maxc[r];
+    if (mc < 0) {
+      if (lane == 0) {
+        out_status[r] = KAD_ST_ERR_SELECT;
+        out_count[r] = 0;
+      }
+      continue;
+    }
+    const int nch = (n + 63) >> 6;
+    int64_t rmin = I64_MAX, rmax = I64_MIN;
+    for (int ch = 0; ch < nch; ++ch) {
+      const int c = ch * WAVE + lane;
+      const bool v = c < n;
+      if (v) {
+        const int64_t t = scores[a + c];
+        tot[c] = t;
+        rmin = t < rmin ? t : rmin;
+        rmax = t > rmax ? t : rmax;
+      }
+      const uint64_t m = ballot(v);
+      if (lane == 0) feas[ch] = m;
+    }
+    rmin = wave_min_i64(rmin);
+    rmax = wave_max_i64(rmax);
+    wave_sync();
+    const int64_t k = mc < n ? mc : n;
+    SelWs ws{tot, feas, selb, idxb, hist};
+    select_topk(ws, n, n, k, rmin, rmax, xs_b, xs_c);
+    int base = 0;
+    for (int ch = 0; ch < nch; ++ch) {
+      const uint64_t m = selb[ch];
+      if ((m >> lane) & 1) out_sel[a + base + mbcnt(m)] = ch * WAVE + lane;
+      base += popc64(m);
+    }
+    if (lane == 0) {
+      out_status[r] = KAD_ST_OK;
+      out_count[r] = base;
+    }
+    wave_sync();
+  }
+}
+
+template <bool GSCR>
+__global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscratch, int wave_bytes, int r_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = lane_id();
+  char* region = GSCR ? gscratch + (size_t)blockIdx.x * wave_bytes : smem;
+  for (int r = blockIdx.x; r < R.n_rows; r += r_stride) {
+    const int a = R.row_off[r], K = R.row_off[r + 1] - a;
+    if (K <= 0) continue;
+    PlanWs ws = plan_ws(region, K);
+    for (int i = lane; i < K; i += WAVE) {
+      ws.cid[i] = i;
+      ws.hash[i] = R.hash[a + i];
+      ws.w[i] = R.weight[a + i];
+      ws.mn[i] = R.min_r[a + i];
+      ws.mx[i] = R.max_r[a + i];
+      ws.cap[i] = R.cap[a + i];
+      ws.cur[i] = R.current[a + i];
+      ws.fl[i] = R.elem_flags[a + i] & (EF_HAS_MAX | EF_HAS_CAP);
+    }
+    wave_sync();
+    plan_row(ws, K, R.total[r], R.row_flags[r] & 1, (R.row_flags[r] >> 1) & 1);
+    for (int i = lane; i < K; i += WAVE) {
+      R.out_plan[a + i] = ws.plan[i];
+      R.out_overflow[a + i] = (ws.ofl[i] & EF_HAS_OVER) ? ws.over[i] : -1;
+    }
+    wave_sync();
+  }
+}
+
+// ================================================================ launchers
+static constexpr int LDS_BUDGET = 64 * 1024;  // per block
+static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
+
+hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
+                           size_t scr_bytes, hipStream_t st) {
+  if (b.W == 0) return hipSuccess;
+  const size_t wb = row_layout(s.C).bytes;
+  if (wb <= (size_t)LDS_BUDGET) {
+    int wpb = (int)(LDS_BUDGET / wb);
+    wpb = wpb > 4 ? 4 : (wpb < 1 ? 1 : wpb);
+    const int grid = (b.W + wpb - 1) / wpb;
+    hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid), dim3(64 * wpb), wb * wpb, st, s, b, o, p, (char*)nullptr,
+                       (int)wb, wpb, grid * wpb);
+  } else {
+    size_t slots = scr_bytes / wb;
+    if (slots < 1) return hipErrorInvalidValue;
+    if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
+    if (slots > (size_t)b.W) slots = b.W;
+    const int grid = (int)slots;
+    hipLaunchKernelGGL(schedule_kernel<true>, dim3(grid), dim3(64), 0, st, s, b, o, p, (char*)gscr, (int)wb, 1,
+                       grid);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,
+                       int n_rows, int kmax, void* gscr, size_t scr_bytes, hipStream_t st) {
+  (void)p;
+  if (n_rows == 0 || kmax <= 0) return hipSuccess;
+  const size_t wb = plan_layout(kmax).bytes;
+  if (wb <= (size_t)LDS_BUDGET) {
+    hipLaunchKernelGGL(plan_kernel<false>, dim3(n_rows), dim3(64), wb, st, s, b, o, rows, n_rows, kmax,
+                       (char*)nullptr, (int)wb, n_rows);
+  } else {
+    size_t slots = scr_bytes / wb;
+    if (slots < 1) return hipErrorInvalidValue;
+    if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
+    if (slots > (size_t)n_rows) slots = n_rows;
+    hipLaunchKernelGGL(plan_kernel<true>, dim3(slots), dim3(64), 0, st, s, b, o, rows, n_rows, kmax, (char*)gscr,
+                       (int)wb, (int)slots);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,
+                              uint32_t pflags, int kmax, int32_t* out_count, int32_t* out_sel, int32_t* out_status,
+                              void* gscr, size_t scr_bytes, hipStream_t st) {
+  if (n_rows == 0) return hipSuccess;
+  const size_t wb = row_layout(kmax < 1 ? 1 : kmax).bytes;
+  if (wb <= (size_t)LDS_BUDGET) {
+    hipLaunchKernelGGL(select_rows_kernel<false>, dim3(n_rows), dim3(64), wb, st, n_rows, row_off, scores, maxc,
+                       pflags, out_count, out_sel, out_status, (char*)nullptr, (int)wb, kmax < 1 ? 1 : kmax, n_rows);
+  } else {
+    size_t slots = scr_bytes / wb;
+    if (slots < 1) return hipErrorInvalidValue;
+    if (slots > (size_t)n_rows) slots = n_rows;
+    hipLaunchKernelGGL(select_rows_kernel<true>, dim3(slots), dim3(64), 0, st, n_rows, row_off, scores, maxc, pflags,
+                       out_count, out_sel, out_status, (char*)gscr, (int)wb, kmax, (int)slots);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, void* gscr, size_t scr_bytes, hipStream_t st) {
+  if (r.n_rows == 0 || kmax <= 0) return hipSuccess;
+  const size_t wb = plan_layout(kmax).bytes;
+  if (wb <= (size_t)LDS_BUDGET) {
+    hipLaunchKernelGGL(plan_rows_kernel<false>, dim3(r.n_rows), dim3(64), wb, st, r, (char*)nullptr, (int)wb,
+                       r.n_rows);
+  } else {
+    size_t slots = scr_bytes / wb;
+    if (slots < 1) return hipErrorInvalidValue;
+    if (slots > (size_t)r.n_rows) slots = r.n_rows;
+    hipLaunchKernelGGL(plan_rows_kernel<true>, dim3(slots), dim3(64), 0, st, r, (char*)gscr, (int)wb, (int)slots);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kad

@@ -1,0 +1,300 @@
+// Divide-mode replica planning on one wavefront:
+//   ClusterCapacityWeight.ReplicaScheduling (plugins/rsp/rsp.go:65-181) and
+//   planner.Plan (pkg/controllers/util/planner/planner.go:83-366).
+//
+// The planner's loops are sequential in `remainingReplicas`, but every step is
+// R ← R − min(min(e_i, R), V_i), i.e. R ← max(R − s_i, t_i) with
+// (s, t) = (min(e_i, V_i), 0) or (min(e_i, V_i), −∞). These clamp functions
+// compose associatively, (s1,t1)∘(s2,t2) = (s1+s2, max(t1−s2, t2)), so each
+// pass over the sorted preferences is a wavefront prefix scan instead of a
+// serial loop (SURVEY.md §7 hard part 5).
+#pragma once
+#include "kad_wave.h"
+
+namespace kad {
+
+constexpr uint32_t EF_HAS_MAX = 2u;
+constexpr uint32_t EF_HAS_CAP = 4u;
+constexpr uint32_t EF_HAS_OVER = 8u;   // overflow entry present
+constexpr uint32_t EF_HAS_PLAN = 16u;  // plan entry present
+
+struct Clamp {
+  int64_t s, t;
+};
+__device__ __forceinline__ Clamp clamp_compose(Clamp a, Clamp b) {  // a then b
+  Clamp r;
+  r.s = wadd(a.s, b.s);
+  int64_t at = a.t == NEG_INF ? NEG_INF : wsub(a.t, b.s);
+  r.t = at > b.t ? at : b.t;
+  return r;
+}
+__device__ __forceinline__ int64_t clamp_apply(Clamp f, int64_t R) {
+  int64_t x = wsub(R, f.s);
+  return x > f.t ? x : f.t;
+}
+// inclusive scan of clamp functions across the wave
+__device__ __forceinline__ Clamp wave_scan_clamp(Clamp v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    Clamp o;
+    o.s = shfl_up_i64(v.s, d);
+    o.t = shfl_up_i64(v.t, d);
+    if (l >= d) v = clamp_compose(o, v);
+  }
+  return v;
+}
+
+// Per-wave planner workspace: arrays indexed by element (K elements).
+struct PlanWs {
+  int32_t* cid;    // snapshot cluster id (ascending) — or row position in kad_plan_rows
+  uint32_t* hash;  // FNV-1 of name ‖ key
+  int64_t* w;      // weight
+  int64_t* mn;     // MinReplicas
+  int64_t* mx;     // MaxReplicas (EF_HAS_MAX)
+  int64_t* cap;    // estimated capacity (EF_HAS_CAP)
+  int64_t* cur;    // current replicas
+  uint32_t* fl;    // EF_* flags
+  int64_t* plan;   // desired plan / result plan
+  int64_t* over;   // overflow
+  uint32_t* ofl;   // EF_HAS_OVER / EF_HAS_PLAN for the plan being built
+  int64_t* w2;     // scale up/down weights
+  int64_t* mx2;    // scale up/down max (I64_MAX = none)
+  int64_t* adj;    // currentPlan
+  int64_t* plan2;  // scale up/down plan
+  int64_t* over2;  // scale up/down overflow (discarded by the reference)
+  uint32_t* ofl2;
+  int32_t* ord;    // sorted order
+  int32_t* act;    // active list / compaction buffer
+  int32_t* act2;
+};
+
+// sort elements in list[0..m) (element ids) by (weight desc, hash asc, id asc) into ord;
+// returns true if two elements tie on (weight, hash) (Go order would be map-order dependent).
+__device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const int32_t* list, int m) {
+  const int lane = lane_id();
+  bool tie = false;
+  for (int i = lane; i < m; i += WAVE) {
+    int e = list[i];
+    int64_t we = wt[e];
+    uint32_t he = ws.hash[e];
+    int rank = 0;
+    for (int j = 0; j < m; j++) {
+      int f = list[j];
+      int64_t wf = wt[f];
+      uint32_t hf = ws.hash[f];
+      bool before = wf > we || (wf == we && (hf < he || (hf == he && f < e)));
+      rank += before;
+      tie |= (f != e && wf == we && hf == he);
+    }
+    ws.act2[rank] = e;
+  }
+  wave_sync();
+  for (int i = lane; i < m; i += WAVE) ws.ord[i] = ws.act2[i];
+  wave_sync();
+  return ballot(tie) != 0;
+}
+
+// getDesiredPlan (planner.go:211-304) over the sorted list ord[0..m).
+// wt/mxv: weights and max (I64_MAX = none) per element; minimums from ws.mn
+// when use_min; capacities from ws.cap/EF_HAS_CAP when use_cap.
+// Writes plan[e], over[e], ofl[e] (EF_HAS_PLAN/EF_HAS_OVER) for listed e.
+__device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64_t* mxv, bool use_min, bool use_cap,
+                                int m, int64_t total, bool keep, int64_t* plan, int64_t* over, uint32_t* ofl) {
+  const int lane = lane_id();
+  // ---- minimum pass
+  int64_t R = total;
+  for (int base = 0; base < m; base += WAVE) {
+    int i = base + lane;
+    bool v = i < m;
+    int e = v ? ws.ord[i] : 0;
+    int64_t Mn = (v && use_min) ? ws.mn[e] : 0;
+    bool hc = v && use_cap && (ws.fl[e] & EF_HAS_CAP);
+    int64_t U = hc ? ws.cap[e] : I64_MAX;
+    Clamp f;
+    if (!v) {
+      f = {0, NEG_INF};
+    } else if (Mn >= 0) {
+      f = {Mn < U ? Mn : U, 0};
+    } else {
+      f = {Mn, NEG_INF};
+    }
+    Clamp inc = wave_scan_clamp(f);
+    Clamp exc;
+    exc.s = shfl_up_i64(inc.s, 1);
+    exc.t = shfl_up_i64(inc.t, 1);
+    if (lane == 0) exc = {0, NEG_INF};
+    int64_t Ri = clamp_apply(exc, R);
+    if (v) {
+      int64_t mt = Mn < Ri ? Mn : Ri;
+      uint32_t of = EF_HAS_PLAN;
+      if (hc && ws.cap[e] < mt) {
+        over[e] = mt - ws.cap[e];
+        of |= EF_HAS_OVER;
+        mt = ws.cap[e];
+      } else {
+        over[e] = 0;
+      }
+      plan[e] = mt;
+      ofl[e] = of;
+    }
+    int last = (m - base) < WAVE ? (m - base - 1) : (WAVE - 1);
+    Clamp tot;
+    tot.s = shfl_i64(inc.s, last);
+    tot.t = shfl_i64(inc.t, last);
+    R = clamp_apply(tot, R);
+  }
+  wave_sync();
+  // ---- weighted rounds
+  for (int i = lane; i < m; i += WAVE) ws.act[i] = ws.ord[i];
+  wave_sync();
+  int na = m;
+  bool modified = true;
+  // The reference loop ends after at most m+1 rounds for non-negative weights
+  // (planner.go:216-220); the bound only guards the GPU against a hang on
+  // adversarial (negative-weight) input, where Go itself would not terminate.
+  int rounds = 0;
+  while (modified && R > 0 && rounds++ < 4 * m + 64) {
+    modified = false;
+    int64_t wsum = 0;
+    for (int i = lane; i < na; i += WAVE) wsum = wadd(wsum, wt[ws.act[i]]);
+    wsum = wave_sum_i64(wsum);
+    if (wsum <= 0) break;
+    const int64_t D = R;
+    int keepn = 0;
+    bool mod = false;
+    for (int base = 0; base < na; base += WAVE) {
+      int i = base + lane;
+      bool v = i < na;
+      int e = v ? ws.act[i] : 0;
+      int64_t start = v ? plan[e] : 0;
+      int64_t ee = v ? go_div(wsub(wadd(wmul(D, wt[e]), wsum), 1), wsum) : 0;
+      bool hm = v && mxv[e] != I64_MAX;
+      bool hc = v && use_cap && (ws.fl[e] & EF_HAS_CAP);
+      int64_t U = I64_MAX;
+      if (hm) U = mxv[e];
+      if (hc && ws.cap[e] < U) U = ws.cap[e];
+      int64_t V = U == I64_MAX ? I64_MAX : wsub(U, start);
+      int64_t mm = ee < V ? ee : V;
+      Clamp f = !v ? Clamp{0, NEG_INF} : (mm >= 0 ? Clamp{mm, 0} : Clamp{mm, NEG_INF});
+      Clamp inc = wave_scan_clamp(f);
+      Clamp exc;
+      exc.s = shfl_up_i64(inc.s, 1);
+      exc.t = shfl_up_i64(inc.t, 1);
+      if (lane == 0) exc = {0, NEG_INF};
+      int64_t Ri = clamp_apply(exc, R);
+      bool full = false;
+      if (v) {
+        int64_t extra = ee < Ri ? ee : Ri;
+        int64_t t = wadd(start, extra);
+        if (hm && t > mxv[e]) {
+          t = mxv[e];
+          full = true;
+        }
+        if (hc && t > ws.cap[e]) {
+          over[e] = wadd((ofl[e] & EF_HAS_OVER) ? over[e] : 0, wsub(t, ws.cap[e]));
+          ofl[e] |= EF_HAS_OVER;
+          t = ws.cap[e];
+          full = true;
+        }
+        plan[e] = t;
+        if (t > start) mod = true;
+      }
+      uint64_t km = ballot(v && !full);
+      if (v && !full) ws.act2[keepn + mbcnt(km)] = e;
+      keepn += popc64(km);
+      int last = (na - base) < WAVE ? (na - base - 1) : (WAVE - 1);
+      Clamp tot;
+      tot.s = shfl_i64(inc.s, last);
+      tot.t = shfl_i64(inc.t, last);
+      R = clamp_apply(tot, R);
+    }
+    modified = ballot(mod) != 0;
+    wave_sync();
+    for (int i = lane; i < keepn; i += WAVE) ws.act[i] = ws.act2[i];
+    na = keepn;
+    wave_sync();
+  }
+  if (!keep) {
+    for (int i = lane; i < m; i += WAVE) {
+      int e = ws.ord[i];
+      if (ofl[e] & EF_HAS_OVER) {
+        int64_t v = over[e] < R ? over[e] : R;
+        if (v > 0) {
+          over[e] = v;
+        } else {
+          over[e] = 0;
+          ofl[e] &= ~EF_HAS_OVER;
+        }
+      }
+    }
+  }
+  wave_sync();
+  return R;
+}
+
+// planner.Plan (planner.go:83-177) for K elements 0..K-1, all with preferences.
+// Leaves the final plan in ws.plan, the overflow in ws.over/EF_HAS_OVER.
+__device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid, bool keep) {
+  const int lane = lane_id();
+  uint32_t rflags = 0;
+  for (int i = lane; i < K; i += WAVE) {
+    ws.act[i] = i;
+    ws.mx2[i] = (ws.fl[i] & EF_HAS_MAX) ? ws.mx[i] : I64_MAX;
+  }
+  wave_sync();
+  if (sort_by_weight_hash(ws, ws.w, ws.act, K)) rflags |= KAD_RF_HASH_TIE;
+  if (!avoid) keep = true;
+  desired_plan(ws, ws.w, ws.mx2, true, true, K, total, keep, ws.plan, ws.over, ws.ofl);
+  if (!avoid) return rflags;
+  // currentPlan, capped by capacity (planner.go:134-146)
+  int64_t cur_total = 0, des_total = 0;
+  for (int i = lane; i < K; i += WAVE) {
+    int64_t r = ws.cur[i];
+    if ((ws.fl[i] & EF_HAS_CAP) && ws.cap[i] < r) r = ws.cap[i];
+    cur_total = wadd(cur_total, r);
+    des_total = wadd(des_total, ws.plan[i]);
+    ws.adj[i] = r;  // adj := currentPlan
+  }
+  cur_total = wave_sum_i64(cur_total);
+  des_total = wave_sum_i64(des_total);
+  wave_sync();
+  if (cur_total != des_total) {
+    const bool up = cur_total < des_total;
+    const int64_t count = up ? des_total - cur_total : cur_total - des_total;
+    // preferences of the clusters to scale (planner.go:306-366)
+    int m = 0;
+    for (int base = 0; base < K; base += WAVE) {
+      int i = base + lane;
+      bool sel = false;
+      if (i < K) {
+        int64_t d = ws.plan[i], c = ws.adj[i];
+        sel = up ? d > c : d < c;
+        if (sel) {
+          ws.w2[i] = up ? d - c : c - d;
+          ws.mx2[i] = up ? ((ws.fl[i] & EF_HAS_MAX) ? ws.mx[i] - c : I64_MAX) : c;
+        }
+      }
+      uint64_t bm = ballot(sel);
+      if (sel) ws.act[m + mbcnt(bm)] = i;
+      m += popc64(bm);
+    }
+    wave_sync();
+    if (m > 0 && sort_by_weight_hash(ws, ws.w2, ws.act, m)) rflags |= KAD_RF_HASH_TIE;
+    // scale plan: no capacity, no minimums, keepUnschedulable = false (its overflow is discarded)
+    for (int i = lane; i < K; i += WAVE) ws.ofl2[i] = 0;
+    wave_sync();
+    if (m > 0) desired_plan(ws, ws.w2, ws.mx2, false, false, m, count, false, ws.plan2, ws.over2, ws.ofl2);
+    for (int i = lane; i < K; i += WAVE) {
+      int64_t a = ws.adj[i];
+      if (ws.ofl2[i] & EF_HAS_PLAN) a = up ? wadd(a, ws.plan2[i]) : wsub(a, ws.plan2[i]);
+      ws.plan[i] = a;
+    }
+  } else {
+    for (int i = lane; i < K; i += WAVE) ws.plan[i] = ws.adj[i];
+  }
+  wave_sync();
+  return rflags;
+}
+
+}  // namespace kad

@@ -1,0 +1,351 @@
+// MaxCluster selection on one wavefront (plugins/maxcluster/max_cluster.go:42-66).
+//
+// The reference sorts the feasible clusters by total score with Go 1.19
+// sort.Slice (pdqsort, unstable) and keeps the first k. Only the SET of the
+// first k matters downstream (Duplicate results are a map; rsp/planner order
+// by weight+FNV). The wave therefore:
+//   1. finds the k-th largest score T by an 8-bit-digit radix select over an
+//      LDS histogram (one pass when scores span < 256 values);
+//   2. counts g = #(> T), e = #(== T); if the cut takes every tied element
+//      (k - g == e), the selection is {score >= T} and no sort is needed;
+//   3. otherwise ("straddle") replays Go's pdqsort restricted to the
+//      sub-ranges that contain position k (tests/test_pdq_select.py proves the
+//      restriction exact) on the compacted index list in LDS.
+#pragma once
+#include "kad_wave.h"
+
+namespace kad {
+
+// ------------------------------------------------ restricted pdqsort replay
+// Operates on v[0..n) (indices into key[]); less(i, j) = key[v[i]] > key[v[j]].
+struct Pdq {
+  uint16_t* v;
+  const int64_t* key;
+  int xs_b, xs_c;
+  __device__ __forceinline__ bool less(int i, int j) const { return key[v[i]] > key[v[j]]; }
+  __device__ __forceinline__ void swap(int i, int j) const {
+    uint16_t t = v[i];
+    v[i] = v[j];
+    v[j] = t;
+  }
+  __device__ void insertion_sort(int a, int b) const {
+    for (int i = a + 1; i < b; i++)
+      for (int j = i; j > a && less(j, j - 1); j--) swap(j, j - 1);
+  }
+  __device__ void sift_down(int lo, int hi, int first) const {
+    int root = lo;
+    for (;;) {
+      int child = 2 * root + 1;
+      if (child >= hi) return;
+      if (child + 1 < hi && less(first + child, first + child + 1)) child++;
+      if (!less(first + root, first + child)) return;
+      swap(first + root, first + child);
+      root = child;
+    }
+  }
+  __device__ void heap_sort(int a, int b) const {
+    int first = a, lo = 0, hi = b - a;
+    for (int i = (hi - 1) / 2; i >= 0; i--) sift_down(i, hi, first);
+    for (int i = hi - 1; i >= 0; i--) {
+      swap(first, first + i);
+      sift_down(lo, i, first);
+    }
+  }
+  __device__ bool partial_insertion_sort(int a, int b) const {
+    int i = a + 1;
+    for (int j = 0; j < 5; j++) {
+      while (i < b && !less(i, i - 1)) i++;
+      if (i == b) return true;
+      if (b - a < 50) return false;
+      swap(i, i - 1);
+      if (i - a >= 2) {
+        for (int k = i - 1; k >= 1; k--) {  // sic: Go's lower bound is 1
+          if (!less(k, k - 1)) break;
+          swap(k, k - 1);
+        }
+      }
+      if (b - i >= 2) {
+        for (int k = i + 1; k < b; k++) {
+          if (!less(k, k - 1)) break;
+          swap(k, k - 1);
+        }
+      }
+    }
+    return false;
+  }
+  __device__ void break_patterns(int a, int b) const {
+    int length = b - a;
+    if (length >= 8) {
+      uint64_t r = (uint64_t)length;
+      uint64_t modulus = 1ull << (64 - __clzll((unsigned long long)length));
+      int idx = a + (length / 4) * 2 - 1;
+      for (int i = 0; i < 3; i++) {
+        r ^= r << 13;
+        r ^= r >> xs_b;
+        r ^= r << xs_c;
+        int other = (int)(r & (modulus - 1));
+        if (other >= length) other -= length;
+        swap(idx - 1 + i, a + other);
+      }
+    }
+  }
+  __device__ __forceinline__ void order2(int& a, int& b, int& swaps) const {
+    if (less(b, a)) {
+      int t = a;
+      a = b;
+      b = t;
+      swaps++;
+    }
+  }
+  __device__ __forceinline__ int median(int a, int b, int c, int& swaps) const {
+    order2(a, b, swaps);
+    order2(b, c, swaps);
+    order2(a, b, swaps);
+    return b;
+  }
+  __device__ int choose_pivot(int a, int b, int& hint) const {
+    int l = b - a, swaps = 0;
+    int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    if (l >= 8) {
+      if (l >= 50) {
+        i = median(i - 1, i, i + 1, swaps);
+        j = median(j - 1, j, j + 1, swaps);
+        k = median(k - 1, k, k + 1, swaps);
+      }
+      j = median(i, j, k, swaps);
+    }
+    hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+    return j;
+  }
+  __device__ void reverse_range(int a, int b) const {
+    for (int i = a, j = b - 1; i < j; i++, j--) swap(i, j);
+  }
+  __device__ int partition_equal(int a, int b, int pivot) const {
+    swap(a, pivot);
+    int i = a + 1, j = b - 1;
+    for (;;) {
+      while (i <= j && !less(a, i)) i++;
+      while (i <= j && less(a, j)) j--;
+      if (i > j) break;
+      swap(i, j);
+      i++;
+      j--;
+    }
+    return i;
+  }
+  __device__ int partition(int a, int b, int pivot, bool& already) const {
+    swap(a, pivot);
+    int i = a + 1, j = b - 1;
+    while (i <= j && less(i, a)) i++;
+    while (i <= j && !less(j, a)) j--;
+    if (i > j) {
+      swap(j, a);
+      already = true;
+      return j;
+    }
+    swap(i, j);
+    i++;
+    j--;
+    for (;;) {
+      while (i <= j && less(i, a)) i++;
+      while (i <= j && !less(j, a)) j--;
+      if (i > j) break;
+      swap(i, j);
+      i++;
+      j--;
+    }
+    swap(j, a);
+    already = false;
+    return j;
+  }
+  // pdqsort_func(data, 0, n, bits.Len(n)) restricted to ranges straddling k.
+  __device__ void select(int n, int k) const {
+    int a = 0, b = n;
+    int limit = 32 - __clz(n);
+    bool wasBalanced = true, wasPartitioned = true;
+    while (a < k && k < b) {
+      int length = b - a;
+      if (length <= 12) {
+        insertion_sort(a, b);
+        return;
+      }
+      if (limit == 0) {
+        heap_sort(a, b);
+        return;
+      }
+      if (!wasBalanced) {
+        break_patterns(a, b);
+        limit--;
+      }
+      int hint;
+      int pivot = choose_pivot(a, b, hint);
+      if (hint == 2) {
+        reverse_range(a, b);
+        pivot = (b - 1) - (pivot - a);
+        hint = 1;
+      }
+      if (wasBalanced && wasPartitioned && hint == 1) {
+        if (partial_insertion_sort(a, b)) return;
+      }
+      if (a > 0 && !less(a - 1, pivot)) {
+        a = partition_equal(a, b, pivot);
+        continue;
+      }
+      bool already;
+      int mid = partition(a, b, pivot, already);
+      wasPartitioned = already;
+      int leftLen = mid - a, rightLen = b - mid, thr = length / 8;
+      if (leftLen < rightLen) {
+        if (k < mid) {  // recursion into the smaller left side
+          b = mid;
+          wasBalanced = wasPartitioned = true;
+        } else if (k > mid + 1) {
+          wasBalanced = leftLen >= thr;
+          a = mid + 1;
+        } else {
+          return;
+        }
+      } else {
+        if (k > mid + 1) {  // recursion into the smaller right side
+          a = mid + 1;
+          wasBalanced = wasPartitioned = true;
+        } else if (k < mid) {
+          wasBalanced = rightLen >= thr;
+          b = mid;
+        } else {
+          return;
+        }
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ uint64_t okey(int64_t x) { return (uint64_t)x ^ 0x8000000000000000ull; }
+
+// Per-wave selection workspace (pointers into LDS or global scratch).
+struct SelWs {
+  int64_t* tot;     // [Cp] total score per cluster (valid where feasible)
+  uint64_t* feas;   // [Cp/64] feasibility bits
+  uint64_t* sel;    // [Cp/64] output: selected bits
+  uint16_t* idx;    // [Cp] compaction buffer for the straddle replay
+  uint32_t* hist;   // [256]
+};
+
+// Select the first-k set of the feasible clusters (n of them, C slots) by
+// total score. Returns KAD_RF_TIE_STRADDLE if the pdqsort replay ran.
+__device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_t row_min, int64_t row_max, int xs_b,
+                                int xs_c) {
+  const int lane = lane_id();
+  const int nch = (C + 63) >> 6;
+  if (k >= n) {
+    for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = ws.feas[ch];
+    wave_sync();
+    return 0;
+  }
+  if (k <= 0) {
+    for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
+    wave_sync();
+    return 0;
+  }
+  // ---- radix select of the k-th largest total
+  const uint64_t umin = okey(row_min);
+  const uint64_t range = okey(row_max) - umin;
+  uint64_t prefix = 0, pmask = 0;
+  int64_t kk = k;
+  if (range != 0) {
+    int bits = 64 - __clzll((unsigned long long)range);
+    for (int shift = ((bits + 7) / 8 - 1) * 8; shift >= 0; shift -= 8) {
+      for (int i = lane; i < 256; i += WAVE) ws.hist[i] = 0;
+      wave_sync();
+      for (int ch = 0; ch < nch; ++ch) {
+        int c = ch * WAVE + lane;
+        bool f = c < C && ((ws.feas[ch] >> lane) & 1);
+        if (f) {
+          uint64_t v = okey(ws.tot[c]) - umin;
+          if ((v & pmask) == prefix) atomicAdd(&ws.hist[(v >> shift) & 255], 1u);
+        }
+      }
+      wave_sync();
+      // lane l owns digits 255-4l .. 252-4l (descending)
+      int h[4];
+      int s4 = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[j] = (int)ws.hist[255 - 4 * lane - j];
+        s4 += h[j];
+      }
+      int64_t incl = wave_incl_sum_i64(s4);
+      int64_t excl = incl - s4;
+      bool mine = excl < kk && kk <= incl;
+      int digit = 0;
+      int64_t above = 0;
+      if (mine) {
+        int64_t cum = excl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (cum + h[j] >= kk) {
+            digit = 255 - 4 * lane - j;
+            above = cum;
+            break;
+          }
+          cum += h[j];
+        }
+      }
+      uint64_t who = ballot(mine);
+      int src = __ffsll((unsigned long long)who) - 1;
+      digit = __shfl(digit, src);
+      above = shfl_i64(above, src);
+      kk -= above;
+      prefix |= (uint64_t)digit << shift;
+      pmask |= 0xFFull << shift;
+      wave_sync();
+    }
+  }
+  const int64_t T = (int64_t)((prefix + umin) ^ 0x8000000000000000ull);
+  // ---- counts above / at the threshold
+  int g = 0, e = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    int c = ch * WAVE + lane;
+    bool f = c < C && ((ws.feas[ch] >> lane) & 1);
+    if (f) {
+      int64_t t = ws.tot[c];
+      g += t > T;
+      e += t == T;
+    }
+  }
+  g = wave_sum_i32(g);
+  e = wave_sum_i32(e);
+  const int64_t need = k - g;
+  if (need == e) {
+    for (int ch = 0; ch < nch; ++ch) {
+      int c = ch * WAVE + lane;
+      bool f = c < C && ((ws.feas[ch] >> lane) & 1) && ws.tot[c] >= T;
+      uint64_t m = ballot(f);
+      if (lane == 0) ws.sel[ch] = m;
+    }
+    wave_sync();
+    return 0;
+  }
+  // ---- straddle: compact the feasible list (input order) and replay pdqsort
+  int base = 0;
+  for (int ch = 0; ch < nch; ++ch) {
+    uint64_t m = ws.feas[ch];
+    if ((m >> lane) & 1) ws.idx[base + mbcnt(m)] = (uint16_t)(ch * WAVE + lane);
+    base += popc64(m);
+  }
+  for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
+  wave_sync();
+  if (lane == 0) {
+    Pdq p{ws.idx, ws.tot, xs_b, xs_c};
+    p.select(n, (int)k);
+  }
+  wave_sync();
+  for (int i = lane; i < k; i += WAVE) {
+    int c = ws.idx[i];
+    atomicOr((unsigned long long*)&ws.sel[c >> 6], 1ull << (c & 63));
+  }
+  wave_sync();
+  return KAD_RF_TIE_STRADDLE;
+}
+
+}  // namespace kad

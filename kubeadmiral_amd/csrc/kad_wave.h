@@ -1,0 +1,123 @@
+// Wavefront (64-lane) primitives for gfx950 and Go integer semantics.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kad {
+
+constexpr int WAVE = 64;
+constexpr int64_t I64_MAX = INT64_MAX;
+constexpr int64_t I64_MIN = INT64_MIN;
+constexpr int64_t NEG_INF = INT64_MIN;  // "no floor" in the clamp monoid
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Order LDS/global traffic between the lanes of one wave (and the CU's L1).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ int popc64(uint64_t x) { return __popcll(x); }
+
+// number of set bits of m in lanes below this lane
+__device__ __forceinline__ int mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
+  int lo = __shfl((int)(uint32_t)v, src);
+  int hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int64_t shfl_up_i64(int64_t v, int d) {
+  int lo = __shfl_up((int)(uint32_t)v, d);
+  int hi = __shfl_up((int)(uint32_t)((uint64_t)v >> 32), d);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int64_t shfl_xor_i64(int64_t v, int m) {
+  int lo = __shfl_xor((int)(uint32_t)v, m);
+  int hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), m);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {  // wrapping (Go int64)
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = (int64_t)((uint64_t)v + (uint64_t)shfl_xor_i64(v, m));
+  return v;
+}
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    int64_t o = shfl_xor_i64(v, m);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    int64_t o = shfl_xor_i64(v, m);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {  // exact for integer-valued sums < 2^53
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+// inclusive scan (sum) of i64 across the wave
+__device__ __forceinline__ int64_t wave_incl_sum_i64(int64_t v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    int64_t o = shfl_up_i64(v, d);
+    if (l >= d) v = (int64_t)((uint64_t)v + (uint64_t)o);
+  }
+  return v;
+}
+
+// ----------------------------------------------------------- Go integer ops
+__device__ __forceinline__ int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+__device__ __forceinline__ int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+__device__ __forceinline__ int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+// Go `a / b` (truncating; MinInt64 / -1 wraps to MinInt64)
+__device__ __forceinline__ int64_t go_div(int64_t a, int64_t b) {
+  if (b == -1) return (int64_t)(0 - (uint64_t)a);
+  return a / b;
+}
+// floor(num / den) for 0 <= num, 0 < den when the quotient is small (< 2^20):
+// f32 reciprocal estimate + exact integer correction — avoids the 64-bit
+// division sequence on the hot score path.
+__device__ __forceinline__ int64_t small_quot(int64_t num, int64_t den) {
+  float q = (float)num * __builtin_amdgcn_rcpf((float)den);
+  int64_t qi = (int64_t)q;
+  int64_t r = num - qi * den;
+  while (r < 0) { qi--; r += den; }
+  while (r >= den) { qi++; r -= den; }
+  return qi;
+}
+// Go float64 → int64 on amd64: NaN / out of range → MinInt64
+__device__ __forceinline__ int64_t go_f2i(double x) {
+  if (!(x < 9223372036854775808.0) || !(x >= -9223372036854775808.0)) return I64_MIN;
+  return (int64_t)x;
+}
+
+// FNV-1 32 continuation (hash/fnv New32)
+__device__ __forceinline__ uint32_t fnv_cont(uint32_t h, const uint8_t* p, int n) {
+  for (int i = 0; i < n; i++) {
+    h *= 16777619u;
+    h ^= p[i];
+  }
+  return h;
+}
+
+}  // namespace kad

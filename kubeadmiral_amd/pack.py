@@ -431,6 +431,37 @@ class _Compiler:
 T_HAS_EXPR, T_EXPR_VALID, T_HAS_FIELD, T_FIELD_VALID = TERM_HAS_EXPR, TERM_EXPR_VALID, TERM_HAS_FIELD, TERM_FIELD_VALID
 
 
+def _count_reqs(fp, sp) -> int:
+    """Label/field requirements a unit evaluates per cluster (SURVEY.md §8(d) R_w)."""
+    n, pc = 0, 0
+    n_sel = fp[pc]
+    pc += 1
+    for _ in range(n_sel):
+        pc += 2 + (fp[pc] >> 8)
+        n += 1
+    present = fp[pc]
+    pc += 1
+    if present:
+        n_terms = fp[pc]
+        pc += 1
+        for _ in range(n_terms):
+            ne, nf = fp[pc + 1], fp[pc + 2]
+            pc += 3
+            for _ in range(ne + nf):
+                pc += 2 + (fp[pc] >> 8)
+                n += 1
+    pc = 0
+    n_terms = sp[pc]
+    pc += 1
+    for _ in range(n_terms):
+        ne = sp[pc + 1]
+        pc += 2
+        for _ in range(ne):
+            pc += 2 + (sp[pc] >> 8)
+            n += 1
+    return n
+
+
 # ===================================================================== batch
 class Batch:
     """A packed batch of SchedulingUnits (against one Snapshot, for one Framework)."""
@@ -451,6 +482,8 @@ class Batch:
         sreq, fprog, sprog, place, cur_id, cur_rep, keys = [], [], [], [], [], [], []
         pref_id, pref_w, pref_min, pref_max, pref_cap, pref_fl = [], [], [], [], [], []
         out_len = np.zeros(W, np.int64)
+        n_reqs = np.zeros(W, np.int64)
+        n_tols = np.zeros(W, np.int64)
         select_max = fwk.select_plugin == 8
         place_on = fwk.has_filter(PlacementFilter)
 
@@ -488,9 +521,12 @@ class Batch:
                 tid = tol_key[tk] = len(tol_rows)
                 tol_rows.append(su.tolerations or [])
             tolset[w] = tid
-            fprog.append(comp.filter_program(su))
+            fp_ = comp.filter_program(su)
+            fprog.append(fp_)
             sp, serr, wsum = comp.score_program(su)
             sprog.append(sp)
+            n_reqs[w] = _count_reqs(fp_, sp)
+            n_tols[w] = len(su.tolerations or [])
             if serr:
                 f |= W_SCORE_ERROR
             if wsum > (1 << 20):
@@ -589,6 +625,8 @@ class Batch:
         hdr.packed_select_plugin = fwk.select_plugin
         hdr.snapshot_fingerprint = snap.fingerprint
         self.blob = _assemble(hdr, arrays)
+        self.n_reqs = n_reqs
+        self.n_tols = n_tols
         self.W = W
         self.n_out_slots = int(out_off[-1])
         self.out_off = out_off

@@ -1,0 +1,227 @@
+"""ctypes binding of libkad.so and the ScheduleAlgorithm-shaped host API.
+
+``BatchScheduler.schedule(fwk, units, clusters)`` is the batch counterpart of
+``core.ScheduleAlgorithm.Schedule(ctx, fwk, su, clusters)``
+(pkg/controllers/scheduler/core/generic_scheduler.go:37-44): same inputs (a
+framework, scheduling units, the cluster list), same per-unit output
+(``ScheduleResult`` or the error class). There is no CPU fallback: if the HIP
+library or a GPU is missing this raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import types as T
+from .framework import Framework
+from .pack import Batch, Snapshot
+from .results import BatchResult, to_schedule_result
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkad.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "kad_sched.h")
+
+KAD_ERRORS = {-1: "KAD_EINVAL", -2: "KAD_EHIP", -3: "KAD_ENOMEM", -4: "KAD_ESTATE", -5: "KAD_EUNSUPPORTED"}
+
+
+class KadError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{KAD_ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class ResultView(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_void_p), ("count", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+                ("cluster", ctypes.c_void_p), ("replicas", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def declared_functions() -> List[str]:
+    """Names of the functions include/kad_sched.h declares."""
+    with open(HEADER) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(kad_\w+)\s*\(", src, re.M)))
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libkad.so (fails loudly: the product path has no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libkad.so not built at {path}: run `python -m kubeadmiral_amd.build`")
+    L = ctypes.CDLL(path)
+    P, I, U32, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_size_t
+    L.kad_abi_version.restype = I
+    L.kad_ctx_create.argtypes = [I, ctypes.POINTER(P)]
+    L.kad_ctx_destroy.argtypes = [P]
+    L.kad_last_error.argtypes = [P]
+    L.kad_last_error.restype = ctypes.c_char_p
+    L.kad_snapshot_upload.argtypes = [P, P, SZ]
+    L.kad_snapshot_upload_device.argtypes = [P, P, SZ]
+    L.kad_batch_upload.argtypes = [P, P, SZ]
+    L.kad_schedule.argtypes = [P, P]
+    L.kad_sync.argtypes = [P]
+    L.kad_last_timing.argtypes = [P, P]
+    L.kad_results_download.argtypes = [P, P]
+    L.kad_schedule_batch.argtypes = [P, P, P, SZ, P]
+    L.kad_select_rows.argtypes = [P, I, P, P, P, U32, P, P, P]
+    L.kad_plan_rows.argtypes = [P, I, P, P, P, P, P, P, P, P, P, P, P, P]
+    L.kad_debug_scores.argtypes = [P, P, P, P]
+    _lib = L
+    return L
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Context:
+    """A kad_ctx: one HIP device, one stream, resident snapshot + batch."""
+
+    def __init__(self, device: int = 0):
+        self.L = load_library()
+        h = ctypes.c_void_p()
+        rc = self.L.kad_ctx_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise KadError(rc, f"kad_ctx_create(device={device}) failed (no GPU?)")
+        self.h = h
+        self.snap: Optional[Snapshot] = None
+        self.batch: Optional[Batch] = None
+
+    def close(self):
+        if self.h:
+            self.L.kad_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise KadError(rc, self.L.kad_last_error(self.h).decode())
+
+    def upload_snapshot(self, snap: Snapshot):
+        self._chk(self.L.kad_snapshot_upload(self.h, _p(snap.blob), snap.blob.nbytes))
+        self.snap = snap
+
+    def upload_snapshot_device(self, dev_ptr: int, nbytes: int, snap: Optional[Snapshot] = None):
+        self._chk(self.L.kad_snapshot_upload_device(self.h, ctypes.c_void_p(dev_ptr), nbytes))
+        self.snap = snap
+
+    def upload_batch(self, batch: Batch):
+        self._chk(self.L.kad_batch_upload(self.h, _p(batch.blob), batch.blob.nbytes))
+        self.batch = batch
+
+    def schedule(self, fwk: Framework):
+        prof = fwk.to_c()
+        self._chk(self.L.kad_schedule(self.h, ctypes.byref(prof)))
+
+    def sync(self):
+        self._chk(self.L.kad_sync(self.h))
+
+    def timing(self):
+        ms = (ctypes.c_float * 3)()
+        self._chk(self.L.kad_last_timing(self.h, ms))
+        return float(ms[0]), float(ms[1]), float(ms[2])
+
+    def download(self) -> BatchResult:
+        res = BatchResult.empty(self.batch)
+        v = ResultView(res.status.ctypes.data, res.count.ctypes.data, res.flags.ctypes.data, res.cluster.ctypes.data,
+                       res.replicas.ctypes.data)
+        self._chk(self.L.kad_results_download(self.h, ctypes.byref(v)))
+        return res
+
+    def run(self, fwk: Framework, batch: Batch) -> BatchResult:
+        self.upload_batch(batch)
+        self.schedule(fwk)
+        return self.download()
+
+    def debug_scores(self, fwk: Framework):
+        W, C = self.batch.W, self.snap.C
+        feas = np.zeros(max(1, W * C), np.uint8)
+        tot = np.zeros(max(1, W * C), np.int64)
+        prof = fwk.to_c()
+        self._chk(self.L.kad_debug_scores(self.h, ctypes.byref(prof), _p(feas), _p(tot)))
+        return feas[:W * C].reshape(W, C), tot[:W * C].reshape(W, C)
+
+    def select_rows(self, rows: Sequence[Sequence[int]], max_clusters: Sequence[Optional[int]], flags: int = 0):
+        """MaxCluster on explicit score rows → per row (status, sorted selected positions)."""
+        off = np.zeros(len(rows) + 1, np.int32)
+        off[1:] = np.cumsum([len(r) for r in rows])
+        scores = np.array([x for r in rows for x in r] or [0], np.int64)
+        mc = np.array([(np.iinfo(np.int64).max if m is None else m) for m in max_clusters], np.int64)
+        cnt = np.zeros(len(rows), np.int32)
+        st = np.zeros(len(rows), np.int32)
+        sel = np.zeros(max(1, int(off[-1])), np.int32)
+        self._chk(self.L.kad_select_rows(self.h, len(rows), _p(off), _p(scores), _p(mc), flags, _p(cnt), _p(sel),
+                                         _p(st)))
+        return [(int(st[r]), sel[off[r]:off[r] + cnt[r]].tolist()) for r in range(len(rows))]
+
+    def plan_rows(self, rows):
+        """planner.Plan on explicit rows.
+
+        rows: list of dicts with ``elems`` (list of dicts hash, weight, min, max(None), cap(None), current),
+        ``total``, ``avoid``, ``keep``. Returns per row (plan list, overflow list with None for absent).
+        """
+        n = len(rows)
+        off = np.zeros(n + 1, np.int32)
+        off[1:] = np.cumsum([len(r["elems"]) for r in rows])
+        tot = max(1, int(off[-1]))
+        hsh = np.zeros(tot, np.uint32)
+        wt, mn, mx, cp, cur = (np.zeros(tot, np.int64) for _ in range(5))
+        ef = np.zeros(tot, np.uint32)
+        i = 0
+        for r in rows:
+            for e in r["elems"]:
+                hsh[i], wt[i], mn[i], cur[i] = e["hash"], e["weight"], e["min"], e["current"]
+                if e.get("max") is not None:
+                    mx[i] = e["max"]
+                    ef[i] |= 2
+                if e.get("cap") is not None:
+                    cp[i] = e["cap"]
+                    ef[i] |= 4
+                i += 1
+        total = np.array([r["total"] for r in rows] or [0], np.int64)
+        rf = np.array([(1 if r["avoid"] else 0) | (2 if r["keep"] else 0) for r in rows] or [0], np.uint32)
+        plan = np.zeros(tot, np.int64)
+        over = np.zeros(tot, np.int64)
+        self._chk(self.L.kad_plan_rows(self.h, n, _p(off), _p(hsh), _p(wt), _p(mn), _p(mx), _p(cp), _p(cur), _p(ef),
+                                       _p(total), _p(rf), _p(plan), _p(over)))
+        out = []
+        for r in range(n):
+            a, b = off[r], off[r + 1]
+            out.append((plan[a:b].tolist(), [None if o < 0 else int(o) for o in over[a:b].tolist()]))
+        return out
+
+
+class BatchScheduler:
+    """Batch ScheduleAlgorithm on the GPU (generic_scheduler.go:37-44 semantics per unit)."""
+
+    def __init__(self, ctx: Optional[Context] = None, device: int = 0):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self._snap_key = None
+
+    def set_clusters(self, clusters: List[T.FederatedCluster]) -> Snapshot:
+        snap = Snapshot(clusters)
+        self.ctx.upload_snapshot(snap)
+        return snap
+
+    def schedule(self, fwk: Framework, units: List[T.SchedulingUnit], clusters: List[T.FederatedCluster]
+                 ) -> List[Union[T.ScheduleResult, T.ScheduleError]]:
+        snap = self.ctx.snap
+        if snap is None or snap.clusters is not clusters:
+            snap = self.set_clusters(clusters)
+        batch = Batch(snap, fwk, units)
+        res = self.ctx.run(fwk, batch)
+        return [to_schedule_result(res, w, su, snap.names) for w, su in enumerate(units)]

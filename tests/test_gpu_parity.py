@@ -1,0 +1,214 @@
+"""HIP path (libkad.so on an MI355X) == the oracle, bit for bit.
+
+* golden vectors of the reference's own tests, through the C ABI: filters,
+  scores (debug output), MaxCluster (stage entry point), planner (stage entry
+  point, with planner_test.go's convergence driver), rsp plugin (full pipeline)
+* fuzz batches covering every branch vs the C oracle and the Python oracle
+* config-scale batches (C1, C2 at full size, C4/C5 subsets) vs the C oracle
+* large-C rows that spill the per-wave state to global scratch
+* determinism (two runs, identical bytes)
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import case_id, load
+from gpu_util import assert_same, c_oracle
+from kubeadmiral_amd import framework as F
+from kubeadmiral_amd import k8s, pack, synth
+from kubeadmiral_amd import types as T
+from kubeadmiral_amd.results import to_schedule_result
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from kubeadmiral_amd import build, runtime
+    build.build()
+    c = runtime.Context(0)
+    yield c
+    c.close()
+
+
+def run(ctx, clusters, units, fwk):
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, units)
+    ctx.upload_snapshot(snap)
+    return snap, batch, ctx.run(fwk, batch)
+
+
+# ------------------------------------------------------------------ golden
+FILTERS = load("filters.json")
+SCORES = load("scores.json")
+MAXC = load("maxcluster.json")
+PLANNER = load("planner.json")
+RSP = load("rsp_plugin.json")
+
+
+@pytest.mark.parametrize("c", FILTERS, ids=[case_id(c) for c in FILTERS])
+def test_golden_filter_on_gpu(ctx, c):
+    su = T.SchedulingUnit.from_json(c["su"])
+    su.scheduling_mode = T.SCHEDULING_MODE_DUPLICATE
+    su.sticky_cluster = False
+    su.max_clusters = None
+    cl = T.FederatedCluster.from_json(c["cluster"])
+    fwk = F.Framework(F.EnabledPlugins([c["plugin"]], [], [], []))
+    _, _, res = run(ctx, [cl], [su], fwk)
+    st, pairs = res.row(0)
+    feasible = st == pack.ST_OK and len(pairs) == 1
+    if c["want"] == "Success":
+        assert feasible
+    else:
+        assert st == pack.ST_NO_FEASIBLE
+
+
+@pytest.mark.parametrize("c", SCORES, ids=[case_id(c) for c in SCORES])
+def test_golden_score_on_gpu(ctx, c):
+    su = T.SchedulingUnit.from_json(c["su"])
+    su.scheduling_mode = T.SCHEDULING_MODE_DUPLICATE
+    clusters = [T.FederatedCluster.from_json(x) for x in c["clusters"]]
+    fwk = F.Framework(F.EnabledPlugins([], [c["plugin"]], [], []))
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, [su])
+    ctx.upload_snapshot(snap)
+    ctx.upload_batch(batch)
+    feas, tot = ctx.debug_scores(fwk)
+    assert feas[0].all()
+    assert tot[0].tolist() == c["want"]
+
+
+@pytest.mark.parametrize("c", MAXC, ids=[case_id(c) for c in MAXC])
+def test_golden_maxcluster_on_gpu(ctx, c):
+    su = T.SchedulingUnit.from_json(c["su"])
+    names = [n for n, _ in c["scores"]]
+    [(st, sel)] = ctx.select_rows([[s for _, s in c["scores"]]], [su.max_clusters])
+    if c["want"] != "Success":
+        assert st == pack.ST_ERR_SELECT
+        return
+    assert st == pack.ST_OK
+    assert sorted(names[i] for i in sel) == sorted(c["want_clusters"])
+
+
+def _gpu_plan(ctx, rsp, replicas, clusters, existing, est, avoid, keep):
+    prefs = []
+    for cl in clusters:
+        p = rsp.get(cl, rsp.get("*"))
+        if p is not None:
+            prefs.append((cl, p))
+    row = {"elems": [{"hash": k8s.fnv1_32(n.encode()), "weight": p.weight, "min": p.min_replicas,
+                      "max": p.max_replicas, "cap": est.get(n), "current": (existing or {}).get(n, 0)}
+                     for n, p in prefs], "total": replicas, "avoid": avoid, "keep": keep}
+    [(plan, over)] = ctx.plan_rows([row])
+    return ({n: v for (n, _), v in zip(prefs, plan)},
+            {n: v for (n, _), v in zip(prefs, over) if v is not None})
+
+
+@pytest.mark.parametrize("c", PLANNER, ids=[f"{case_id(c)}-a{int(c['avoidDisruption'])}k{int(c['keepUnschedulableReplicas'])}"
+                                            for c in PLANNER])
+def test_golden_planner_on_gpu(ctx, c):
+    from test_oracle_golden import run_planner_case
+    converged, plan, over = run_planner_case(
+        c, lambda rsp, r, cl, ex, est, key, av, kp: _gpu_plan(ctx, rsp, r, cl, ex, est, av, kp))
+    assert converged
+    if plan or c["want_plan"]:
+        assert plan == c["want_plan"]
+    if over or c["want_overflow"]:
+        assert over == c["want_overflow"]
+
+
+@pytest.mark.parametrize("c", RSP, ids=[case_id(c) for c in RSP])
+def test_golden_rsp_on_gpu(ctx, c):
+    su = T.SchedulingUnit.from_json(c["su"])
+    clusters = [T.FederatedCluster.from_json(x) for x in c["clusters"]]
+    fwk = F.Framework(F.EnabledPlugins([], [], [], [F.ClusterCapacityWeight]))
+    snap, _, res = run(ctx, clusters, [su], fwk)
+    st, pairs = res.row(0)
+    assert st == pack.ST_OK
+    assert [[snap.names[cid], r] for cid, r in pairs] == c["want"]
+
+
+# -------------------------------------------------------------------- fuzz
+@pytest.mark.parametrize("seed", range(48))
+def test_fuzz_gpu_equals_c_oracle(ctx, seed):
+    clusters, units = synth.gen_fuzz(seed, W=80)
+    fwk = synth.fuzz_framework(seed)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), f"fuzz seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_gpu_equals_python_oracle(ctx, seed):
+    from test_c_oracle import py_results, same
+    clusters, units = synth.gen_fuzz(1000 + seed, W=60)
+    fwk = synth.fuzz_framework(seed)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    want = py_results(fwk, units, clusters)
+    for w, su in enumerate(units):
+        got = to_schedule_result(res, w, su, snap.names)
+        assert same(got, want[w]), (w, got, want[w])
+
+
+def test_xorshift_variant_profile_flag(ctx):
+    clusters, units = synth.gen_fuzz(77, W=80, C=200)
+    fwk = F.Framework(F.default_enabled_plugins(), flags=F.PROFILE_XORSHIFT_GO121)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), "go1.21 xorshift")
+
+
+# ------------------------------------------------------------ config scale
+def test_c1_full(ctx):
+    clusters, units, fwk = synth.make_config("c1")
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), "c1")
+
+
+def test_c2_full_size(ctx):
+    clusters, units, fwk = synth.make_config("c2")
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert (res.status == pack.ST_OK).mean() > 0.5
+    assert_same(res, c_oracle(snap, batch, fwk), "c2 100k x 256")
+    # determinism: a second run gives identical bytes
+    ctx.schedule(fwk)
+    res2 = ctx.download()
+    assert_same(res2, res, "c2 rerun")
+
+
+def test_c4_subset(ctx):
+    clusters, units, fwk = synth.make_config("c4", W=20_000)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), "c4 20k x 512")
+
+
+def test_c5_subset(ctx):
+    clusters, units, fwk = synth.make_config("c5", W=1500, C=2000)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), "c5 1.5k x 2k")
+
+
+def test_large_c_global_scratch(ctx):
+    """C = 6000 does not fit the per-wave LDS budget: rows run from global scratch slabs."""
+    clusters, units = synth.gen_fuzz(4242, W=200, C=6000)
+    fwk = F.Framework(F.default_enabled_plugins())
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), "C=6000")
+
+
+def test_tie_heavy_selection_rows(ctx):
+    """Adversarial ties: the straddle path (pdqsort replay) against Go's full sort."""
+    from test_pdq_select import full_first_k
+    rng = np.random.default_rng(5)
+    rows, ks, want = [], [], []
+    for it in range(400):
+        n = int(rng.integers(1, 1500))
+        s = rng.integers(0, int(rng.integers(1, 6)), n).tolist()
+        k = int(rng.integers(0, n + 1))
+        rows.append(s)
+        ks.append(k)
+        want.append(full_first_k(s, k))
+    got = ctx.select_rows(rows, ks)
+    for (st, sel), w in zip(got, want):
+        assert st == pack.ST_OK
+        assert set(sel) == w
