@@ -73,7 +73,7 @@ template <class T>
 static int to_dev(kad_ctx* c, const T* h, size_t n, T** d, std::vector<void*>& owned) {
   HIPCHK(c, hipMalloc((void**)d, (n ? n : 1) * sizeof(T)));
   owned.push_back(*d);
-  if (n) HIPCHK(c, hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  if (n && h) HIPCHK(c, hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
   return 0;
 }
 

@@ -672,6 +672,7 @@ static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
                            size_t scr_bytes, hipStream_t st) {
+  (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (b.W == 0) return hipSuccess;
   const size_t wb = row_layout(s.C).bytes;
   if (wb <= (size_t)LDS_BUDGET) {
@@ -694,6 +695,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
 
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,
                        int n_rows, int kmax, void* gscr, size_t scr_bytes, hipStream_t st) {
+  (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   (void)p;
   if (n_rows == 0 || kmax <= 0) return hipSuccess;
   const size_t wb = plan_layout(kmax).bytes;
@@ -714,6 +716,7 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
 hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,
                               uint32_t pflags, int kmax, int32_t* out_count, int32_t* out_sel, int32_t* out_status,
                               void* gscr, size_t scr_bytes, hipStream_t st) {
+  (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (n_rows == 0) return hipSuccess;
   const size_t wb = row_layout(kmax < 1 ? 1 : kmax).bytes;
   if (wb <= (size_t)LDS_BUDGET) {
@@ -730,6 +733,7 @@ hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t*
 }
 
 hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, void* gscr, size_t scr_bytes, hipStream_t st) {
+  (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (r.n_rows == 0 || kmax <= 0) return hipSuccess;
   const size_t wb = plan_layout(kmax).bytes;
   if (wb <= (size_t)LDS_BUDGET) {

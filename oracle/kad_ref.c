@@ -780,10 +780,14 @@ int kad_ref_schedule(const void* snap_blob, const void* batch_blob, const kad_pr
   job_t* jobs = malloc(sizeof(job_t) * n_threads);
   for (int t = 0; t < n_threads; t++) {
     jobs[t] = (job_t){&s, &b, prof, begin + t, end, n_threads, status, count, cluster, flags, replicas, dbg_feas, dbg_total};
-    if (n_threads == 1) worker(&jobs[t]);
-    else pthread_create(&th[t], NULL, worker, &jobs[t]);
   }
-  if (n_threads > 1) for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+  int* started = calloc(n_threads, sizeof(int));
+  for (int t = 0; t < n_threads; t++) {
+    if (n_threads > 1 && pthread_create(&th[t], NULL, worker, &jobs[t]) == 0) started[t] = 1;
+    else worker(&jobs[t]); /* single thread, or thread creation refused: run inline */
+  }
+  for (int t = 0; t < n_threads; t++) if (started[t]) pthread_join(th[t], NULL);
+  free(started);
   free(th);
   free(jobs);
   return 0;
