@@ -189,6 +189,8 @@ enum kad_batch_array {
   KAD_B_KEY_OFF,       /* i32[W+1] su.Key() bytes (types.go:123-128)                      */
   KAD_B_KEY,           /* u8[]                                                            */
   KAD_B_OUT_OFF,       /* i64[W+1] output slot ranges (host-computed upper bounds)        */
+  KAD_B_REQ_OFF,       /* i32[NR+1] batch-wide table of distinct label/field requirements */
+  KAD_B_REQ,           /* i32[]     requirement words (see KAD_OP_*)                       */
   KAD_B_NARRAYS
 };
 
@@ -207,14 +209,15 @@ typedef struct kad_batch_header {
   int32_t max_row_slots; /* max_w OUT_OFF[w+1]-OUT_OFF[w]            */
   uint32_t packed_filter_mask;  /* profile the output bounds were sized for:  */
   int32_t packed_select_plugin; /* kad_schedule rejects any other profile     */
-  int32_t reserved1;
+  int32_t n_reqs;       /* NR: distinct requirements in KAD_B_REQ                         */
   uint64_t total_bytes;
   uint64_t snapshot_fingerprint;
   uint64_t off[KAD_B_NARRAYS];
 } kad_batch_header;
 
 /* ------------------------------------------------ predicate programs
- * A requirement is  [op | n_payload<<8, key, payload...]  (i32 words):
+ * Requirements are interned batch-wide: KAD_B_REQ holds each distinct one
+ * once as  [op | n_payload<<8, key, payload...]  (i32 words):
  *   KAD_OP_IN / NOTIN / EQ : payload = value ids of that key (labels.Requirement
  *                            In / NotIn / SelectorFromSet's Equals)
  *   KAD_OP_EXISTS / DNE    : no payload
@@ -224,13 +227,17 @@ typedef struct kad_batch_header {
  *                            (util/clusterselector/util.go:65-93)
  *   KAD_OP_TRUE / FALSE    : folded on the host (key or value absent from
  *                            every cluster, field keys other than metadata.name)
+ * The device evaluates every distinct requirement once per cluster into a
+ * bitmask row (NR × ⌈C/64⌉ u64); a unit's programs then combine rows with
+ * word-wide AND/OR instead of re-evaluating selectors per (unit, cluster) pair
+ * as the reference does (clusterselector/util.go:35-58 per call).
  * Filter program (cluster_affinity.go:50-94, clusterselector/util.go:97-132):
- *   n_sel, <n_sel requirements: ClusterSelector map>,
- *   req_present, [n_terms, { tflags, n_expr, n_field, <exprs>, <fields> } ...]
+ *   n_sel, <n_sel requirement ids: ClusterSelector map>,
+ *   req_present, [n_terms, { tflags, n_expr, n_field, <expr ids>, <field ids> } ...]
  *   tflags: bit0 has_expr, bit1 expr_valid, bit2 has_field, bit3 field_valid
  *   (invalid parts carry no requirements; reaching one makes the whole
  *    MatchClusterSelectorTerms return false, as the reference's error does).
- * Score program (cluster_affinity.go:96-135): n_terms, { weight, n_expr, <exprs> } ...
+ * Score program (cluster_affinity.go:96-135): n_terms, { weight, n_expr, <expr ids> } ...
  *   (only valid, non-empty terms with weight != 0)                           */
 enum kad_op {
   KAD_OP_IN = 1, KAD_OP_NOTIN = 2, KAD_OP_EXISTS = 3, KAD_OP_DNE = 4,

@@ -36,6 +36,8 @@ struct kad_ctx {
   uint32_t* d_flags = nullptr;
   int64_t* d_replicas = nullptr;
   size_t out_w_cap = 0, out_slot_cap = 0;
+  uint64_t* d_req_mask = nullptr;
+  size_t req_mask_cap = 0;
   // scratch (per-wave slabs for rows that do not fit LDS)
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -105,7 +107,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   if (!c) return KAD_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_status, (void*)c->d_count,
+  for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
                   (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -254,6 +256,8 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
     HIPCHK(c, hipMalloc(&c->d_scratch, need));
     c->scratch_bytes = need;
   }
+  const size_t nch = (size_t)((c->sd.C + 63) / 64);
+  if (int r = grow(c, (void**)&c->d_req_mask, &c->req_mask_cap, (size_t)h.n_reqs * nch * 8)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->batch_hdr = h;
   const char* base = static_cast<const char*>(c->d_batch);
@@ -292,6 +296,10 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   b.key_off = at<int32_t>(base, h.off, KAD_B_KEY_OFF);
   b.key = at<uint8_t>(base, h.off, KAD_B_KEY);
   b.out_off = at<int64_t>(base, h.off, KAD_B_OUT_OFF);
+  b.NR = h.n_reqs;
+  b.req_off = at<int32_t>(base, h.off, KAD_B_REQ_OFF);
+  b.req = at<int32_t>(base, h.off, KAD_B_REQ);
+  b.req_mask = c->d_req_mask;
   c->have_batch = true;
   c->ran = false;
   return KAD_OK;
@@ -335,6 +343,7 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   o.dbg_feas = dbg_feas;
   o.dbg_total = dbg_total;
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
   HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream));
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())

@@ -34,6 +34,9 @@ struct BatchDev {
   const int32_t* key_off;
   const uint8_t* key;
   const int64_t* out_off;
+  int NR;                   // distinct requirements
+  const int32_t *req_off, *req;
+  uint64_t* req_mask;       // device workspace [NR][ceil(C/64)]: requirement × cluster bitmask
 };
 
 struct OutDev {
@@ -68,6 +71,7 @@ struct PlanRowsDev {
 size_t select_wave_bytes(int C);
 size_t plan_wave_bytes(int K);
 
+hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st);
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p,
                            void* global_scratch, size_t scratch_bytes, hipStream_t st);
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,

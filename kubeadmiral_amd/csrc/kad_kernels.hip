@@ -41,10 +41,11 @@ __host__ __device__ inline RowLayout row_layout(int C) {
 size_t select_wave_bytes(int C) { return row_layout(C).bytes; }
 
 // ---------------------------------------------------------- predicate programs
-__device__ __forceinline__ bool eval_req(const SnapDev& s, const int32_t* p, int c, int& used) {
-  const int w0 = p[0];
-  const int op = w0 & 0xff, n = w0 >> 8, key = p[1];
-  used = 2 + n;
+// labels.Requirement.Matches / fields one-term selectors (apimachinery v0.26.6)
+// for one interned requirement on cluster c. `p` is wave-uniform (scalar loads).
+__device__ __forceinline__ bool eval_req(const SnapDev& s, const int32_t* p, int c) {
+  const int w0 = ldc(p);
+  const int op = w0 & 0xff, n = w0 >> 8, key = ldc(p + 1);
   switch (op) {
     case KAD_OP_TRUE: return true;
     case KAD_OP_FALSE: return false;
@@ -60,18 +61,18 @@ __device__ __forceinline__ bool eval_req(const SnapDev& s, const int32_t* p, int
     case KAD_OP_EQ:
     case KAD_OP_IN: {
       bool hit = false;
-      for (int i = 0; i < n; i++) hit |= (p[2 + i] == v);
+      for (int i = 0; i < n; i++) hit |= (ldc(p + 2 + i) == v);
       return v >= 0 && hit;
     }
     case KAD_OP_NOTIN: {
       bool hit = false;
-      for (int i = 0; i < n; i++) hit |= (p[2 + i] == v);
+      for (int i = 0; i < n; i++) hit |= (ldc(p + 2 + i) == v);
       return v < 0 || !hit;
     }
     case KAD_OP_GT:
     case KAD_OP_LT: {
       if (v < 0 || !s.lok[at]) return false;
-      const int64_t thr = (int64_t)(((uint64_t)(uint32_t)p[3] << 32) | (uint32_t)p[2]);
+      const int64_t thr = (int64_t)(((uint64_t)(uint32_t)ldc(p + 3) << 32) | (uint32_t)ldc(p + 2));
       const int64_t lv = s.lint[at];
       return op == KAD_OP_GT ? lv > thr : lv < thr;
     }
@@ -79,60 +80,71 @@ __device__ __forceinline__ bool eval_req(const SnapDev& s, const int32_t* p, int
   return false;
 }
 
-// ClusterAffinity.Filter (cluster_affinity.go:50-94) with
-// clusterselector.MatchClusterSelectorTerms (clusterselector/util.go:97-132).
-__device__ bool filter_affinity(const SnapDev& s, const int32_t* p, int c) {
-  int used, pc = 0;
-  const int n_sel = p[pc++];
-  bool ok = true;
-  for (int i = 0; i < n_sel; i++) {
-    ok &= eval_req(s, p + pc, c, used);
-    pc += used;
-  }
-  if (!ok) return false;
-  if (!p[pc++]) return true;  // Required == nil
-  const int n_terms = p[pc++];
-  for (int t = 0; t < n_terms; t++) {
-    const int tf = p[pc], ne = p[pc + 1], nf = p[pc + 2];
-    pc += 3;
-    bool me = true;
-    for (int i = 0; i < ne; i++) {
-      me &= eval_req(s, p + pc, c, used);
-      pc += used;
-    }
-    bool mf = true;
-    for (int i = 0; i < nf; i++) {
-      mf &= eval_req(s, p + pc, c, used);
-      pc += used;
-    }
-    if (!(tf & (KAD_TERM_HAS_EXPR | KAD_TERM_HAS_FIELD))) continue;  // empty term: skipped
-    if (tf & KAD_TERM_HAS_EXPR) {
-      if (!(tf & KAD_TERM_EXPR_VALID)) return false;  // error when reached ⇒ false
-      if (!me) continue;
-    }
-    if (tf & KAD_TERM_HAS_FIELD) {
-      if (!(tf & KAD_TERM_FIELD_VALID)) return false;
-      if (!mf) continue;
-    }
-    return true;
-  }
-  return false;
+// Requirement × cluster bitmask rows: M[r][ch] bit l = requirement r holds on
+// cluster 64*ch + l. Every distinct requirement of the batch is evaluated once
+// per cluster here, instead of once per (unit, cluster) pair.
+__global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b) {
+  const int lane = lane_id();
+  const int nch = (s.C + 63) >> 6;
+  const long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= (long)b.NR * nch) return;
+  const int r = (int)(g / nch), ch = (int)(g % nch);
+  const int c = ch * WAVE + lane;
+  const bool v = c < s.C && eval_req(s, b.req + ldc(b.req_off + r), c);
+  const uint64_t m = ballot(v);
+  if (lane == 0) b.req_mask[g] = m;
 }
 
-// ClusterAffinity.Score raw (cluster_affinity.go:96-135)
-__device__ int64_t score_affinity(const SnapDev& s, const int32_t* p, int c) {
-  int used, pc = 0;
-  const int n_terms = p[pc++];
+__device__ __forceinline__ uint64_t req_row(const BatchDev& b, int nch, int id, int ch) {
+  return ldc(b.req_mask + (size_t)id * nch + ch);
+}
+
+// ClusterAffinity.Filter (cluster_affinity.go:50-94) with
+// clusterselector.MatchClusterSelectorTerms (clusterselector/util.go:97-132),
+// for the 64 clusters of chunk ch at once: all operands are wave-uniform words.
+__device__ uint64_t affinity_filter_mask(const BatchDev& b, const int32_t* p, int nch, int ch, uint64_t m) {
+  int pc = 0;
+  const int n_sel = ldc(p + pc++);
+  for (int i = 0; i < n_sel; i++) m &= req_row(b, nch, ldc(p + pc + i), ch);  // SelectorFromSet
+  pc += n_sel;
+  if (!ldc(p + pc++)) return m;  // Required == nil: Success
+  const int n_terms = ldc(p + pc++);
+  uint64_t matched = 0, undecided = m;
+  for (int t = 0; t < n_terms && undecided; t++) {
+    const int tf = ldc(p + pc), ne = ldc(p + pc + 1), nf = ldc(p + pc + 2);
+    const int32_t* ids = p + pc + 3;
+    pc += 3 + ne + nf;
+    if (!(tf & (KAD_TERM_HAS_EXPR | KAD_TERM_HAS_FIELD))) continue;  // nil/empty term selects nothing
+    uint64_t cand = undecided;
+    if (tf & KAD_TERM_HAS_EXPR) {
+      if (!(tf & KAD_TERM_EXPR_VALID)) break;  // invalid selector reached: false for every undecided cluster
+      for (int i = 0; i < ne; i++) cand &= req_row(b, nch, ldc(ids + i), ch);
+    }
+    if (tf & KAD_TERM_HAS_FIELD) {
+      if (!(tf & KAD_TERM_FIELD_VALID)) {  // reached only where the expressions matched
+        undecided &= ~cand;
+        continue;
+      }
+      for (int i = 0; i < nf; i++) cand &= req_row(b, nch, ldc(ids + ne + i), ch);
+    }
+    matched |= cand;
+    undecided &= ~cand;
+  }
+  return matched;
+}
+
+// ClusterAffinity.Score raw (cluster_affinity.go:96-135) for this lane's cluster.
+__device__ int64_t affinity_score(const BatchDev& b, const int32_t* p, int nch, int ch, int lane) {
+  int pc = 0;
+  const int n_terms = ldc(p + pc++);
   int64_t score = 0;
   for (int t = 0; t < n_terms; t++) {
-    const int32_t wgt = p[pc], ne = p[pc + 1];
-    pc += 2;
-    bool m = true;
-    for (int i = 0; i < ne; i++) {
-      m &= eval_req(s, p + pc, c, used);
-      pc += used;
-    }
-    if (m) score = wadd(score, wgt);
+    const int32_t wgt = ldc(p + pc), ne = ldc(p + pc + 1);
+    const int32_t* ids = p + pc + 2;
+    pc += 2 + ne;
+    uint64_t m = ~0ull;
+    for (int i = 0; i < ne; i++) m &= req_row(b, nch, ldc(ids + i), ch);
+    if ((m >> lane) & 1) score = wadd(score, wgt);
   }
   return score;
 }
@@ -168,7 +180,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
                                                        int wave_bytes, int waves_per_block, int w_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: per-unit loads go scalar
   const int gw = blockIdx.x * waves_per_block + wv;
   char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem + (size_t)wv * wave_bytes;
   const int C = s.C;
@@ -188,7 +200,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
   const int xs_c = (p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
 
   for (int w = gw; w < b.W; w += w_stride) {
-    const uint32_t f = b.flags[w];
+    const uint32_t f = ldc(b.flags + w);
     if (f & KAD_W_STICKY) {  // generic_scheduler.go:101-104
       if (lane == 0) {
         o.status[w] = KAD_ST_STICKY;
@@ -217,15 +229,15 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
         }
       wave_sync();
     }
-    const int gv = b.gvk[w];
-    const int ts = b.tolset[w];
+    const int gv = ldc(b.gvk + w);
+    const int ts = ldc(b.tolset + w);
     const uint64_t* tolA = b.tol_all + (size_t)ts * TW;
     const uint64_t* tolP = b.tol_pns + (size_t)ts * TW;
-    const int32_t* fp = b.fprog + b.fprog_off[w];
-    const int32_t* sp = b.sprog + b.sprog_off[w];
-    const int64_t rq_cpu = b.req_cpu[w], rq_mem = b.req_mem[w];
+    const int32_t* fp = b.fprog + ldc(b.fprog_off + w);
+    const int32_t* sp = b.sprog + ldc(b.sprog_off + w);
+    const int64_t rq_cpu = ldc(b.req_cpu + w), rq_mem = ldc(b.req_mem + w);
     const bool fit_on = (fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO);
-    const int s0 = b.sreq_off[w], s1 = b.sreq_off[w + 1];
+    const int s0 = ldc(b.sreq_off + w), s1 = ldc(b.sreq_off + w + 1);
 
     // ---------------- pass 1: filters + raw scores (findClustersThatFitWorkload)
     int cnt = 0;
@@ -238,19 +250,22 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
       if (ok && (fm & BIT(KAD_PL_TAINT_TOLERATION))) {
         const bool sch = use_cur && ((curb[ch] >> lane) & 1);
         const uint64_t* mt = sch ? s.ne : s.nsne;
-        for (int t = 0; t < TW; ++t) ok &= (mt[(size_t)t * C + c] & ~tolA[t]) == 0;
+        for (int t = 0; t < TW; ++t) ok &= (mt[(size_t)t * C + c] & ~ldc(tolA + t)) == 0;
       }
       if (ok && fit_on) {
         ok = s.alloc_cpu[c] >= wadd(rq_cpu, s.used_cpu[c]) && s.alloc_mem[c] >= wadd(rq_mem, s.used_mem[c]);
-        for (int j = s0; j < s1 && ok; ++j) {
-          const int sid = b.sreq_id[j];
+        for (int j = s0; j < s1; ++j) {
+          const int sid = ldc(b.sreq_id + j);
           const int64_t a = sid >= 0 ? s.alloc_s[(size_t)sid * C + c] : 0;
           const int64_t u = sid >= 0 ? s.used_s[(size_t)sid * C + c] : 0;
-          ok = a >= wadd(b.sreq_val[j], u);
+          ok &= a >= wadd(ldc(b.sreq_val + j), u);
         }
       }
-      if (ok && use_place) ok = (plb[ch] >> lane) & 1;
-      if (ok && (fm & BIT(KAD_PL_CLUSTER_AFFINITY))) ok = filter_affinity(s, fp, c);
+      if (use_place) ok &= (plb[ch] >> lane) & 1;
+      if (fm & BIT(KAD_PL_CLUSTER_AFFINITY)) {
+        const uint64_t am = affinity_filter_mask(b, fp, nch, ch, ballot(ok));
+        ok &= (am >> lane) & 1;
+      }
       const uint64_t m = ballot(ok);
       if (lane == 0) feas[ch] = m;
       if (ok) {
@@ -264,9 +279,9 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
         if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) fixed += balanced(rc, cc, rm, cm);
         int tt = 0;
         if (sm & BIT(KAD_PL_TAINT_TOLERATION))
-          for (int t = 0; t < TW; ++t) tt += popc64(s.pns[(size_t)t * C + c] & ~tolP[t]);
+          for (int t = 0; t < TW; ++t) tt += popc64(s.pns[(size_t)t * C + c] & ~ldc(tolP + t));
         int64_t aff = 0;
-        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) aff = score_affinity(s, sp, c);
+        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) aff = affinity_score(b, sp, nch, ch, lane);
         fx[c] = (uint32_t)fixed | ((uint32_t)tt << 16);
         tot[c] = aff;
         ttmax = tt > ttmax ? tt : ttmax;
@@ -669,6 +684,15 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
 // ================================================================ launchers
 static constexpr int LDS_BUDGET = 64 * 1024;  // per block
 static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
+
+hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st) {
+  (void)hipGetLastError();
+  const long waves = (long)b.NR * ((s.C + 63) >> 6);
+  if (waves == 0) return hipSuccess;
+  const long grid = (waves + 3) / 4;
+  hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b);
+  return hipGetLastError();
+}
 
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
                            size_t scr_bytes, hipStream_t st) {

@@ -12,6 +12,14 @@ constexpr int64_t NEG_INF = INT64_MIN;  // "no floor" in the clamp monoid
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Load through the constant address space: for a wave-uniform address this
+// becomes a scalar (s_load) access served by the scalar cache. Only for data
+// that no kernel writes while it runs (packed snapshot / batch, requirement rows).
+template <class T>
+__device__ __forceinline__ T ldc(const T* p) {
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
+}
+
 // Order LDS/global traffic between the lanes of one wave (and the CU's L1).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

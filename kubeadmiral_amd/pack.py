@@ -36,7 +36,7 @@ S_ALLOC_CPU, S_ALLOC_MEM, S_USED_CPU, S_USED_MEM, S_ALLOC_SCALAR, S_USED_SCALAR,
 (B_FLAGS, B_GVK, B_REQ_CPU, B_REQ_MEM, B_DESIRED, B_MAX_CLUSTERS, B_TOLSET, B_TOL_ALL, B_TOL_PNS, B_SREQ_OFF,
  B_SREQ_ID, B_SREQ_VAL, B_FPROG_OFF, B_FPROG, B_SPROG_OFF, B_SPROG, B_PLACE_OFF, B_PLACE, B_CUR_OFF, B_CUR_ID,
  B_CUR_REP, B_PREF_OFF, B_PREF_ID, B_PREF_W, B_PREF_MIN, B_PREF_MAX, B_PREF_CAP, B_PREF_FLAGS, B_KEY_OFF, B_KEY,
- B_OUT_OFF, B_NARRAYS) = range(32)
+ B_OUT_OFF, B_REQ_OFF, B_REQ, B_NARRAYS) = range(34)
 
 SNAPSHOT_MAGIC = 0x5344414B
 BATCH_MAGIC = 0x4241444B
@@ -76,7 +76,7 @@ class BatchHeader(ctypes.Structure):
                 ("n_clusters", ctypes.c_int32), ("n_taint_words", ctypes.c_int32), ("n_tolsets", ctypes.c_int32),
                 ("n_out_slots", ctypes.c_int64), ("max_row_slots", ctypes.c_int32),
                 ("packed_filter_mask", ctypes.c_uint32), ("packed_select_plugin", ctypes.c_int32),
-                ("reserved1", ctypes.c_int32), ("total_bytes", ctypes.c_uint64),
+                ("n_reqs", ctypes.c_int32), ("total_bytes", ctypes.c_uint64),
                 ("snapshot_fingerprint", ctypes.c_uint64), ("off", ctypes.c_uint64 * B_NARRAYS)]
 
 
@@ -330,6 +330,16 @@ def _i64_words(v: int):
 class _Compiler:
     def __init__(self, snap: Snapshot):
         self.snap = snap
+        self.req_id: Dict[tuple, int] = {}
+        self.reqs: List[list] = []
+
+    def intern(self, words: list) -> int:
+        key = tuple(words)
+        rid = self.req_id.get(key)
+        if rid is None:
+            rid = self.req_id[key] = len(self.reqs)
+            self.reqs.append(list(words))
+        return rid
 
     def label_req(self, r: T.ClusterSelectorRequirement) -> list:
         op = _OPS[r.operator]
@@ -374,7 +384,7 @@ class _Compiler:
         sel = su.cluster_selector or {}
         prog.append(len(sel))
         for k, v in sel.items():
-            prog += self.eq_req(k, v)
+            prog.append(self.intern(self.eq_req(k, v)))
         ca = su.affinity.cluster_affinity if su.affinity is not None else None
         if ca is None or ca.required is None:
             prog.append(0)
@@ -393,14 +403,14 @@ class _Compiler:
                 if all(_valid_requirement(r) for r in exprs):
                     flags |= T_EXPR_VALID
                     for r in exprs:
-                        body_e += self.label_req(r)
+                        body_e.append(self.intern(self.label_req(r)))
                     n_e = len(exprs)
             if fields:
                 flags |= T_HAS_FIELD
                 if self._valid_fields(fields):
                     flags |= T_FIELD_VALID
                     for r in fields:
-                        body_f += self.field_req(r)
+                        body_f.append(self.intern(self.field_req(r)))
                     n_f = len(fields)
             prog += [flags, n_e, n_f] + body_e + body_f
         return prog
@@ -424,7 +434,7 @@ class _Compiler:
             wsum += abs(p.weight)
             body += [int(p.weight), len(exprs)]
             for r in exprs:
-                body += self.label_req(r)
+                body.append(self.intern(self.label_req(r)))
         return [n] + body, err, wsum
 
 
@@ -433,12 +443,7 @@ T_HAS_EXPR, T_EXPR_VALID, T_HAS_FIELD, T_FIELD_VALID = TERM_HAS_EXPR, TERM_EXPR_
 
 def _count_reqs(fp, sp) -> int:
     """Label/field requirements a unit evaluates per cluster (SURVEY.md §8(d) R_w)."""
-    n, pc = 0, 0
-    n_sel = fp[pc]
-    pc += 1
-    for _ in range(n_sel):
-        pc += 2 + (fp[pc] >> 8)
-        n += 1
+    n, pc = fp[0], 1 + fp[0]
     present = fp[pc]
     pc += 1
     if present:
@@ -446,19 +451,13 @@ def _count_reqs(fp, sp) -> int:
         pc += 1
         for _ in range(n_terms):
             ne, nf = fp[pc + 1], fp[pc + 2]
-            pc += 3
-            for _ in range(ne + nf):
-                pc += 2 + (fp[pc] >> 8)
-                n += 1
-    pc = 0
-    n_terms = sp[pc]
-    pc += 1
-    for _ in range(n_terms):
+            pc += 3 + ne + nf
+            n += ne + nf
+    pc = 1
+    for _ in range(sp[0]):
         ne = sp[pc + 1]
-        pc += 2
-        for _ in range(ne):
-            pc += 2 + (sp[pc] >> 8)
-            n += 1
+        pc += 2 + ne
+        n += ne
     return n
 
 
@@ -609,13 +608,14 @@ class Batch:
         _, pref_cap_a = _csr(pref_cap, np.int64)
         _, pref_fl_a = _csr(pref_fl, np.uint32)
         key_off, key_a = _csr(keys, np.uint8)
+        req_off, req_a = _csr(comp.reqs, np.int32)
         out_off = np.zeros(W + 1, np.int64)
         out_off[1:] = np.cumsum(out_len)
 
         arrays = [flags, gvk, req_cpu, req_mem, desired, maxc, tolset, tol_all, tol_pns, sreq_off, sreq_id,
                   sreq_val, fprog_off, fprog_a, sprog_off, sprog_a, place_off, place_a, cur_off, cur_id_a, cur_rep_a,
                   pref_off, pref_id_a, pref_w_a, pref_min_a, pref_max_a, pref_cap_a, pref_fl_a, key_off, key_a,
-                  out_off]
+                  out_off, req_off, req_a]
         hdr = BatchHeader()
         hdr.magic, hdr.abi_version = BATCH_MAGIC, ABI_VERSION
         hdr.n_units, hdr.n_clusters, hdr.n_taint_words, hdr.n_tolsets = W, C, TW, NT
@@ -623,9 +623,11 @@ class Batch:
         hdr.max_row_slots = int(out_len.max()) if W else 0
         hdr.packed_filter_mask = fwk.filter_mask
         hdr.packed_select_plugin = fwk.select_plugin
+        hdr.n_reqs = len(comp.reqs)
         hdr.snapshot_fingerprint = snap.fingerprint
         self.blob = _assemble(hdr, arrays)
         self.n_reqs = n_reqs
+        self.n_distinct_reqs = len(comp.reqs)
         self.n_tols = n_tols
         self.W = W
         self.n_out_slots = int(out_off[-1])

@@ -55,6 +55,7 @@ typedef struct {
   const int32_t* key_off;
   const uint8_t* key;
   const int64_t* out_off;
+  const int32_t *req_off, *req;
 } batch_t;
 
 #define PTR(base, hdr, i) ((const void*)((const uint8_t*)(base) + (hdr)->off[i]))
@@ -91,6 +92,7 @@ static int parse_batch(const void* blob, batch_t* b) {
   b->pref_max = PTR(blob, h, KAD_B_PREF_MAX); b->pref_cap = PTR(blob, h, KAD_B_PREF_CAP);
   b->pref_fl = PTR(blob, h, KAD_B_PREF_FLAGS);
   b->key_off = PTR(blob, h, KAD_B_KEY_OFF); b->key = PTR(blob, h, KAD_B_KEY); b->out_off = PTR(blob, h, KAD_B_OUT_OFF);
+  b->req_off = PTR(blob, h, KAD_B_REQ_OFF); b->req = PTR(blob, h, KAD_B_REQ);
   return 0;
 }
 
@@ -266,9 +268,11 @@ static void pdqsort(gosort_t* d, int a, int b, int limit) {
 static void go_sort(gosort_t* d, int n) { pdqsort(d, 0, n, bits_len((unsigned long long)n)); }
 
 /* --------------------------------------------------- predicate programs */
-static int eval_req(const snap_t* s, const int32_t* p, int c, int* used) {
+/* labels.Requirement.Matches / fields one-term selectors on cluster c for the
+ * interned requirement `id` (apimachinery v0.26.6). */
+static int eval_req(const snap_t* s, const batch_t* b, int id, int c) {
+  const int32_t* p = b->req + b->req_off[id];
   int op = p[0] & 0xff, n = p[0] >> 8, key = p[1];
-  *used = 2 + n;
   switch (op) {
     case KAD_OP_TRUE: return 1;
     case KAD_OP_FALSE: return 0;
@@ -301,48 +305,47 @@ static int eval_req(const snap_t* s, const int32_t* p, int c, int* used) {
 }
 
 /* clusterselector.MatchClusterSelectorTerms + ClusterAffinity.Filter (cluster_affinity.go:50-94) */
-static int filter_affinity(const snap_t* s, const int32_t* p, int c) {
-  int used, pc = 0;
+static int filter_affinity(const snap_t* s, const batch_t* b, const int32_t* p, int c) {
+  int pc = 0;
   int n_sel = p[pc++];
-  int ok = 1;
-  for (int i = 0; i < n_sel; i++) { if (!eval_req(s, p + pc, c, &used)) ok = 0; pc += used; }
-  if (!ok) return 0;
+  for (int i = 0; i < n_sel; i++)
+    if (!eval_req(s, b, p[pc + i], c)) return 0; /* SelectorFromSet: every (k, v) must match */
+  pc += n_sel;
   int present = p[pc++];
   if (!present) return 1;
   int n_terms = p[pc++];
   for (int t = 0; t < n_terms; t++) {
     int tf = p[pc], ne = p[pc + 1], nf = p[pc + 2];
-    pc += 3;
-    const int32_t* pe = p + pc;
-    int m = 1;
-    for (int i = 0; i < ne; i++) { if (!eval_req(s, p + pc, c, &used)) m = 0; pc += used; }
-    const int32_t* pf = p + pc;
-    int mf = 1;
-    for (int i = 0; i < nf; i++) { if (!eval_req(s, p + pc, c, &used)) mf = 0; pc += used; }
-    (void)pe; (void)pf;
+    const int32_t* ids = p + pc + 3;
+    pc += 3 + ne + nf;
     if (!(tf & KAD_TERM_HAS_EXPR) && !(tf & KAD_TERM_HAS_FIELD)) continue;
     if (tf & KAD_TERM_HAS_EXPR) {
       if (!(tf & KAD_TERM_EXPR_VALID)) return 0; /* error ⇒ false */
+      int m = 1;
+      for (int i = 0; i < ne && m; i++) m = eval_req(s, b, ids[i], c);
       if (!m) continue;
     }
     if (tf & KAD_TERM_HAS_FIELD) {
       if (!(tf & KAD_TERM_FIELD_VALID)) return 0;
-      if (!mf) continue;
+      int m = 1;
+      for (int i = 0; i < nf && m; i++) m = eval_req(s, b, ids[ne + i], c);
+      if (!m) continue;
     }
     return 1;
   }
   return 0;
 }
 
-static int64_t score_affinity(const snap_t* s, const int32_t* p, int c) {
-  int pc = 0, used;
+static int64_t score_affinity(const snap_t* s, const batch_t* b, const int32_t* p, int c) {
+  int pc = 0;
   int n_terms = p[pc++];
   int64_t score = 0;
   for (int t = 0; t < n_terms; t++) {
     int32_t w = p[pc], ne = p[pc + 1];
-    pc += 2;
+    const int32_t* ids = p + pc + 2;
+    pc += 2 + ne;
     int m = 1;
-    for (int i = 0; i < ne; i++) { if (!eval_req(s, p + pc, c, &used)) m = 0; pc += used; }
+    for (int i = 0; i < ne && m; i++) m = eval_req(s, b, ids[i], c);
     if (m) score = wadd(score, w);
   }
   return score;
@@ -390,7 +393,7 @@ static int run_filter(const snap_t* s, const batch_t* b, int w, int c, int plugi
       return 0;
     }
     case KAD_PL_CLUSTER_AFFINITY:
-      return filter_affinity(s, b->fprog + b->fprog_off[w], c);
+      return filter_affinity(s, b, b->fprog + b->fprog_off[w], c);
   }
   return 1;
 }
@@ -428,7 +431,7 @@ static int64_t run_score(const snap_t* s, const batch_t* b, int w, int c, int pl
       return go_f2i(one_minus * 100.0);
     }
     case KAD_PL_CLUSTER_AFFINITY:
-      return score_affinity(s, b->sprog + b->sprog_off[w], c);
+      return score_affinity(s, b, b->sprog + b->sprog_off[w], c);
   }
   return 0;
 }
