@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
         plb[i] = 0;
         curb[i] = 0;
       }
-      wave_sync();
+      wsync<GSCR>();
       if (use_place)
         for (int j = b.place_off[w] + lane; j < b.place_off[w + 1]; j += WAVE) {
           const int c = b.place[j];
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
           const int c = b.cur_id[j];
           atomicOr((unsigned long long*)&curb[c >> 6], 1ull << (c & 63));
         }
-      wave_sync();
+      wsync<GSCR>();
     }
     const int gv = ldc(b.gvk + w);
     const int ts = ldc(b.tolset + w);
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
     }
     ttmax = wave_max_i64(ttmax);
     affmax = wave_max_i64(affmax);
-    wave_sync();
+    wsync<GSCR>();
 
     // ---------------- pass 2: DefaultNormalizeScore (framework/util.go:455-483) + sum
     int64_t rmin = I64_MAX, rmax = I64_MIN;
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
     }
     rmin = wave_min_i64(rmin);
     rmax = wave_max_i64(rmax);
-    wave_sync();
+    wsync<GSCR>();
 
     // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
     int64_t k = n;
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
       if (hm && mc < k) k = mc;
     }
     SelWs ws{tot, feas, selb, idxb, hist};
-    const uint32_t rflags = select_topk(ws, C, n, k, rmin, rmax, xs_b, xs_c);
+    const uint32_t rflags = select_topk<GSCR>(ws, C, n, k, rmin, rmax, xs_b, xs_c);
 
     // ---------------- output: ascending cluster ids
     const bool dup = f & KAD_W_DUPLICATE;
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
       const int ci = find_sorted(b.cur_id, c0, c1, c);
       ws.cur[i] = ci >= 0 ? b.cur_rep[ci] : 0;
     }
-    wave_sync();
+    wsync<GSCR>();
     uint32_t rflags = o.flags[w];
     if (f & KAD_W_DYNAMIC_WEIGHTS) {
       // CalcWeightLimit (rsp.go:183-213) + AvailableToPercentage (rsp.go:215-272)
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
         }
         other = wave_sum_i64(other);
         maxw = wave_max_i64(maxw);
-        wave_sync();
+        wsync<GSCR>();
         if (maxw > 0) {  // remainder → first strict maximum (lowest cluster id among ties)
           int first = K, ties = 0;
           for (int i = lane; i < K; i += WAVE) {
@@ -563,11 +563,11 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
           if (lane == 0) ws.w[first] = wadd(ws.w[first], wsub(1000, other));
         }
       }
-      wave_sync();
+      wsync<GSCR>();
     }
     const bool avoid = f & KAD_W_AVOID_DISRUPTION;
     const bool keep = f & KAD_W_KEEP_UNSCHED;
-    rflags |= plan_row(ws, K, total, avoid, keep);
+    rflags |= plan_row<GSCR>(ws, K, total, avoid, keep);
     // result = plan + overflow, zeros dropped (rsp.go:162-179), ascending cluster id
     int base = 0;
     for (int i0 = 0; i0 < K; i0 += WAVE) {
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
       o.count[w] = base;
       o.flags[w] = rflags;
     }
-    wave_sync();
+    wsync<GSCR>();
   }
 }
 
@@ -634,10 +634,10 @@ __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32
     }
     rmin = wave_min_i64(rmin);
     rmax = wave_max_i64(rmax);
-    wave_sync();
+    wsync<GSCR>();
     const int64_t k = mc < n ? mc : n;
     SelWs ws{tot, feas, selb, idxb, hist};
-    select_topk(ws, n, n, k, rmin, rmax, xs_b, xs_c);
+    select_topk<GSCR>(ws, n, n, k, rmin, rmax, xs_b, xs_c);
     int base = 0;
     for (int ch = 0; ch < nch; ++ch) {
       const uint64_t m = selb[ch];
@@ -648,7 +648,7 @@ __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32
       out_status[r] = KAD_ST_OK;
       out_count[r] = base;
     }
-    wave_sync();
+    wsync<GSCR>();
   }
 }
 
@@ -671,13 +671,13 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
       ws.cur[i] = R.current[a + i];
       ws.fl[i] = R.elem_flags[a + i] & (EF_HAS_MAX | EF_HAS_CAP);
     }
-    wave_sync();
-    plan_row(ws, K, R.total[r], R.row_flags[r] & 1, (R.row_flags[r] >> 1) & 1);
+    wsync<GSCR>();
+    plan_row<GSCR>(ws, K, R.total[r], R.row_flags[r] & 1, (R.row_flags[r] >> 1) & 1);
     for (int i = lane; i < K; i += WAVE) {
       R.out_plan[a + i] = ws.plan[i];
       R.out_overflow[a + i] = (ws.ofl[i] & EF_HAS_OVER) ? ws.over[i] : -1;
     }
-    wave_sync();
+    wsync<GSCR>();
   }
 }
 

@@ -71,6 +71,7 @@ struct PlanWs {
 
 // sort elements in list[0..m) (element ids) by (weight desc, hash asc, id asc) into ord;
 // returns true if two elements tie on (weight, hash) (Go order would be map-order dependent).
+template <bool GSCR>
 __device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const int32_t* list, int m) {
   const int lane = lane_id();
   bool tie = false;
@@ -89,9 +90,9 @@ __device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const i
     }
     ws.act2[rank] = e;
   }
-  wave_sync();
+  wsync<GSCR>();
   for (int i = lane; i < m; i += WAVE) ws.ord[i] = ws.act2[i];
-  wave_sync();
+  wsync<GSCR>();
   return ballot(tie) != 0;
 }
 
@@ -99,6 +100,7 @@ __device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const i
 // wt/mxv: weights and max (I64_MAX = none) per element; minimums from ws.mn
 // when use_min; capacities from ws.cap/EF_HAS_CAP when use_cap.
 // Writes plan[e], over[e], ofl[e] (EF_HAS_PLAN/EF_HAS_OVER) for listed e.
+template <bool GSCR>
 __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64_t* mxv, bool use_min, bool use_cap,
                                 int m, int64_t total, bool keep, int64_t* plan, int64_t* over, uint32_t* ofl) {
   const int lane = lane_id();
@@ -144,10 +146,10 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
     tot.t = shfl_i64(inc.t, last);
     R = clamp_apply(tot, R);
   }
-  wave_sync();
+  wsync<GSCR>();
   // ---- weighted rounds
   for (int i = lane; i < m; i += WAVE) ws.act[i] = ws.ord[i];
-  wave_sync();
+  wsync<GSCR>();
   int na = m;
   bool modified = true;
   // The reference loop ends after at most m+1 rounds for non-negative weights
@@ -210,10 +212,10 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       R = clamp_apply(tot, R);
     }
     modified = ballot(mod) != 0;
-    wave_sync();
+    wsync<GSCR>();
     for (int i = lane; i < keepn; i += WAVE) ws.act[i] = ws.act2[i];
     na = keepn;
-    wave_sync();
+    wsync<GSCR>();
   }
   if (!keep) {
     for (int i = lane; i < m; i += WAVE) {
@@ -229,12 +231,13 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       }
     }
   }
-  wave_sync();
+  wsync<GSCR>();
   return R;
 }
 
 // planner.Plan (planner.go:83-177) for K elements 0..K-1, all with preferences.
 // Leaves the final plan in ws.plan, the overflow in ws.over/EF_HAS_OVER.
+template <bool GSCR>
 __device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid, bool keep) {
   const int lane = lane_id();
   uint32_t rflags = 0;
@@ -242,10 +245,10 @@ __device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid,
     ws.act[i] = i;
     ws.mx2[i] = (ws.fl[i] & EF_HAS_MAX) ? ws.mx[i] : I64_MAX;
   }
-  wave_sync();
-  if (sort_by_weight_hash(ws, ws.w, ws.act, K)) rflags |= KAD_RF_HASH_TIE;
+  wsync<GSCR>();
+  if (sort_by_weight_hash<GSCR>(ws, ws.w, ws.act, K)) rflags |= KAD_RF_HASH_TIE;
   if (!avoid) keep = true;
-  desired_plan(ws, ws.w, ws.mx2, true, true, K, total, keep, ws.plan, ws.over, ws.ofl);
+  desired_plan<GSCR>(ws, ws.w, ws.mx2, true, true, K, total, keep, ws.plan, ws.over, ws.ofl);
   if (!avoid) return rflags;
   // currentPlan, capped by capacity (planner.go:134-146)
   int64_t cur_total = 0, des_total = 0;
@@ -258,7 +261,7 @@ __device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid,
   }
   cur_total = wave_sum_i64(cur_total);
   des_total = wave_sum_i64(des_total);
-  wave_sync();
+  wsync<GSCR>();
   if (cur_total != des_total) {
     const bool up = cur_total < des_total;
     const int64_t count = up ? des_total - cur_total : cur_total - des_total;
@@ -279,12 +282,12 @@ __device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid,
       if (sel) ws.act[m + mbcnt(bm)] = i;
       m += popc64(bm);
     }
-    wave_sync();
-    if (m > 0 && sort_by_weight_hash(ws, ws.w2, ws.act, m)) rflags |= KAD_RF_HASH_TIE;
+    wsync<GSCR>();
+    if (m > 0 && sort_by_weight_hash<GSCR>(ws, ws.w2, ws.act, m)) rflags |= KAD_RF_HASH_TIE;
     // scale plan: no capacity, no minimums, keepUnschedulable = false (its overflow is discarded)
     for (int i = lane; i < K; i += WAVE) ws.ofl2[i] = 0;
-    wave_sync();
-    if (m > 0) desired_plan(ws, ws.w2, ws.mx2, false, false, m, count, false, ws.plan2, ws.over2, ws.ofl2);
+    wsync<GSCR>();
+    if (m > 0) desired_plan<GSCR>(ws, ws.w2, ws.mx2, false, false, m, count, false, ws.plan2, ws.over2, ws.ofl2);
     for (int i = lane; i < K; i += WAVE) {
       int64_t a = ws.adj[i];
       if (ws.ofl2[i] & EF_HAS_PLAN) a = up ? wadd(a, ws.plan2[i]) : wsub(a, ws.plan2[i]);
@@ -293,7 +296,7 @@ __device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid,
   } else {
     for (int i = lane; i < K; i += WAVE) ws.plan[i] = ws.adj[i];
   }
-  wave_sync();
+  wsync<GSCR>();
   return rflags;
 }
 

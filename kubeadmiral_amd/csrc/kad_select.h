@@ -233,18 +233,19 @@ struct SelWs {
 
 // Select the first-k set of the feasible clusters (n of them, C slots) by
 // total score. Returns KAD_RF_TIE_STRADDLE if the pdqsort replay ran.
+template <bool GSCR>
 __device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_t row_min, int64_t row_max, int xs_b,
                                 int xs_c) {
   const int lane = lane_id();
   const int nch = (C + 63) >> 6;
   if (k >= n) {
     for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = ws.feas[ch];
-    wave_sync();
+    wsync<GSCR>();
     return 0;
   }
   if (k <= 0) {
     for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
-    wave_sync();
+    wsync<GSCR>();
     return 0;
   }
   // ---- radix select of the k-th largest total
@@ -256,7 +257,7 @@ __device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_
     int bits = 64 - __clzll((unsigned long long)range);
     for (int shift = ((bits + 7) / 8 - 1) * 8; shift >= 0; shift -= 8) {
       for (int i = lane; i < 256; i += WAVE) ws.hist[i] = 0;
-      wave_sync();
+      wsync<GSCR>();
       for (int ch = 0; ch < nch; ++ch) {
         int c = ch * WAVE + lane;
         bool f = c < C && ((ws.feas[ch] >> lane) & 1);
@@ -265,7 +266,7 @@ __device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_
           if ((v & pmask) == prefix) atomicAdd(&ws.hist[(v >> shift) & 255], 1u);
         }
       }
-      wave_sync();
+      wsync<GSCR>();
       // lane l owns digits 255-4l .. 252-4l (descending)
       int h[4];
       int s4 = 0;
@@ -298,7 +299,7 @@ __device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_
       kk -= above;
       prefix |= (uint64_t)digit << shift;
       pmask |= 0xFFull << shift;
-      wave_sync();
+      wsync<GSCR>();
     }
   }
   const int64_t T = (int64_t)((prefix + umin) ^ 0x8000000000000000ull);
@@ -323,7 +324,7 @@ __device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_
       uint64_t m = ballot(f);
       if (lane == 0) ws.sel[ch] = m;
     }
-    wave_sync();
+    wsync<GSCR>();
     return 0;
   }
   // ---- straddle: compact the feasible list (input order) and replay pdqsort
@@ -334,17 +335,17 @@ __device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_
     base += popc64(m);
   }
   for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
-  wave_sync();
+  wsync<GSCR>();
   if (lane == 0) {
     Pdq p{ws.idx, ws.tot, xs_b, xs_c};
     p.select(n, (int)k);
   }
-  wave_sync();
+  wsync<GSCR>();
   for (int i = lane; i < k; i += WAVE) {
     int c = ws.idx[i];
     atomicOr((unsigned long long*)&ws.sel[c >> 6], 1ull << (c & 63));
   }
-  wave_sync();
+  wsync<GSCR>();
   return KAD_RF_TIE_STRADDLE;
 }
 

@@ -20,10 +20,23 @@ __device__ __forceinline__ T ldc(const T* p) {
   return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
 }
 
-// Order LDS/global traffic between the lanes of one wave (and the CU's L1).
+// Order LDS traffic between the lanes of one wave: one wave's LDS operations
+// execute in order, so this only has to stop the compiler from moving them.
 __device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+// Same for per-wave state kept in a global scratch slab (rows too large for LDS).
+__device__ __forceinline__ void wave_sync_global() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();
+}
+template <bool GSCR>
+__device__ __forceinline__ void wsync() {
+  if (GSCR)
+    wave_sync_global();
+  else
+    wave_sync();
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
