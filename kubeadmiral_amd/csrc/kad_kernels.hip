@@ -21,17 +21,18 @@ namespace kad {
 
 // ----------------------------------------------------------- per-wave layout
 struct RowLayout {
-  size_t tot, fx, idx, feas, sel, place, cur, hist, bytes;
+  size_t tot, fx, idx, perm, feas, sel, place, cur, hist, bytes;
 };
 __host__ __device__ inline RowLayout row_layout(int C) {
-  size_t Cp = (size_t)((C + 63) & ~63);
-  size_t nw = Cp / 64;
+  const size_t Cp = (size_t)((C + 63) & ~63);
+  const size_t nw = Cp / 64;
   RowLayout L;
-  L.tot = 0;
-  L.fx = L.tot + 8 * Cp;
-  L.idx = L.fx + 4 * Cp;
-  L.feas = (L.idx + 2 * Cp + 15) & ~(size_t)15;
-  L.sel = L.feas + 8 * nw;
+  L.tot = 0;                                     // i64[Cp] total per feasible position
+  L.fx = L.tot + 8 * Cp;                         // u32[Cp] fixed scores | TT raw << 16
+  L.idx = L.fx + 4 * Cp;                         // u16[Cp] feasible position → cluster id
+  L.perm = L.idx + 2 * Cp;                       // u16[Cp] pdqsort replay permutation
+  L.feas = (L.perm + 2 * Cp + 15) & ~(size_t)15;  // u64[nw] feasibility by cluster
+  L.sel = L.feas + 8 * nw;                       // u64[nw] selection by position
   L.place = L.sel + 8 * nw;
   L.cur = L.place + 8 * nw;
   L.hist = L.cur + 8 * nw;
@@ -133,18 +134,19 @@ __device__ uint64_t affinity_filter_mask(const BatchDev& b, const int32_t* p, in
   return matched;
 }
 
-// ClusterAffinity.Score raw (cluster_affinity.go:96-135) for this lane's cluster.
-__device__ int64_t affinity_score(const BatchDev& b, const int32_t* p, int nch, int ch, int lane) {
+// ClusterAffinity.Score raw (cluster_affinity.go:96-135) for cluster c (per lane).
+__device__ int64_t affinity_score(const BatchDev& b, const int32_t* p, int nch, int c) {
   int pc = 0;
   const int n_terms = ldc(p + pc++);
   int64_t score = 0;
+  const int ch = c >> 6, bit = c & 63;
   for (int t = 0; t < n_terms; t++) {
     const int32_t wgt = ldc(p + pc), ne = ldc(p + pc + 1);
     const int32_t* ids = p + pc + 2;
     pc += 2 + ne;
-    uint64_t m = ~0ull;
-    for (int i = 0; i < ne; i++) m &= req_row(b, nch, ldc(ids + i), ch);
-    if ((m >> lane) & 1) score = wadd(score, wgt);
+    bool m = true;
+    for (int i = 0; i < ne; i++) m = m && ((b.req_mask[(size_t)ldc(ids + i) * nch + ch] >> bit) & 1);
+    if (m) score = wadd(score, wgt);
   }
   return score;
 }
@@ -187,7 +189,8 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
   const RowLayout L = row_layout(C);
   int64_t* tot = (int64_t*)(region + L.tot);
   uint32_t* fx = (uint32_t*)(region + L.fx);
-  uint16_t* idxb = (uint16_t*)(region + L.idx);
+  uint16_t* idx = (uint16_t*)(region + L.idx);
+  uint16_t* perm = (uint16_t*)(region + L.perm);
   uint64_t* feas = (uint64_t*)(region + L.feas);
   uint64_t* selb = (uint64_t*)(region + L.sel);
   uint64_t* plb = (uint64_t*)(region + L.place);
@@ -218,12 +221,12 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
       }
       wsync<GSCR>();
       if (use_place)
-        for (int j = b.place_off[w] + lane; j < b.place_off[w + 1]; j += WAVE) {
+        for (int j = ldc(b.place_off + w) + lane; j < ldc(b.place_off + w + 1); j += WAVE) {
           const int c = b.place[j];
           atomicOr((unsigned long long*)&plb[c >> 6], 1ull << (c & 63));
         }
       if (use_cur)
-        for (int j = b.cur_off[w] + lane; j < b.cur_off[w + 1]; j += WAVE) {
+        for (int j = ldc(b.cur_off + w) + lane; j < ldc(b.cur_off + w + 1); j += WAVE) {
           const int c = b.cur_id[j];
           atomicOr((unsigned long long*)&curb[c >> 6], 1ull << (c & 63));
         }
@@ -239,57 +242,36 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
     const bool fit_on = (fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO);
     const int s0 = ldc(b.sreq_off + w), s1 = ldc(b.sreq_off + w + 1);
 
-    // ---------------- pass 1: filters + raw scores (findClustersThatFitWorkload)
-    int cnt = 0;
-    int64_t ttmax = 0, affmax = 0;
+    // ---------------- A: filters → feasibility bitmask (findClustersThatFitWorkload, :152-169)
+    int n = 0;
     for (int ch = 0; ch < nch; ++ch) {
       const int c = ch * WAVE + lane;
       bool ok = c < C;
-      if (ok && (fm & BIT(KAD_PL_API_RESOURCES)))
-        ok = gv >= 0 && ((s.gvk[(size_t)(gv >> 6) * C + c] >> (gv & 63)) & 1);
-      if (ok && (fm & BIT(KAD_PL_TAINT_TOLERATION))) {
+      if (fm & BIT(KAD_PL_TAINT_TOLERATION)) {
         const bool sch = use_cur && ((curb[ch] >> lane) & 1);
         const uint64_t* mt = sch ? s.ne : s.nsne;
-        for (int t = 0; t < TW; ++t) ok &= (mt[(size_t)t * C + c] & ~ldc(tolA + t)) == 0;
+        for (int t = 0; t < TW; ++t) ok = ok && (mt[(size_t)t * C + c] & ~ldc(tolA + t)) == 0;
       }
-      if (ok && fit_on) {
-        ok = s.alloc_cpu[c] >= wadd(rq_cpu, s.used_cpu[c]) && s.alloc_mem[c] >= wadd(rq_mem, s.used_mem[c]);
+      if (fm & BIT(KAD_PL_API_RESOURCES))
+        ok = ok && gv >= 0 && ((s.gvk[(size_t)(gv >> 6) * C + c] >> (gv & 63)) & 1);
+      if (use_place) ok = ok && ((plb[ch] >> lane) & 1);
+      uint64_t m = ballot(ok);
+      if (m && fit_on) {
+        ok = ok && s.alloc_cpu[c] >= wadd(rq_cpu, s.used_cpu[c]) && s.alloc_mem[c] >= wadd(rq_mem, s.used_mem[c]);
         for (int j = s0; j < s1; ++j) {
           const int sid = ldc(b.sreq_id + j);
-          const int64_t a = sid >= 0 ? s.alloc_s[(size_t)sid * C + c] : 0;
-          const int64_t u = sid >= 0 ? s.used_s[(size_t)sid * C + c] : 0;
-          ok &= a >= wadd(ldc(b.sreq_val + j), u);
+          const int64_t a = (ok && sid >= 0) ? s.alloc_s[(size_t)sid * C + c] : 0;
+          const int64_t u = (ok && sid >= 0) ? s.used_s[(size_t)sid * C + c] : 0;
+          ok = ok && a >= wadd(ldc(b.sreq_val + j), u);
         }
+        m = ballot(ok);
       }
-      if (use_place) ok &= (plb[ch] >> lane) & 1;
-      if (fm & BIT(KAD_PL_CLUSTER_AFFINITY)) {
-        const uint64_t am = affinity_filter_mask(b, fp, nch, ch, ballot(ok));
-        ok &= (am >> lane) & 1;
-      }
-      const uint64_t m = ballot(ok);
+      if (m && (fm & BIT(KAD_PL_CLUSTER_AFFINITY))) m = affinity_filter_mask(b, fp, nch, ch, m);
       if (lane == 0) feas[ch] = m;
-      if (ok) {
-        const int64_t rc = wadd(s.used_cpu[c], rq_cpu), rm = wadd(s.used_mem[c], rq_mem);
-        const int64_t cc = s.alloc_cpu[c], cm = s.alloc_mem[c];
-        int64_t fixed = 0;
-        if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
-          fixed += go_div(wadd(least_requested(rm, cm), least_requested(rc, cc)), 2);
-        if (sm & BIT(KAD_PL_MOST_ALLOCATED))
-          fixed += go_div(wadd(most_requested(rm, cm), most_requested(rc, cc)), 2);
-        if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) fixed += balanced(rc, cc, rm, cm);
-        int tt = 0;
-        if (sm & BIT(KAD_PL_TAINT_TOLERATION))
-          for (int t = 0; t < TW; ++t) tt += popc64(s.pns[(size_t)t * C + c] & ~ldc(tolP + t));
-        int64_t aff = 0;
-        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) aff = affinity_score(b, sp, nch, ch, lane);
-        fx[c] = (uint32_t)fixed | ((uint32_t)tt << 16);
-        tot[c] = aff;
-        ttmax = tt > ttmax ? tt : ttmax;
-        affmax = aff > affmax ? aff : affmax;
-        cnt++;
-      }
+      if ((m >> lane) & 1) idx[n + mbcnt(m)] = (uint16_t)c;  // compact feasible clusters, snapshot order
+      n += popc64(m);
+      if (o.dbg_feas && c < C) o.dbg_feas[(size_t)w * C + c] = (m >> lane) & 1;
     }
-    const int n = wave_sum_i32(cnt);
     if (n == 0) {  // generic_scheduler.go:112-114
       if (lane == 0) {
         o.status[w] = KAD_ST_NO_FEASIBLE;
@@ -306,41 +288,59 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
       }
       continue;
     }
+    wsync<GSCR>();
+
+    // ---------------- B: raw scores on the compacted feasible list (RunScorePlugins, framework.go:139-181)
+    int64_t ttmax = 0, affmax = 0;
+    for (int j = lane; j < n; j += WAVE) {
+      const int c = idx[j];
+      const int64_t rc = wadd(s.used_cpu[c], rq_cpu), rm = wadd(s.used_mem[c], rq_mem);
+      const int64_t cc = s.alloc_cpu[c], cm = s.alloc_mem[c];
+      int64_t fixed = 0;
+      if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
+        fixed += go_div(wadd(least_requested(rm, cm), least_requested(rc, cc)), 2);
+      if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+        fixed += go_div(wadd(most_requested(rm, cm), most_requested(rc, cc)), 2);
+      if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) fixed += balanced(rc, cc, rm, cm);
+      int tt = 0;
+      if (sm & BIT(KAD_PL_TAINT_TOLERATION))
+        for (int t = 0; t < TW; ++t) tt += popc64(s.pns[(size_t)t * C + c] & ~ldc(tolP + t));
+      int64_t aff = 0;
+      if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) aff = affinity_score(b, sp, nch, c);
+      fx[j] = (uint32_t)fixed | ((uint32_t)tt << 16);
+      tot[j] = aff;
+      ttmax = tt > ttmax ? tt : ttmax;
+      affmax = aff > affmax ? aff : affmax;
+    }
     ttmax = wave_max_i64(ttmax);
     affmax = wave_max_i64(affmax);
     wsync<GSCR>();
 
-    // ---------------- pass 2: DefaultNormalizeScore (framework/util.go:455-483) + sum
+    // ---------------- C: DefaultNormalizeScore (framework/util.go:455-483) + sum
     int64_t rmin = I64_MAX, rmax = I64_MIN;
-    for (int ch = 0; ch < nch; ++ch) {
-      const int c = ch * WAVE + lane;
-      if (c < C && ((feas[ch] >> lane) & 1)) {
-        const uint32_t x = fx[c];
-        int64_t t = (int64_t)(x & 0xFFFF);
-        if (sm & BIT(KAD_PL_TAINT_TOLERATION)) {
-          const int64_t tt = (int64_t)(x >> 16);
-          t += ttmax == 0 ? 100 : 100 - (100 * tt) / ttmax;
-        }
-        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {
-          const int64_t a = tot[c];
-          t = wadd(t, affmax == 0 ? a : go_div(wmul(100, a), affmax));
-        }
-        tot[c] = t;
-        rmin = t < rmin ? t : rmin;
-        rmax = t > rmax ? t : rmax;
-        if (o.dbg_total) o.dbg_total[(size_t)w * C + c] = t;
+    const int tmax = (int)ttmax;
+    for (int j = lane; j < n; j += WAVE) {
+      const uint32_t x = fx[j];
+      int64_t t = (int64_t)(x & 0xFFFF);
+      if (sm & BIT(KAD_PL_TAINT_TOLERATION)) t += tmax == 0 ? 100 : 100 - (100 * (int)(x >> 16)) / tmax;
+      if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {
+        const int64_t a = tot[j];
+        t = wadd(t, affmax == 0 ? a : go_div(wmul(100, a), affmax));
       }
-      if (o.dbg_feas && c < C) o.dbg_feas[(size_t)w * C + c] = (feas[ch] >> lane) & 1;
+      tot[j] = t;
+      rmin = t < rmin ? t : rmin;
+      rmax = t > rmax ? t : rmax;
+      if (o.dbg_total) o.dbg_total[(size_t)w * C + idx[j]] = t;
     }
     rmin = wave_min_i64(rmin);
     rmax = wave_max_i64(rmax);
     wsync<GSCR>();
 
-    // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
+    // ---------------- D: select (framework.go:183-209, max_cluster.go:42-66)
     int64_t k = n;
     if (p.select_plugin == KAD_PL_MAX_CLUSTER) {
       const bool hm = f & KAD_W_HAS_MAX_CLUSTERS;
-      const int64_t mc = b.maxc[w];
+      const int64_t mc = ldc(b.maxc + w);
       if (hm && mc < 0) {
         if (lane == 0) {
           o.status[w] = KAD_ST_ERR_SELECT;
@@ -351,21 +351,21 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
       }
       if (hm && mc < k) k = mc;
     }
-    SelWs ws{tot, feas, selb, idxb, hist};
-    const uint32_t rflags = select_topk<GSCR>(ws, C, n, k, rmin, rmax, xs_b, xs_c);
+    SelWs ws{tot, selb, perm, hist};
+    const uint32_t rflags = select_topk<GSCR>(ws, n, k, rmin, rmax, xs_b, xs_c);
 
-    // ---------------- output: ascending cluster ids
+    // ---------------- E: output, ascending cluster id (idx is ascending in j)
     const bool dup = f & KAD_W_DUPLICATE;
     const bool replicas = !dup && p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (f & KAD_W_HAS_DESIRED) &&
-                          b.desired[w] > 0 && k > 0;
-    const int64_t off = b.out_off[w];
+                          ldc(b.desired + w) > 0 && k > 0;
+    const int64_t off = ldc(b.out_off + w);
     if (dup || replicas) {
       int base = 0;
-      for (int ch = 0; ch < nch; ++ch) {
-        const uint64_t m = selb[ch];
+      for (int jc = 0; jc < ((n + 63) >> 6); ++jc) {
+        const uint64_t m = selb[jc];
         if ((m >> lane) & 1) {
           const int64_t at = off + base + mbcnt(m);
-          o.cluster[at] = ch * WAVE + lane;
+          o.cluster[at] = idx[jc * WAVE + lane];
           o.replicas[at] = dup ? -1 : 0;
         }
         base += popc64(m);
@@ -376,6 +376,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, Ou
       o.count[w] = (dup || replicas) ? (int32_t)k : 0;  // Divide without replicas plugin: empty map
       o.flags[w] = rflags;
     }
+    wsync<GSCR>();
   }
 }
 
@@ -602,8 +603,7 @@ __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32
   char* region = GSCR ? gscratch + (size_t)blockIdx.x * wave_bytes : smem;
   const RowLayout L = row_layout(kmax);
   int64_t* tot = (int64_t*)(region + L.tot);
-  uint16_t* idxb = (uint16_t*)(region + L.idx);
-  uint64_t* feas = (uint64_t*)(region + L.feas);
+  uint16_t* perm = (uint16_t*)(region + L.perm);
   uint64_t* selb = (uint64_t*)(region + L.sel);
   uint32_t* hist = (uint32_t*)(region + L.hist);
   const int xs_b = (pflags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
@@ -618,30 +618,23 @@ __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32
       }
       continue;
     }
-    const int nch = (n + 63) >> 6;
     int64_t rmin = I64_MAX, rmax = I64_MIN;
-    for (int ch = 0; ch < nch; ++ch) {
-      const int c = ch * WAVE + lane;
-      const bool v = c < n;
-      if (v) {
-        const int64_t t = scores[a + c];
-        tot[c] = t;
-        rmin = t < rmin ? t : rmin;
-        rmax = t > rmax ? t : rmax;
-      }
-      const uint64_t m = ballot(v);
-      if (lane == 0) feas[ch] = m;
+    for (int j = lane; j < n; j += WAVE) {
+      const int64_t t = scores[a + j];
+      tot[j] = t;
+      rmin = t < rmin ? t : rmin;
+      rmax = t > rmax ? t : rmax;
     }
     rmin = wave_min_i64(rmin);
     rmax = wave_max_i64(rmax);
     wsync<GSCR>();
     const int64_t k = mc < n ? mc : n;
-    SelWs ws{tot, feas, selb, idxb, hist};
-    select_topk<GSCR>(ws, n, n, k, rmin, rmax, xs_b, xs_c);
+    SelWs ws{tot, selb, perm, hist};
+    select_topk<GSCR>(ws, n, k, rmin, rmax, xs_b, xs_c);
     int base = 0;
-    for (int ch = 0; ch < nch; ++ch) {
-      const uint64_t m = selb[ch];
-      if ((m >> lane) & 1) out_sel[a + base + mbcnt(m)] = ch * WAVE + lane;
+    for (int jc = 0; jc < ((n + 63) >> 6); ++jc) {
+      const uint64_t m = selb[jc];
+      if ((m >> lane) & 1) out_sel[a + base + mbcnt(m)] = jc * WAVE + lane;
       base += popc64(m);
     }
     if (lane == 0) {

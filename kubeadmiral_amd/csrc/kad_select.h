@@ -222,80 +222,80 @@ struct Pdq {
 
 __device__ __forceinline__ uint64_t okey(int64_t x) { return (uint64_t)x ^ 0x8000000000000000ull; }
 
-// Per-wave selection workspace (pointers into LDS or global scratch).
+// Per-wave selection workspace (pointers into LDS or global scratch). The
+// feasible clusters have been compacted, in snapshot order, to positions
+// j = 0..n-1 (the order of the reference's feasible list).
 struct SelWs {
-  int64_t* tot;     // [Cp] total score per cluster (valid where feasible)
-  uint64_t* feas;   // [Cp/64] feasibility bits
-  uint64_t* sel;    // [Cp/64] output: selected bits
-  uint16_t* idx;    // [Cp] compaction buffer for the straddle replay
+  int64_t* tot;     // [n] total score of position j
+  uint64_t* sel;    // [ceil(n/64)] output: selected positions
+  uint16_t* perm;   // [n] permutation buffer for the straddle replay
   uint32_t* hist;   // [256]
 };
 
-// Select the first-k set of the feasible clusters (n of them, C slots) by
-// total score. Returns KAD_RF_TIE_STRADDLE if the pdqsort replay ran.
+// Select the first-k set of positions 0..n-1 under Go's sort.Slice by
+// descending total. Returns KAD_RF_TIE_STRADDLE if the pdqsort replay ran.
 template <bool GSCR>
-__device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_t row_min, int64_t row_max, int xs_b,
+__device__ uint32_t select_topk(const SelWs& ws, int n, int64_t k, int64_t row_min, int64_t row_max, int xs_b,
                                 int xs_c) {
   const int lane = lane_id();
-  const int nch = (C + 63) >> 6;
-  if (k >= n) {
-    for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = ws.feas[ch];
+  const int nch = (n + 63) >> 6;
+  if (k >= n || k <= 0) {
+    const bool all = k > 0;
+    for (int ch = lane; ch < nch; ch += WAVE) {
+      const int rem = n - ch * WAVE;
+      ws.sel[ch] = all ? (rem >= WAVE ? ~0ull : ((1ull << rem) - 1)) : 0ull;
+    }
     wsync<GSCR>();
     return 0;
   }
-  if (k <= 0) {
-    for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
-    wsync<GSCR>();
-    return 0;
-  }
-  // ---- radix select of the k-th largest total
+  // ---- radix select of the k-th largest total (8-bit digits over total - min)
   const uint64_t umin = okey(row_min);
   const uint64_t range = okey(row_max) - umin;
   uint64_t prefix = 0, pmask = 0;
   int64_t kk = k;
   if (range != 0) {
-    int bits = 64 - __clzll((unsigned long long)range);
+    const int bits = 64 - __clzll((unsigned long long)range);
     for (int shift = ((bits + 7) / 8 - 1) * 8; shift >= 0; shift -= 8) {
       for (int i = lane; i < 256; i += WAVE) ws.hist[i] = 0;
       wsync<GSCR>();
-      for (int ch = 0; ch < nch; ++ch) {
-        int c = ch * WAVE + lane;
-        bool f = c < C && ((ws.feas[ch] >> lane) & 1);
-        if (f) {
-          uint64_t v = okey(ws.tot[c]) - umin;
-          if ((v & pmask) == prefix) atomicAdd(&ws.hist[(v >> shift) & 255], 1u);
-        }
+      for (int j = lane; j < n; j += WAVE) {
+        const uint64_t v = okey(ws.tot[j]) - umin;
+        if ((v & pmask) == prefix) atomicAdd(&ws.hist[(v >> shift) & 255], 1u);
       }
       wsync<GSCR>();
       // lane l owns digits 255-4l .. 252-4l (descending)
       int h[4];
       int s4 = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        h[j] = (int)ws.hist[255 - 4 * lane - j];
-        s4 += h[j];
+      for (int q = 0; q < 4; ++q) {
+        h[q] = (int)ws.hist[255 - 4 * lane - q];
+        s4 += h[q];
       }
-      int64_t incl = wave_incl_sum_i64(s4);
-      int64_t excl = incl - s4;
-      bool mine = excl < kk && kk <= incl;
-      int digit = 0;
-      int64_t above = 0;
-      if (mine) {
-        int64_t cum = excl;
+      int incl = s4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (cum + h[j] >= kk) {
-            digit = 255 - 4 * lane - j;
+      for (int d = 1; d < WAVE; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+      }
+      const int excl = incl - s4;
+      const bool mine = excl < kk && kk <= incl;
+      int digit = 0, above = 0;
+      if (mine) {
+        int cum = excl;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (cum + h[q] >= kk) {
+            digit = 255 - 4 * lane - q;
             above = cum;
             break;
           }
-          cum += h[j];
+          cum += h[q];
         }
       }
-      uint64_t who = ballot(mine);
-      int src = __ffsll((unsigned long long)who) - 1;
+      const uint64_t who = ballot(mine);
+      const int src = __ffsll((unsigned long long)who) - 1;
       digit = __shfl(digit, src);
-      above = shfl_i64(above, src);
+      above = __shfl(above, src);
       kk -= above;
       prefix |= (uint64_t)digit << shift;
       pmask |= 0xFFull << shift;
@@ -305,45 +305,34 @@ __device__ uint32_t select_topk(const SelWs& ws, int C, int n, int64_t k, int64_
   const int64_t T = (int64_t)((prefix + umin) ^ 0x8000000000000000ull);
   // ---- counts above / at the threshold
   int g = 0, e = 0;
-  for (int ch = 0; ch < nch; ++ch) {
-    int c = ch * WAVE + lane;
-    bool f = c < C && ((ws.feas[ch] >> lane) & 1);
-    if (f) {
-      int64_t t = ws.tot[c];
-      g += t > T;
-      e += t == T;
-    }
+  for (int j = lane; j < n; j += WAVE) {
+    const int64_t t = ws.tot[j];
+    g += t > T;
+    e += t == T;
   }
   g = wave_sum_i32(g);
   e = wave_sum_i32(e);
-  const int64_t need = k - g;
-  if (need == e) {
+  if (k - g == e) {  // the cut takes every tied element: no sort needed
     for (int ch = 0; ch < nch; ++ch) {
-      int c = ch * WAVE + lane;
-      bool f = c < C && ((ws.feas[ch] >> lane) & 1) && ws.tot[c] >= T;
-      uint64_t m = ballot(f);
+      const int j = ch * WAVE + lane;
+      const uint64_t m = ballot(j < n && ws.tot[j] >= T);
       if (lane == 0) ws.sel[ch] = m;
     }
     wsync<GSCR>();
     return 0;
   }
-  // ---- straddle: compact the feasible list (input order) and replay pdqsort
-  int base = 0;
-  for (int ch = 0; ch < nch; ++ch) {
-    uint64_t m = ws.feas[ch];
-    if ((m >> lane) & 1) ws.idx[base + mbcnt(m)] = (uint16_t)(ch * WAVE + lane);
-    base += popc64(m);
-  }
+  // ---- straddle: replay pdqsort on positions (input order) restricted to k
+  for (int j = lane; j < n; j += WAVE) ws.perm[j] = (uint16_t)j;
   for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
   wsync<GSCR>();
   if (lane == 0) {
-    Pdq p{ws.idx, ws.tot, xs_b, xs_c};
+    Pdq p{ws.perm, ws.tot, xs_b, xs_c};
     p.select(n, (int)k);
   }
   wsync<GSCR>();
   for (int i = lane; i < k; i += WAVE) {
-    int c = ws.idx[i];
-    atomicOr((unsigned long long*)&ws.sel[c >> 6], 1ull << (c & 63));
+    const int j = ws.perm[i];
+    atomicOr((unsigned long long*)&ws.sel[j >> 6], 1ull << (j & 63));
   }
   wsync<GSCR>();
   return KAD_RF_TIE_STRADDLE;
