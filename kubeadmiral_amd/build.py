@@ -34,18 +34,19 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in _inputs())
 
 
-def build(force: bool = False, verbose: bool = False, extra=()) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) -> str:
+    """Compile libkad.so (or a variant at `out`, e.g. the -DKAD_PHASE_PROF profiling build)."""
+    if out == LIB and not force and up_to_date():
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-fno-fast-math", "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"]
+           "-fno-fast-math", "-Wall", "-Wno-unused-function", "-o", out + ".tmp"]
     cmd += list(extra)
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

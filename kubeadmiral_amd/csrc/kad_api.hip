@@ -404,6 +404,8 @@ int kad_schedule_batch(kad_ctx* c, const kad_profile* p, const void* blob, size_
   return kad_results_download(c, out);
 }
 
+int kad_debug_phase_counters(uint64_t* out, int reset) { return kad::debug_phase_counters(out, reset); }
+
 int kad_debug_scores(kad_ctx* c, const kad_profile* p, uint8_t* feasible, int64_t* total) {
   if (!c || !feasible || !total) return KAD_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);

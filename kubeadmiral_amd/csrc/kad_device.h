@@ -71,6 +71,9 @@ struct PlanRowsDev {
 size_t select_wave_bytes(int C);
 size_t plan_wave_bytes(int K);
 
+// phase counters of a -DKAD_PHASE_PROF build (returns 0 in product builds)
+int debug_phase_counters(uint64_t* out, int reset);
+
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st);
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p,
                            void* global_scratch, size_t scratch_bytes, hipStream_t st);

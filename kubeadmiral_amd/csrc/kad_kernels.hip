@@ -19,6 +19,25 @@
 
 namespace kad {
 
+// Phase profiling (only in builds with -DKAD_PHASE_PROF; scripts/phase_prof.py):
+// per-phase s_memtime cycles summed over units, plus event counters.
+// Accumulated per wave in registers, flushed once at wave exit into one of
+// 256 stripes (a shared counter per phase would serialise the waves).
+#ifdef KAD_PHASE_PROF
+__device__ unsigned long long g_phase[256 * 16];
+#define KAD_PT(v) const unsigned long long v = __builtin_readcyclecounter()
+#define KAD_PACC uint32_t pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
+#define KAD_PFLUSH                                                                       \
+  if (lane_id() == 0)                                                                    \
+    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 16 + i_], pacc[i_])
+#else
+#define KAD_PT(v)
+#define KAD_PACC
+#define KAD_PADD(i, x)
+#define KAD_PFLUSH
+#endif
+
 // ----------------------------------------------------------- per-wave layout
 struct RowLayout {
   size_t tot, fx, idx, perm, feas, sel, place, cur, hist, bytes;
@@ -96,37 +115,63 @@ __global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b) {
   if (lane == 0) b.req_mask[g] = m;
 }
 
-__device__ __forceinline__ uint64_t req_row(const BatchDev& b, int nch, int id, int ch) {
-  return ldc(b.req_mask + (size_t)id * nch + ch);
+// A unit's program (filter / score words) held in VGPR lanes: word i < 64 is
+// read with v_readlane (no memory latency on the interpretation chain);
+// longer programs fall back to scalar loads for the tail.
+struct ProgRegs {
+  const int32_t* p;
+  int v;  // lane l holds p[l] (l < len)
+  __device__ __forceinline__ int operator[](int i) const {
+    return i < WAVE ? __builtin_amdgcn_readlane(v, i) : ldc(p + i);
+  }
+};
+__device__ __forceinline__ ProgRegs load_prog(const int32_t* p, int len) {
+  const int l = lane_id();
+  return ProgRegs{p, l < len ? ldg(p, (uint32_t)l) : 0};
 }
 
 // ClusterAffinity.Filter (cluster_affinity.go:50-94) with
-// clusterselector.MatchClusterSelectorTerms (clusterselector/util.go:97-132),
-// for the 64 clusters of chunk ch at once: all operands are wave-uniform words.
-__device__ uint64_t affinity_filter_mask(const BatchDev& b, const int32_t* p, int nch, int ch, uint64_t m) {
+// clusterselector.MatchClusterSelectorTerms (clusterselector/util.go:97-132)
+// over requirement bitmask rows, one lane per 64-cluster chunk: lane l
+// returns the affinity word of chunk ch0 + l (every cluster evaluated
+// independently, so the result ANDs with the other filters afterwards).
+__device__ uint64_t affinity_filter_chunks(const uint64_t* rows, const ProgRegs& P, int nch, int ch0) {
+  const int ch = ch0 + lane_id();
+  const uint32_t chc = ch < nch ? (uint32_t)ch : 0u;
+  auto row = [&](int id) { return ldg(rows, (uint32_t)id * (uint32_t)nch + chc); };
+  auto and_rows = [&](uint64_t m, int at, int n) {
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {  // four independent loads in flight
+      const uint64_t r0 = row(P[at + i]), r1 = row(P[at + i + 1]), r2 = row(P[at + i + 2]), r3 = row(P[at + i + 3]);
+      m &= r0 & r1 & r2 & r3;
+    }
+    for (; i < n; ++i) m &= row(P[at + i]);
+    return m;
+  };
   int pc = 0;
-  const int n_sel = ldc(p + pc++);
-  for (int i = 0; i < n_sel; i++) m &= req_row(b, nch, ldc(p + pc + i), ch);  // SelectorFromSet
+  const int n_sel = P[pc++];
+  uint64_t m = and_rows(~0ull, pc, n_sel);  // SelectorFromSet
   pc += n_sel;
-  if (!ldc(p + pc++)) return m;  // Required == nil: Success
-  const int n_terms = ldc(p + pc++);
+  if (!P[pc++]) return m;  // Required == nil: Success
+  const int n_terms = P[pc++];
   uint64_t matched = 0, undecided = m;
-  for (int t = 0; t < n_terms && undecided; t++) {
-    const int tf = ldc(p + pc), ne = ldc(p + pc + 1), nf = ldc(p + pc + 2);
-    const int32_t* ids = p + pc + 3;
+  for (int t = 0; t < n_terms; t++) {
+    if (!ballot(undecided != 0)) break;
+    const int tf = P[pc], ne = P[pc + 1], nf = P[pc + 2];
+    const int at = pc + 3;
     pc += 3 + ne + nf;
     if (!(tf & (KAD_TERM_HAS_EXPR | KAD_TERM_HAS_FIELD))) continue;  // nil/empty term selects nothing
     uint64_t cand = undecided;
     if (tf & KAD_TERM_HAS_EXPR) {
       if (!(tf & KAD_TERM_EXPR_VALID)) break;  // invalid selector reached: false for every undecided cluster
-      for (int i = 0; i < ne; i++) cand &= req_row(b, nch, ldc(ids + i), ch);
+      cand = and_rows(cand, at, ne);
     }
     if (tf & KAD_TERM_HAS_FIELD) {
       if (!(tf & KAD_TERM_FIELD_VALID)) {  // reached only where the expressions matched
         undecided &= ~cand;
         continue;
       }
-      for (int i = 0; i < nf; i++) cand &= req_row(b, nch, ldc(ids + ne + i), ch);
+      cand = and_rows(cand, at + ne, nf);
     }
     matched |= cand;
     undecided &= ~cand;
@@ -135,7 +180,7 @@ __device__ uint64_t affinity_filter_mask(const BatchDev& b, const int32_t* p, in
 }
 
 // ClusterAffinity.Score raw (cluster_affinity.go:96-135) for cluster c (per lane).
-__device__ int64_t affinity_score(const BatchDev& b, const int32_t* p, int nch, int c) {
+__device__ int64_t affinity_score(const uint64_t* rows, const int32_t* p, int nch, int c) {
   int pc = 0;
   const int n_terms = ldc(p + pc++);
   int64_t score = 0;
@@ -145,7 +190,7 @@ __device__ int64_t affinity_score(const BatchDev& b, const int32_t* p, int nch, 
     const int32_t* ids = p + pc + 2;
     pc += 2 + ne;
     bool m = true;
-    for (int i = 0; i < ne; i++) m = m && ((b.req_mask[(size_t)ldc(ids + i) * nch + ch] >> bit) & 1);
+    for (int i = 0; i < ne; i++) m = m && ((ldg(rows, (uint32_t)ldc(ids + i) * (uint32_t)nch + ch) >> bit) & 1);
     if (m) score = wadd(score, wgt);
   }
   return score;
@@ -177,207 +222,308 @@ __device__ __forceinline__ int64_t balanced(int64_t rc, int64_t cc, int64_t rm, 
 constexpr uint32_t BIT(int pl) { return 1u << pl; }
 
 // ========================================================= schedule kernel
+// The kernel takes one by-value argument block and reads it through the
+// kernarg segment pointer, laundered per phase (kargs()): argument loads then
+// sit next to their uses instead of being hoisted to the entry, where ~60
+// live pointers overflow the SGPR file and spill to VGPR lanes.
+struct SchedArgs {
+  SnapDev s;
+  BatchDev b;
+  OutDev o;
+  ProfDev p;
+  char* gscratch;
+  int wave_bytes, waves_per_block, w_stride;
+};
+typedef const __attribute__((address_space(4))) SchedArgs* KArgs;
+__device__ __forceinline__ KArgs kargs() {
+  return (KArgs)opq((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+// q = num / den for Go int64 when 0 <= num < 2^24, den > 0 (f32 path), else go_div
+__device__ __forceinline__ int64_t div_fast(int64_t num, int64_t den) {
+  if (num >= 0 && num < (1 << 24) && den > 0) return small_quot(num, den);
+  return go_div(num, den);
+}
+
+__device__ __forceinline__ void unit_status(KArgs a, int w, int32_t st) {
+  if (lane_id() == 0) {
+    a->o.status[w] = st;
+    a->o.count[w] = 0;
+    a->o.flags[w] = 0;
+  }
+}
+
 template <bool GSCR>
-__global__ __launch_bounds__(256) void schedule_kernel(SnapDev s, BatchDev b, OutDev o, ProfDev p, char* gscratch,
-                                                       int wave_bytes, int waves_per_block, int w_stride) {
+__global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
+  (void)args;  // read through kargs()
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: per-unit loads go scalar
-  const int gw = blockIdx.x * waves_per_block + wv;
-  char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem + (size_t)wv * wave_bytes;
-  const int C = s.C;
+  int gw, w_stride, C, TW, W;
+  char* region;
+  uint32_t fm, sm;
+  int xs_b, xs_c;
+  {
+    KArgs a = kargs();
+    const int wpb = a->waves_per_block, wbytes = a->wave_bytes;
+    gw = blockIdx.x * wpb + wv;
+    w_stride = a->w_stride;
+    region = GSCR ? a->gscratch + (size_t)gw * wbytes : smem + (size_t)wv * wbytes;
+    C = a->s.C;
+    TW = a->s.TW;
+    W = a->b.W;
+    fm = a->p.filter_mask;
+    sm = a->p.score_mask;
+    xs_b = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
+    xs_c = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+  }
   const RowLayout L = row_layout(C);
   int64_t* tot = (int64_t*)(region + L.tot);
   uint32_t* fx = (uint32_t*)(region + L.fx);
   uint16_t* idx = (uint16_t*)(region + L.idx);
   uint16_t* perm = (uint16_t*)(region + L.perm);
-  uint64_t* feas = (uint64_t*)(region + L.feas);
   uint64_t* selb = (uint64_t*)(region + L.sel);
   uint64_t* plb = (uint64_t*)(region + L.place);
   uint64_t* curb = (uint64_t*)(region + L.cur);
   uint32_t* hist = (uint32_t*)(region + L.hist);
   const int nch = (C + 63) >> 6;
-  const int TW = s.TW;
-  const uint32_t fm = p.filter_mask, sm = p.score_mask;
-  const int xs_b = (p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
-  const int xs_c = (p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+  const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
+  const bool f_aff = fm & BIT(KAD_PL_CLUSTER_AFFINITY), f_place = fm & BIT(KAD_PL_PLACEMENT_FILTER);
 
-  for (int w = gw; w < b.W; w += w_stride) {
-    const uint32_t f = ldc(b.flags + w);
+  KAD_PACC;
+  for (int w = gw; w < W; w += w_stride) {
+    KAD_PT(t0);
+    KArgs a = kargs();
+    const uint32_t f = ldc(a->b.flags + w);
     if (f & KAD_W_STICKY) {  // generic_scheduler.go:101-104
-      if (lane == 0) {
-        o.status[w] = KAD_ST_STICKY;
-        o.count[w] = 0;
-        o.flags[w] = 0;
-      }
+      unit_status(a, w, KAD_ST_STICKY);
       continue;
     }
-    const bool use_place = (fm & BIT(KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
-    const bool use_cur = (fm & BIT(KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
+    const bool use_place = f_place && (f & KAD_W_HAS_PLACEMENT);
+    const bool use_cur = f_taint && (f & KAD_W_HAS_CURRENT);
     if (use_place || use_cur) {
       for (int i = lane; i < nch; i += WAVE) {
         plb[i] = 0;
         curb[i] = 0;
       }
       wsync<GSCR>();
-      if (use_place)
-        for (int j = ldc(b.place_off + w) + lane; j < ldc(b.place_off + w + 1); j += WAVE) {
-          const int c = b.place[j];
+      if (use_place) {
+        const int32_t* pl = a->b.place;
+        for (int j = ldc(a->b.place_off + w) + lane; j < ldc(a->b.place_off + w + 1); j += WAVE) {
+          const int c = ldg(pl, (uint32_t)j);
           atomicOr((unsigned long long*)&plb[c >> 6], 1ull << (c & 63));
         }
-      if (use_cur)
-        for (int j = ldc(b.cur_off + w) + lane; j < ldc(b.cur_off + w + 1); j += WAVE) {
-          const int c = b.cur_id[j];
+      }
+      if (use_cur) {
+        const int32_t* cu = a->b.cur_id;
+        for (int j = ldc(a->b.cur_off + w) + lane; j < ldc(a->b.cur_off + w + 1); j += WAVE) {
+          const int c = ldg(cu, (uint32_t)j);
           atomicOr((unsigned long long*)&curb[c >> 6], 1ull << (c & 63));
         }
+      }
       wsync<GSCR>();
     }
-    const int gv = ldc(b.gvk + w);
-    const int ts = ldc(b.tolset + w);
-    const uint64_t* tolA = b.tol_all + (size_t)ts * TW;
-    const uint64_t* tolP = b.tol_pns + (size_t)ts * TW;
-    const int32_t* fp = b.fprog + ldc(b.fprog_off + w);
-    const int32_t* sp = b.sprog + ldc(b.sprog_off + w);
-    const int64_t rq_cpu = ldc(b.req_cpu + w), rq_mem = ldc(b.req_mem + w);
+    const int gv = ldc(a->b.gvk + w);
+    const int ts = ldc(a->b.tolset + w);
+    const int64_t rq_cpu = ldc(a->b.req_cpu + w), rq_mem = ldc(a->b.req_mem + w);
     const bool fit_on = (fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO);
-    const int s0 = ldc(b.sreq_off + w), s1 = ldc(b.sreq_off + w + 1);
-
-    // ---------------- A: filters → feasibility bitmask (findClustersThatFitWorkload, :152-169)
-    int n = 0;
-    for (int ch = 0; ch < nch; ++ch) {
-      const int c = ch * WAVE + lane;
-      bool ok = c < C;
-      if (fm & BIT(KAD_PL_TAINT_TOLERATION)) {
-        const bool sch = use_cur && ((curb[ch] >> lane) & 1);
-        const uint64_t* mt = sch ? s.ne : s.nsne;
-        for (int t = 0; t < TW; ++t) ok = ok && (mt[(size_t)t * C + c] & ~ldc(tolA + t)) == 0;
-      }
-      if (fm & BIT(KAD_PL_API_RESOURCES))
-        ok = ok && gv >= 0 && ((s.gvk[(size_t)(gv >> 6) * C + c] >> (gv & 63)) & 1);
-      if (use_place) ok = ok && ((plb[ch] >> lane) & 1);
-      uint64_t m = ballot(ok);
-      if (m && fit_on) {
-        ok = ok && s.alloc_cpu[c] >= wadd(rq_cpu, s.used_cpu[c]) && s.alloc_mem[c] >= wadd(rq_mem, s.used_mem[c]);
-        for (int j = s0; j < s1; ++j) {
-          const int sid = ldc(b.sreq_id + j);
-          const int64_t a = (ok && sid >= 0) ? s.alloc_s[(size_t)sid * C + c] : 0;
-          const int64_t u = (ok && sid >= 0) ? s.used_s[(size_t)sid * C + c] : 0;
-          ok = ok && a >= wadd(ldc(b.sreq_val + j), u);
-        }
-        m = ballot(ok);
-      }
-      if (m && (fm & BIT(KAD_PL_CLUSTER_AFFINITY))) m = affinity_filter_mask(b, fp, nch, ch, m);
-      if (lane == 0) feas[ch] = m;
-      if ((m >> lane) & 1) idx[n + mbcnt(m)] = (uint16_t)c;  // compact feasible clusters, snapshot order
-      n += popc64(m);
-      if (o.dbg_feas && c < C) o.dbg_feas[(size_t)w * C + c] = (m >> lane) & 1;
+    const int s0 = ldc(a->b.sreq_off + w), s1 = ldc(a->b.sreq_off + w + 1);
+    ProgRegs FP{nullptr, 0};
+    if (f_aff) {
+      const int fo = ldc(a->b.fprog_off + w), fl = ldc(a->b.fprog_off + w + 1) - fo;
+      FP = load_prog(a->b.fprog + fo, fl);
     }
-    if (n == 0) {  // generic_scheduler.go:112-114
-      if (lane == 0) {
-        o.status[w] = KAD_ST_NO_FEASIBLE;
-        o.count[w] = 0;
-        o.flags[w] = 0;
+
+    // ---------------- A: filters → compacted feasible list (findClustersThatFitWorkload, :152-169)
+    // Per chunk of 64 clusters every attribute load is unconditional, so one
+    // memory round trip serves all filters; ClusterAffinity comes from the
+    // lane-per-chunk bitmask evaluation.
+    int n = 0;
+    uint64_t affv = ~0ull;
+    for (int ch = 0; ch < nch; ++ch) {
+      KArgs ac = kargs();
+      if (f_aff && (ch & 63) == 0) affv = affinity_filter_chunks(ac->b.req_mask, FP, nch, ch);
+      const int c = ch * WAVE + lane;
+      const uint32_t cl = c < C ? (uint32_t)c : 0u;
+      bool ok = c < C;
+      if (f_aff) ok &= (readlane64(affv, ch & 63) >> lane) & 1;
+      if (use_place) ok &= (plb[ch] >> lane) & 1;
+      if (f_taint) {  // taint_toleration.go:50-77: NoSchedule/NoExecute (NoExecute only if not yet scheduled)
+        const uint64_t* tolA = ac->b.tol_all + (size_t)ts * TW;
+        const uint64_t* nsne = ac->s.nsne;
+        const uint64_t* ne = ac->s.ne;
+        const bool sch = use_cur && ((curb[ch] >> lane) & 1);
+        for (int t = 0; t < TW; ++t) {
+          uint64_t x = ldg(nsne, (uint32_t)(t * C) + cl);
+          if (use_cur) {
+            const uint64_t y = ldg(ne, (uint32_t)(t * C) + cl);
+            x = sch ? y : x;
+          }
+          ok &= (x & ~ldc(tolA + t)) == 0;
+        }
       }
+      if (f_api) {  // api_resources.go:42-63
+        if (gv >= 0)
+          ok &= (ldg(ac->s.gvk, (uint32_t)((gv >> 6) * C) + cl) >> (gv & 63)) & 1;
+        else
+          ok = false;
+      }
+      if (fit_on) {  // cluster_resources_fit.go:48-90
+        const int64_t acpu = ldg(ac->s.alloc_cpu, cl), ucpu = ldg(ac->s.used_cpu, cl);
+        const int64_t amem = ldg(ac->s.alloc_mem, cl), umem = ldg(ac->s.used_mem, cl);
+        ok &= (int)(acpu >= wadd(rq_cpu, ucpu)) & (int)(amem >= wadd(rq_mem, umem));
+        for (int j = s0; j < s1; ++j) {
+          KArgs aj = kargs();
+          const int sid = ldc(aj->b.sreq_id + j);
+          const int64_t v = ldc(aj->b.sreq_val + j);
+          int64_t al = 0, us = 0;
+          if (sid >= 0) {
+            al = ldg(aj->s.alloc_s, (uint32_t)(sid * C) + cl);
+            us = ldg(aj->s.used_s, (uint32_t)(sid * C) + cl);
+          }
+          ok &= al >= wadd(v, us);
+        }
+      }
+      const uint64_t m = ballot(ok);
+      if (ok) idx[n + mbcnt(m)] = (uint16_t)c;  // compact feasible clusters, snapshot order
+      n += popc64(m);
+      uint8_t* dbg = ac->o.dbg_feas;
+      if (dbg && c < C) dbg[(size_t)w * C + c] = ok;
+    }
+    KAD_PT(t1);
+    KAD_PADD(0, t1 - t0);
+    if (n == 0) {  // generic_scheduler.go:112-114
+      unit_status(kargs(), w, KAD_ST_NO_FEASIBLE);
       continue;
     }
     if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && (f & KAD_W_SCORE_ERROR)) {  // framework.go:149-159
-      if (lane == 0) {
-        o.status[w] = KAD_ST_ERR_SCORE;
-        o.count[w] = 0;
-        o.flags[w] = 0;
-      }
+      unit_status(kargs(), w, KAD_ST_ERR_SCORE);
       continue;
     }
     wsync<GSCR>();
 
     // ---------------- B: raw scores on the compacted feasible list (RunScorePlugins, framework.go:139-181)
-    int64_t ttmax = 0, affmax = 0;
-    for (int j = lane; j < n; j += WAVE) {
-      const int c = idx[j];
-      const int64_t rc = wadd(s.used_cpu[c], rq_cpu), rm = wadd(s.used_mem[c], rq_mem);
-      const int64_t cc = s.alloc_cpu[c], cm = s.alloc_mem[c];
-      int64_t fixed = 0;
-      if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
-        fixed += go_div(wadd(least_requested(rm, cm), least_requested(rc, cc)), 2);
-      if (sm & BIT(KAD_PL_MOST_ALLOCATED))
-        fixed += go_div(wadd(most_requested(rm, cm), most_requested(rc, cc)), 2);
-      if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) fixed += balanced(rc, cc, rm, cm);
-      int tt = 0;
-      if (sm & BIT(KAD_PL_TAINT_TOLERATION))
-        for (int t = 0; t < TW; ++t) tt += popc64(s.pns[(size_t)t * C + c] & ~ldc(tolP + t));
-      int64_t aff = 0;
-      if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) aff = affinity_score(b, sp, nch, c);
-      fx[j] = (uint32_t)fixed | ((uint32_t)tt << 16);
-      tot[j] = aff;
-      ttmax = tt > ttmax ? tt : ttmax;
-      affmax = aff > affmax ? aff : affmax;
+    int ttmax = 0;
+    int64_t affmax = 0;
+    {
+      KArgs ab = kargs();
+      const uint64_t* tolP = ab->b.tol_pns + (size_t)ts * TW;
+      const int32_t* sp = ab->b.sprog + ldc(ab->b.sprog_off + w);
+      for (int j = lane; j < n; j += WAVE) {
+        const uint32_t c = idx[j];
+        int64_t fixed = 0;
+        if (sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION))) {
+          const int64_t rc = wadd(ldg(ab->s.used_cpu, c), rq_cpu), rm = wadd(ldg(ab->s.used_mem, c), rq_mem);
+          const int64_t cc = ldg(ab->s.alloc_cpu, c), cm = ldg(ab->s.alloc_mem, c);
+          if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
+            fixed += go_div(wadd(least_requested(rm, cm), least_requested(rc, cc)), 2);
+          if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+            fixed += go_div(wadd(most_requested(rm, cm), most_requested(rc, cc)), 2);
+          if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) fixed += balanced(rc, cc, rm, cm);
+        }
+        int tt = 0;
+        if (sm & BIT(KAD_PL_TAINT_TOLERATION))
+          for (int t = 0; t < TW; ++t) tt += popc64(ldg(ab->s.pns, (uint32_t)(t * C) + c) & ~ldc(tolP + t));
+        int64_t aff = 0;
+        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) aff = affinity_score(ab->b.req_mask, sp, nch, c);
+        fx[j] = (uint32_t)fixed | ((uint32_t)tt << 16);
+        tot[j] = aff;
+        ttmax = tt > ttmax ? tt : ttmax;
+        affmax = aff > affmax ? aff : affmax;
+      }
     }
-    ttmax = wave_max_i64(ttmax);
-    affmax = wave_max_i64(affmax);
+    if (sm & BIT(KAD_PL_TAINT_TOLERATION)) ttmax = wave_max_u_i32(ttmax);
+    if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) affmax = wave_max_u_i64(affmax);
     wsync<GSCR>();
+    KAD_PT(t2);
+    KAD_PADD(1, t2 - t1);
 
     // ---------------- C: DefaultNormalizeScore (framework/util.go:455-483) + sum
     int64_t rmin = I64_MAX, rmax = I64_MIN;
-    const int tmax = (int)ttmax;
-    for (int j = lane; j < n; j += WAVE) {
-      const uint32_t x = fx[j];
-      int64_t t = (int64_t)(x & 0xFFFF);
-      if (sm & BIT(KAD_PL_TAINT_TOLERATION)) t += tmax == 0 ? 100 : 100 - (100 * (int)(x >> 16)) / tmax;
-      if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {
-        const int64_t a = tot[j];
-        t = wadd(t, affmax == 0 ? a : go_div(wmul(100, a), affmax));
+    {
+      int64_t* dbt = kargs()->o.dbg_total;
+      for (int j = lane; j < n; j += WAVE) {
+        const uint32_t x = fx[j];
+        int64_t t = (int64_t)(x & 0xFFFF);
+        if (sm & BIT(KAD_PL_TAINT_TOLERATION))
+          t += ttmax == 0 ? 100 : 100 - (int64_t)small_quot(100 * (int)(x >> 16), ttmax);
+        if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {
+          const int64_t av = tot[j];
+          t = wadd(t, affmax == 0 ? av : div_fast(wmul(100, av), affmax));
+        }
+        tot[j] = t;
+        rmin = t < rmin ? t : rmin;
+        rmax = t > rmax ? t : rmax;
+        if (dbt) dbt[(size_t)w * C + idx[j]] = t;
       }
-      tot[j] = t;
-      rmin = t < rmin ? t : rmin;
-      rmax = t > rmax ? t : rmax;
-      if (o.dbg_total) o.dbg_total[(size_t)w * C + idx[j]] = t;
     }
-    rmin = wave_min_i64(rmin);
-    rmax = wave_max_i64(rmax);
+    rmin = wave_min_u_i64(rmin);
+    rmax = wave_max_u_i64(rmax);
     wsync<GSCR>();
+    KAD_PT(t3);
+    KAD_PADD(2, t3 - t2);
 
     // ---------------- D: select (framework.go:183-209, max_cluster.go:42-66)
     int64_t k = n;
-    if (p.select_plugin == KAD_PL_MAX_CLUSTER) {
-      const bool hm = f & KAD_W_HAS_MAX_CLUSTERS;
-      const int64_t mc = ldc(b.maxc + w);
-      if (hm && mc < 0) {
-        if (lane == 0) {
-          o.status[w] = KAD_ST_ERR_SELECT;
-          o.count[w] = 0;
-          o.flags[w] = 0;
+    {
+      KArgs ad = kargs();
+      if (ad->p.select_plugin == KAD_PL_MAX_CLUSTER) {
+        const bool hm = f & KAD_W_HAS_MAX_CLUSTERS;
+        const int64_t mc = ldc(ad->b.maxc + w);
+        if (hm && mc < 0) {
+          unit_status(ad, w, KAD_ST_ERR_SELECT);
+          continue;
         }
-        continue;
+        if (hm && mc < k) k = mc;
       }
-      if (hm && mc < k) k = mc;
     }
     SelWs ws{tot, selb, perm, hist};
     const uint32_t rflags = select_topk<GSCR>(ws, n, k, rmin, rmax, xs_b, xs_c);
+    KAD_PT(t4);
+    KAD_PADD(3, t4 - t3);
+    KAD_PADD(6, 1);
+    KAD_PADD(7, n);
+    if (rflags & KAD_RF_TIE_STRADDLE) {
+      KAD_PADD(5, 1);
+      KAD_PADD(8, t4 - t3);
+    }
 
     // ---------------- E: output, ascending cluster id (idx is ascending in j)
-    const bool dup = f & KAD_W_DUPLICATE;
-    const bool replicas = !dup && p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (f & KAD_W_HAS_DESIRED) &&
-                          ldc(b.desired + w) > 0 && k > 0;
-    const int64_t off = ldc(b.out_off + w);
-    if (dup || replicas) {
-      int base = 0;
-      for (int jc = 0; jc < ((n + 63) >> 6); ++jc) {
-        const uint64_t m = selb[jc];
-        if ((m >> lane) & 1) {
-          const int64_t at = off + base + mbcnt(m);
-          o.cluster[at] = idx[jc * WAVE + lane];
-          o.replicas[at] = dup ? -1 : 0;
+    {
+      KArgs ae = kargs();
+      const bool dup = f & KAD_W_DUPLICATE;
+      const bool replicas = !dup && ae->p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT &&
+                            (f & KAD_W_HAS_DESIRED) && ldc(ae->b.desired + w) > 0 && k > 0;
+      if (dup || replicas) {
+        const int64_t off = ldc(ae->b.out_off + w);
+        int32_t* oc = ae->o.cluster + off;
+        int64_t* orp = ae->o.replicas + off;
+        int base = 0;
+        for (int jc = 0; jc < ((n + 63) >> 6); ++jc) {
+          const uint64_t m = selb[jc];
+          if ((m >> lane) & 1) {
+            const uint32_t at = (uint32_t)(base + mbcnt(m));
+            stg(oc, at, (int32_t)idx[jc * WAVE + lane]);
+            stg(orp, at, (int64_t)(dup ? -1 : 0));
+          }
+          base += popc64(m);
         }
-        base += popc64(m);
+      }
+      if (lane == 0) {
+        ae->o.status[w] = KAD_ST_OK;
+        ae->o.count[w] = (dup || replicas) ? (int32_t)k : 0;  // Divide without replicas plugin: empty map
+        ae->o.flags[w] = rflags;
       }
     }
-    if (lane == 0) {
-      o.status[w] = KAD_ST_OK;
-      o.count[w] = (dup || replicas) ? (int32_t)k : 0;  // Divide without replicas plugin: empty map
-      o.flags[w] = rflags;
-    }
     wsync<GSCR>();
+    KAD_PT(t5);
+    KAD_PADD(4, t5 - t4);
   }
+  KAD_PFLUSH;
 }
 
 // ============================================================ plan kernel
@@ -675,6 +821,26 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
 }
 
 // ================================================================ launchers
+int debug_phase_counters(uint64_t* out, int reset) {
+#ifdef KAD_PHASE_PROF
+  static unsigned long long h[256 * 16];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof h) != hipSuccess) return -1;
+  for (int i = 0; i < 16; ++i) {
+    out[i] = 0;
+    for (int s = 0; s < 256; ++s) out[i] += h[s * 16 + i];
+  }
+  if (reset) {
+    static const unsigned long long z[256 * 16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 16;
+#else
+  (void)out;
+  (void)reset;
+  return 0;
+#endif
+}
+
 static constexpr int LDS_BUDGET = 64 * 1024;  // per block
 static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 
@@ -696,16 +862,16 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     int wpb = (int)(LDS_BUDGET / wb);
     wpb = wpb > 4 ? 4 : (wpb < 1 ? 1 : wpb);
     const int grid = (b.W + wpb - 1) / wpb;
-    hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid), dim3(64 * wpb), wb * wpb, st, s, b, o, p, (char*)nullptr,
-                       (int)wb, wpb, grid * wpb);
+    const SchedArgs A{s, b, o, p, nullptr, (int)wb, wpb, grid * wpb};
+    hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid), dim3(64 * wpb), wb * wpb, st, A);
   } else {
     size_t slots = scr_bytes / wb;
     if (slots < 1) return hipErrorInvalidValue;
     if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
     if (slots > (size_t)b.W) slots = b.W;
     const int grid = (int)slots;
-    hipLaunchKernelGGL(schedule_kernel<true>, dim3(grid), dim3(64), 0, st, s, b, o, p, (char*)gscr, (int)wb, 1,
-                       grid);
+    const SchedArgs A{s, b, o, p, (char*)gscr, (int)wb, 1, grid};
+    hipLaunchKernelGGL(schedule_kernel<true>, dim3(grid), dim3(64), 0, st, A);
   }
   return hipGetLastError();
 }

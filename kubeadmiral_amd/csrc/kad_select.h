@@ -271,12 +271,7 @@ __device__ uint32_t select_topk(const SelWs& ws, int n, int64_t k, int64_t row_m
         h[q] = (int)ws.hist[255 - 4 * lane - q];
         s4 += h[q];
       }
-      int incl = s4;
-#pragma unroll
-      for (int d = 1; d < WAVE; d <<= 1) {
-        const int o = __shfl_up(incl, d);
-        if (lane >= d) incl += o;
-      }
+      const int incl = wave_incl_sum_i32(s4);
       const int excl = incl - s4;
       const bool mine = excl < kk && kk <= incl;
       int digit = 0, above = 0;

@@ -20,6 +20,27 @@ __device__ __forceinline__ T ldc(const T* p) {
   return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
 }
 
+// Launder a wave-uniform value through an empty asm: the compiler can neither
+// hoist loads that depend on it out of the enclosing loop nor keep their
+// results live across the kernel (each use re-loads from the scalar cache
+// instead of spilling SGPRs to VGPR lanes).
+template <class T>
+__device__ __forceinline__ T opq(T v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+// Global load at a 32-bit element index from a wave-uniform base: selects the
+// saddr form (SGPR base + 32-bit VGPR byte offset), one VALU op per address.
+template <class T>
+__device__ __forceinline__ T ldg(const T* base, uint32_t i) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (size_t)(uint32_t)(i * (uint32_t)sizeof(T)));
+}
+template <class T>
+__device__ __forceinline__ void stg(T* base, uint32_t i, T v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (size_t)(uint32_t)(i * (uint32_t)sizeof(T))) = v;
+}
+
 // Order LDS traffic between the lanes of one wave: one wave's LDS operations
 // execute in order, so this only has to stop the compiler from moving them.
 __device__ __forceinline__ void wave_sync() {
@@ -64,30 +85,62 @@ __device__ __forceinline__ int64_t shfl_xor_i64(int64_t v, int m) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// ------------------------------------------------ DPP wave reductions (gfx9)
+// row_shr 1/2/4/8 then row_bcast 15/31 leave the reduction of all 64 lanes in
+// lane 63; readlane makes it wave-uniform (SGPR). Every lane must be active.
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp32(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, 0xf, false);
+}
+#define KAD_DPP_STEPS(OP, ID)              \
+  v = OP(v, dpp32<0x111, 0xf>(ID, v));     \
+  v = OP(v, dpp32<0x112, 0xf>(ID, v));     \
+  v = OP(v, dpp32<0x114, 0xf>(ID, v));     \
+  v = OP(v, dpp32<0x118, 0xf>(ID, v));     \
+  v = OP(v, dpp32<0x142, 0xa>(ID, v));     \
+  v = OP(v, dpp32<0x143, 0xc>(ID, v));     \
+  return __builtin_amdgcn_readlane(v, 63)
+__device__ __forceinline__ int imax_(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int imin_(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int iadd_(int a, int b) { return a + b; }
+__device__ __forceinline__ int wave_max_u_i32(int v) { KAD_DPP_STEPS(imax_, INT32_MIN); }
+__device__ __forceinline__ int wave_min_u_i32(int v) { KAD_DPP_STEPS(imin_, INT32_MAX); }
+__device__ __forceinline__ int wave_sum_u_i32(int v) { KAD_DPP_STEPS(iadd_, 0); }
+#undef KAD_DPP_STEPS
+
+// 64-bit max / min: reduce the high words, then the low words of the lanes
+// holding the winning high word (unsigned), all wave-uniform results.
+__device__ __forceinline__ int64_t wave_max_u_i64(int64_t v) {
+  const int hi = (int)(v >> 32);
+  const int mh = wave_max_u_i32(hi);
+  const uint32_t lo = hi == mh ? (uint32_t)v : 0u;
+  const uint32_t ml = (uint32_t)wave_max_u_i32((int)(lo ^ 0x80000000u)) ^ 0x80000000u;
+  return (int64_t)(((uint64_t)(uint32_t)mh << 32) | ml);
+}
+__device__ __forceinline__ int64_t wave_min_u_i64(int64_t v) {
+  const int hi = (int)(v >> 32);
+  const int mh = wave_min_u_i32(hi);
+  const uint32_t lo = hi == mh ? (uint32_t)v : 0xFFFFFFFFu;
+  const uint32_t ml = (uint32_t)wave_min_u_i32((int)(lo ^ 0x80000000u)) ^ 0x80000000u;
+  return (int64_t)(((uint64_t)(uint32_t)mh << 32) | ml);
+}
+
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {  // wrapping (Go int64)
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = (int64_t)((uint64_t)v + (uint64_t)shfl_xor_i64(v, m));
   return v;
 }
-__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    int64_t o = shfl_xor_i64(v, m);
-    v = o > v ? o : v;
-  }
-  return v;
-}
-__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    int64_t o = shfl_xor_i64(v, m);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-__device__ __forceinline__ int wave_sum_i32(int v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) { return wave_max_u_i64(v); }
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) { return wave_min_u_i64(v); }
+__device__ __forceinline__ int wave_sum_i32(int v) { return wave_sum_u_i32(v); }
+// inclusive prefix sum of i32 across the wave (DPP Hillis-Steele within rows, then row broadcasts)
+__device__ __forceinline__ int wave_incl_sum_i32(int v) {
+  v += dpp32<0x111, 0xf>(0, v);
+  v += dpp32<0x112, 0xf>(0, v);
+  v += dpp32<0x114, 0xf>(0, v);
+  v += dpp32<0x118, 0xf>(0, v);
+  v += dpp32<0x142, 0xa>(0, v);
+  v += dpp32<0x143, 0xc>(0, v);
   return v;
 }
 __device__ __forceinline__ double wave_sum_f64(double v) {  // exact for integer-valued sums < 2^53

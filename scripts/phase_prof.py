@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of schedule_kernel (profiling build, GPU only).
+
+    python scripts/phase_prof.py [--config c2] [--units N] [--build]
+
+Builds kubeadmiral_amd/libkad_prof.so with -DKAD_PHASE_PROF (s_memtime at the
+phase boundaries of each SchedulingUnit, summed with atomics), runs a few
+launches of the config and prints mean cycles per unit per phase. The
+instrumentation perturbs timing (s_memtime ≈ +11 % wave cycles); the
+counters are shader-clock cycles of wall time per unit, including cycles
+the wave waits while other waves issue: use them for the relative split.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from kubeadmiral_amd import build as kbuild  # noqa: E402
+
+PROF_LIB = os.path.join(kbuild.HERE, "libkad_prof.so")
+NAMES = ["A_filter", "B_score", "C_normalize", "D_select", "E_output", "n_straddle", "n_select", "sum_feasible",
+         "D_select_straddle"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--units", type=int, default=0)
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    if a.build or not os.path.exists(PROF_LIB):
+        kbuild.build(force=True, extra=["-DKAD_PHASE_PROF"], out=PROF_LIB)
+        if a.build:
+            return
+    from kubeadmiral_amd import runtime, synth
+    from kubeadmiral_amd.pack import Batch, Snapshot
+
+    L = runtime.load_library(PROF_LIB)
+    L.kad_debug_phase_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    clusters, units, fwk = synth.make_config(a.config, W=a.units or None)
+    snap = Snapshot(clusters)
+    batch = Batch(snap, fwk, units)
+    ctx = runtime.Context(0)
+    ctx.upload_snapshot(snap)
+    ctx.upload_batch(batch)
+    cnt = np.zeros(16, dtype=np.uint64)
+    ctx.schedule(fwk)
+    ctx.sync()
+    L.kad_debug_phase_counters(cnt.ctypes.data, 1)
+    for _ in range(a.reps):
+        ctx.schedule(fwk)
+        ctx.sync()
+    L.kad_debug_phase_counters(cnt.ctypes.data, 1)
+    W = batch.W * a.reps
+    out = {"config": a.config, "units": batch.W, "reps": a.reps}
+    for i, nm in enumerate(NAMES):
+        v = float(cnt[i])
+        if nm.startswith(("A_", "B_", "C_", "D_", "E_")):
+            out[nm + "_cycles_per_unit"] = round(v / W, 1)
+        else:
+            out[nm + "_per_unit"] = round(v / W, 4)
+    print(json.dumps(out, indent=1))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
