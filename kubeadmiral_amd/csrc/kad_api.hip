@@ -38,6 +38,14 @@ struct kad_ctx {
   size_t out_w_cap = 0, out_slot_cap = 0;
   uint64_t* d_req_mask = nullptr;
   size_t req_mask_cap = 0;
+  void* d_rec = nullptr;  // UnitRec[W] (prep_kernel)
+  size_t rec_cap = 0;
+  void* d_sw = nullptr;   // u64[W][nch] static filter words (prep_kernel)
+  size_t sw_cap = 0;
+  void* d_cw = nullptr;   // u64[W][nch] current-cluster words (prep_kernel)
+  size_t cw_cap = 0;
+  void* d_defer = nullptr;  // i32[W + 1]: defer_n, then the defer list
+  size_t defer_cap = 0;
   // scratch (per-wave slabs for rows that do not fit LDS)
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -108,7 +116,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch})
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_sw, c->d_cw, c->d_defer})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -258,6 +266,10 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   }
   const size_t nch = (size_t)((c->sd.C + 63) / 64);
   if (int r = grow(c, (void**)&c->d_req_mask, &c->req_mask_cap, (size_t)h.n_reqs * nch * 8)) return r;
+  if (int r = grow(c, &c->d_rec, &c->rec_cap, (size_t)W * sizeof(UnitRec))) return r;
+  if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
+  if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
+  if (int r = grow(c, &c->d_defer, &c->defer_cap, ((size_t)W + 1) * 4)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->batch_hdr = h;
   const char* base = static_cast<const char*>(c->d_batch);
@@ -300,6 +312,11 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   b.req_off = at<int32_t>(base, h.off, KAD_B_REQ_OFF);
   b.req = at<int32_t>(base, h.off, KAD_B_REQ);
   b.req_mask = c->d_req_mask;
+  b.rec = static_cast<UnitRec*>(c->d_rec);
+  b.sw = static_cast<uint64_t*>(c->d_sw);
+  b.cw = static_cast<uint64_t*>(c->d_cw);
+  b.defer_n = static_cast<int32_t*>(c->d_defer);
+  b.defer = b.defer_n + 1;
   c->have_batch = true;
   c->ran = false;
   return KAD_OK;
@@ -344,6 +361,8 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   o.dbg_total = dbg_total;
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
+  if (fast_path(c->sd.C))
+    HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream));
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())

@@ -37,7 +37,31 @@ struct BatchDev {
   int NR;                   // distinct requirements
   const int32_t *req_off, *req;
   uint64_t* req_mask;       // device workspace [NR][ceil(C/64)]: requirement × cluster bitmask
+  // device workspace written by prep_kernel at every launch
+  struct UnitRec* rec;      // [W] per-unit records
+  uint64_t* sw;             // [W][ceil(C/64)] static filter words: ClusterAffinity ∧ PlacementFilter
+  uint64_t* cw;             // [W][ceil(C/64)] CurrentClusters words (units that have them)
+  int32_t* defer;           // [W] units the lean kernel hands to schedule_kernel
+  int32_t* defer_n;         // [1] length of defer
 };
+
+// Per-unit record, rebuilt by prep_kernel at every kad_schedule: the fixed-size
+// fields schedule_lean_kernel reads for one SchedulingUnit, in one 64-B line
+// that lanes 0-15 fetch with a single coalesced load one unit ahead of use.
+struct UnitRec {
+  uint32_t flags;       // KAD_W_* | REC_DESIRED_POS
+  int32_t gvk;          // snapshot GVK id (-1: none)
+  int32_t tolset;       // toleration-set id
+  int32_t sprog_off;    // ClusterAffinity score program offset
+  int64_t req_cpu, req_mem;
+  int64_t maxc;         // *MaxClusters
+  int64_t out_off;      // first output slot
+  uint64_t tol0;        // tol_all[tolset][0]
+  uint64_t tolp0;       // tol_pns[tolset][0]
+};
+static_assert(sizeof(UnitRec) == 64, "UnitRec is one 64-B line");
+constexpr uint32_t REC_DESIRED_POS = 1u << 31;  // DesiredReplicas != nil && *DesiredReplicas > 0
+constexpr uint32_t REC_FULL = 1u << 30;         // scheduled by schedule_kernel (features the lean kernel omits)
 
 struct OutDev {
   int32_t* status;
@@ -75,6 +99,10 @@ size_t plan_wave_bytes(int K);
 int debug_phase_counters(uint64_t* out, int reset);
 
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st);
+// true if the batch runs on schedule_lean_kernel (+ schedule_kernel over its
+// defer list); then launch_prep must run between launch_req_masks and launch_schedule.
+bool fast_path(int C);
+hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st);
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p,
                            void* global_scratch, size_t scratch_bytes, hipStream_t st);
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,

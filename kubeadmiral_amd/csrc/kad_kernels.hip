@@ -31,7 +31,12 @@ __device__ unsigned long long g_phase[256 * 16];
 #define KAD_PFLUSH                                                                       \
   if (lane_id() == 0)                                                                    \
     for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 16 + i_], pacc[i_])
+// lean kernel: its own slots 10..15 (A, B, D, E, straddles, D on straddles)
+#define KAD_PFLUSH_LEAN                                                                  \
+  if (lane_id() == 0)                                                                    \
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 16 + 10 + i_], pacc[i_])
 #else
+#define KAD_PFLUSH_LEAN
 #define KAD_PT(v)
 #define KAD_PACC
 #define KAD_PADD(i, x)
@@ -233,6 +238,8 @@ struct SchedArgs {
   ProfDev p;
   char* gscratch;
   int wave_bytes, waves_per_block, w_stride;
+  const int32_t* list;    // non-null: schedule units list[0 .. *list_n) (the lean kernel's defer list)
+  const int32_t* list_n;
 };
 typedef const __attribute__((address_space(4))) SchedArgs* KArgs;
 __device__ __forceinline__ KArgs kargs() {
@@ -275,7 +282,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
     region = GSCR ? a->gscratch + (size_t)gw * wbytes : smem + (size_t)wv * wbytes;
     C = a->s.C;
     TW = a->s.TW;
-    W = a->b.W;
+    W = a->list ? *a->list_n : a->b.W;
     fm = a->p.filter_mask;
     sm = a->p.score_mask;
     xs_b = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
@@ -295,9 +302,10 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
   const bool f_aff = fm & BIT(KAD_PL_CLUSTER_AFFINITY), f_place = fm & BIT(KAD_PL_PLACEMENT_FILTER);
 
   KAD_PACC;
-  for (int w = gw; w < W; w += w_stride) {
+  for (int wi = gw; wi < W; wi += w_stride) {
     KAD_PT(t0);
     KArgs a = kargs();
+    const int w = a->list ? ldc(a->list + wi) : wi;
     const uint32_t f = ldc(a->b.flags + w);
     if (f & KAD_W_STICKY) {  // generic_scheduler.go:101-104
       unit_status(a, w, KAD_ST_STICKY);
@@ -524,6 +532,597 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
     KAD_PADD(4, t5 - t4);
   }
   KAD_PFLUSH;
+}
+
+// ============================================================ prep kernel
+// One lane per (unit, 64-cluster chunk), every launch, before the lean
+// schedule kernel:
+//  * chunk 0's lane writes the unit's 64-B UnitRec, routing units that use a
+//    feature the lean kernel leaves out (scalar resource requests, more than
+//    64 taint ids or GVKs, debug capture) to schedule_kernel (REC_FULL);
+//  * every lane writes the unit's static filter word for its chunk: the
+//    ClusterAffinity filter (cluster_affinity.go:50-94,
+//    MatchClusterSelectorTerms clusterselector/util.go:97-132) evaluated over
+//    the requirement rows, ANDed with the PlacementFilter's ClusterNames
+//    bitmap (placement/filter.go:37-57); and, for units with
+//    CurrentClusters, the current-cluster word (TaintToleration's NoExecute
+//    rule, taint_toleration.go:64-78).
+// This takes the program → requirement-row load chain off every unit's
+// critical path in the schedule kernel.
+__device__ uint64_t affinity_word(const uint64_t* rows, const int32_t* p, uint32_t nch, uint32_t ch) {
+  auto row = [&](int id) { return ldg(rows, (uint32_t)id * nch + ch); };
+  int pc = 0;
+  const int n_sel = p[pc++];
+  uint64_t m = ~0ull;  // SelectorFromSet: AND of the ClusterSelector entries
+  for (int i = 0; i < n_sel; i++) m &= row(p[pc + i]);
+  pc += n_sel;
+  if (!p[pc++]) return m;  // Required == nil: Success
+  const int n_terms = p[pc++];
+  uint64_t matched = 0, undecided = m;
+  for (int t = 0; t < n_terms && undecided; t++) {
+    const int tf = p[pc], ne = p[pc + 1], nf = p[pc + 2];
+    const int at = pc + 3;
+    pc += 3 + ne + nf;
+    if (!(tf & (KAD_TERM_HAS_EXPR | KAD_TERM_HAS_FIELD))) continue;  // nil/empty term selects nothing
+    uint64_t cand = undecided;
+    if (tf & KAD_TERM_HAS_EXPR) {
+      if (!(tf & KAD_TERM_EXPR_VALID)) break;  // invalid selector reached: false for every undecided cluster
+      for (int i = 0; i < ne; i++) cand &= row(p[at + i]);
+    }
+    if (tf & KAD_TERM_HAS_FIELD) {
+      if (!(tf & KAD_TERM_FIELD_VALID)) {  // reached only where the expressions matched
+        undecided &= ~cand;
+        continue;
+      }
+      for (int i = 0; i < nf; i++) cand &= row(p[at + ne + i]);
+    }
+    matched |= cand;
+    undecided &= ~cand;
+  }
+  return matched;
+}
+
+// bits of the sorted cluster-id list ids[lo, hi) that fall in chunk ch
+__device__ uint64_t id_list_word(const int32_t* ids, int lo, int hi, uint32_t ch) {
+  const int base = (int)ch * WAVE;
+  int a = lo, b = hi;
+  while (a < b) {  // lower bound of base
+    const int mid = (a + b) >> 1;
+    if (ids[mid] < base)
+      a = mid + 1;
+    else
+      b = mid;
+  }
+  uint64_t m = 0;
+  for (int j = a; j < hi && ids[j] < base + WAVE; ++j) m |= 1ull << (ids[j] - base);
+  return m;
+}
+
+__global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
+  const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
+  const uint32_t per = nch > 0 ? nch : 1u;
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g == 0) *b.defer_n = 0;
+  if (g >= (uint32_t)b.W * per) return;
+  const uint32_t w = g / per, ch = g - w * per;
+  const uint32_t f = b.flags[w];
+  const uint32_t fm = p.filter_mask;
+  if (ch == 0) {
+    UnitRec r;
+    bool full = force_full != 0;
+    if ((fm & (1u << KAD_PL_TAINT_TOLERATION)) && s.TW > 1) full = true;
+    if ((fm & (1u << KAD_PL_API_RESOURCES)) && b.gvk[w] >= 64) full = true;
+    if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && b.sreq_off[w] < b.sreq_off[w + 1])
+      full = true;
+    if ((p.score_mask & (1u << KAD_PL_TAINT_TOLERATION)) && s.TW > 1) full = true;
+    r.flags = f | (((f & KAD_W_HAS_DESIRED) && b.desired[w] > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
+    r.gvk = b.gvk[w];
+    r.tolset = b.tolset[w];
+    r.sprog_off = b.sprog_off[w];
+    r.req_cpu = b.req_cpu[w];
+    r.req_mem = b.req_mem[w];
+    r.maxc = b.maxc[w];
+    r.out_off = b.out_off[w];
+    r.tol0 = b.tol_all[(size_t)r.tolset * b.TW];
+    r.tolp0 = b.tol_pns[(size_t)r.tolset * b.TW];
+    b.rec[w] = r;
+  }
+  if (ch < nch && !(f & KAD_W_STICKY)) {
+    uint64_t m = ~0ull;
+    if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) m = affinity_word(b.req_mask, b.fprog + b.fprog_off[w], nch, ch);
+    if ((fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT))
+      m &= id_list_word(b.place, b.place_off[w], b.place_off[w + 1], ch);
+    b.sw[g] = m;
+    if ((fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT))
+      b.cw[g] = id_list_word(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch);
+  }
+}
+
+// ================================================= lean schedule kernel
+// schedule_lean_kernel<NCH> — the common case, used whenever C fits the
+// per-wave LDS budget (fast_path). Each wave owns a run of consecutive units.
+// For NCH > 0 (C <= 64*NCH) the block first copies the cluster attributes the
+// path reads (fit resources, taint words, GVK word) into an LDS cache shared
+// by its waves, and a unit's fixed fields and static filter words arrive
+// through scalar loads issued one unit ahead: the common path issues NO
+// vector load after the prologue, so no s_waitcnt vmcnt ever waits behind the
+// previous unit's output stores (gfx9 counts stores and loads in one in-order
+// counter), and the cache costs no VGPRs (occupancy).
+// The feasible list is compacted into LDS (snapshot order = the reference's
+// feasible list, generic_scheduler.go:152-169); then each lane owns
+// positions lane + 64q (q < QMAX), and scores, normalisation and MaxCluster's
+// first-k set are computed in registers:
+//   * the k-th largest total T by ballot bisection over [min, max];
+//   * cut takes every tie (k - #(>T) == #(==T)): selection = {total >= T};
+//   * n <= 12: Go's pdqsort is one stable insertionSort, so the selection is
+//     {> T} plus the first k - #(>T) ties in input order;
+//   * otherwise the restricted pdqsort replay (kad_select.h) on registers
+//     (keys as u32 offsets from the row minimum; LDS for wider rows).
+// Units routed REC_FULL by prep, or (NCH == 0) with more than 64*QMAX
+// feasible clusters, go to the defer list and schedule_kernel afterwards.
+constexpr int LEAN_QMAX_DYN = 4;
+__host__ __device__ constexpr int lean_qmax(int nch_t) { return nch_t > 0 ? nch_t : LEAN_QMAX_DYN; }
+constexpr int LEAN_CACHE_ATTRS = 8;  // alloc/used cpu & mem, NS|NE, NE, PNS, GVK word 0
+struct LeanLayout {
+  size_t key, idx, inv, pid, bytes;
+};
+// per-wave region
+__host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
+  const size_t Cp = (size_t)((C + 63) & ~63);
+  const size_t P = (size_t)qmax * 64;  // positions held in registers
+  LeanLayout L;
+  L.key = 0;                     // i64[P] replay keys of wide rows
+  L.idx = L.key + 8 * P;         // u16[Cp] feasible position → cluster id
+  L.inv = L.idx + 2 * Cp;        // u16[P] replay: original position → rank
+  L.pid = L.inv + 2 * P;         // u16[P] replay: permutation of wide rows
+  L.bytes = (L.pid + 2 * P + 15) & ~(size_t)15;
+  return L;
+}
+// block-shared cluster cache (NCH > 0): LEAN_CACHE_ATTRS arrays of Cp i64
+__host__ __device__ inline size_t lean_cache_bytes(int C) { return (size_t)LEAN_CACHE_ATTRS * 8 * ((C + 63) & ~63); }
+static constexpr int LDS_BUDGET = 64 * 1024;  // per block
+bool fast_path(int C) { return row_layout(C).bytes <= (size_t)LDS_BUDGET; }
+
+struct LeanArgs {
+  SnapDev s;
+  BatchDev b;
+  OutDev o;
+  ProfDev p;
+  int wave_bytes, waves_per_block, units_per_wave;
+};
+typedef const __attribute__((address_space(4))) LeanArgs* LArgs;
+__device__ __forceinline__ LArgs largs() {
+  return (LArgs)opq((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
+}
+__device__ __forceinline__ void lean_status(int w, int32_t st) {
+  if (lane_id() == 0) {
+    LArgs a = largs();
+    a->o.status[w] = st;
+    a->o.count[w] = 0;
+    a->o.flags[w] = 0;
+  }
+}
+// (inline: the kernarg segment pointer is only defined inside the kernel body)
+__device__ __forceinline__ void lean_defer(int w) {
+  if (lane_id() == 0) {
+    LArgs a = largs();
+    const int slot = atomicAdd(a->b.defer_n, 1);
+    a->b.defer[slot] = w;
+  }
+}
+
+// pdqsort storage: LDS keys swapped in place with their original positions
+struct KeyLdsStore {
+  int64_t* key;
+  uint16_t* id;
+  __device__ __forceinline__ bool gt(int i, int j) const { return key[i] > key[j]; }
+  __device__ __forceinline__ void swap(int i, int j) const {
+    const int64_t a = key[i], b = key[j];
+    const uint16_t x = id[i], y = id[j];
+    key[i] = b;
+    key[j] = a;
+    id[i] = y;
+    id[j] = x;
+  }
+};
+
+template <int NCH>
+__global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
+  (void)args;  // read through largs()
+  constexpr int Q = lean_qmax(NCH);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int C, W, w0, w1;
+  uint32_t fm, sm;
+  char* region;
+  {
+    LArgs a = largs();
+    const int gw = blockIdx.x * a->waves_per_block + wv;
+    region = smem + (size_t)wv * a->wave_bytes;
+    C = a->s.C;
+    W = a->b.W;
+    fm = a->p.filter_mask;
+    sm = a->p.score_mask;
+    const int upw = a->units_per_wave;
+    w0 = gw * upw;
+    w1 = w0 + upw < W ? w0 + upw : W;
+  }
+  const int nch = (C + 63) >> 6;
+  const LeanLayout L = lean_layout(C, Q);
+  constexpr int P = Q * 64;
+  const int Cp = nch * 64;
+  int64_t* key = (int64_t*)(region + L.key);
+  uint16_t* idx = (uint16_t*)(region + L.idx);
+  uint16_t* inv = (uint16_t*)(region + L.inv);
+  uint16_t* pid = (uint16_t*)(region + L.pid);
+  const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
+  const bool f_sw = fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER));
+  const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
+  const bool s_res =
+      sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
+  const bool s_tt = sm & BIT(KAD_PL_TAINT_TOLERATION);
+
+  // block-shared LDS cache of the cluster attributes (NCH > 0), after the wave regions
+  int64_t* cache = (int64_t*)(smem + (size_t)blockDim.x / 64 * largs()->wave_bytes);
+  int64_t* c_ac = cache;
+  int64_t* c_uc = cache + Cp;
+  int64_t* c_am = cache + 2 * Cp;
+  int64_t* c_um = cache + 3 * Cp;
+  uint64_t* c_ns = (uint64_t*)(cache + 4 * Cp);
+  uint64_t* c_ne = (uint64_t*)(cache + 5 * Cp);
+  uint64_t* c_pn = (uint64_t*)(cache + 6 * Cp);
+  uint64_t* c_gv = (uint64_t*)(cache + 7 * Cp);
+  if constexpr (NCH > 0) {
+    LArgs a = largs();
+    for (int c = threadIdx.x; c < Cp; c += blockDim.x) {
+      const bool in = c < C;
+      const uint32_t cl = in ? (uint32_t)c : 0u;
+      c_ac[c] = in ? ldg(a->s.alloc_cpu, cl) : 0;
+      c_uc[c] = in ? ldg(a->s.used_cpu, cl) : 0;
+      c_am[c] = in ? ldg(a->s.alloc_mem, cl) : 0;
+      c_um[c] = in ? ldg(a->s.used_mem, cl) : 0;
+      c_ns[c] = in ? ldg(a->s.nsne, cl) : 0;
+      c_ne[c] = in ? ldg(a->s.ne, cl) : 0;
+      c_pn[c] = in ? ldg(a->s.pns, cl) : 0;
+      c_gv[c] = in ? ldg(a->s.gvk, cl) : 0;
+    }
+    __syncthreads();
+  }
+  constexpr int NR = NCH > 0 ? NCH : 1;
+
+  if (w0 >= W) return;
+  // hot fields of the current unit, loaded (scalar) one unit ahead
+  const UnitRec* recs = largs()->b.rec;
+  const uint64_t* sws = largs()->b.sw;
+  uint32_t f = ldc(&recs[w0].flags);
+  int gv = ldc(&recs[w0].gvk);
+  int64_t rq_cpu = ldc(&recs[w0].req_cpu), rq_mem = ldc(&recs[w0].req_mem);
+  uint64_t tol0 = ldc(&recs[w0].tol0);
+  uint64_t swv[NR];
+#pragma unroll
+  for (int ch = 0; ch < NR; ++ch) swv[ch] = (NCH > 0 && f_sw) ? ldc(sws + (size_t)w0 * nch + ch) : ~0ull;
+
+  KAD_PACC;
+  for (int w = w0; w < w1; ++w) {
+    KAD_PT(t0);
+    // this unit's hot fields → locals; issue the next unit's scalar loads
+    const uint32_t fc = f;
+    const int gvc = gv;
+    const int64_t rqc = rq_cpu, rqm = rq_mem;
+    const uint64_t tolc = tol0;
+    uint64_t swc[NR];
+#pragma unroll
+    for (int ch = 0; ch < NR; ++ch) swc[ch] = swv[ch];
+    if (w + 1 < w1) {
+      const UnitRec* R = recs + w + 1;
+      f = ldc(&R->flags);
+      gv = ldc(&R->gvk);
+      rq_cpu = ldc(&R->req_cpu);
+      rq_mem = ldc(&R->req_mem);
+      tol0 = ldc(&R->tol0);
+#pragma unroll
+      for (int ch = 0; ch < NR; ++ch) swv[ch] = (NCH > 0 && f_sw) ? ldc(sws + (size_t)(w + 1) * nch + ch) : ~0ull;
+    }
+    if (fc & KAD_W_STICKY) {  // generic_scheduler.go:101-104
+      lean_status(w, KAD_ST_STICKY);
+      continue;
+    }
+    if (fc & REC_FULL) {
+      lean_defer(w);
+      continue;
+    }
+    // cold fields of this unit (scalar; first needed after the filter)
+    const UnitRec* Rc = recs + w;
+    const int spo = ldc(&Rc->sprog_off);
+    const int64_t mc = ldc(&Rc->maxc), ooff = ldc(&Rc->out_off);
+    const uint64_t tolp0 = ldc(&Rc->tolp0);
+    const bool use_cur = f_taint && (fc & KAD_W_HAS_CURRENT);
+    const bool fit_on = f_fit && (fc & KAD_W_FIT_NONZERO);
+    uint64_t dsw = ~0ull, dcw = 0;  // dynamic-NCH path: words in lanes < nch
+    if constexpr (NCH == 0) {
+      LArgs a = largs();
+      if (f_sw && lane < nch) dsw = ldg(a->b.sw, (uint32_t)(w * nch + lane));
+      if (use_cur && lane < nch) dcw = ldg(a->b.cw, (uint32_t)(w * nch + lane));
+    }
+
+    // ---------------- filters → compacted feasible list (findClustersThatFitWorkload, :152-169)
+    int n = 0;
+    const int NC = NCH > 0 ? NCH : nch;
+#pragma unroll
+    for (int ch = 0; ch < NC; ++ch) {
+      const int c = ch * WAVE + lane;
+      int64_t acpu, ucpu, amem, umem;
+      uint64_t ns0, ne0, pn0, gv0, sw0, cw0;
+      if constexpr (NCH > 0) {
+        acpu = c_ac[c];
+        ucpu = c_uc[c];
+        amem = c_am[c];
+        umem = c_um[c];
+        ns0 = c_ns[c];
+        ne0 = use_cur ? c_ne[c] : 0ull;
+        pn0 = 0;
+        gv0 = c_gv[c];
+        sw0 = swc[ch];
+        cw0 = use_cur ? ldc(largs()->b.cw + (size_t)w * nch + ch) : 0ull;
+      } else {
+        LArgs a = largs();
+        const uint32_t cl = c < C ? (uint32_t)c : 0u;
+        acpu = ldg(a->s.alloc_cpu, cl);
+        ucpu = ldg(a->s.used_cpu, cl);
+        amem = ldg(a->s.alloc_mem, cl);
+        umem = ldg(a->s.used_mem, cl);
+        ns0 = ldg(a->s.nsne, cl);
+        ne0 = ldg(a->s.ne, cl);
+        pn0 = 0;
+        gv0 = ldg(a->s.gvk, cl);
+        sw0 = readlane64(dsw, ch);
+        cw0 = readlane64(dcw, ch);
+      }
+      bool ok = c < C;
+      if (f_sw) ok &= (sw0 >> lane) & 1;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
+      if (f_taint) {  // taint_toleration.go:50-77: NoSchedule|NoExecute, only NoExecute once scheduled there
+        const uint64_t x = (use_cur && ((cw0 >> lane) & 1)) ? ne0 : ns0;
+        ok &= (x & ~tolc) == 0;
+      }
+      if (f_api) ok &= gvc >= 0 && ((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
+      if (fit_on)  // clusterresources/fit.go:73-134
+        ok &= (int)(acpu >= wadd(rqc, ucpu)) & (int)(amem >= wadd(rqm, umem));
+      const uint64_t m = ballot(ok);
+      (void)pn0;
+      if (ok) idx[n + mbcnt(m)] = (uint16_t)c;
+      n += popc64(m);
+    }
+    KAD_PT(t1);
+    KAD_PADD(0, t1 - t0);
+    if (n == 0) {  // generic_scheduler.go:112-114
+      lean_status(w, KAD_ST_NO_FEASIBLE);
+      continue;
+    }
+    if (NCH == 0 && n > P) {
+      lean_defer(w);
+      continue;
+    }
+    if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && (fc & KAD_W_SCORE_ERROR)) {  // framework.go:149-159
+      lean_status(w, KAD_ST_ERR_SCORE);
+      continue;
+    }
+    wave_sync();
+
+    // ---------------- scores of positions 64q + lane (RunScorePlugins, framework.go:139-181)
+    const int nq = (n + 63) >> 6;
+    int64_t t[Q];
+    uint32_t cid[Q];
+    int ttv[Q];
+    int ttmax = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      t[q] = 0;
+      cid[q] = 0;
+      ttv[q] = 0;
+      if (q >= nq) continue;
+      const int p = q * 64 + lane;
+      const bool v = p < n;
+      cid[q] = v ? idx[p] : 0u;
+      const uint32_t cq = cid[q];
+      if (s_res) {
+        int64_t cc, cm, uc, um;
+        if constexpr (NCH > 0) {
+          cc = c_ac[cq];
+          cm = c_am[cq];
+          uc = c_uc[cq];
+          um = c_um[cq];
+        } else {
+          LArgs a = largs();
+          cc = ldg(a->s.alloc_cpu, cq);
+          cm = ldg(a->s.alloc_mem, cq);
+          uc = ldg(a->s.used_cpu, cq);
+          um = ldg(a->s.used_mem, cq);
+        }
+        if (!v) {
+          cc = cm = 1;
+          uc = um = 0;
+        }
+        const int64_t rc = wadd(uc, rqc), rm = wadd(um, rqm);
+        int64_t x = 0;
+        if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
+          x = wadd(x, go_div(wadd(least_requested(rm, cm), least_requested(rc, cc)), 2));
+        if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+          x = wadd(x, go_div(wadd(most_requested(rm, cm), most_requested(rc, cc)), 2));
+        if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x = wadd(x, balanced(rc, cc, rm, cm));
+        t[q] = x;
+      }
+      if (s_tt) {  // taint_toleration.go:91-118: PreferNoSchedule taints not tolerated
+        uint64_t pn;
+        if constexpr (NCH > 0)
+          pn = c_pn[cq];
+        else
+          pn = ldg(largs()->s.pns, cq);
+        ttv[q] = v ? popc64(pn & ~tolp0) : 0;
+        ttmax = ttv[q] > ttmax ? ttv[q] : ttmax;
+      }
+    }
+    if (s_tt) {  // DefaultNormalizeScore(100, reverse=true), framework/util.go:455-483
+      ttmax = wave_max_u_i32(ttmax);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (q < nq) t[q] = wadd(t[q], ttmax == 0 ? 100 : 100 - (int64_t)small_quot(100 * ttv[q], ttmax));
+    }
+    if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {  // cluster_affinity.go:96-140 + DefaultNormalizeScore(100, false)
+      LArgs a = largs();
+      const int32_t* sp = a->b.sprog + spo;
+      if (ldc(sp) > 0) {  // units without preferred terms score 0 everywhere
+        int64_t afs[Q];
+        int64_t amax = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          afs[q] = 0;
+          if (q < nq && q * 64 + lane < n) afs[q] = affinity_score(a->b.req_mask, sp, nch, (int)cid[q]);
+          amax = afs[q] > amax ? afs[q] : amax;
+        }
+        amax = wave_max_u_i64(amax);
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (q < nq) t[q] = wadd(t[q], amax == 0 ? afs[q] : div_fast(wmul(100, afs[q]), amax));
+      }
+    }
+    KAD_PT(t2);
+    KAD_PADD(1, t2 - t1);
+
+    // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
+    LArgs ad = largs();
+    int64_t k = n;
+    if (ad->p.select_plugin == KAD_PL_MAX_CLUSTER) {
+      const bool hm = fc & KAD_W_HAS_MAX_CLUSTERS;
+      if (hm && mc < 0) {
+        lean_status(w, KAD_ST_ERR_SELECT);
+        continue;
+      }
+      if (hm && mc < k) k = mc;
+    }
+    uint64_t sel[Q];
+    uint32_t rflags = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) sel[q] = 0;
+    if (k >= n) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) sel[q] = ballot(q * 64 + lane < n);
+    } else if (k > 0) {
+      // k-th largest total: the largest T with #(total >= T) >= k
+      int64_t mn = I64_MAX, mx = I64_MIN;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (q < nq && q * 64 + lane < n) {
+          mn = t[q] < mn ? t[q] : mn;
+          mx = t[q] > mx ? t[q] : mx;
+        }
+      const int64_t rmin = wave_min_u_i64(mn);
+      int64_t lo = rmin, hi = wave_max_u_i64(mx);
+      const uint64_t span = (uint64_t)hi - (uint64_t)lo;
+      while (lo < hi) {
+        const uint64_t d = (uint64_t)hi - (uint64_t)lo;
+        const int64_t mid = (int64_t)((uint64_t)lo + (d >> 1) + (d & 1));
+        int64_t cnt = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (q < nq) cnt += popc64(ballot(q * 64 + lane < n && t[q] >= mid));
+        if (cnt >= k)
+          lo = mid;
+        else
+          hi = (int64_t)((uint64_t)mid - 1);
+      }
+      uint64_t gm[Q], em[Q];
+      int64_t g = 0, e = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const bool v = q < nq && q * 64 + lane < n;
+        gm[q] = ballot(v && t[q] > lo);
+        em[q] = ballot(v && t[q] == lo);
+        g += popc64(gm[q]);
+        e += popc64(em[q]);
+      }
+      const int64_t need = k - g;
+      if (need == e) {  // the cut takes every tie: no sort needed
+#pragma unroll
+        for (int q = 0; q < Q; ++q) sel[q] = gm[q] | em[q];
+      } else {
+        rflags = KAD_RF_TIE_STRADDLE;
+        const int xs_b = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
+        const int xs_c = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+        if (n <= 12) {  // pdqsort_func: a single (stable) insertionSort
+          sel[0] = gm[0] | ballot(lane < n && t[0] == lo && mbcnt(em[0]) < need);
+        } else {
+          if (n <= WAVE && span <= 0xFFFFFFFFull) {  // restricted pdqsort replay in registers
+            RegStore st{(uint32_t)((uint64_t)t[0] - (uint64_t)rmin), (uint32_t)lane};
+            PdqT<RegStore> pq{st, xs_b, xs_c};
+            pq.select(n, (int)k);
+            // rank of every original position: invert the permutation with ds_permute
+            const int rank = __builtin_amdgcn_ds_permute((int)(st.iv * 4), lane);
+            sel[0] = ballot(lane < n && rank < k);
+          } else {  // longer or wide-key rows: the LDS replay (keys swapped in place)
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq && q * 64 + lane < n) {
+                key[q * 64 + lane] = t[q];
+                pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
+              }
+            wave_sync();
+            if (lane == 0) {
+              KeyLdsStore st{key, pid};
+              PdqT<KeyLdsStore> pq{st, xs_b, xs_c};
+              pq.select(n, (int)k);
+            }
+            wave_sync();
+            for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq) {
+                const int p = q * 64 + lane;
+                sel[q] = ballot(p < n && inv[p] < k);
+              }
+          }
+        }
+      }
+    }
+    KAD_PT(t3);
+    KAD_PADD(2, t3 - t2);
+    if (rflags) {
+      KAD_PADD(4, 1);
+      KAD_PADD(5, t3 - t2);
+    }
+
+    // ---------------- output, ascending cluster id (= ascending position)
+    {
+      LArgs ae = largs();
+      const bool dup = fc & KAD_W_DUPLICATE;
+      const bool replicas =
+          !dup && ae->p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (fc & REC_DESIRED_POS) && k > 0;
+      int base = 0;
+      if (dup || replicas) {
+        int32_t* oc = ae->o.cluster + ooff;
+        int64_t* orp = ae->o.replicas + ooff;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          if ((sel[q] >> lane) & 1) {
+            const uint32_t at = (uint32_t)(base + mbcnt(sel[q]));
+            stg(oc, at, (int32_t)cid[q]);
+            stg(orp, at, (int64_t)(dup ? -1 : 0));
+          }
+          base += popc64(sel[q]);
+        }
+      }
+      if (lane == 0) {
+        ae->o.status[w] = KAD_ST_OK;
+        ae->o.count[w] = base;  // Divide without replicas plugin: empty map
+        ae->o.flags[w] = rflags;
+      }
+    }
+    wave_sync();
+    KAD_PT(t4);
+    KAD_PADD(3, t4 - t3);
+  }
+  KAD_PFLUSH_LEAN;
 }
 
 // ============================================================ plan kernel
@@ -841,7 +1440,6 @@ int debug_phase_counters(uint64_t* out, int reset) {
 #endif
 }
 
-static constexpr int LDS_BUDGET = 64 * 1024;  // per block
 static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st) {
@@ -853,16 +1451,61 @@ hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st)
   return hipGetLastError();
 }
 
+hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st) {
+  (void)hipGetLastError();
+  const int nch = (s.C + 63) >> 6;
+  const long lanes = (long)b.W * (nch > 0 ? nch : 1);
+  const long grid = lanes > 0 ? (lanes + 255) / 256 : 1;  // one block at W = 0 still resets defer_n
+  hipLaunchKernelGGL(prep_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, p, force_full ? 1 : 0);
+  return hipGetLastError();
+}
+
+template <int NCH>
+static void launch_lean(const LeanArgs& A, int grid, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL(schedule_lean_kernel<NCH>, dim3(grid), dim3(64 * A.waves_per_block), lds, st, A);
+}
+
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
                            size_t scr_bytes, hipStream_t st) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (b.W == 0) return hipSuccess;
   const size_t wb = row_layout(s.C).bytes;
+  if (fast_path(s.C)) {
+    const int nch = (s.C + 63) >> 6;
+    const size_t lb = lean_layout(s.C, lean_qmax(nch <= 4 ? nch : 0)).bytes;
+    const int wpb = 4;
+    // runs of consecutive units per wave: long enough to amortise the
+    // register-resident cluster attributes, short enough that the grid is
+    // many times the resident wave count
+    int upw = b.W / (256 * 64);
+    upw = upw < 1 ? 1 : (upw > 16 ? 16 : upw);
+    const long waves = ((long)b.W + upw - 1) / upw;
+    const int grid = (int)((waves + wpb - 1) / wpb);
+    const LeanArgs A{s, b, o, p, (int)lb, wpb, upw};
+    const size_t lds = lb * wpb + (nch <= 4 ? lean_cache_bytes(s.C) : 0);
+    switch (nch) {
+      case 1: launch_lean<1>(A, grid, lds, st); break;
+      case 2: launch_lean<2>(A, grid, lds, st); break;
+      case 3: launch_lean<3>(A, grid, lds, st); break;
+      case 4: launch_lean<4>(A, grid, lds, st); break;
+      default: launch_lean<0>(A, grid, lds, st); break;
+    }
+    if (hipError_t e = hipGetLastError()) return e;
+    // the defer list: its length is only known on the device, so the grid
+    // strides over it (waves past its end exit at once)
+    int wpb2 = (int)(LDS_BUDGET / wb);
+    wpb2 = wpb2 > 4 ? 4 : (wpb2 < 1 ? 1 : wpb2);
+    long waves2 = b.W < 256 * 16 ? b.W : 256 * 16;
+    const int grid2 = (int)((waves2 + wpb2 - 1) / wpb2);
+    const SchedArgs A2{s, b, o, p, nullptr, (int)wb, wpb2, grid2 * wpb2, b.defer, b.defer_n};
+    hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid2), dim3(64 * wpb2), wb * wpb2, st, A2);
+    return hipGetLastError();
+  }
   if (wb <= (size_t)LDS_BUDGET) {
     int wpb = (int)(LDS_BUDGET / wb);
     wpb = wpb > 4 ? 4 : (wpb < 1 ? 1 : wpb);
     const int grid = (b.W + wpb - 1) / wpb;
-    const SchedArgs A{s, b, o, p, nullptr, (int)wb, wpb, grid * wpb};
+    const SchedArgs A{s, b, o, p, nullptr, (int)wb, wpb, grid * wpb, nullptr, nullptr};
     hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid), dim3(64 * wpb), wb * wpb, st, A);
   } else {
     size_t slots = scr_bytes / wb;
@@ -870,7 +1513,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
     if (slots > (size_t)b.W) slots = b.W;
     const int grid = (int)slots;
-    const SchedArgs A{s, b, o, p, (char*)gscr, (int)wb, 1, grid};
+    const SchedArgs A{s, b, o, p, (char*)gscr, (int)wb, 1, grid, nullptr, nullptr};
     hipLaunchKernelGGL(schedule_kernel<true>, dim3(grid), dim3(64), 0, st, A);
   }
   return hipGetLastError();

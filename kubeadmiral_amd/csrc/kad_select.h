@@ -17,22 +17,53 @@
 namespace kad {
 
 // ------------------------------------------------ restricted pdqsort replay
-// Operates on v[0..n) (indices into key[]); less(i, j) = key[v[i]] > key[v[j]].
-struct Pdq {
+// The algorithm is written once over a storage policy S providing
+//   gt(i, j)  : key at position i > key at position j  (Go less(i, j))
+//   swap(i, j): exchange positions i and j.
+// LdsStore: positions index v[] (LDS), keys int64 by original position.
+// RegStore: one position per lane of two VGPRs (u32 key offset, original
+//   position); the whole wave runs the scalar control flow and reads / writes
+//   single lanes with v_readlane / v_writelane — no memory round trip per
+//   comparison (rows of <= 64 entries whose key range fits 32 bits).
+struct LdsStore {
   uint16_t* v;
   const int64_t* key;
-  int xs_b, xs_c;
-  __device__ __forceinline__ bool less(int i, int j) const { return key[v[i]] > key[v[j]]; }
+  __device__ __forceinline__ bool gt(int i, int j) const { return key[v[i]] > key[v[j]]; }
   __device__ __forceinline__ void swap(int i, int j) const {
     uint16_t t = v[i];
     v[i] = v[j];
     v[j] = t;
   }
-  __device__ void insertion_sort(int a, int b) const {
+};
+// v_writelane_b32 (no clang builtin on this toolchain: bind the LLVM intrinsic)
+extern "C" __device__ int kad_writelane_i32(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+struct RegStore {
+  uint32_t kv, iv;
+  __device__ __forceinline__ uint32_t rl(uint32_t x, int l) const {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, l);
+  }
+  __device__ __forceinline__ bool gt(int i, int j) const { return rl(kv, i) > rl(kv, j); }
+  __device__ __forceinline__ void swap(int i, int j) {
+    const uint32_t ki = rl(kv, i), kj = rl(kv, j), ii = rl(iv, i), ij = rl(iv, j);
+    kv = (uint32_t)kad_writelane_i32((int)kj, i, (int)kv);
+    kv = (uint32_t)kad_writelane_i32((int)ki, j, (int)kv);
+    iv = (uint32_t)kad_writelane_i32((int)ij, i, (int)iv);
+    iv = (uint32_t)kad_writelane_i32((int)ii, j, (int)iv);
+  }
+};
+
+template <class S>
+struct PdqT {
+  S& st;
+  int xs_b, xs_c;
+  __device__ __forceinline__ bool less(int i, int j) const { return st.gt(i, j); }
+  __device__ __forceinline__ void swap(int i, int j) const { st.swap(i, j); }
+  __device__ __forceinline__ void insertion_sort(int a, int b) const {
     for (int i = a + 1; i < b; i++)
       for (int j = i; j > a && less(j, j - 1); j--) swap(j, j - 1);
   }
-  __device__ void sift_down(int lo, int hi, int first) const {
+  __device__ __forceinline__ void sift_down(int lo, int hi, int first) const {
     int root = lo;
     for (;;) {
       int child = 2 * root + 1;
@@ -43,7 +74,7 @@ struct Pdq {
       root = child;
     }
   }
-  __device__ void heap_sort(int a, int b) const {
+  __device__ __forceinline__ void heap_sort(int a, int b) const {
     int first = a, lo = 0, hi = b - a;
     for (int i = (hi - 1) / 2; i >= 0; i--) sift_down(i, hi, first);
     for (int i = hi - 1; i >= 0; i--) {
@@ -51,7 +82,7 @@ struct Pdq {
       sift_down(lo, i, first);
     }
   }
-  __device__ bool partial_insertion_sort(int a, int b) const {
+  __device__ __forceinline__ bool partial_insertion_sort(int a, int b) const {
     int i = a + 1;
     for (int j = 0; j < 5; j++) {
       while (i < b && !less(i, i - 1)) i++;
@@ -73,7 +104,7 @@ struct Pdq {
     }
     return false;
   }
-  __device__ void break_patterns(int a, int b) const {
+  __device__ __forceinline__ void break_patterns(int a, int b) const {
     int length = b - a;
     if (length >= 8) {
       uint64_t r = (uint64_t)length;
@@ -103,7 +134,7 @@ struct Pdq {
     order2(a, b, swaps);
     return b;
   }
-  __device__ int choose_pivot(int a, int b, int& hint) const {
+  __device__ __forceinline__ int choose_pivot(int a, int b, int& hint) const {
     int l = b - a, swaps = 0;
     int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
     if (l >= 8) {
@@ -117,10 +148,10 @@ struct Pdq {
     hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
     return j;
   }
-  __device__ void reverse_range(int a, int b) const {
+  __device__ __forceinline__ void reverse_range(int a, int b) const {
     for (int i = a, j = b - 1; i < j; i++, j--) swap(i, j);
   }
-  __device__ int partition_equal(int a, int b, int pivot) const {
+  __device__ __forceinline__ int partition_equal(int a, int b, int pivot) const {
     swap(a, pivot);
     int i = a + 1, j = b - 1;
     for (;;) {
@@ -133,7 +164,7 @@ struct Pdq {
     }
     return i;
   }
-  __device__ int partition(int a, int b, int pivot, bool& already) const {
+  __device__ __forceinline__ int partition(int a, int b, int pivot, bool& already) const {
     swap(a, pivot);
     int i = a + 1, j = b - 1;
     while (i <= j && less(i, a)) i++;
@@ -159,7 +190,7 @@ struct Pdq {
     return j;
   }
   // pdqsort_func(data, 0, n, bits.Len(n)) restricted to ranges straddling k.
-  __device__ void select(int n, int k) const {
+  __device__ __forceinline__ void select(int n, int k) const {
     int a = 0, b = n;
     int limit = 32 - __clz(n);
     bool wasBalanced = true, wasPartitioned = true;
@@ -321,7 +352,8 @@ __device__ uint32_t select_topk(const SelWs& ws, int n, int64_t k, int64_t row_m
   for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
   wsync<GSCR>();
   if (lane == 0) {
-    Pdq p{ws.perm, ws.tot, xs_b, xs_c};
+    LdsStore st{ws.perm, ws.tot};
+    PdqT<LdsStore> p{st, xs_b, xs_c};
     p.select(n, (int)k);
   }
   wsync<GSCR>();

@@ -10,13 +10,14 @@ step() {  # name, timeout, cmd...
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"; tail -n 8 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "aborting after $name (rc=$rc)"; exit $rc; fi
+  if [ $rc -ne 0 ] && { [ $rc -ne 1 ] || [ "$name" = smoke ] || grep -q "illegal memory\|HSA_STATUS_ERROR\|hipError" "gpurun_out/$name.log"; }; then
+    echo "aborting after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
 what=${1:-all}
 if [ "$what" = all ] || [ "$what" = test ]; then
   step smoke 300 python __graft_entry__.py
-  step pytest_gpu 1500 python -m pytest tests -m gpu -q --timeout 600 -rf
+  step pytest_gpu 900 python -m pytest tests -m gpu -x -q --timeout 300 -rf
 fi
 if [ "$what" = all ] || [ "$what" = bench ]; then
   step bench 600 python bench.py --steps 20 --warmup 3

@@ -25,7 +25,8 @@ from kubeadmiral_amd import build as kbuild  # noqa: E402
 
 PROF_LIB = os.path.join(kbuild.HERE, "libkad_prof.so")
 NAMES = ["A_filter", "B_score", "C_normalize", "D_select", "E_output", "n_straddle", "n_select", "sum_feasible",
-         "D_select_straddle"]
+         "D_select_straddle", "-", "lean_A_filter", "lean_B_score", "lean_D_select", "lean_E_output",
+         "lean_n_straddle", "lean_D_select_straddle"]
 
 
 def main():
@@ -63,7 +64,9 @@ def main():
     out = {"config": a.config, "units": batch.W, "reps": a.reps}
     for i, nm in enumerate(NAMES):
         v = float(cnt[i])
-        if nm.startswith(("A_", "B_", "C_", "D_", "E_")):
+        if nm == "-":
+            continue
+        if nm.startswith(("A_", "B_", "C_", "D_", "E_", "lean_A", "lean_B", "lean_D", "lean_E")):
             out[nm + "_cycles_per_unit"] = round(v / W, 1)
         else:
             out[nm + "_per_unit"] = round(v / W, 4)
