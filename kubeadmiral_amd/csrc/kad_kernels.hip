@@ -45,7 +45,7 @@ __device__ unsigned long long g_phase[256 * 16];
 
 // ----------------------------------------------------------- per-wave layout
 struct RowLayout {
-  size_t tot, fx, idx, perm, feas, sel, place, cur, hist, bytes;
+  size_t tot, fx, idx, perm, posl, posr, feas, sel, place, cur, hist, bytes;
 };
 __host__ __device__ inline RowLayout row_layout(int C) {
   const size_t Cp = (size_t)((C + 63) & ~63);
@@ -55,7 +55,9 @@ __host__ __device__ inline RowLayout row_layout(int C) {
   L.fx = L.tot + 8 * Cp;                         // u32[Cp] fixed scores | TT raw << 16
   L.idx = L.fx + 4 * Cp;                         // u16[Cp] feasible position → cluster id
   L.perm = L.idx + 2 * Cp;                       // u16[Cp] pdqsort replay permutation
-  L.feas = (L.perm + 2 * Cp + 15) & ~(size_t)15;  // u64[nw] feasibility by cluster
+  L.posl = L.perm + 2 * Cp;                      // u16[Cp] replay scratch (partition stoppers)
+  L.posr = L.posl + 2 * Cp;                      // u16[Cp]
+  L.feas = (L.posr + 2 * Cp + 15) & ~(size_t)15;  // u64[nw] feasibility by cluster
   L.sel = L.feas + 8 * nw;                       // u64[nw] selection by position
   L.place = L.sel + 8 * nw;
   L.cur = L.place + 8 * nw;
@@ -297,6 +299,8 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
   uint64_t* plb = (uint64_t*)(region + L.place);
   uint64_t* curb = (uint64_t*)(region + L.cur);
   uint32_t* hist = (uint32_t*)(region + L.hist);
+  uint16_t* posl = (uint16_t*)(region + L.posl);
+  uint16_t* posr = (uint16_t*)(region + L.posr);
   const int nch = (C + 63) >> 6;
   const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
   const bool f_aff = fm & BIT(KAD_PL_CLUSTER_AFFINITY), f_place = fm & BIT(KAD_PL_PLACEMENT_FILTER);
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
         if (hm && mc < k) k = mc;
       }
     }
-    SelWs ws{tot, selb, perm, hist};
+    SelWs ws{tot, selb, perm, hist, posl, posr};
     const uint32_t rflags = select_topk<GSCR>(ws, n, k, rmin, rmax, xs_b, xs_c);
     KAD_PT(t4);
     KAD_PADD(3, t4 - t3);
@@ -664,18 +668,20 @@ constexpr int LEAN_QMAX_DYN = 4;
 __host__ __device__ constexpr int lean_qmax(int nch_t) { return nch_t > 0 ? nch_t : LEAN_QMAX_DYN; }
 constexpr int LEAN_CACHE_ATTRS = 8;  // alloc/used cpu & mem, NS|NE, NE, PNS, GVK word 0
 struct LeanLayout {
-  size_t key, idx, inv, pid, bytes;
+  size_t key, idx, inv, pid, posl, posr, bytes;
 };
 // per-wave region
 __host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
   const size_t Cp = (size_t)((C + 63) & ~63);
   const size_t P = (size_t)qmax * 64;  // positions held in registers
   LeanLayout L;
-  L.key = 0;                     // i64[P] replay keys of wide rows
+  L.key = 0;                     // i64[P] replay keys
   L.idx = L.key + 8 * P;         // u16[Cp] feasible position → cluster id
   L.inv = L.idx + 2 * Cp;        // u16[P] replay: original position → rank
-  L.pid = L.inv + 2 * P;         // u16[P] replay: permutation of wide rows
-  L.bytes = (L.pid + 2 * P + 15) & ~(size_t)15;
+  L.pid = L.inv + 2 * P;         // u16[P] replay: original position at each position
+  L.posl = L.pid + 2 * P;        // u16[P] replay scratch (partition stoppers)
+  L.posr = L.posl + 2 * P;       // u16[P]
+  L.bytes = (L.posr + 2 * P + 15) & ~(size_t)15;
   return L;
 }
 // block-shared cluster cache (NCH > 0): LEAN_CACHE_ATTRS arrays of Cp i64
@@ -711,21 +717,6 @@ __device__ __forceinline__ void lean_defer(int w) {
   }
 }
 
-// pdqsort storage: LDS keys swapped in place with their original positions
-struct KeyLdsStore {
-  int64_t* key;
-  uint16_t* id;
-  __device__ __forceinline__ bool gt(int i, int j) const { return key[i] > key[j]; }
-  __device__ __forceinline__ void swap(int i, int j) const {
-    const int64_t a = key[i], b = key[j];
-    const uint16_t x = id[i], y = id[j];
-    key[i] = b;
-    key[j] = a;
-    id[i] = y;
-    id[j] = x;
-  }
-};
-
 template <int NCH>
 __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
   (void)args;  // read through largs()
@@ -756,6 +747,8 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
   uint16_t* idx = (uint16_t*)(region + L.idx);
   uint16_t* inv = (uint16_t*)(region + L.inv);
   uint16_t* pid = (uint16_t*)(region + L.pid);
+  uint16_t* posl = (uint16_t*)(region + L.posl);
+  uint16_t* posr = (uint16_t*)(region + L.posr);
   const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
   const bool f_sw = fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER));
   const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
@@ -1018,7 +1011,6 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
         }
       const int64_t rmin = wave_min_u_i64(mn);
       int64_t lo = rmin, hi = wave_max_u_i64(mx);
-      const uint64_t span = (uint64_t)hi - (uint64_t)lo;
       while (lo < hi) {
         const uint64_t d = (uint64_t)hi - (uint64_t)lo;
         const int64_t mid = (int64_t)((uint64_t)lo + (d >> 1) + (d & 1));
@@ -1052,36 +1044,24 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
         if (n <= 12) {  // pdqsort_func: a single (stable) insertionSort
           sel[0] = gm[0] | ballot(lane < n && t[0] == lo && mbcnt(em[0]) < need);
         } else {
-          if (n <= WAVE && span <= 0xFFFFFFFFull) {  // restricted pdqsort replay in registers
-            RegStore st{(uint32_t)((uint64_t)t[0] - (uint64_t)rmin), (uint32_t)lane};
-            PdqT<RegStore> pq{st, xs_b, xs_c};
-            pq.select(n, (int)k);
-            // rank of every original position: invert the permutation with ds_permute
-            const int rank = __builtin_amdgcn_ds_permute((int)(st.iv * 4), lane);
-            sel[0] = ballot(lane < n && rank < k);
-          } else {  // longer or wide-key rows: the LDS replay (keys swapped in place)
+          // restricted pdqsort replay, wave-parallel (kad_select.h PdqWave)
 #pragma unroll
-            for (int q = 0; q < Q; ++q)
-              if (q < nq && q * 64 + lane < n) {
-                key[q * 64 + lane] = t[q];
-                pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
-              }
-            wave_sync();
-            if (lane == 0) {
-              KeyLdsStore st{key, pid};
-              PdqT<KeyLdsStore> pq{st, xs_b, xs_c};
-              pq.select(n, (int)k);
+          for (int q = 0; q < Q; ++q)
+            if (q < nq && q * 64 + lane < n) {
+              key[q * 64 + lane] = t[q];
+              pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
             }
-            wave_sync();
-            for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
-            wave_sync();
+          wave_sync();
+          PdqWave pw{key, pid, posl, posr, xs_b, xs_c};
+          pw.select(n, (int)k);
+          for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
+          wave_sync();
 #pragma unroll
-            for (int q = 0; q < Q; ++q)
-              if (q < nq) {
-                const int p = q * 64 + lane;
-                sel[q] = ballot(p < n && inv[p] < k);
-              }
-          }
+          for (int q = 0; q < Q; ++q)
+            if (q < nq) {
+              const int p = q * 64 + lane;
+              sel[q] = ballot(p < n && inv[p] < k);
+            }
         }
       }
     }
@@ -1351,6 +1331,8 @@ __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32
   uint16_t* perm = (uint16_t*)(region + L.perm);
   uint64_t* selb = (uint64_t*)(region + L.sel);
   uint32_t* hist = (uint32_t*)(region + L.hist);
+  uint16_t* posl = (uint16_t*)(region + L.posl);
+  uint16_t* posr = (uint16_t*)(region + L.posr);
   const int xs_b = (pflags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
   const int xs_c = (pflags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
   for (int r = blockIdx.x; r < n_rows; r += r_stride) {
@@ -1374,7 +1356,7 @@ __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32
     rmax = wave_max_i64(rmax);
     wsync<GSCR>();
     const int64_t k = mc < n ? mc : n;
-    SelWs ws{tot, selb, perm, hist};
+    SelWs ws{tot, selb, perm, hist, posl, posr};
     select_topk<GSCR>(ws, n, k, rmin, rmax, xs_b, xs_c);
     int base = 0;
     for (int jc = 0; jc < ((n + 63) >> 6); ++jc) {

@@ -251,6 +251,369 @@ struct PdqT {
   }
 };
 
+// storage: LDS keys swapped in place with their original positions
+struct KeyLdsStore {
+  int64_t* key;
+  uint16_t* id;
+  __device__ __forceinline__ bool gt(int i, int j) const { return key[i] > key[j]; }
+  __device__ __forceinline__ void swap(int i, int j) const {
+    const int64_t a = key[i], b = key[j];
+    const uint16_t x = id[i], y = id[j];
+    key[i] = b;
+    key[j] = a;
+    id[i] = y;
+    id[j] = x;
+  }
+};
+
+// ------------------------------------------- wave-parallel restricted replay
+// PdqWave runs the same control flow as PdqT::select — Go 1.19 pdqsort_func
+// restricted to the ranges that straddle k — with the whole wave. The scalar
+// decisions (pivot choice, branch structure, limit/balance bookkeeping) are
+// uniform; the data-parallel steps are computed with ballots and prefix
+// counts and applied as disjoint moves in LDS:
+//   * partition / partitionEqual: Hoare's scans swap the t-th left stopper
+//     with the t-th right stopper for every t with l_t < r_t (l_t rises, r_t
+//     falls, so those t form a prefix); the split point is a + #(right
+//     stoppers), so the result is exactly the serial one;
+//   * insertionSort (<= 12 elements): stable rank = #greater + #equal before;
+//   * reverseRange: disjoint pair swaps;
+//   * partialInsertionSort: first descent by ballot, then each shift is a
+//     rotation whose stop position is found by ballot.
+// heapSort (only after log2(n) unbalanced partitions) falls back to lane 0.
+// key/id: the n positions' keys (swapped in place) and original positions;
+// posL/posR: u16 scratch of n entries each.
+struct PdqWave {
+  int64_t* key;
+  uint16_t* id;
+  uint16_t* posL;
+  uint16_t* posR;
+  int xs_b, xs_c;
+
+  __device__ __forceinline__ int64_t K(int p) const {
+    const int64_t v = key[p];
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  }
+  __device__ __forceinline__ bool less(int i, int j) const { return K(i) > K(j); }
+  __device__ __forceinline__ void swap1(int i, int j) const {
+    const int64_t ki = key[i], kj = key[j];
+    const uint16_t ii = id[i], ij = id[j];
+    wave_sync();
+    if (lane_id() == 0) {
+      key[i] = kj;
+      key[j] = ki;
+      id[i] = ij;
+      id[j] = ii;
+    }
+    wave_sync();
+  }
+  __device__ void insertion_sort(int a, int b) const {
+    const int m = b - a, lane = lane_id();
+    int64_t kp = 0;
+    uint16_t ip = 0;
+    if (lane < m) {
+      kp = key[a + lane];
+      ip = id[a + lane];
+    }
+    int r = 0;
+    for (int q = 0; q < m; ++q) {
+      const int64_t kq = key[a + q];
+      r += (int)(kq > kp) | (int)((kq == kp) & (q < lane));
+    }
+    wave_sync();
+    if (lane < m) {
+      key[a + r] = kp;
+      id[a + r] = ip;
+    }
+    wave_sync();
+  }
+  __device__ void reverse_range(int a, int b) const {
+    const int h = (b - a) / 2;
+    for (int x0 = 0; x0 < h; x0 += WAVE) {
+      const int x = x0 + lane_id();
+      if (x < h) {
+        const int i = a + x, j = b - 1 - x;
+        const int64_t ki = key[i], kj = key[j];
+        const uint16_t ii = id[i], ij = id[j];
+        key[i] = kj;
+        key[j] = ki;
+        id[i] = ij;
+        id[j] = ii;
+      }
+    }
+    wave_sync();
+  }
+  __device__ __forceinline__ void order2(int& a, int& b, int& swaps) const {
+    if (less(b, a)) {
+      int t = a;
+      a = b;
+      b = t;
+      swaps++;
+    }
+  }
+  __device__ __forceinline__ int median(int a, int b, int c, int& swaps) const {
+    order2(a, b, swaps);
+    order2(b, c, swaps);
+    order2(a, b, swaps);
+    return b;
+  }
+  __device__ int choose_pivot(int a, int b, int& hint) const {
+    int l = b - a, swaps = 0;
+    int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    if (l >= 8) {
+      if (l >= 50) {
+        i = median(i - 1, i, i + 1, swaps);
+        j = median(j - 1, j, j + 1, swaps);
+        k = median(k - 1, k, k + 1, swaps);
+      }
+      j = median(i, j, k, swaps);
+    }
+    hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+    return j;
+  }
+  __device__ void break_patterns(int a, int b) const {
+    int length = b - a;
+    if (length >= 8) {
+      uint64_t r = (uint64_t)length;
+      uint64_t modulus = 1ull << (64 - __clzll((unsigned long long)length));
+      int idx = a + (length / 4) * 2 - 1;
+      for (int i = 0; i < 3; i++) {
+        r ^= r << 13;
+        r ^= r >> xs_b;
+        r ^= r << xs_c;
+        int other = (int)(r & (modulus - 1));
+        if (other >= length) other -= length;
+        swap1(idx - 1 + i, a + other);
+      }
+    }
+  }
+  // first p in [i, b) with less(p, p-1), else b
+  __device__ int first_descent(int i, int b) const {
+    for (int p0 = i; p0 < b; p0 += WAVE) {
+      const int p = p0 + lane_id();
+      const uint64_t m = ballot(p < b && key[p] > key[p - 1]);
+      if (m) return p0 + __ffsll((unsigned long long)m) - 1;
+    }
+    return b;
+  }
+  // the element at j0 moves left while it is less than its left neighbour
+  // (Go's loop runs down to position 1, i.e. the element may reach 0)
+  __device__ void shift_left(int j0) const {
+    const int lane = lane_id();
+    const int64_t X = K(j0);
+    const uint16_t XI = (uint16_t)__builtin_amdgcn_readfirstlane((int)id[j0]);
+    int m = 0;
+    for (int q1 = j0; q1 > 0; q1 -= WAVE) {
+      const int q = q1 - 1 - lane;
+      const uint64_t mm = ballot(q >= 0 && key[q] >= X);
+      if (mm) {
+        m = q1 - 1 - (__ffsll((unsigned long long)mm) - 1) + 1;
+        break;
+      }
+    }
+    for (int p1 = j0; p1 > m; p1 -= WAVE) {  // [m, j0) → +1, high chunks first
+      const int p = p1 - 1 - lane;
+      const bool in = p >= m;
+      int64_t kk = 0;
+      uint16_t ii = 0;
+      if (in) {
+        kk = key[p];
+        ii = id[p];
+      }
+      wave_sync();
+      if (in) {
+        key[p + 1] = kk;
+        id[p + 1] = ii;
+      }
+      wave_sync();
+    }
+    if (lane == 0) {
+      key[m] = X;
+      id[m] = XI;
+    }
+    wave_sync();
+  }
+  // the element at j0-1 moves right while its right neighbour is less than it
+  __device__ void shift_right(int j0, int b) const {
+    const int lane = lane_id();
+    const int64_t Y = K(j0 - 1);
+    const uint16_t YI = (uint16_t)__builtin_amdgcn_readfirstlane((int)id[j0 - 1]);
+    int mp = b - 1;
+    for (int q0 = j0; q0 < b; q0 += WAVE) {
+      const int q = q0 + lane;
+      const uint64_t mm = ballot(q < b && key[q] <= Y);
+      if (mm) {
+        mp = q0 + __ffsll((unsigned long long)mm) - 2;
+        break;
+      }
+    }
+    for (int p0 = j0; p0 <= mp; p0 += WAVE) {  // (j0-1, mp] → -1, low chunks first
+      const int p = p0 + lane;
+      const bool in = p <= mp;
+      int64_t kk = 0;
+      uint16_t ii = 0;
+      if (in) {
+        kk = key[p];
+        ii = id[p];
+      }
+      wave_sync();
+      if (in) {
+        key[p - 1] = kk;
+        id[p - 1] = ii;
+      }
+      wave_sync();
+    }
+    if (lane == 0) {
+      key[mp] = Y;
+      id[mp] = YI;
+    }
+    wave_sync();
+  }
+  __device__ bool partial_insertion_sort(int a, int b) const {
+    int i = a + 1;
+    for (int step = 0; step < 5; step++) {
+      i = first_descent(i, b);
+      if (i == b) return true;
+      if (b - a < 50) return false;
+      swap1(i, i - 1);
+      if (i - a >= 2) shift_left(i - 1);
+      if (b - i >= 2) shift_right(i + 1, b);
+    }
+    return false;
+  }
+  // Hoare pairing over [lo, hi): right stoppers R (strict ? key > P : key >= P)
+  // end on the left; swaps l_t <-> r_t for the prefix of t with l_t < r_t.
+  // Returns #R; *T = number of swaps.
+  __device__ int pair_partition(int lo, int hi, int64_t P, bool strict, int* T) const {
+    const int lane = lane_id();
+    int totR = 0;
+    for (int c0 = lo; c0 < hi; c0 += WAVE) {
+      const int p = c0 + lane;
+      const bool in = p < hi;
+      const int64_t kk = in ? key[p] : 0;
+      totR += popc64(ballot(in && (strict ? kk > P : kk >= P)));
+    }
+    const int totL = (hi - lo) - totR;
+    int cL = 0, cR = 0;
+    for (int c0 = lo; c0 < hi; c0 += WAVE) {
+      const int p = c0 + lane;
+      const bool in = p < hi;
+      const int64_t kk = in ? key[p] : 0;
+      const bool isR = in && (strict ? kk > P : kk >= P), isL = in && !isR;
+      const uint64_t mR = ballot(isR), mL = ballot(isL);
+      if (isL) posL[cL + mbcnt(mL)] = (uint16_t)p;
+      if (isR) posR[totR - 1 - (cR + mbcnt(mR))] = (uint16_t)p;
+      cL += popc64(mL);
+      cR += popc64(mR);
+    }
+    wave_sync();
+    const int np = totL < totR ? totL : totR;
+    int t_n = 0;
+    for (int t0 = 0; t0 < np; t0 += WAVE) {
+      const int t = t0 + lane;
+      const uint64_t m = ballot(t < np && posL[t] < posR[t]);
+      t_n += popc64(m);
+      if (~m) break;  // a prefix: once a t fails, every later t fails
+    }
+    for (int t0 = 0; t0 < t_n; t0 += WAVE) {
+      const int t = t0 + lane;
+      if (t < t_n) {
+        const int l = posL[t], r = posR[t];
+        const int64_t kl = key[l], kr = key[r];
+        const uint16_t il = id[l], ir = id[r];
+        key[l] = kr;
+        key[r] = kl;
+        id[l] = ir;
+        id[r] = il;
+      }
+    }
+    wave_sync();
+    *T = t_n;
+    return totR;
+  }
+  __device__ int partition(int a, int b, int pivot, bool& already) const {
+    swap1(a, pivot);
+    const int64_t P = K(a);
+    int T;
+    const int j = a + pair_partition(a + 1, b, P, true, &T);
+    swap1(j, a);
+    already = T == 0;
+    return j;
+  }
+  __device__ int partition_equal(int a, int b, int pivot) const {
+    swap1(a, pivot);
+    const int64_t P = K(a);
+    int T;
+    return a + 1 + pair_partition(a + 1, b, P, false, &T);
+  }
+  __device__ void select(int n, int k) const {
+    int a = 0, b = n;
+    int limit = 32 - __clz(n);
+    bool wasBalanced = true, wasPartitioned = true;
+    while (a < k && k < b) {
+      const int length = b - a;
+      if (length <= 12) {
+        insertion_sort(a, b);
+        return;
+      }
+      if (limit == 0) {
+        if (lane_id() == 0) {
+          KeyLdsStore st{key, id};
+          PdqT<KeyLdsStore> s{st, xs_b, xs_c};
+          s.heap_sort(a, b);
+        }
+        wave_sync();
+        return;
+      }
+      if (!wasBalanced) {
+        break_patterns(a, b);
+        limit--;
+      }
+      int hint;
+      int pivot = choose_pivot(a, b, hint);
+      if (hint == 2) {
+        reverse_range(a, b);
+        pivot = (b - 1) - (pivot - a);
+        hint = 1;
+      }
+      if (wasBalanced && wasPartitioned && hint == 1) {
+        if (partial_insertion_sort(a, b)) return;
+      }
+      if (a > 0 && !less(a - 1, pivot)) {
+        a = partition_equal(a, b, pivot);
+        continue;
+      }
+      bool already;
+      const int mid = partition(a, b, pivot, already);
+      wasPartitioned = already;
+      const int leftLen = mid - a, rightLen = b - mid, thr = length / 8;
+      if (leftLen < rightLen) {
+        if (k < mid) {  // recursion into the smaller left side
+          b = mid;
+          wasBalanced = wasPartitioned = true;
+        } else if (k > mid + 1) {
+          wasBalanced = leftLen >= thr;
+          a = mid + 1;
+        } else {
+          return;
+        }
+      } else {
+        if (k > mid + 1) {  // recursion into the smaller right side
+          a = mid + 1;
+          wasBalanced = wasPartitioned = true;
+        } else if (k < mid) {
+          wasBalanced = rightLen >= thr;
+          b = mid;
+        } else {
+          return;
+        }
+      }
+    }
+  }
+};
+
 __device__ __forceinline__ uint64_t okey(int64_t x) { return (uint64_t)x ^ 0x8000000000000000ull; }
 
 // Per-wave selection workspace (pointers into LDS or global scratch). The
@@ -261,6 +624,8 @@ struct SelWs {
   uint64_t* sel;    // [ceil(n/64)] output: selected positions
   uint16_t* perm;   // [n] permutation buffer for the straddle replay
   uint32_t* hist;   // [256]
+  uint16_t* posl;   // [n] replay scratch
+  uint16_t* posr;   // [n]
 };
 
 // Select the first-k set of positions 0..n-1 under Go's sort.Slice by
@@ -347,14 +712,20 @@ __device__ uint32_t select_topk(const SelWs& ws, int n, int64_t k, int64_t row_m
     wsync<GSCR>();
     return 0;
   }
-  // ---- straddle: replay pdqsort on positions (input order) restricted to k
+  // ---- straddle: replay pdqsort on positions (input order) restricted to k,
+  // keys permuted in place (tot is not read after the selection)
   for (int j = lane; j < n; j += WAVE) ws.perm[j] = (uint16_t)j;
   for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
   wsync<GSCR>();
-  if (lane == 0) {
-    LdsStore st{ws.perm, ws.tot};
-    PdqT<LdsStore> p{st, xs_b, xs_c};
-    p.select(n, (int)k);
+  if (GSCR) {  // global-scratch rows: serial replay (LDS-only wave primitives)
+    if (lane == 0) {
+      KeyLdsStore st{ws.tot, ws.perm};
+      PdqT<KeyLdsStore> p{st, xs_b, xs_c};
+      p.select(n, (int)k);
+    }
+  } else {
+    PdqWave pw{ws.tot, ws.perm, ws.posl, ws.posr, xs_b, xs_c};
+    pw.select(n, (int)k);
   }
   wsync<GSCR>();
   for (int i = lane; i < k; i += WAVE) {
