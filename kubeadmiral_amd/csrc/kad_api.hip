@@ -44,7 +44,7 @@ struct kad_ctx {
   size_t sw_cap = 0;
   void* d_cw = nullptr;   // u64[W][nch] current-cluster words (prep_kernel)
   size_t cw_cap = 0;
-  void* d_defer = nullptr;  // i32[W + 1]: defer_n, then the defer list
+  void* d_defer = nullptr;  // i32[W + 2]: defer_n, work_n, then the defer list
   size_t defer_cap = 0;
   // scratch (per-wave slabs for rows that do not fit LDS)
   void* d_scratch = nullptr;
@@ -269,7 +269,7 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   if (int r = grow(c, &c->d_rec, &c->rec_cap, (size_t)W * sizeof(UnitRec))) return r;
   if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
-  if (int r = grow(c, &c->d_defer, &c->defer_cap, ((size_t)W + 1) * 4)) return r;
+  if (int r = grow(c, &c->d_defer, &c->defer_cap, ((size_t)W + 2) * 4)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->batch_hdr = h;
   const char* base = static_cast<const char*>(c->d_batch);
@@ -316,7 +316,8 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   b.sw = static_cast<uint64_t*>(c->d_sw);
   b.cw = static_cast<uint64_t*>(c->d_cw);
   b.defer_n = static_cast<int32_t*>(c->d_defer);
-  b.defer = b.defer_n + 1;
+  b.work_n = b.defer_n + 1;
+  b.defer = b.defer_n + 2;
   c->have_batch = true;
   c->ran = false;
   return KAD_OK;

@@ -43,6 +43,7 @@ struct BatchDev {
   uint64_t* cw;             // [W][ceil(C/64)] CurrentClusters words (units that have them)
   int32_t* defer;           // [W] units the lean kernel hands to schedule_kernel
   int32_t* defer_n;         // [1] length of defer
+  int32_t* work_n;          // [1] lean kernel work queue: next batch of LEAN_BATCH units
 };
 
 // Per-unit record, rebuilt by prep_kernel at every kad_schedule: the fixed-size

@@ -12,6 +12,8 @@
 // attribute-major (attr[i*C + c]) so each wave's 64 lanes read 64 consecutive
 // clusters: one coalesced 512-B access per i64 attribute. Per-row state lives
 // in LDS (per-wave region) when it fits, else in a per-wave global scratch slab.
+#include <cstdlib>
+
 #include "kad_device.h"
 #include "kad_plan.h"
 #include "kad_select.h"
@@ -606,7 +608,10 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
   const uint32_t per = nch > 0 ? nch : 1u;
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  if (g == 0) *b.defer_n = 0;
+  if (g == 0) {
+    *b.defer_n = 0;
+    *b.work_n = 0;
+  }
   if (g >= (uint32_t)b.W * per) return;
   const uint32_t w = g / per, ch = g - w * per;
   const uint32_t f = b.flags[w];
@@ -665,6 +670,7 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
 // Units routed REC_FULL by prep, or (NCH == 0) with more than 64*QMAX
 // feasible clusters, go to the defer list and schedule_kernel afterwards.
 constexpr int LEAN_QMAX_DYN = 4;
+constexpr int LEAN_BATCH = 4;  // units per work-queue batch (one VGPR of UnitRecs)
 __host__ __device__ constexpr int lean_qmax(int nch_t) { return nch_t > 0 ? nch_t : LEAN_QMAX_DYN; }
 constexpr int LEAN_CACHE_ATTRS = 8;  // alloc/used cpu & mem, NS|NE, NE, PNS, GVK word 0
 struct LeanLayout {
@@ -724,20 +730,16 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int C, W, w0, w1;
+  int C, W;
   uint32_t fm, sm;
   char* region;
   {
     LArgs a = largs();
-    const int gw = blockIdx.x * a->waves_per_block + wv;
     region = smem + (size_t)wv * a->wave_bytes;
     C = a->s.C;
     W = a->b.W;
     fm = a->p.filter_mask;
     sm = a->p.score_mask;
-    const int upw = a->units_per_wave;
-    w0 = gw * upw;
-    w1 = w0 + upw < W ? w0 + upw : W;
   }
   const int nch = (C + 63) >> 6;
   const LeanLayout L = lean_layout(C, Q);
@@ -784,38 +786,53 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
   }
   constexpr int NR = NCH > 0 ? NCH : 1;
 
-  if (w0 >= W) return;
-  // hot fields of the current unit, loaded (scalar) one unit ahead
+  // UnitRecs and static filter words of a batch of up to 8 units, loaded
+  // with two vector loads at the batch start into VGPRs (record dword d of
+  // batch unit u in lane 16*(u&3)+d of rvA/rvB; filter word ch of unit u in
+  // lanes 2*(u*nch+ch)+{0,1} of svv) and read per unit with v_readlane: no
+  // scalar or vector memory round trip per unit (an SMEM load would be
+  // waited by the next LDS wait; a vector load by the last unit's stores).
+  // Each wave owns a contiguous share of the units; the grid is the resident
+  // wave count (launch_schedule), so every wave runs from start to finish
+  // concurrently and shares differ by at most one unit. Records are loaded
+  // in batches of LEAN_BATCH units.
   const UnitRec* recs = largs()->b.rec;
   const uint64_t* sws = largs()->b.sw;
-  uint32_t f = ldc(&recs[w0].flags);
-  int gv = ldc(&recs[w0].gvk);
-  int64_t rq_cpu = ldc(&recs[w0].req_cpu), rq_mem = ldc(&recs[w0].req_mem);
-  uint64_t tol0 = ldc(&recs[w0].tol0);
-  uint64_t swv[NR];
-#pragma unroll
-  for (int ch = 0; ch < NR; ++ch) swv[ch] = (NCH > 0 && f_sw) ? ldc(sws + (size_t)w0 * nch + ch) : ~0ull;
-
+  int w, wend;
+  {
+    LArgs a = largs();
+    const long G = (long)gridDim.x * a->waves_per_block;
+    const long gw = (long)blockIdx.x * a->waves_per_block + wv;
+    w = (int)(W * gw / G) - 1;
+    wend = (int)(W * (gw + 1) / G);
+  }
+  uint32_t rvA = 0, svv = ~0u;
+  int w1 = w + 1, u = 0;
   KAD_PACC;
-  for (int w = w0; w < w1; ++w) {
+  for (;;) {
+    ++w;
+    ++u;
+    if (w >= wend) break;
+    if (w >= w1) {  // next batch
+      w1 = w + LEAN_BATCH < wend ? w + LEAN_BATCH : wend;
+      const int nb = w1 - w;
+      rvA = lane < nb * 16 ? ldg((const uint32_t*)(recs + w), (uint32_t)lane) : 0u;
+      if (NCH > 0 && f_sw) svv = lane < nb * 2 * nch ? ldg((const uint32_t*)(sws + (size_t)w * nch), (uint32_t)lane) : ~0u;
+      u = 0;
+    }
     KAD_PT(t0);
-    // this unit's hot fields → locals; issue the next unit's scalar loads
-    const uint32_t fc = f;
-    const int gvc = gv;
-    const int64_t rqc = rq_cpu, rqm = rq_mem;
-    const uint64_t tolc = tol0;
+    auto fld = [&](int d) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)rvA, (u << 4) + d); };
+    auto fld64 = [&](int d) -> int64_t { return (int64_t)(((uint64_t)fld(d + 1) << 32) | fld(d)); };
+    const uint32_t fc = fld(0);
+    const int gvc = (int)fld(1);
+    const int64_t rqc = fld64(4), rqm = fld64(6);
+    const uint64_t tolc = (uint64_t)fld64(12);
     uint64_t swc[NR];
 #pragma unroll
-    for (int ch = 0; ch < NR; ++ch) swc[ch] = swv[ch];
-    if (w + 1 < w1) {
-      const UnitRec* R = recs + w + 1;
-      f = ldc(&R->flags);
-      gv = ldc(&R->gvk);
-      rq_cpu = ldc(&R->req_cpu);
-      rq_mem = ldc(&R->req_mem);
-      tol0 = ldc(&R->tol0);
-#pragma unroll
-      for (int ch = 0; ch < NR; ++ch) swv[ch] = (NCH > 0 && f_sw) ? ldc(sws + (size_t)(w + 1) * nch + ch) : ~0ull;
+    for (int ch = 0; ch < NR; ++ch) {
+      const int l = 2 * (u * nch + ch);
+      swc[ch] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)svv, l + 1) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)svv, l);
     }
     if (fc & KAD_W_STICKY) {  // generic_scheduler.go:101-104
       lean_status(w, KAD_ST_STICKY);
@@ -825,11 +842,9 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
       lean_defer(w);
       continue;
     }
-    // cold fields of this unit (scalar; first needed after the filter)
-    const UnitRec* Rc = recs + w;
-    const int spo = ldc(&Rc->sprog_off);
-    const int64_t mc = ldc(&Rc->maxc), ooff = ldc(&Rc->out_off);
-    const uint64_t tolp0 = ldc(&Rc->tolp0);
+    const int spo = (int)fld(3);
+    const int64_t mc = fld64(8), ooff = fld64(10);
+    const uint64_t tolp0 = (uint64_t)fld64(14);
     const bool use_cur = f_taint && (fc & KAD_W_HAS_CURRENT);
     const bool fit_on = f_fit && (fc & KAD_W_FIT_NONZERO);
     uint64_t dsw = ~0ull, dcw = 0;  // dynamic-NCH path: words in lanes < nch
@@ -1459,18 +1474,34 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     // runs of consecutive units per wave: long enough to amortise the
     // register-resident cluster attributes, short enough that the grid is
     // many times the resident wave count
-    int upw = b.W / (256 * 64);
-    upw = upw < 1 ? 1 : (upw > 16 ? 16 : upw);
-    const long waves = ((long)b.W + upw - 1) / upw;
-    const int grid = (int)((waves + wpb - 1) / wpb);
-    const LeanArgs A{s, b, o, p, (int)lb, wpb, upw};
     const size_t lds = lb * wpb + (nch <= 4 ? lean_cache_bytes(s.C) : 0);
+    // one wave per resident slot: contiguous equal shares, no tail of late blocks
+    static int n_cu = 0;
+    if (n_cu == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+    }
+    int per_cu = 0;
+    hipError_t oe;
     switch (nch) {
-      case 1: launch_lean<1>(A, grid, lds, st); break;
-      case 2: launch_lean<2>(A, grid, lds, st); break;
-      case 3: launch_lean<3>(A, grid, lds, st); break;
-      case 4: launch_lean<4>(A, grid, lds, st); break;
-      default: launch_lean<0>(A, grid, lds, st); break;
+      case 1: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<1>, 64 * wpb, lds); break;
+      case 2: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<2>, 64 * wpb, lds); break;
+      case 3: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<3>, 64 * wpb, lds); break;
+      case 4: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<4>, 64 * wpb, lds); break;
+      default: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<0>, 64 * wpb, lds); break;
+    }
+    if (oe != hipSuccess || per_cu < 1) per_cu = 1;
+    if (getenv("KAD_LEAN_BLOCKS_PER_CU")) per_cu = atoi(getenv("KAD_LEAN_BLOCKS_PER_CU"));
+    long grid = (long)n_cu * per_cu;
+    const long need = ((long)b.W + wpb - 1) / wpb;  // at least one unit per wave
+    if (grid > need) grid = need;
+    const LeanArgs A{s, b, o, p, (int)lb, wpb, LEAN_BATCH};
+    switch (nch) {
+      case 1: launch_lean<1>(A, (int)grid, lds, st); break;
+      case 2: launch_lean<2>(A, (int)grid, lds, st); break;
+      case 3: launch_lean<3>(A, (int)grid, lds, st); break;
+      case 4: launch_lean<4>(A, (int)grid, lds, st); break;
+      default: launch_lean<0>(A, (int)grid, lds, st); break;
     }
     if (hipError_t e = hipGetLastError()) return e;
     // the defer list: its length is only known on the device, so the grid
