@@ -64,16 +64,23 @@ def cpu_baseline(snap, batch, fwk, C, target_s):
     t0 = time.perf_counter()
     ref.schedule(snap, batch, fwk, 0, n, threads)
     dt = time.perf_counter() - t0
-    # grow the sample to ~target_s of CPU work (bounded by the batch)
+    # grow the sample to ~target_s of CPU work: first more units (bounded by
+    # the batch), then repeated passes over them
     n2 = int(min(batch.W, max(n, n * target_s / max(dt, 1e-6))))
     if n2 > n:
         t0 = time.perf_counter()
         ref.schedule(snap, batch, fwk, 0, n2, threads)
         dt = time.perf_counter() - t0
         n = n2
-    return {"value": n * C / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} of {batch.W} units x {C} clusters, oracle/kad_ref.c (C restatement of the Go "
-                      f"reference, one unit per worker thread), {dt:.2f}s wall"}
+    reps = max(1, int(target_s / max(dt, 1e-6)))
+    if reps > 1:
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ref.schedule(snap, batch, fwk, 0, n, threads)
+        dt = time.perf_counter() - t0
+    return {"value": reps * n * C / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} pass(es) over the first {n} of {batch.W} units x {C} clusters, oracle/kad_ref.c "
+                      f"(C restatement of the Go reference, one unit per worker thread), {dt:.2f}s wall"}
 
 
 def main():

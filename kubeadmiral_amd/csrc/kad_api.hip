@@ -221,8 +221,10 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   const uint32_t* fl = at<uint32_t>(blob, h.off, KAD_B_FLAGS);
   const int64_t* des = at<int64_t>(blob, h.off, KAD_B_DESIRED);
   c->plan_rows.clear();
+  uint32_t flags_or = 0;
   for (int w = 0; w < W; w++) {
     const uint32_t f = fl[w];
+    flags_or |= f;
     if (!(f & KAD_W_DUPLICATE) && !(f & KAD_W_STICKY) && (f & KAD_W_HAS_DESIRED) && des[w] > 0) c->plan_rows.push_back(w);
   }
   if (int r = grow(c, (void**)&c->d_plan_rows, &c->plan_rows_cap, c->plan_rows.size() * 4)) return r;
@@ -275,6 +277,7 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   const char* base = static_cast<const char*>(c->d_batch);
   BatchDev& b = c->bd;
   b.W = W;
+  b.flags_or = flags_or;
   b.NT = h.n_tolsets;
   b.TW = h.n_taint_words;
   b.flags = at<uint32_t>(base, h.off, KAD_B_FLAGS);

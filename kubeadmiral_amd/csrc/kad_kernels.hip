@@ -672,7 +672,8 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
 constexpr int LEAN_QMAX_DYN = 4;
 constexpr int LEAN_BATCH = 4;  // units per work-queue batch (one VGPR of UnitRecs)
 __host__ __device__ constexpr int lean_qmax(int nch_t) { return nch_t > 0 ? nch_t : LEAN_QMAX_DYN; }
-constexpr int LEAN_CACHE_ATTRS = 8;  // alloc/used cpu & mem, NS|NE, NE, PNS, GVK word 0
+// cached attributes: alloc/used cpu & mem, NS|NE taints, GVK word 0 (always),
+// NE taints (taint filter and some unit has CurrentClusters), PNS taints (TaintToleration score)
 struct LeanLayout {
   size_t key, idx, inv, pid, posl, posr, bytes;
 };
@@ -690,8 +691,8 @@ __host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
   L.bytes = (L.posr + 2 * P + 15) & ~(size_t)15;
   return L;
 }
-// block-shared cluster cache (NCH > 0): LEAN_CACHE_ATTRS arrays of Cp i64
-__host__ __device__ inline size_t lean_cache_bytes(int C) { return (size_t)LEAN_CACHE_ATTRS * 8 * ((C + 63) & ~63); }
+// block-shared cluster cache (NCH > 0): n_attrs arrays of Cp i64
+__host__ __device__ inline size_t lean_cache_bytes(int C, int n_attrs) { return (size_t)n_attrs * 8 * ((C + 63) & ~63); }
 static constexpr int LDS_BUDGET = 64 * 1024;  // per block
 bool fast_path(int C) { return row_layout(C).bytes <= (size_t)LDS_BUDGET; }
 
@@ -701,6 +702,7 @@ struct LeanArgs {
   OutDev o;
   ProfDev p;
   int wave_bytes, waves_per_block, units_per_wave;
+  int cache_ne, cache_pn;  // optional cache arrays present
 };
 typedef const __attribute__((address_space(4))) LeanArgs* LArgs;
 __device__ __forceinline__ LArgs largs() {
@@ -765,9 +767,15 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
   int64_t* c_am = cache + 2 * Cp;
   int64_t* c_um = cache + 3 * Cp;
   uint64_t* c_ns = (uint64_t*)(cache + 4 * Cp);
-  uint64_t* c_ne = (uint64_t*)(cache + 5 * Cp);
-  uint64_t* c_pn = (uint64_t*)(cache + 6 * Cp);
-  uint64_t* c_gv = (uint64_t*)(cache + 7 * Cp);
+  uint64_t* c_gv = (uint64_t*)(cache + 5 * Cp);
+  uint64_t* c_ne = nullptr;
+  uint64_t* c_pn = nullptr;
+  {
+    LArgs a = largs();
+    int nx = 6;
+    if (a->cache_ne) c_ne = (uint64_t*)(cache + (nx++) * Cp);
+    if (a->cache_pn) c_pn = (uint64_t*)(cache + (nx++) * Cp);
+  }
   if constexpr (NCH > 0) {
     LArgs a = largs();
     for (int c = threadIdx.x; c < Cp; c += blockDim.x) {
@@ -778,9 +786,9 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
       c_am[c] = in ? ldg(a->s.alloc_mem, cl) : 0;
       c_um[c] = in ? ldg(a->s.used_mem, cl) : 0;
       c_ns[c] = in ? ldg(a->s.nsne, cl) : 0;
-      c_ne[c] = in ? ldg(a->s.ne, cl) : 0;
-      c_pn[c] = in ? ldg(a->s.pns, cl) : 0;
       c_gv[c] = in ? ldg(a->s.gvk, cl) : 0;
+      if (c_ne) c_ne[c] = in ? ldg(a->s.ne, cl) : 0;
+      if (c_pn) c_pn[c] = in ? ldg(a->s.pns, cl) : 0;
     }
     __syncthreads();
   }
@@ -1474,7 +1482,9 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     // runs of consecutive units per wave: long enough to amortise the
     // register-resident cluster attributes, short enough that the grid is
     // many times the resident wave count
-    const size_t lds = lb * wpb + (nch <= 4 ? lean_cache_bytes(s.C) : 0);
+    const int cache_ne = (p.filter_mask & (1u << KAD_PL_TAINT_TOLERATION)) && (b.flags_or & KAD_W_HAS_CURRENT);
+    const int cache_pn = (p.score_mask >> KAD_PL_TAINT_TOLERATION) & 1;
+    const size_t lds = lb * wpb + (nch <= 4 ? lean_cache_bytes(s.C, 6 + cache_ne + cache_pn) : 0);
     // one wave per resident slot: contiguous equal shares, no tail of late blocks
     static int n_cu = 0;
     if (n_cu == 0) {
@@ -1495,7 +1505,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     long grid = (long)n_cu * per_cu;
     const long need = ((long)b.W + wpb - 1) / wpb;  // at least one unit per wave
     if (grid > need) grid = need;
-    const LeanArgs A{s, b, o, p, (int)lb, wpb, LEAN_BATCH};
+    const LeanArgs A{s, b, o, p, (int)lb, wpb, LEAN_BATCH, cache_ne, cache_pn};
     switch (nch) {
       case 1: launch_lean<1>(A, (int)grid, lds, st); break;
       case 2: launch_lean<2>(A, (int)grid, lds, st); break;
