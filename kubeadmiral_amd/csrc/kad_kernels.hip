@@ -675,18 +675,17 @@ __host__ __device__ constexpr int lean_qmax(int nch_t) { return nch_t > 0 ? nch_
 // cached attributes: alloc/used cpu & mem, NS|NE taints, GVK word 0 (always),
 // NE taints (taint filter and some unit has CurrentClusters), PNS taints (TaintToleration score)
 struct LeanLayout {
-  size_t key, idx, inv, pid, posl, posr, bytes;
+  size_t key, idx, pid, posl, posr, bytes;
 };
 // per-wave region
 __host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
   const size_t Cp = (size_t)((C + 63) & ~63);
   const size_t P = (size_t)qmax * 64;  // positions held in registers
   LeanLayout L;
-  L.key = 0;                     // i64[P] replay keys
-  L.idx = L.key + 8 * P;         // u16[Cp] feasible position → cluster id
-  L.inv = L.idx + 2 * Cp;        // u16[P] replay: original position → rank
-  L.pid = L.inv + 2 * P;         // u16[P] replay: original position at each position
-  L.posl = L.pid + 2 * P;        // u16[P] replay scratch (partition stoppers)
+  L.key = 0;                     // u32[P] replay keys (total - row minimum)
+  L.idx = L.key + 4 * P;         // u16[Cp] feasible position → cluster id
+  L.pid = L.idx + 2 * Cp;        // u16[P] replay: original position at each position
+  L.posl = L.pid + 2 * P;        // u16[P] replay scratch (partition stoppers; then ranks)
   L.posr = L.posl + 2 * P;       // u16[P]
   L.bytes = (L.posr + 2 * P + 15) & ~(size_t)15;
   return L;
@@ -726,7 +725,7 @@ __device__ __forceinline__ void lean_defer(int w) {
 }
 
 template <int NCH>
-__global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
+__global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   (void)args;  // read through largs()
   constexpr int Q = lean_qmax(NCH);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -747,12 +746,12 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
   const LeanLayout L = lean_layout(C, Q);
   constexpr int P = Q * 64;
   const int Cp = nch * 64;
-  int64_t* key = (int64_t*)(region + L.key);
+  uint32_t* key = (uint32_t*)(region + L.key);
   uint16_t* idx = (uint16_t*)(region + L.idx);
-  uint16_t* inv = (uint16_t*)(region + L.inv);
   uint16_t* pid = (uint16_t*)(region + L.pid);
   uint16_t* posl = (uint16_t*)(region + L.posl);
   uint16_t* posr = (uint16_t*)(region + L.posr);
+  uint16_t* inv = posl;  // ranks after the replay
   const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
   const bool f_sw = fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER));
   const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
@@ -1033,7 +1032,8 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
           mx = t[q] > mx ? t[q] : mx;
         }
       const int64_t rmin = wave_min_u_i64(mn);
-      int64_t lo = rmin, hi = wave_max_u_i64(mx);
+      const int64_t rmax = wave_max_u_i64(mx);
+      int64_t lo = rmin, hi = rmax;
       while (lo < hi) {
         const uint64_t d = (uint64_t)hi - (uint64_t)lo;
         const int64_t mid = (int64_t)((uint64_t)lo + (d >> 1) + (d & 1));
@@ -1067,15 +1067,20 @@ __global__ __launch_bounds__(256) void schedule_lean_kernel(LeanArgs args) {
         if (n <= 12) {  // pdqsort_func: a single (stable) insertionSort
           sel[0] = gm[0] | ballot(lane < n && t[0] == lo && mbcnt(em[0]) < need);
         } else {
-          // restricted pdqsort replay, wave-parallel (kad_select.h PdqWave)
+          // restricted pdqsort replay, wave-parallel (kad_select.h PdqWave), on
+          // u32 keys t - min (order-preserving); rows spanning >= 2^32 go to schedule_kernel
+          if ((uint64_t)rmax - (uint64_t)rmin > 0xFFFFFFFFull) {
+            lean_defer(w);
+            continue;
+          }
 #pragma unroll
           for (int q = 0; q < Q; ++q)
             if (q < nq && q * 64 + lane < n) {
-              key[q * 64 + lane] = t[q];
+              key[q * 64 + lane] = (uint32_t)((uint64_t)t[q] - (uint64_t)rmin);
               pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
             }
           wave_sync();
-          PdqWave pw{key, pid, posl, posr, xs_b, xs_c};
+          PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
           pw.select(n, (int)k);
           for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
           wave_sync();

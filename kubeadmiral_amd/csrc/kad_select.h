@@ -252,12 +252,13 @@ struct PdqT {
 };
 
 // storage: LDS keys swapped in place with their original positions
-struct KeyLdsStore {
-  int64_t* key;
+template <class KeyT>
+struct KeyLdsStoreT {
+  KeyT* key;
   uint16_t* id;
   __device__ __forceinline__ bool gt(int i, int j) const { return key[i] > key[j]; }
   __device__ __forceinline__ void swap(int i, int j) const {
-    const int64_t a = key[i], b = key[j];
+    const KeyT a = key[i], b = key[j];
     const uint16_t x = id[i], y = id[j];
     key[i] = b;
     key[j] = a;
@@ -283,22 +284,27 @@ struct KeyLdsStore {
 // heapSort (only after log2(n) unbalanced partitions) falls back to lane 0.
 // key/id: the n positions' keys (swapped in place) and original positions;
 // posL/posR: u16 scratch of n entries each.
+template <class KeyT>
 struct PdqWave {
-  int64_t* key;
+  KeyT* key;
   uint16_t* id;
   uint16_t* posL;
   uint16_t* posR;
   int xs_b, xs_c;
 
-  __device__ __forceinline__ int64_t K(int p) const {
-    const int64_t v = key[p];
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
+  __device__ __forceinline__ KeyT K(int p) const {
+    const KeyT v = key[p];
+    if constexpr (sizeof(KeyT) == 8) {
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+      return (KeyT)(((uint64_t)hi << 32) | lo);
+    } else {
+      return (KeyT)__builtin_amdgcn_readfirstlane((int)v);
+    }
   }
   __device__ __forceinline__ bool less(int i, int j) const { return K(i) > K(j); }
   __device__ __forceinline__ void swap1(int i, int j) const {
-    const int64_t ki = key[i], kj = key[j];
+    const KeyT ki = key[i], kj = key[j];
     const uint16_t ii = id[i], ij = id[j];
     wave_sync();
     if (lane_id() == 0) {
@@ -311,7 +317,7 @@ struct PdqWave {
   }
   __device__ void insertion_sort(int a, int b) const {
     const int m = b - a, lane = lane_id();
-    int64_t kp = 0;
+    KeyT kp = 0;
     uint16_t ip = 0;
     if (lane < m) {
       kp = key[a + lane];
@@ -319,7 +325,7 @@ struct PdqWave {
     }
     int r = 0;
     for (int q = 0; q < m; ++q) {
-      const int64_t kq = key[a + q];
+      const KeyT kq = key[a + q];
       r += (int)(kq > kp) | (int)((kq == kp) & (q < lane));
     }
     wave_sync();
@@ -335,7 +341,7 @@ struct PdqWave {
       const int x = x0 + lane_id();
       if (x < h) {
         const int i = a + x, j = b - 1 - x;
-        const int64_t ki = key[i], kj = key[j];
+        const KeyT ki = key[i], kj = key[j];
         const uint16_t ii = id[i], ij = id[j];
         key[i] = kj;
         key[j] = ki;
@@ -402,7 +408,7 @@ struct PdqWave {
   // (Go's loop runs down to position 1, i.e. the element may reach 0)
   __device__ void shift_left(int j0) const {
     const int lane = lane_id();
-    const int64_t X = K(j0);
+    const KeyT X = K(j0);
     const uint16_t XI = (uint16_t)__builtin_amdgcn_readfirstlane((int)id[j0]);
     int m = 0;
     for (int q1 = j0; q1 > 0; q1 -= WAVE) {
@@ -416,7 +422,7 @@ struct PdqWave {
     for (int p1 = j0; p1 > m; p1 -= WAVE) {  // [m, j0) → +1, high chunks first
       const int p = p1 - 1 - lane;
       const bool in = p >= m;
-      int64_t kk = 0;
+      KeyT kk = 0;
       uint16_t ii = 0;
       if (in) {
         kk = key[p];
@@ -438,7 +444,7 @@ struct PdqWave {
   // the element at j0-1 moves right while its right neighbour is less than it
   __device__ void shift_right(int j0, int b) const {
     const int lane = lane_id();
-    const int64_t Y = K(j0 - 1);
+    const KeyT Y = K(j0 - 1);
     const uint16_t YI = (uint16_t)__builtin_amdgcn_readfirstlane((int)id[j0 - 1]);
     int mp = b - 1;
     for (int q0 = j0; q0 < b; q0 += WAVE) {
@@ -452,7 +458,7 @@ struct PdqWave {
     for (int p0 = j0; p0 <= mp; p0 += WAVE) {  // (j0-1, mp] → -1, low chunks first
       const int p = p0 + lane;
       const bool in = p <= mp;
-      int64_t kk = 0;
+      KeyT kk = 0;
       uint16_t ii = 0;
       if (in) {
         kk = key[p];
@@ -486,13 +492,13 @@ struct PdqWave {
   // Hoare pairing over [lo, hi): right stoppers R (strict ? key > P : key >= P)
   // end on the left; swaps l_t <-> r_t for the prefix of t with l_t < r_t.
   // Returns #R; *T = number of swaps.
-  __device__ int pair_partition(int lo, int hi, int64_t P, bool strict, int* T) const {
+  __device__ int pair_partition(int lo, int hi, KeyT P, bool strict, int* T) const {
     const int lane = lane_id();
     int totR = 0;
     for (int c0 = lo; c0 < hi; c0 += WAVE) {
       const int p = c0 + lane;
       const bool in = p < hi;
-      const int64_t kk = in ? key[p] : 0;
+      const KeyT kk = in ? key[p] : (KeyT)0;
       totR += popc64(ballot(in && (strict ? kk > P : kk >= P)));
     }
     const int totL = (hi - lo) - totR;
@@ -500,7 +506,7 @@ struct PdqWave {
     for (int c0 = lo; c0 < hi; c0 += WAVE) {
       const int p = c0 + lane;
       const bool in = p < hi;
-      const int64_t kk = in ? key[p] : 0;
+      const KeyT kk = in ? key[p] : (KeyT)0;
       const bool isR = in && (strict ? kk > P : kk >= P), isL = in && !isR;
       const uint64_t mR = ballot(isR), mL = ballot(isL);
       if (isL) posL[cL + mbcnt(mL)] = (uint16_t)p;
@@ -521,7 +527,7 @@ struct PdqWave {
       const int t = t0 + lane;
       if (t < t_n) {
         const int l = posL[t], r = posR[t];
-        const int64_t kl = key[l], kr = key[r];
+        const KeyT kl = key[l], kr = key[r];
         const uint16_t il = id[l], ir = id[r];
         key[l] = kr;
         key[r] = kl;
@@ -535,7 +541,7 @@ struct PdqWave {
   }
   __device__ int partition(int a, int b, int pivot, bool& already) const {
     swap1(a, pivot);
-    const int64_t P = K(a);
+    const KeyT P = K(a);
     int T;
     const int j = a + pair_partition(a + 1, b, P, true, &T);
     swap1(j, a);
@@ -544,7 +550,7 @@ struct PdqWave {
   }
   __device__ int partition_equal(int a, int b, int pivot) const {
     swap1(a, pivot);
-    const int64_t P = K(a);
+    const KeyT P = K(a);
     int T;
     return a + 1 + pair_partition(a + 1, b, P, false, &T);
   }
@@ -560,8 +566,8 @@ struct PdqWave {
       }
       if (limit == 0) {
         if (lane_id() == 0) {
-          KeyLdsStore st{key, id};
-          PdqT<KeyLdsStore> s{st, xs_b, xs_c};
+          KeyLdsStoreT<KeyT> st{key, id};
+          PdqT<KeyLdsStoreT<KeyT>> s{st, xs_b, xs_c};
           s.heap_sort(a, b);
         }
         wave_sync();
@@ -719,12 +725,12 @@ __device__ uint32_t select_topk(const SelWs& ws, int n, int64_t k, int64_t row_m
   wsync<GSCR>();
   if (GSCR) {  // global-scratch rows: serial replay (LDS-only wave primitives)
     if (lane == 0) {
-      KeyLdsStore st{ws.tot, ws.perm};
-      PdqT<KeyLdsStore> p{st, xs_b, xs_c};
+      KeyLdsStoreT<int64_t> st{ws.tot, ws.perm};
+      PdqT<KeyLdsStoreT<int64_t>> p{st, xs_b, xs_c};
       p.select(n, (int)k);
     }
   } else {
-    PdqWave pw{ws.tot, ws.perm, ws.posl, ws.posr, xs_b, xs_c};
+    PdqWave<int64_t> pw{ws.tot, ws.perm, ws.posl, ws.posr, xs_b, xs_c};
     pw.select(n, (int)k);
   }
   wsync<GSCR>();
