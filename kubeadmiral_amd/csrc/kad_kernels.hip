@@ -894,18 +894,20 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         sw0 = readlane64(dsw, ch);
         cw0 = readlane64(dcw, ch);
       }
-      bool ok = c < C;
-      if (f_sw) ok &= (sw0 >> lane) & 1;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
-      if (f_taint) {  // taint_toleration.go:50-77: NoSchedule|NoExecute, only NoExecute once scheduled there
-        const uint64_t x = (use_cur && ((cw0 >> lane) & 1)) ? ne0 : ns0;
-        ok &= (x & ~tolc) == 0;
-      }
-      if (f_api) ok &= gvc >= 0 && ((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
-      if (fit_on)  // clusterresources/fit.go:73-134
-        ok &= (int)(acpu >= wadd(rqc, ucpu)) & (int)(amem >= wadd(rqm, umem));
-      const uint64_t m = ballot(ok);
+      // each filter as a lane mask (v_cmp → SGPR pair), combined with scalar
+      // ANDs under uniform selects (no branches inside the unrolled loop)
+      const int rem = C - ch * WAVE;
+      uint64_t m = rem >= WAVE ? ~0ull : ((1ull << rem) - 1);
+      const uint64_t x = (use_cur && ((cw0 >> lane) & 1)) ? ne0 : ns0;
+      const uint64_t m_taint = ballot((x & ~tolc) == 0);      // taint_toleration.go:50-77
+      const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
+      const uint64_t m_fit = ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));  // fit.go:73-134
+      m &= f_sw ? sw0 : ~0ull;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
+      m &= f_taint ? m_taint : ~0ull;
+      m &= f_api ? (gvc >= 0 ? m_api : 0ull) : ~0ull;
+      m &= fit_on ? m_fit : ~0ull;
       (void)pn0;
-      if (ok) idx[n + mbcnt(m)] = (uint16_t)c;
+      if ((m >> lane) & 1) idx[n + mbcnt(m)] = (uint16_t)c;
       n += popc64(m);
     }
     KAD_PT(t1);
@@ -1023,36 +1025,68 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) sel[q] = ballot(q * 64 + lane < n);
     } else if (k > 0) {
-      // k-th largest total: the largest T with #(total >= T) >= k
+      // lanes holding a total, per position chunk
+      uint64_t vm[Q];
       int64_t mn = I64_MAX, mx = I64_MIN;
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (q < nq && q * 64 + lane < n) {
+      for (int q = 0; q < Q; ++q) {
+        const int r = n - q * 64;
+        vm[q] = q < nq ? (r >= 64 ? ~0ull : ((1ull << r) - 1)) : 0ull;
+        if ((vm[q] >> lane) & 1) {
           mn = t[q] < mn ? t[q] : mn;
           mx = t[q] > mx ? t[q] : mx;
         }
-      const int64_t rmin = wave_min_u_i64(mn);
-      const int64_t rmax = wave_max_u_i64(mx);
-      int64_t lo = rmin, hi = rmax;
-      while (lo < hi) {
-        const uint64_t d = (uint64_t)hi - (uint64_t)lo;
-        const int64_t mid = (int64_t)((uint64_t)lo + (d >> 1) + (d & 1));
-        int64_t cnt = 0;
+      }
+      // k-th largest total T: the largest T with #(total >= T) >= k, by
+      // bisection over [min, max] — in 32 bits when every total fits (the
+      // usual case: totals are sums of 0..100 plugin scores)
+      const bool hv = lane < n;
+      int64_t rmin, rmax, lo;
+      if (!ballot(hv && (mn < INT32_MIN || mx > INT32_MAX))) {
+        const int mn32 = wave_min_u_i32(hv ? (int)mn : INT32_MAX), mx32 = wave_max_u_i32(hv ? (int)mx : INT32_MIN);
+        int t32[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if (q < nq) cnt += popc64(ballot(q * 64 + lane < n && t[q] >= mid));
-        if (cnt >= k)
-          lo = mid;
-        else
-          hi = (int64_t)((uint64_t)mid - 1);
+        for (int q = 0; q < Q; ++q) t32[q] = (int)t[q];
+        int lo32 = mn32, hi32 = mx32;
+        while (lo32 < hi32) {
+          const uint32_t d = (uint32_t)hi32 - (uint32_t)lo32;
+          const int mid = (int)((uint32_t)lo32 + (d >> 1) + (d & 1));
+          int cnt = 0;
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (q < nq) cnt += popc64(ballot(t32[q] >= mid) & vm[q]);
+          if (cnt >= k)
+            lo32 = mid;
+          else
+            hi32 = mid - 1;
+        }
+        rmin = mn32;
+        rmax = mx32;
+        lo = lo32;
+      } else {
+        rmin = wave_min_u_i64(mn);
+        rmax = wave_max_u_i64(mx);
+        lo = rmin;
+        int64_t hi = rmax;
+        while (lo < hi) {
+          const uint64_t d = (uint64_t)hi - (uint64_t)lo;
+          const int64_t mid = (int64_t)((uint64_t)lo + (d >> 1) + (d & 1));
+          int64_t cnt = 0;
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (q < nq) cnt += popc64(ballot(t[q] >= mid) & vm[q]);
+          if (cnt >= k)
+            lo = mid;
+          else
+            hi = (int64_t)((uint64_t)mid - 1);
+        }
       }
       uint64_t gm[Q], em[Q];
       int64_t g = 0, e = 0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        const bool v = q < nq && q * 64 + lane < n;
-        gm[q] = ballot(v && t[q] > lo);
-        em[q] = ballot(v && t[q] == lo);
+        gm[q] = ballot(t[q] > lo) & vm[q];
+        em[q] = ballot(t[q] == lo) & vm[q];
         g += popc64(gm[q]);
         e += popc64(em[q]);
       }
