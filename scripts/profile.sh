@@ -18,4 +18,6 @@ run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD 
 run sq2 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
-python scripts/pmc_summary.py "$out" "$cfg" > "$out/summary.txt"; cat "$out/summary.txt"
+read W C < <(python -c "from kubeadmiral_amd import synth; print(*synth.SIZES['$cfg'])")
+python scripts/pmc_summary.py "$out" "$cfg" --units "$W" --clusters "$C" --json "$out/pmc_$cfg.json" > "$out/summary.txt"
+cat "$out/summary.txt" | tail -30
