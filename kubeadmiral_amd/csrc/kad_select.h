@@ -365,16 +365,48 @@ struct PdqWave {
     order2(a, b, swaps);
     return b;
   }
+  // choosePivot with the candidate keys gathered by one LDS read across lanes
+  // (lane x reads position x of the candidate list), medians on scalars.
   __device__ int choose_pivot(int a, int b, int& hint) const {
-    int l = b - a, swaps = 0;
+    const int lane = lane_id();
+    const int l = b - a;
     int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    int swaps = 0;
     if (l >= 8) {
-      if (l >= 50) {
-        i = median(i - 1, i, i + 1, swaps);
-        j = median(j - 1, j, j + 1, swaps);
-        k = median(k - 1, k, k + 1, swaps);
+      // candidates: l >= 50: i-1,i,i+1, j-1,j,j+1, k-1,k,k+1 ; else i, j, k
+      const bool adj = l >= 50;
+      const int g = adj ? lane / 3 : lane, d = adj ? lane % 3 - 1 : 0;
+      const int base = g == 0 ? i : (g == 1 ? j : k);
+      const KeyT v = key[lane < (adj ? 9 : 3) ? base + d : a];
+      auto kv = [&](int x) -> KeyT {
+        if constexpr (sizeof(KeyT) == 8) {
+          const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, x);
+          const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), x);
+          return (KeyT)(((uint64_t)hi << 32) | lo);
+        } else {
+          return (KeyT)__builtin_amdgcn_readlane((int)v, x);
+        }
+      };
+      // (position, key) triples; order2/median exactly as Go's (less = key greater)
+      auto med = [&](int pa, KeyT ka, int pb, KeyT kb, int pc, KeyT kc, KeyT& km) -> int {
+        if (kb > ka) { int tp = pa; pa = pb; pb = tp; KeyT tk = ka; ka = kb; kb = tk; swaps++; }
+        if (kc > kb) { int tp = pb; pb = pc; pc = tp; KeyT tk = kb; kb = kc; kc = tk; swaps++; }
+        if (kb > ka) { int tp = pa; pa = pb; pb = tp; KeyT tk = ka; ka = kb; kb = tk; swaps++; }
+        km = kb;
+        return pb;
+      };
+      KeyT ki, kj, kk;
+      if (adj) {
+        i = med(i - 1, kv(0), i, kv(1), i + 1, kv(2), ki);
+        j = med(j - 1, kv(3), j, kv(4), j + 1, kv(5), kj);
+        k = med(k - 1, kv(6), k, kv(7), k + 1, kv(8), kk);
+      } else {
+        ki = kv(0);
+        kj = kv(1);
+        kk = kv(2);
       }
-      j = median(i, j, k, swaps);
+      KeyT km;
+      j = med(i, ki, j, kj, k, kk, km);
     }
     hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
     return j;
@@ -491,17 +523,11 @@ struct PdqWave {
   }
   // Hoare pairing over [lo, hi): right stoppers R (strict ? key > P : key >= P)
   // end on the left; swaps l_t <-> r_t for the prefix of t with l_t < r_t.
+  // One pass ranks and scatters both stopper kinds (L from the left, R from
+  // the left too: r_t = posR[#R - 1 - t]); a second swaps every valid pair.
   // Returns #R; *T = number of swaps.
   __device__ int pair_partition(int lo, int hi, KeyT P, bool strict, int* T) const {
     const int lane = lane_id();
-    int totR = 0;
-    for (int c0 = lo; c0 < hi; c0 += WAVE) {
-      const int p = c0 + lane;
-      const bool in = p < hi;
-      const KeyT kk = in ? key[p] : (KeyT)0;
-      totR += popc64(ballot(in && (strict ? kk > P : kk >= P)));
-    }
-    const int totL = (hi - lo) - totR;
     int cL = 0, cR = 0;
     for (int c0 = lo; c0 < hi; c0 += WAVE) {
       const int p = c0 + lane;
@@ -510,23 +536,24 @@ struct PdqWave {
       const bool isR = in && (strict ? kk > P : kk >= P), isL = in && !isR;
       const uint64_t mR = ballot(isR), mL = ballot(isL);
       if (isL) posL[cL + mbcnt(mL)] = (uint16_t)p;
-      if (isR) posR[totR - 1 - (cR + mbcnt(mR))] = (uint16_t)p;
+      if (isR) posR[cR + mbcnt(mR)] = (uint16_t)p;
       cL += popc64(mL);
       cR += popc64(mR);
     }
     wave_sync();
-    const int np = totL < totR ? totL : totR;
+    const int np = cL < cR ? cL : cR;
     int t_n = 0;
     for (int t0 = 0; t0 < np; t0 += WAVE) {
       const int t = t0 + lane;
-      const uint64_t m = ballot(t < np && posL[t] < posR[t]);
+      int l = 0, r = 0;
+      if (t < np) {
+        l = posL[t];
+        r = posR[cR - 1 - t];
+      }
+      const bool sw = t < np && l < r;
+      const uint64_t m = ballot(sw);
       t_n += popc64(m);
-      if (~m) break;  // a prefix: once a t fails, every later t fails
-    }
-    for (int t0 = 0; t0 < t_n; t0 += WAVE) {
-      const int t = t0 + lane;
-      if (t < t_n) {
-        const int l = posL[t], r = posR[t];
+      if (sw) {  // pairs are disjoint: every valid pair swaps at once
         const KeyT kl = key[l], kr = key[r];
         const uint16_t il = id[l], ir = id[r];
         key[l] = kr;
@@ -534,10 +561,11 @@ struct PdqWave {
         id[l] = ir;
         id[r] = il;
       }
+      if (~m) break;  // a prefix: once a t fails, every later t fails
     }
     wave_sync();
     *T = t_n;
-    return totR;
+    return cR;
   }
   __device__ int partition(int a, int b, int pivot, bool& already) const {
     swap1(a, pivot);
