@@ -205,19 +205,30 @@ __device__ int64_t affinity_score(const uint64_t* rows, const int32_t* p, int nc
   return score;
 }
 
-// least_allocated.go:88-94 / most_allocated.go:90-97
-__device__ __forceinline__ int64_t least_requested(int64_t req, int64_t cap) {
+// least_allocated.go:88-94 / most_allocated.go:90-97:
+//   capacity == 0 || requested > capacity ? 0 : (x * 100) / capacity
+// with x = capacity - requested (least) or requested (most). Fast path for
+// 0 <= requested <= capacity < 2^46 (every real cluster): x*100 < 2^53 and the
+// quotient is in [0, 100], so an f64 reciprocal estimate corrected twice with
+// exact f64 products gives the exact integer quotient; anything else takes the
+// Go-wrapping int64 path.
+__device__ __forceinline__ int64_t alloc_score(int64_t req, int64_t cap, bool most) {
   if (cap == 0 || req > cap) return 0;
-  const int64_t num = wmul(wsub(cap, req), 100);
-  if (cap > 0 && req >= 0 && num >= 0) return small_quot(num, cap);
+  if (cap > 0 && req >= 0 && cap < (1ll << 46)) {
+    const double cd = (double)cap;
+    const double ad = (double)(most ? req : cap - req) * 100.0;  // exact
+    int q = (int)(ad * __builtin_amdgcn_rcp(cd));
+    double r = ad - (double)q * cd;  // exact: q * cd < 2^53
+    q += (r >= cd) - (r < 0.0);
+    r = ad - (double)q * cd;
+    q += (r >= cd) - (r < 0.0);
+    return q;
+  }
+  const int64_t num = wmul(most ? req : wsub(cap, req), 100);
   return go_div(num, cap);
 }
-__device__ __forceinline__ int64_t most_requested(int64_t req, int64_t cap) {
-  if (cap == 0 || req > cap) return 0;
-  const int64_t num = wmul(req, 100);
-  if (cap > 0 && req >= 0 && num >= 0) return small_quot(num, cap);
-  return go_div(num, cap);
-}
+__device__ __forceinline__ int64_t least_requested(int64_t req, int64_t cap) { return alloc_score(req, cap, false); }
+__device__ __forceinline__ int64_t most_requested(int64_t req, int64_t cap) { return alloc_score(req, cap, true); }
 // balanced_allocation.go:45-88 — IEEE float64, no contraction (-ffp-contract=off)
 __device__ __forceinline__ int64_t balanced(int64_t rc, int64_t cc, int64_t rm, int64_t cm) {
   const double cf = cc == 0 ? 1.0 : (double)rc / (double)cc;
@@ -863,6 +874,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 
     // ---------------- filters → compacted feasible list (findClustersThatFitWorkload, :152-169)
     int n = 0;
+    uint64_t mk[NR];
     const int NC = NCH > 0 ? NCH : nch;
 #pragma unroll
     for (int ch = 0; ch < NC; ++ch) {
@@ -907,8 +919,19 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       m &= f_api ? (gvc >= 0 ? m_api : 0ull) : ~0ull;
       m &= fit_on ? m_fit : ~0ull;
       (void)pn0;
-      if ((m >> lane) & 1) idx[n + mbcnt(m)] = (uint16_t)c;
-      n += popc64(m);
+      if constexpr (NCH > 0) {
+        mk[ch] = m;  // compaction after every chunk's mask: no LDS store between the cache reads
+      } else {
+        if ((m >> lane) & 1) idx[n + mbcnt(m)] = (uint16_t)c;
+        n += popc64(m);
+      }
+    }
+    if constexpr (NCH > 0) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        if ((mk[ch] >> lane) & 1) idx[n + mbcnt(mk[ch])] = (uint16_t)(ch * WAVE + lane);
+        n += popc64(mk[ch]);
+      }
     }
     KAD_PT(t1);
     KAD_PADD(0, t1 - t0);
