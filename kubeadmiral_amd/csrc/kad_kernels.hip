@@ -1066,22 +1066,34 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       const bool hv = lane < n;
       int64_t rmin, rmax, lo;
       if (!ballot(hv && (mn < INT32_MIN || mx > INT32_MAX))) {
-        const int mn32 = wave_min_u_i32(hv ? (int)mn : INT32_MAX), mx32 = wave_max_u_i32(hv ? (int)mx : INT32_MIN);
+        int mn32, mx32;
+        wave_minmax_u_i32(hv ? (int)mn : INT32_MAX, hv ? (int)mx : INT32_MIN, mn32, mx32);
         int t32[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) t32[q] = (int)t[q];
         int lo32 = mn32, hi32 = mx32;
-        while (lo32 < hi32) {
-          const uint32_t d = (uint32_t)hi32 - (uint32_t)lo32;
-          const int mid = (int)((uint32_t)lo32 + (d >> 1) + (d & 1));
-          int cnt = 0;
+        if (nq == 1) {  // one position per lane: one ballot per step
+          while (lo32 < hi32) {
+            const uint32_t d = (uint32_t)hi32 - (uint32_t)lo32;
+            const int mid = (int)((uint32_t)lo32 + (d >> 1) + (d & 1));
+            if (popc64(ballot(t32[0] >= mid) & vm[0]) >= k)
+              lo32 = mid;
+            else
+              hi32 = mid - 1;
+          }
+        } else {
+          while (lo32 < hi32) {
+            const uint32_t d = (uint32_t)hi32 - (uint32_t)lo32;
+            const int mid = (int)((uint32_t)lo32 + (d >> 1) + (d & 1));
+            int cnt = 0;
 #pragma unroll
-          for (int q = 0; q < Q; ++q)
-            if (q < nq) cnt += popc64(ballot(t32[q] >= mid) & vm[q]);
-          if (cnt >= k)
-            lo32 = mid;
-          else
-            hi32 = mid - 1;
+            for (int q = 0; q < Q; ++q)
+              if (q < nq) cnt += popc64(ballot(t32[q] >= mid) & vm[q]);
+            if (cnt >= k)
+              lo32 = mid;
+            else
+              hi32 = mid - 1;
+          }
         }
         rmin = mn32;
         rmax = mx32;

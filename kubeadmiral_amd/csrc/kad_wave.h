@@ -108,6 +108,25 @@ __device__ __forceinline__ int wave_min_u_i32(int v) { KAD_DPP_STEPS(imin_, INT3
 __device__ __forceinline__ int wave_sum_u_i32(int v) { KAD_DPP_STEPS(iadd_, 0); }
 #undef KAD_DPP_STEPS
 
+// min and max of one value together: the two DPP chains interleave, so each
+// fills the other's DPP read-after-write wait states
+__device__ __forceinline__ void wave_minmax_u_i32(int vmin, int vmax, int& rmin, int& rmax) {
+  vmin = imin_(vmin, dpp32<0x111, 0xf>(INT32_MAX, vmin));
+  vmax = imax_(vmax, dpp32<0x111, 0xf>(INT32_MIN, vmax));
+  vmin = imin_(vmin, dpp32<0x112, 0xf>(INT32_MAX, vmin));
+  vmax = imax_(vmax, dpp32<0x112, 0xf>(INT32_MIN, vmax));
+  vmin = imin_(vmin, dpp32<0x114, 0xf>(INT32_MAX, vmin));
+  vmax = imax_(vmax, dpp32<0x114, 0xf>(INT32_MIN, vmax));
+  vmin = imin_(vmin, dpp32<0x118, 0xf>(INT32_MAX, vmin));
+  vmax = imax_(vmax, dpp32<0x118, 0xf>(INT32_MIN, vmax));
+  vmin = imin_(vmin, dpp32<0x142, 0xa>(INT32_MAX, vmin));
+  vmax = imax_(vmax, dpp32<0x142, 0xa>(INT32_MIN, vmax));
+  vmin = imin_(vmin, dpp32<0x143, 0xc>(INT32_MAX, vmin));
+  vmax = imax_(vmax, dpp32<0x143, 0xc>(INT32_MIN, vmax));
+  rmin = __builtin_amdgcn_readlane(vmin, 63);
+  rmax = __builtin_amdgcn_readlane(vmax, 63);
+}
+
 // 64-bit max / min: reduce the high words, then the low words of the lanes
 // holding the winning high word (unsigned), all wave-uniform results.
 __device__ __forceinline__ int64_t wave_max_u_i64(int64_t v) {
