@@ -212,3 +212,61 @@ def test_tie_heavy_selection_rows(ctx):
     for (st, sel), w in zip(got, want):
         assert st == pack.ST_OK
         assert set(sel) == w
+
+
+# ------------------------------------------------------- extreme values
+def _extreme_batch(seed, C=200, W=120):
+    """Fuzz batch pushed to the edges of the lean kernel's fast paths: capacities
+    above 2^46 (Least/MostAllocated's exact int64 path), zero and negative
+    quantities, and preferred-affinity weights of +-2^31 so totals span more
+    than 2^32 (64-bit bisection; wide-key straddles go to the full kernel)."""
+    rng = np.random.default_rng(seed)
+    clusters, units = synth.gen_fuzz(seed, W=W, C=C)
+    for c in clusters:
+        r = rng.random()
+        if r < 0.25:
+            c.allocatable["memory"] = str(int(rng.integers(1 << 46, 1 << 52)))
+            c.available["memory"] = str(int(rng.integers(0, 1 << 46)))
+        elif r < 0.35:
+            c.allocatable["cpu"] = "0"
+            c.available["cpu"] = "0"
+        elif r < 0.45:
+            c.allocatable["cpu"] = f"{int(rng.integers(1, 1 << 40))}m"
+            c.available["cpu"] = "1m"
+    for su in units:
+        ca = su.affinity.cluster_affinity if su.affinity is not None else None
+        if ca is not None and ca.preferred:
+            for p in ca.preferred:
+                if rng.random() < 0.5:
+                    p.weight = int(rng.choice([-(1 << 31), (1 << 31) - 1, -123456789, 987654321]))
+    return clusters, units
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_extreme_values_gpu_equals_c_oracle(ctx, seed):
+    clusters, units = _extreme_batch(500 + seed)
+    fwk = F.Framework(F.default_enabled_plugins()) if seed % 2 == 0 else synth.fuzz_framework(seed)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), f"extreme seed {seed}")
+
+
+def test_ties_straddle_many_feasible(ctx):
+    """C = 256 with identical clusters: every total ties, MaxCluster cuts inside the
+    tie run on every unit (wave-parallel pdqsort replay over up to 256 positions)."""
+    rng = np.random.default_rng(9)
+    clusters = synth.gen_clusters(rng, 256, n_taints=0)
+    for c in clusters:
+        c.allocatable = {"cpu": "64", "memory": "256Gi"}
+        c.available = {"cpu": str(int(rng.integers(30, 34))), "memory": "128Gi"}
+        c.labels = {"key0": "val0"}
+    units = synth.gen_units_c2(np.random.default_rng(10), 300)
+    for su in units:
+        su.affinity = None
+        su.cluster_selector = None
+        su.tolerations = None
+        su.resource_request = T.Resource(int(rng.integers(0, 100)), int(rng.integers(0, 1 << 30)))
+        su.max_clusters = int(rng.integers(1, 250))
+    fwk = synth.profile_for("c2")
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert (res.flags & 1).mean() > 0.5  # most rows straddle
+    assert_same(res, c_oracle(snap, batch, fwk), "tie-heavy 256")
