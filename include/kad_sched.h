@@ -326,8 +326,8 @@ int kad_plan_rows(kad_ctx* ctx, int n_rows, const int32_t* row_off, const uint32
  * kad_schedule (feasible: u8[W*C]; total: i64[W*C], meaningful where feasible). */
 int kad_debug_scores(kad_ctx* ctx, const kad_profile* profile, uint8_t* feasible, int64_t* total);
 
-/* Profiling builds only (-DKAD_PHASE_PROF): copy 16 per-phase cycle / event
- * counters of schedule_kernel to out (and zero them if reset). Returns 16, or
+/* Profiling builds only (-DKAD_PHASE_PROF): copy 32 per-phase cycle / event
+ * counters of the kernels to out (and zero them if reset). Returns 32, or
  * 0 in product builds (no counters compiled in). Not part of the reference. */
 int kad_debug_phase_counters(uint64_t* out, int reset);
 

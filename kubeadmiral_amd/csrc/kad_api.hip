@@ -50,6 +50,8 @@ struct kad_ctx {
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   bool have_snapshot = false, have_batch = false, ran = false;
+  bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
+  bool batch_defer = false;    // some unit uses a feature the lean kernel defers
 };
 
 static int fail(kad_ctx* c, int code, const std::string& msg) {
@@ -176,6 +178,11 @@ int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->snap_hdr = h;
   if (int r = bind_snapshot(c, h)) return r;
+  c->snap_negative = false;
+  for (int a : {KAD_S_ALLOC_CPU, KAD_S_ALLOC_MEM, KAD_S_USED_CPU, KAD_S_USED_MEM}) {
+    const int64_t* v = at<int64_t>(blob, h.off, a);
+    for (int i = 0; i < h.n_clusters; i++) c->snap_negative |= v[i] < 0 || v[i] >= (1ll << 46);
+  }
   c->have_snapshot = true;
   c->have_batch = false;
   return KAD_OK;
@@ -193,6 +200,15 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->snap_hdr = h;
   if (int r = bind_snapshot(c, h)) return r;
+  c->snap_negative = false;
+  {
+    std::vector<int64_t> v((size_t)h.n_clusters);
+    for (int a : {KAD_S_ALLOC_CPU, KAD_S_ALLOC_MEM, KAD_S_USED_CPU, KAD_S_USED_MEM}) {
+      if (h.n_clusters)
+        HIPCHK(c, hipMemcpy(v.data(), static_cast<const char*>(dev_blob) + h.off[a], v.size() * 8, hipMemcpyDeviceToHost));
+      for (int64_t x : v) c->snap_negative |= x < 0 || x >= (1ll << 46);
+    }
+  }
   c->have_snapshot = true;
   c->have_batch = false;
   return KAD_OK;
@@ -222,6 +238,20 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   const int64_t* des = at<int64_t>(blob, h.off, KAD_B_DESIRED);
   c->plan_rows.clear();
   uint32_t flags_or = 0;
+  // units the lean kernel would defer whatever the profile (prep_kernel's
+  // REC_FULL reasons; wide affinity weights or negative requests can give
+  // totals spanning >= 2^32)
+  bool defer = false;
+  {
+    const int32_t* gv = at<int32_t>(blob, h.off, KAD_B_GVK);
+    const int32_t* so = at<int32_t>(blob, h.off, KAD_B_SREQ_OFF);
+    const int64_t* rc = at<int64_t>(blob, h.off, KAD_B_REQ_CPU);
+    const int64_t* rm = at<int64_t>(blob, h.off, KAD_B_REQ_MEM);
+    for (int w = 0; w < W && !defer; w++)
+      defer = gv[w] >= 64 || so[w] < so[w + 1] || rc[w] < 0 || rm[w] < 0 || rc[w] >= (1ll << 46) ||
+              rm[w] >= (1ll << 46) || (fl[w] & KAD_W_WIDE_SCORES);
+  }
+  c->batch_defer = defer;
   for (int w = 0; w < W; w++) {
     const uint32_t f = fl[w];
     flags_or |= f;
@@ -365,6 +395,7 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   o.dbg_total = dbg_total;
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
+  c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total;
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream));

@@ -21,6 +21,7 @@ struct SnapDev {
 struct BatchDev {
   int W, NT, TW;
   uint32_t flags_or;        // OR of every unit's KAD_W_* flags (host, at upload)
+  int may_defer;            // host: some unit may reach the lean kernel's defer list (else that pass is skipped)
   const uint32_t* flags;
   const int32_t *gvk, *tolset;
   const int64_t *req_cpu, *req_mem, *desired, *maxc;

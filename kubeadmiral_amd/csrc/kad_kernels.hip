@@ -26,19 +26,24 @@ namespace kad {
 // Accumulated per wave in registers, flushed once at wave exit into one of
 // 256 stripes (a shared counter per phase would serialise the waves).
 #ifdef KAD_PHASE_PROF
-__device__ unsigned long long g_phase[256 * 16];
+__device__ unsigned long long g_phase[256 * 32];
 #define KAD_PT(v) const unsigned long long v = __builtin_readcyclecounter()
 #define KAD_PACC uint32_t pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
 #define KAD_PFLUSH                                                                       \
   if (lane_id() == 0)                                                                    \
-    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 16 + i_], pacc[i_])
+    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + i_], pacc[i_])
 // lean kernel: its own slots 10..15 (A, B, D, E, straddles, D on straddles)
 #define KAD_PFLUSH_LEAN                                                                  \
   if (lane_id() == 0)                                                                    \
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 16 + 10 + i_], pacc[i_])
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 10 + i_], pacc[i_])
+// plan kernel: slots 16..23 (setup, dynamic weights, first plan, avoid-disruption, output, units)
+#define KAD_PFLUSH_PLAN                                                                  \
+  if (lane_id() == 0)                                                                    \
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 16 + i_], pacc[i_])
 #else
 #define KAD_PFLUSH_LEAN
+#define KAD_PFLUSH_PLAN
 #define KAD_PT(v)
 #define KAD_PACC
 #define KAD_PADD(i, x)
@@ -876,6 +881,21 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     int n = 0;
     uint64_t mk[NR];
     const int NC = NCH > 0 ? NCH : nch;
+    // NCH == 0 (no LDS cache): the attributes of chunk ch+1 are loaded while
+    // chunk ch is filtered (software pipeline; one exposed round trip per unit)
+    int64_t p_ac = 0, p_uc = 0, p_am = 0, p_um = 0;
+    uint64_t p_ns = 0, p_ne = 0, p_gv = 0;
+    if constexpr (NCH == 0) {
+      LArgs a = largs();
+      const uint32_t cl = lane < C ? (uint32_t)lane : 0u;
+      p_ac = ldg(a->s.alloc_cpu, cl);
+      p_uc = ldg(a->s.used_cpu, cl);
+      p_am = ldg(a->s.alloc_mem, cl);
+      p_um = ldg(a->s.used_mem, cl);
+      p_ns = ldg(a->s.nsne, cl);
+      p_ne = ldg(a->s.ne, cl);
+      p_gv = ldg(a->s.gvk, cl);
+    }
 #pragma unroll
     for (int ch = 0; ch < NC; ++ch) {
       const int c = ch * WAVE + lane;
@@ -893,16 +913,26 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         sw0 = swc[ch];
         cw0 = use_cur ? ldc(largs()->b.cw + (size_t)w * nch + ch) : 0ull;
       } else {
-        LArgs a = largs();
-        const uint32_t cl = c < C ? (uint32_t)c : 0u;
-        acpu = ldg(a->s.alloc_cpu, cl);
-        ucpu = ldg(a->s.used_cpu, cl);
-        amem = ldg(a->s.alloc_mem, cl);
-        umem = ldg(a->s.used_mem, cl);
-        ns0 = ldg(a->s.nsne, cl);
-        ne0 = ldg(a->s.ne, cl);
+        acpu = p_ac;
+        ucpu = p_uc;
+        amem = p_am;
+        umem = p_um;
+        ns0 = p_ns;
+        ne0 = p_ne;
+        gv0 = p_gv;
         pn0 = 0;
-        gv0 = ldg(a->s.gvk, cl);
+        if (ch + 1 < NC) {
+          LArgs a = largs();
+          const int cn = c + WAVE;
+          const uint32_t cl = cn < C ? (uint32_t)cn : 0u;
+          p_ac = ldg(a->s.alloc_cpu, cl);
+          p_uc = ldg(a->s.used_cpu, cl);
+          p_am = ldg(a->s.alloc_mem, cl);
+          p_um = ldg(a->s.used_mem, cl);
+          p_ns = ldg(a->s.nsne, cl);
+          p_ne = ldg(a->s.ne, cl);
+          p_gv = ldg(a->s.gvk, cl);
+        }
         sw0 = readlane64(dsw, ch);
         cw0 = readlane64(dcw, ch);
       }
@@ -1282,12 +1312,24 @@ __device__ __forceinline__ int find_sorted(const int32_t* a, int lo, int hi, int
 
 template <bool GSCR>
 __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev o, const int32_t* rows, int n_rows,
-                                                  int kmax, char* gscratch, int wave_bytes, int r_stride) {
+                                                  int kmax, char* gscratch, int wave_bytes, int r_stride, int tbl_cp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   const int gw = blockIdx.x;
   char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem;
+  // cluster id → (preference / current-cluster index + 1) lookup tables in LDS
+  // (tbl_cp > 0), set and cleared per unit: replaces two binary searches in
+  // global memory per selected cluster
+  uint16_t* tbl_p = (uint16_t*)(smem + plan_layout(kmax).bytes);
+  uint16_t* tbl_c = tbl_p + tbl_cp;
+  const bool use_tbl = !GSCR && tbl_cp > 0;
+  if (use_tbl) {
+    for (int i = lane; i < 2 * tbl_cp; i += WAVE) tbl_p[i] = 0;
+    wsync<GSCR>();
+  }
+  KAD_PACC;
   for (int r = gw; r < n_rows; r += r_stride) {
+    KAD_PT(t0);
     const int w = rows[r];
     if (o.status[w] != KAD_ST_OK) continue;
     const int K = o.count[w];
@@ -1301,35 +1343,71 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
     const int klen = b.key_off[w + 1] - b.key_off[w];
     const int64_t total = (f & KAD_W_HAS_DESIRED) ? b.desired[w] : 0;
     // preferences (rsp.go:99-126)
-    for (int i = lane; i < K; i += WAVE) {
-      const int c = o.cluster[off + i];
-      ws.cid[i] = c;
-      ws.hash[i] = fnv_cont(s.name_fnv[c], key, klen);
-      const int pi = find_sorted(b.pref_id, p0, p1, c);
-      uint32_t fl = 0;
-      int64_t wt = 0, mn = 0, mx = 0, cp = 0;
-      if (pi >= 0) {
-        const uint32_t pf = b.pref_fl[pi];
-        if (pf & KAD_PREF_HAS_WEIGHT) wt = b.pref_w[pi];
-        mn = b.pref_min[pi];
-        if (pf & KAD_PREF_HAS_MAX) {
-          fl |= EF_HAS_MAX;
-          mx = b.pref_max[pi];
-        }
-        if (pf & KAD_PREF_HAS_CAP) {
-          fl |= EF_HAS_CAP;
-          cp = b.pref_cap[pi];
+    if (use_tbl) {
+      for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = (uint16_t)(j - p0 + 1);
+      for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = (uint16_t)(j - c0 + 1);
+      wsync<GSCR>();
+    }
+    // su.Key() bytes in lanes (uniform): the FNV-1 continuation of every element
+    // reads them with v_readlane instead of one dependent load per byte
+    const uint32_t kb0 = lane < klen ? (uint32_t)key[lane] : 0u;
+    for (int i0 = 0; i0 < K; i0 += WAVE) {
+      const int i = i0 + lane;
+      const bool v = i < K;
+      const int c = v ? o.cluster[off + i] : 0;
+      uint32_t h = s.name_fnv[c];
+      for (int k0 = 0; k0 < klen; k0 += WAVE) {
+        const uint32_t kb = k0 == 0 ? kb0 : (k0 + lane < klen ? (uint32_t)key[k0 + lane] : 0u);
+        const int m = klen - k0 < WAVE ? klen - k0 : WAVE;
+        for (int q = 0; q < m; ++q) {
+          h *= 16777619u;
+          h ^= (uint32_t)__builtin_amdgcn_readlane((int)kb, q);
         }
       }
-      ws.w[i] = wt;
-      ws.mn[i] = mn;
-      ws.mx[i] = mx;
-      ws.cap[i] = cp;
-      ws.fl[i] = fl;
-      const int ci = find_sorted(b.cur_id, c0, c1, c);
-      ws.cur[i] = ci >= 0 ? b.cur_rep[ci] : 0;
+      if (v) {
+        ws.cid[i] = c;
+        ws.hash[i] = h;
+        int pi, ci;
+        if (use_tbl) {
+          const int tp = tbl_p[c], tc = tbl_c[c];
+          pi = tp ? p0 + tp - 1 : -1;
+          ci = tc ? c0 + tc - 1 : -1;
+        } else {
+          pi = find_sorted(b.pref_id, p0, p1, c);
+          ci = find_sorted(b.cur_id, c0, c1, c);
+        }
+        uint32_t fl = 0;
+        int64_t wt = 0, mn = 0, mx = 0, cp = 0;
+        if (pi >= 0) {
+          const uint32_t pf = b.pref_fl[pi];
+          if (pf & KAD_PREF_HAS_WEIGHT) wt = b.pref_w[pi];
+          mn = b.pref_min[pi];
+          if (pf & KAD_PREF_HAS_MAX) {
+            fl |= EF_HAS_MAX;
+            mx = b.pref_max[pi];
+          }
+          if (pf & KAD_PREF_HAS_CAP) {
+            fl |= EF_HAS_CAP;
+            cp = b.pref_cap[pi];
+          }
+        }
+        ws.w[i] = wt;
+        ws.mn[i] = mn;
+        ws.mx[i] = mx;
+        ws.cap[i] = cp;
+        ws.fl[i] = fl;
+        ws.cur[i] = ci >= 0 ? b.cur_rep[ci] : 0;
+      }
     }
     wsync<GSCR>();
+    if (use_tbl) {
+      for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = 0;
+      for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = 0;
+      wsync<GSCR>();
+    }
+    KAD_PT(t1);
+    KAD_PADD(0, t1 - t0);
+    KAD_PADD(5, 1);
     uint32_t rflags = o.flags[w];
     if (f & KAD_W_DYNAMIC_WEIGHTS) {
       // CalcWeightLimit (rsp.go:183-213) + AvailableToPercentage (rsp.go:215-272)
@@ -1390,7 +1468,11 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
     }
     const bool avoid = f & KAD_W_AVOID_DISRUPTION;
     const bool keep = f & KAD_W_KEEP_UNSCHED;
+    KAD_PT(t2);
+    KAD_PADD(1, t2 - t1);
     rflags |= plan_row<GSCR>(ws, K, total, avoid, keep);
+    KAD_PT(t3);
+    KAD_PADD(2, t3 - t2);
     // result = plan + overflow, zeros dropped (rsp.go:162-179), ascending cluster id
     int base = 0;
     for (int i0 = 0; i0 < K; i0 += WAVE) {
@@ -1411,7 +1493,10 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
       o.flags[w] = rflags;
     }
     wsync<GSCR>();
+    KAD_PT(t4);
+    KAD_PADD(3, t4 - t3);
   }
+  KAD_PFLUSH_PLAN;
 }
 
 // ============================================= stand-alone stage entry points
@@ -1501,17 +1586,17 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
 // ================================================================ launchers
 int debug_phase_counters(uint64_t* out, int reset) {
 #ifdef KAD_PHASE_PROF
-  static unsigned long long h[256 * 16];
+  static unsigned long long h[256 * 32];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof h) != hipSuccess) return -1;
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 32; ++i) {
     out[i] = 0;
-    for (int s = 0; s < 256; ++s) out[i] += h[s * 16 + i];
+    for (int s = 0; s < 256; ++s) out[i] += h[s * 32 + i];
   }
   if (reset) {
-    static const unsigned long long z[256 * 16] = {};
+    static const unsigned long long z[256 * 32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return -1;
   }
-  return 16;
+  return 32;
 #else
   (void)out;
   (void)reset;
@@ -1588,6 +1673,9 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
       default: launch_lean<0>(A, (int)grid, lds, st); break;
     }
     if (hipError_t e = hipGetLastError()) return e;
+    // nothing can be deferred (host-checked: every unit and cluster is in the
+    // lean kernel's range and every feasible list fits its registers)
+    if (nch <= 4 && !b.may_defer) return hipSuccess;
     // the defer list: its length is only known on the device, so the grid
     // strides over it (waves past its end exit at once)
     int wpb2 = (int)(LDS_BUDGET / wb);
@@ -1622,16 +1710,20 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
   (void)p;
   if (n_rows == 0 || kmax <= 0) return hipSuccess;
   const size_t wb = plan_layout(kmax).bytes;
-  if (wb <= (size_t)LDS_BUDGET) {
-    hipLaunchKernelGGL(plan_kernel<false>, dim3(n_rows), dim3(64), wb, st, s, b, o, rows, n_rows, kmax,
-                       (char*)nullptr, (int)wb, n_rows);
+  const int cp = (s.C + 63) & ~63;
+  // per-wave lookup tables (4 B per cluster) when they fit beside the row state
+  const int tbl_cp = (cp <= 1024 && wb + (size_t)cp * 4 <= (size_t)LDS_BUDGET) ? cp : 0;
+  const size_t wbt = wb + (size_t)tbl_cp * 4;
+  if (wbt <= (size_t)LDS_BUDGET) {
+    hipLaunchKernelGGL(plan_kernel<false>, dim3(n_rows), dim3(64), wbt, st, s, b, o, rows, n_rows, kmax,
+                       (char*)nullptr, (int)wb, n_rows, tbl_cp);
   } else {
     size_t slots = scr_bytes / wb;
     if (slots < 1) return hipErrorInvalidValue;
     if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
     if (slots > (size_t)n_rows) slots = n_rows;
     hipLaunchKernelGGL(plan_kernel<true>, dim3(slots), dim3(64), 0, st, s, b, o, rows, n_rows, kmax, (char*)gscr,
-                       (int)wb, (int)slots);
+                       (int)wb, (int)slots, 0);
   }
   return hipGetLastError();
 }

@@ -32,17 +32,58 @@ __device__ __forceinline__ int64_t clamp_apply(Clamp f, int64_t R) {
   int64_t x = wsub(R, f.s);
   return x > f.t ? x : f.t;
 }
-// inclusive scan of clamp functions across the wave
+// inclusive scan of clamp functions across the wave: DPP Hillis-Steele within
+// 16-lane rows (row_shr 1/2/4/8), then row_bcast 15/31 across rows; lanes
+// without a source combine with the identity (0, -inf). Every lane active.
+template <int CTRL, int RM>
+__device__ __forceinline__ Clamp dpp_clamp(Clamp v) {
+  Clamp o;
+  o.s = dpp64<CTRL, RM>(0, v.s);
+  o.t = dpp64<CTRL, RM>(NEG_INF, v.t);
+  return o;
+}
 __device__ __forceinline__ Clamp wave_scan_clamp(Clamp v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < WAVE; d <<= 1) {
-    Clamp o;
-    o.s = shfl_up_i64(v.s, d);
-    o.t = shfl_up_i64(v.t, d);
-    if (l >= d) v = clamp_compose(o, v);
-  }
+  v = clamp_compose(dpp_clamp<0x111, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x112, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x114, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x118, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x142, 0xa>(v), v);
+  v = clamp_compose(dpp_clamp<0x143, 0xc>(v), v);
   return v;
+}
+// exclusive value: the inclusive scan shifted one lane up (wave_shr:1); lane 0 gets the identity
+__device__ __forceinline__ Clamp wave_shr1_clamp(Clamp v) {
+  Clamp o;
+  o.s = dpp64<0x138, 0xf>(0, v.s);
+  o.t = dpp64<0x138, 0xf>(NEG_INF, v.t);
+  return o;
+}
+__device__ __forceinline__ Clamp readlane_clamp(Clamp v, int l) {
+  Clamp o;
+  o.s = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v.s >> 32), l) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.s, l));
+  o.t = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v.t >> 32), l) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v.t, l));
+  return o;
+}
+
+// planner.go:249: extra = (remainingReplicas*weight + weightSum - 1) / weightSum
+// (Go int64, truncating). For 0 <= the numerator < 2^52 and 0 < weightSum < 2^52
+// an f64 quotient corrected twice with exact f64 products is the exact integer
+// quotient (no 64-bit division sequence); otherwise the wrapping int64 path.
+__device__ __forceinline__ int64_t ceil_extra(int64_t D, int64_t w, int64_t wsum) {
+  const int64_t num = wsub(wadd(wmul(D, w), wsum), 1);
+  const bool small = D >= 0 && D < (1ll << 26) && w >= 0 && w < (1ll << 26) && wsum > 0 && wsum < (1ll << 52);
+  if (small && num >= 0 && num < (1ll << 52)) {
+    const double nd = (double)num, sd = (double)wsum;
+    int64_t q = (int64_t)(nd / sd);
+    double r = nd - (double)q * sd;  // exact: q * sd <= nd + sd < 2^53
+    q += (r >= sd) - (r < 0.0);
+    r = nd - (double)q * sd;
+    q += (r >= sd) - (r < 0.0);
+    return q;
+  }
+  return go_div(num, wsum);
 }
 
 // Per-wave planner workspace: arrays indexed by element (K elements).
@@ -74,6 +115,26 @@ struct PlanWs {
 template <bool GSCR>
 __device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const int32_t* list, int m) {
   const int lane = lane_id();
+  if (m <= WAVE) {  // one element per lane: compare against the others with v_readlane, no memory
+    const int e = lane < m ? list[lane] : 0;
+    const int64_t we = lane < m ? wt[e] : 0;
+    const uint32_t he = lane < m ? ws.hash[e] : 0u;
+    int rank = 0;
+    bool tie = false;
+    for (int j = 0; j < m; j++) {
+      const int f = __builtin_amdgcn_readlane(e, j);
+      const int64_t wf = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)we >> 32), j)
+                                    << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)we, j));
+      const uint32_t hf = (uint32_t)__builtin_amdgcn_readlane((int)he, j);
+      rank += wf > we || (wf == we && (hf < he || (hf == he && f < e)));
+      tie |= (j != lane && wf == we && hf == he);
+    }
+    wsync<GSCR>();
+    if (lane < m) ws.ord[rank] = e;
+    wsync<GSCR>();
+    return ballot(lane < m && tie) != 0;
+  }
   bool tie = false;
   for (int i = lane; i < m; i += WAVE) {
     int e = list[i];
@@ -122,10 +183,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       f = {Mn, NEG_INF};
     }
     Clamp inc = wave_scan_clamp(f);
-    Clamp exc;
-    exc.s = shfl_up_i64(inc.s, 1);
-    exc.t = shfl_up_i64(inc.t, 1);
-    if (lane == 0) exc = {0, NEG_INF};
+    Clamp exc = wave_shr1_clamp(inc);
     int64_t Ri = clamp_apply(exc, R);
     if (v) {
       int64_t mt = Mn < Ri ? Mn : Ri;
@@ -141,10 +199,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       ofl[e] = of;
     }
     int last = (m - base) < WAVE ? (m - base - 1) : (WAVE - 1);
-    Clamp tot;
-    tot.s = shfl_i64(inc.s, last);
-    tot.t = shfl_i64(inc.t, last);
-    R = clamp_apply(tot, R);
+    R = clamp_apply(readlane_clamp(inc, last), R);
   }
   wsync<GSCR>();
   // ---- weighted rounds
@@ -170,7 +225,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       bool v = i < na;
       int e = v ? ws.act[i] : 0;
       int64_t start = v ? plan[e] : 0;
-      int64_t ee = v ? go_div(wsub(wadd(wmul(D, wt[e]), wsum), 1), wsum) : 0;
+      int64_t ee = v ? ceil_extra(D, wt[e], wsum) : 0;
       bool hm = v && mxv[e] != I64_MAX;
       bool hc = v && use_cap && (ws.fl[e] & EF_HAS_CAP);
       int64_t U = I64_MAX;
@@ -180,10 +235,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       int64_t mm = ee < V ? ee : V;
       Clamp f = !v ? Clamp{0, NEG_INF} : (mm >= 0 ? Clamp{mm, 0} : Clamp{mm, NEG_INF});
       Clamp inc = wave_scan_clamp(f);
-      Clamp exc;
-      exc.s = shfl_up_i64(inc.s, 1);
-      exc.t = shfl_up_i64(inc.t, 1);
-      if (lane == 0) exc = {0, NEG_INF};
+      Clamp exc = wave_shr1_clamp(inc);
       int64_t Ri = clamp_apply(exc, R);
       bool full = false;
       if (v) {
@@ -206,10 +258,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       if (v && !full) ws.act2[keepn + mbcnt(km)] = e;
       keepn += popc64(km);
       int last = (na - base) < WAVE ? (na - base - 1) : (WAVE - 1);
-      Clamp tot;
-      tot.s = shfl_i64(inc.s, last);
-      tot.t = shfl_i64(inc.t, last);
-      R = clamp_apply(tot, R);
+      R = clamp_apply(readlane_clamp(inc, last), R);
     }
     modified = ballot(mod) != 0;
     wsync<GSCR>();

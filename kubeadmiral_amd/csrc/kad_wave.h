@@ -144,10 +144,24 @@ __device__ __forceinline__ int64_t wave_min_u_i64(int64_t v) {
   return (int64_t)(((uint64_t)(uint32_t)mh << 32) | ml);
 }
 
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {  // wrapping (Go int64)
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v = (int64_t)((uint64_t)v + (uint64_t)shfl_xor_i64(v, m));
-  return v;
+// 64-bit DPP move: lanes without a source in this step get `old`
+template <int CTRL, int RM>
+__device__ __forceinline__ int64_t dpp64(int64_t old, int64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)old, (int)(uint32_t)v, CTRL, RM, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)((uint64_t)old >> 32), (int)(uint32_t)((uint64_t)v >> 32),
+                                             CTRL, RM, 0xf, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {  // wrapping (Go int64); every lane active
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x111, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x112, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x114, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x118, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x142, 0xa>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x143, 0xc>(0, v));
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), 63);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ int64_t wave_max_i64(int64_t v) { return wave_max_u_i64(v); }
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) { return wave_min_u_i64(v); }

@@ -26,7 +26,8 @@ from kubeadmiral_amd import build as kbuild  # noqa: E402
 PROF_LIB = os.path.join(kbuild.HERE, "libkad_prof.so")
 NAMES = ["A_filter", "B_score", "C_normalize", "D_select", "E_output", "n_straddle", "n_select", "sum_feasible",
          "D_select_straddle", "-", "lean_A_filter", "lean_B_score", "lean_D_select", "lean_E_output",
-         "lean_n_straddle", "lean_D_select_straddle"]
+         "lean_n_straddle", "lean_D_select_straddle", "plan_P0_setup", "plan_P1_weights", "plan_P2_plan",
+         "plan_P3_output", "-", "plan_rows"]
 
 
 def main():
@@ -52,7 +53,7 @@ def main():
     ctx = runtime.Context(0)
     ctx.upload_snapshot(snap)
     ctx.upload_batch(batch)
-    cnt = np.zeros(16, dtype=np.uint64)
+    cnt = np.zeros(32, dtype=np.uint64)
     ctx.schedule(fwk)
     ctx.sync()
     L.kad_debug_phase_counters(cnt.ctypes.data, 1)
@@ -65,6 +66,9 @@ def main():
     for i, nm in enumerate(NAMES):
         v = float(cnt[i])
         if nm == "-":
+            continue
+        if nm.startswith("plan_P"):
+            out[nm + "_cycles_per_row"] = round(v / max(1.0, float(cnt[21])), 1)
             continue
         if nm.startswith(("A_", "B_", "C_", "D_", "E_", "lean_A", "lean_B", "lean_D", "lean_E")):
             out[nm + "_cycles_per_unit"] = round(v / W, 1)

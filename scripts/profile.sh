@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 cfg=${1:-c2}; tag=${2:-run}
 out=gpurun_out/prof_${cfg}_${tag}
 mkdir -p "$out"
-B="python bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline"
+B="python bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline ${UNITS:+--units $UNITS}"
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$out/$name" -o "$name" -- $B > "$out/$name.log" 2>&1
@@ -19,5 +19,6 @@ run sq2 --pmc SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_W
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 read W C < <(python -c "from kubeadmiral_amd import synth; print(*synth.SIZES['$cfg'])")
+W=${UNITS:-$W}
 python scripts/pmc_summary.py "$out" "$cfg" --units "$W" --clusters "$C" --json "$out/pmc_$cfg.json" > "$out/summary.txt"
 cat "$out/summary.txt" | tail -30
