@@ -635,11 +635,9 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   if (ch == 0) {
     UnitRec r;
     bool full = force_full != 0;
-    if ((fm & (1u << KAD_PL_TAINT_TOLERATION)) && s.TW > 1) full = true;
     if ((fm & (1u << KAD_PL_API_RESOURCES)) && b.gvk[w] >= 64) full = true;
     if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && b.sreq_off[w] < b.sreq_off[w + 1])
       full = true;
-    if ((p.score_mask & (1u << KAD_PL_TAINT_TOLERATION)) && s.TW > 1) full = true;
     r.flags = f | (((f & KAD_W_HAS_DESIRED) && b.desired[w] > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
     r.gvk = b.gvk[w];
     r.tolset = b.tolset[w];
@@ -695,12 +693,12 @@ struct LeanLayout {
 };
 // per-wave region
 __host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
-  const size_t Cp = (size_t)((C + 63) & ~63);
+ (void)C;
   const size_t P = (size_t)qmax * 64;  // positions held in registers
   LeanLayout L;
   L.key = 0;                     // u32[P] replay keys (total - row minimum)
-  L.idx = L.key + 4 * P;         // u16[Cp] feasible position → cluster id
-  L.pid = L.idx + 2 * Cp;        // u16[P] replay: original position at each position
+  L.idx = L.key + 4 * P;         // u16[P] feasible position → cluster id (NCH > 0: P = Cp)
+  L.pid = L.idx + 2 * P;         // u16[P] replay: original position at each position
   L.posl = L.pid + 2 * P;        // u16[P] replay scratch (partition stoppers; then ranks)
   L.posr = L.posl + 2 * P;       // u16[P]
   L.bytes = (L.posr + 2 * P + 15) & ~(size_t)15;
@@ -709,7 +707,7 @@ __host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
 // block-shared cluster cache (NCH > 0): n_attrs arrays of Cp i64
 __host__ __device__ inline size_t lean_cache_bytes(int C, int n_attrs) { return (size_t)n_attrs * 8 * ((C + 63) & ~63); }
 static constexpr int LDS_BUDGET = 64 * 1024;  // per block
-bool fast_path(int C) { return row_layout(C).bytes <= (size_t)LDS_BUDGET; }
+bool fast_path(int C) { return C >= 0; }  // the lean kernel runs for every C; the full kernel takes its defer list
 
 struct LeanArgs {
   SnapDev s;
@@ -747,13 +745,14 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int C, W;
+  int C, W, TWs;
   uint32_t fm, sm;
   char* region;
   {
     LArgs a = largs();
     region = smem + (size_t)wv * a->wave_bytes;
     C = a->s.C;
+    TWs = a->s.TW;
     W = a->b.W;
     fm = a->p.filter_mask;
     sm = a->p.score_mask;
@@ -848,6 +847,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     auto fld64 = [&](int d) -> int64_t { return (int64_t)(((uint64_t)fld(d + 1) << 32) | fld(d)); };
     const uint32_t fc = fld(0);
     const int gvc = (int)fld(1);
+    const int tsc = (int)fld(2);
     const int64_t rqc = fld64(4), rqm = fld64(6);
     const uint64_t tolc = (uint64_t)fld64(12);
     uint64_t swc[NR];
@@ -870,12 +870,14 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     const uint64_t tolp0 = (uint64_t)fld64(14);
     const bool use_cur = f_taint && (fc & KAD_W_HAS_CURRENT);
     const bool fit_on = f_fit && (fc & KAD_W_FIT_NONZERO);
-    uint64_t dsw = ~0ull, dcw = 0;  // dynamic-NCH path: words in lanes < nch
-    if constexpr (NCH == 0) {
+    uint64_t dsw = ~0ull, dcw = 0;  // dynamic-NCH path: words of chunks 64g..64g+63 in lanes
+    auto load_words = [&](int ch0) {
       LArgs a = largs();
-      if (f_sw && lane < nch) dsw = ldg(a->b.sw, (uint32_t)(w * nch + lane));
-      if (use_cur && lane < nch) dcw = ldg(a->b.cw, (uint32_t)(w * nch + lane));
-    }
+      const int ch = ch0 + lane;
+      dsw = (f_sw && ch < nch) ? ldg(a->b.sw, (uint32_t)(w * nch + ch)) : ~0ull;
+      dcw = (use_cur && ch < nch) ? ldg(a->b.cw, (uint32_t)(w * nch + ch)) : 0ull;
+    };
+    if constexpr (NCH == 0) load_words(0);
 
     // ---------------- filters → compacted feasible list (findClustersThatFitWorkload, :152-169)
     int n = 0;
@@ -933,15 +935,24 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           p_ne = ldg(a->s.ne, cl);
           p_gv = ldg(a->s.gvk, cl);
         }
-        sw0 = readlane64(dsw, ch);
-        cw0 = readlane64(dcw, ch);
+        if (ch > 0 && (ch & 63) == 0) load_words(ch);
+        sw0 = readlane64(dsw, ch & 63);
+        cw0 = readlane64(dcw, ch & 63);
       }
       // each filter as a lane mask (v_cmp → SGPR pair), combined with scalar
       // ANDs under uniform selects (no branches inside the unrolled loop)
       const int rem = C - ch * WAVE;
       uint64_t m = rem >= WAVE ? ~0ull : ((1ull << rem) - 1);
-      const uint64_t x = (use_cur && ((cw0 >> lane) & 1)) ? ne0 : ns0;
-      const uint64_t m_taint = ballot((x & ~tolc) == 0);      // taint_toleration.go:50-77
+      const bool sch = use_cur && ((cw0 >> lane) & 1);
+      const uint64_t x = sch ? ne0 : ns0;
+      bool tok = (x & ~tolc) == 0;
+      for (int tw = 1; tw < TWs; ++tw) {  // more than 64 taint ids (C5): words 1.. from global
+        LArgs a = largs();
+        const uint32_t cl = c < C ? (uint32_t)c : 0u;
+        const uint64_t xt = sch ? ldg(a->s.ne, (uint32_t)(tw * C) + cl) : ldg(a->s.nsne, (uint32_t)(tw * C) + cl);
+        tok &= (xt & ~ldc(a->b.tol_all + (size_t)tsc * TWs + tw)) == 0;
+      }
+      const uint64_t m_taint = ballot(tok);      // taint_toleration.go:50-77
       const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
       const uint64_t m_fit = ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));  // fit.go:73-134
       m &= f_sw ? sw0 : ~0ull;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
@@ -952,7 +963,10 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       if constexpr (NCH > 0) {
         mk[ch] = m;  // compaction after every chunk's mask: no LDS store between the cache reads
       } else {
-        if ((m >> lane) & 1) idx[n + mbcnt(m)] = (uint16_t)c;
+        if ((m >> lane) & 1) {
+          const int pos = n + mbcnt(m);
+          if (pos < P) idx[pos] = (uint16_t)c;  // more than P feasible: the unit is deferred
+        }
         n += popc64(m);
       }
     }
@@ -1028,7 +1042,12 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           pn = c_pn[cq];
         else
           pn = ldg(largs()->s.pns, cq);
-        ttv[q] = v ? popc64(pn & ~tolp0) : 0;
+        int tc = popc64(pn & ~tolp0);
+        for (int tw = 1; tw < TWs; ++tw) {
+          LArgs a = largs();
+          tc += popc64(ldg(a->s.pns, (uint32_t)(tw * C) + cq) & ~ldc(a->b.tol_pns + (size_t)tsc * TWs + tw));
+        }
+        ttv[q] = v ? tc : 0;
         ttmax = ttv[q] > ttmax ? ttv[q] : ttmax;
       }
     }
@@ -1678,12 +1697,21 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (nch <= 4 && !b.may_defer) return hipSuccess;
     // the defer list: its length is only known on the device, so the grid
     // strides over it (waves past its end exit at once)
-    int wpb2 = (int)(LDS_BUDGET / wb);
-    wpb2 = wpb2 > 4 ? 4 : (wpb2 < 1 ? 1 : wpb2);
-    long waves2 = b.W < 256 * 16 ? b.W : 256 * 16;
-    const int grid2 = (int)((waves2 + wpb2 - 1) / wpb2);
-    const SchedArgs A2{s, b, o, p, nullptr, (int)wb, wpb2, grid2 * wpb2, b.defer, b.defer_n};
-    hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid2), dim3(64 * wpb2), wb * wpb2, st, A2);
+    if (wb <= (size_t)LDS_BUDGET) {
+      int wpb2 = (int)(LDS_BUDGET / wb);
+      wpb2 = wpb2 > 4 ? 4 : (wpb2 < 1 ? 1 : wpb2);
+      long waves2 = b.W < 256 * 16 ? b.W : 256 * 16;
+      const int grid2 = (int)((waves2 + wpb2 - 1) / wpb2);
+      const SchedArgs A2{s, b, o, p, nullptr, (int)wb, wpb2, grid2 * wpb2, b.defer, b.defer_n};
+      hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid2), dim3(64 * wpb2), wb * wpb2, st, A2);
+    } else {  // rows too large for LDS: per-wave global scratch slabs
+      size_t slots = scr_bytes / wb;
+      if (slots < 1) return hipErrorInvalidValue;
+      if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
+      if (slots > (size_t)b.W) slots = b.W;
+      const SchedArgs A2{s, b, o, p, (char*)gscr, (int)wb, 1, (int)slots, b.defer, b.defer_n};
+      hipLaunchKernelGGL(schedule_kernel<true>, dim3((int)slots), dim3(64), 0, st, A2);
+    }
     return hipGetLastError();
   }
   if (wb <= (size_t)LDS_BUDGET) {

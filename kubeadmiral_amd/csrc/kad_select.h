@@ -284,8 +284,8 @@ struct KeyLdsStoreT {
 // heapSort (only after log2(n) unbalanced partitions) falls back to lane 0.
 // key/id: the n positions' keys (swapped in place) and original positions;
 // posL/posR: u16 scratch of n entries each.
-template <class KeyT>
-struct PdqWave {
+template <class KeyT, bool GS = false>
+struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
   KeyT* key;
   uint16_t* id;
   uint16_t* posL;
@@ -306,14 +306,14 @@ struct PdqWave {
   __device__ __forceinline__ void swap1(int i, int j) const {
     const KeyT ki = key[i], kj = key[j];
     const uint16_t ii = id[i], ij = id[j];
-    wave_sync();
+    wsync<GS>();
     if (lane_id() == 0) {
       key[i] = kj;
       key[j] = ki;
       id[i] = ij;
       id[j] = ii;
     }
-    wave_sync();
+    wsync<GS>();
   }
   __device__ void insertion_sort(int a, int b) const {
     const int m = b - a, lane = lane_id();
@@ -328,12 +328,12 @@ struct PdqWave {
       const KeyT kq = key[a + q];
       r += (int)(kq > kp) | (int)((kq == kp) & (q < lane));
     }
-    wave_sync();
+    wsync<GS>();
     if (lane < m) {
       key[a + r] = kp;
       id[a + r] = ip;
     }
-    wave_sync();
+    wsync<GS>();
   }
   __device__ void reverse_range(int a, int b) const {
     const int h = (b - a) / 2;
@@ -349,7 +349,7 @@ struct PdqWave {
         id[j] = ii;
       }
     }
-    wave_sync();
+    wsync<GS>();
   }
   __device__ __forceinline__ void order2(int& a, int& b, int& swaps) const {
     if (less(b, a)) {
@@ -460,18 +460,18 @@ struct PdqWave {
         kk = key[p];
         ii = id[p];
       }
-      wave_sync();
+      wsync<GS>();
       if (in) {
         key[p + 1] = kk;
         id[p + 1] = ii;
       }
-      wave_sync();
+      wsync<GS>();
     }
     if (lane == 0) {
       key[m] = X;
       id[m] = XI;
     }
-    wave_sync();
+    wsync<GS>();
   }
   // the element at j0-1 moves right while its right neighbour is less than it
   __device__ void shift_right(int j0, int b) const {
@@ -496,18 +496,18 @@ struct PdqWave {
         kk = key[p];
         ii = id[p];
       }
-      wave_sync();
+      wsync<GS>();
       if (in) {
         key[p - 1] = kk;
         id[p - 1] = ii;
       }
-      wave_sync();
+      wsync<GS>();
     }
     if (lane == 0) {
       key[mp] = Y;
       id[mp] = YI;
     }
-    wave_sync();
+    wsync<GS>();
   }
   __device__ bool partial_insertion_sort(int a, int b) const {
     int i = a + 1;
@@ -540,7 +540,7 @@ struct PdqWave {
       cL += popc64(mL);
       cR += popc64(mR);
     }
-    wave_sync();
+    wsync<GS>();
     const int np = cL < cR ? cL : cR;
     int t_n = 0;
     for (int t0 = 0; t0 < np; t0 += WAVE) {
@@ -563,7 +563,7 @@ struct PdqWave {
       }
       if (~m) break;  // a prefix: once a t fails, every later t fails
     }
-    wave_sync();
+    wsync<GS>();
     *T = t_n;
     return cR;
   }
@@ -598,7 +598,7 @@ struct PdqWave {
           PdqT<KeyLdsStoreT<KeyT>> s{st, xs_b, xs_c};
           s.heap_sort(a, b);
         }
-        wave_sync();
+        wsync<GS>();
         return;
       }
       if (!wasBalanced) {
@@ -751,14 +751,8 @@ __device__ uint32_t select_topk(const SelWs& ws, int n, int64_t k, int64_t row_m
   for (int j = lane; j < n; j += WAVE) ws.perm[j] = (uint16_t)j;
   for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
   wsync<GSCR>();
-  if (GSCR) {  // global-scratch rows: serial replay (LDS-only wave primitives)
-    if (lane == 0) {
-      KeyLdsStoreT<int64_t> st{ws.tot, ws.perm};
-      PdqT<KeyLdsStoreT<int64_t>> p{st, xs_b, xs_c};
-      p.select(n, (int)k);
-    }
-  } else {
-    PdqWave<int64_t> pw{ws.tot, ws.perm, ws.posl, ws.posr, xs_b, xs_c};
+  {
+    PdqWave<int64_t, GSCR> pw{ws.tot, ws.perm, ws.posl, ws.posr, xs_b, xs_c};
     pw.select(n, (int)k);
   }
   wsync<GSCR>();
