@@ -39,7 +39,12 @@ WORKLOAD_DESC = {
     "c3": "1M SchedulingUnits x 1k FederatedClusters (c2 generator), sharded over GPUs",
     "c4": "1M Divide SchedulingUnits x 512 clusters: weights, min/max replicas, capacity caps",
     "c5": "100k SchedulingUnits x 10k clusters: dense label affinity, many taints, API-resource gaps",
+    "t1": "scheduling-trigger hashes: 1k federated Deployments x 16 joined clusters",
+    "t2": "scheduling-trigger hashes: 100k federated Deployments x 256 joined clusters (~1.6 MB cluster part)",
 }
+# VALU issue bound of one FNV-1 step per lane (v_mul_lo_u32 at quarter rate + one v_bitop3/v_xor):
+# 20 SIMD cycles per 64 steps → 3.2 steps/cycle/SIMD × 4 SIMDs × 256 CUs × 2.4 GHz
+FNV_STEP_PEAK = 3.2 * 4 * 256 * 2.4e9
 
 
 def log(*a):
@@ -83,6 +88,88 @@ def cpu_baseline(snap, batch, fwk, C, target_s):
                       f"(C restatement of the Go reference, one unit per worker thread), {dt:.2f}s wall"}
 
 
+def bench_trigger(args, cfg, rank, world, local, dist):
+    """§8(f) f4: computeSchedulingTriggerHash for a batch of objects (kad_trigger_*)."""
+    from kubeadmiral_amd import objects as O
+    from kubeadmiral_amd import synth
+    from kubeadmiral_amd.runtime import Context
+
+    W0, C = synth.TRIGGER_SIZES[cfg]
+    W = args.units if args.units is not None else W0
+    rng = np.random.default_rng(0x7 + rank)
+    ftc, clusters, objs, pols = synth.gen_trigger_workload(rng, W, C)
+    suffix = O.trigger_suffix(clusters)
+    prefixes = [O.trigger_prefix(ftc, o, p) for o, p in zip(objs, pols)]
+    pre_bytes = sum(len(p) for p in prefixes)
+    log(f"[rank {rank}] {cfg}: {W} objects, cluster part {len(suffix)} B, object parts {pre_bytes / max(1, W):.0f} B avg")
+    ctx = Context(local)
+    ctx.trigger_suffix_upload(suffix)
+    ctx.trigger_prefixes_upload(prefixes)
+    for _ in range(args.warmup):
+        ctx.trigger_run()
+        ctx.sync()
+    if dist is not None:
+        dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.trigger_run()
+    ctx.sync()
+    if dist is not None:
+        dist.barrier()
+    ms = (time.perf_counter() - t0) / max(1, args.steps) * 1e3
+    tot, summ = [], []
+    for _ in range(max(3, min(args.steps, 10))):
+        ctx.trigger_run()
+        a, b = ctx.trigger_timing()
+        tot.append(a)
+        summ.append(b)
+    tot_ms, sum_ms = float(np.mean(tot)), float(np.mean(summ))
+    units_total = W * world
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([ms, tot_ms, sum_ms], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms, tot_ms, sum_ms = t.tolist()
+    if rank == 0:
+        steps = 256.0 * len(suffix)  # FNV steps of the cluster-part summary (256 residue chains)
+        obj_bytes = pre_bytes + 8 * (W + 1) + 4 * W
+        out = {
+            "metric": "scheduling-trigger hashes/sec (objects/s)", "value": units_total / (ms * 1e-3),
+            "unit": "objects/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded federated Deployments, policies and joined clusters)",
+            "config": {"workload": f"{cfg}: {WORKLOAD_DESC[cfg]}", "objects_per_gpu": W, "objects_total": units_total,
+                       "clusters": C, "cluster_part_bytes": len(suffix), "object_part_bytes_avg": pre_bytes / max(1, W),
+                       "parallelism": f"dp{world}",
+                       "kernel_ms": {"cluster_part_summary": sum_ms, "objects": tot_ms - sum_ms}},
+            "roofline": {"bound": "valu", "achieved": steps / (sum_ms * 1e-3), "peak": FNV_STEP_PEAK,
+                         "unit": "FNV steps/s", "frac": steps / (sum_ms * 1e-3) / FNV_STEP_PEAK, "traffic": None,
+                         "kernel": "trig_segment_kernel + trig_compose_kernel (256 residue chains over the cluster part)",
+                         "objects_kernel_gbs": obj_bytes / max(1e-9, (tot_ms - sum_ms) * 1e-3) / 1e9},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import ref
+
+            threads = min(16, os.cpu_count() or 1)
+            n = min(W, 64)
+            t0 = time.perf_counter()
+            ref.trigger_hashes(prefixes[:n], suffix, threads)
+            dt = time.perf_counter() - t0
+            n = int(min(W, max(n, n * args.cpu_seconds / max(dt, 1e-6))))
+            t0 = time.perf_counter()
+            ref.trigger_hashes(prefixes[:n], suffix, threads)
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": n / dt, "unit": "objects/s", "cores": threads, "kind": "port",
+                                   "sample": f"first {n} of {W} objects, oracle/kad_trigger_ref.c (each object's "
+                                             f"bytes folded end to end, as schedulingtriggers.go:141-145; JSON "
+                                             f"building not timed), {dt:.2f}s wall"}
+        print(json.dumps(out), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +202,12 @@ def main():
         dist.barrier()
 
     cfg = args.config
+    if cfg.startswith("t"):
+        bench_trigger(args, cfg, rank, world, local, dist)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     W0, C = synth.SIZES[cfg]
     W = args.units if args.units is not None else (W0 if cfg not in ("c3", "c4") else W0 // max(1, world))
     log(f"[rank {rank}] generating {cfg}: {W} units x {C} clusters")

@@ -326,6 +326,31 @@ int kad_plan_rows(kad_ctx* ctx, int n_rows, const int32_t* row_off, const uint32
  * kad_schedule (feasible: u8[W*C]; total: i64[W*C], meaningful where feasible). */
 int kad_debug_scores(kad_ctx* ctx, const kad_profile* profile, uint8_t* feasible, int64_t* total);
 
+/* ------------------------------------------- scheduling-trigger hashes
+ * Replaces the FNV-1 half of Scheduler.computeSchedulingTriggerHash
+ * (pkg/controllers/scheduler/schedulingtriggers.go:106-147, called per object
+ * from prepareToSchedule, scheduler.go:394). The caller splits each object's
+ * json.Marshal(schedulingTriggers) bytes at the "clusterLabels" value: the
+ * object part (prefix: scheduling annotations, replica count, resource
+ * request, auto-migration info, policy name + generation, up to and including
+ * `"clusterLabels":`) and the cluster part (suffix: clusterLabels value,
+ * clusterTaints, clusterAPIResourceTypes, closing brace), which is identical
+ * for every object scheduled against the same joined-cluster list. Output:
+ * hash.Sum32() per object (the reference formats it with strconv.FormatInt).
+ *   suffix: uploaded once per cluster-set change (bytes, any alignment)
+ *   prefixes: CSR, prefix_off[0] = 0, non-decreasing, n+1 entries
+ *   run: asynchronous on the ctx stream (summarises the suffix into a
+ *        256-entry FNV table, then hashes every object); download blocks.  */
+int kad_trigger_suffix_upload(kad_ctx* ctx, const uint8_t* suffix, size_t nbytes);
+int kad_trigger_prefixes_upload(kad_ctx* ctx, int n, const int64_t* prefix_off, const uint8_t* prefix);
+int kad_trigger_run(kad_ctx* ctx);
+/* ms[0] = whole trigger run, ms[1] = the cluster-part summary kernels */
+int kad_trigger_timing(kad_ctx* ctx, float ms[2]);
+int kad_trigger_download(kad_ctx* ctx, uint32_t* out_hash);
+/* All in one (blocking): both uploads, run, download. */
+int kad_trigger_hashes(kad_ctx* ctx, int n, const int64_t* prefix_off, const uint8_t* prefix, const uint8_t* suffix,
+                       size_t suffix_len, uint32_t* out_hash);
+
 /* Profiling builds only (-DKAD_PHASE_PROF): copy 32 per-phase cycle / event
  * counters of the kernels to out (and zero them if reset). Returns 32, or
  * 0 in product builds (no counters compiled in). Not part of the reference. */

@@ -52,6 +52,20 @@ struct kad_ctx {
   bool have_snapshot = false, have_batch = false, ran = false;
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
   bool batch_defer = false;    // some unit uses a feature the lean kernel defers
+  // scheduling-trigger hashes (kad_trigger_*)
+  void* t_suffix = nullptr;
+  size_t t_suffix_cap = 0;
+  int64_t t_suffix_len = -1;   // -1: no suffix uploaded
+  void* t_prefix = nullptr;
+  size_t t_prefix_cap = 0;
+  void* t_work = nullptr;      // prefix_off, out
+  size_t t_work_cap = 0;
+  void* t_tabs = nullptr;      // segment / composed tables + powers of the suffix
+  size_t t_tabs_cap = 0;
+  int t_n = -1;                // -1: no prefixes uploaded
+  bool t_ran = false;
+  TriggerDev td{};
+  hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 static int fail(kad_ctx* c, int code, const std::string& msg) {
@@ -109,6 +123,11 @@ int kad_ctx_create(int hip_device, kad_ctx** out) {
       delete c;
       return KAD_EHIP;
     }
+  for (auto& e : c->tev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      delete c;
+      return KAD_EHIP;
+    }
   *out = c;
   return KAD_OK;
 }
@@ -118,9 +137,12 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_sw, c->d_cw, c->d_defer})
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_sw, c->d_cw, c->d_defer,
+                  c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->tev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -585,6 +607,100 @@ int kad_plan_rows(kad_ctx* c, int n_rows, const int32_t* row_off, const uint32_t
   for (void* p : owned) (void)hipFree(p);
   if (e != hipSuccess) return fail(c, KAD_EHIP, hipGetErrorString(e));
   return KAD_OK;
+}
+
+/* ------------------------------------------------ scheduling-trigger hashes */
+int kad_trigger_suffix_upload(kad_ctx* c, const uint8_t* suffix, size_t nbytes) {
+  if (!c || (!suffix && nbytes)) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(c, hipSetDevice(c->device));
+  int r = grow(c, &c->t_suffix, &c->t_suffix_cap, ((nbytes + 63) & ~(size_t)63) + 64);
+  if (r) return r;
+  const int64_t ntab = trigger_table_count((int64_t)nbytes);
+  r = grow(c, &c->t_tabs, &c->t_tabs_cap, (size_t)ntab * 256 * 4 + (size_t)ntab * 4 + 256);
+  if (r) return r;
+  if (nbytes) HIPCHK(c, hipMemcpyAsync(c->t_suffix, suffix, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  TriggerDev& t = c->td;
+  t.suffix = static_cast<const uint32_t*>(c->t_suffix);
+  t.suffix_len = (int64_t)nbytes;
+  t.tables = static_cast<uint32_t*>(c->t_tabs);
+  t.powers = t.tables + (size_t)ntab * 256;
+  c->t_suffix_len = (int64_t)nbytes;
+  c->t_ran = false;
+  return KAD_OK;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int kad_trigger_prefixes_upload(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix) {
+  if (!c || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
+  for (int i = 0; i < n; i++)
+    if (prefix_off[i + 1] < prefix_off[i]) return fail(c, KAD_EINVAL, "prefix_off must be non-decreasing");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t nbytes = (size_t)prefix_off[n];
+  int r = grow(c, &c->t_prefix, &c->t_prefix_cap, nbytes + 64);
+  if (r) return r;
+  const size_t nn = (size_t)(n > 0 ? n : 1);
+  const size_t o_out = align256((nn + 1) * 8);
+  r = grow(c, &c->t_work, &c->t_work_cap, o_out + align256(nn * 4));
+  if (r) return r;
+  char* w = static_cast<char*>(c->t_work);
+  if (nbytes) HIPCHK(c, hipMemcpyAsync(c->t_prefix, prefix, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(w, prefix_off, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  TriggerDev& t = c->td;
+  t.n = n;
+  t.prefix = static_cast<const uint8_t*>(c->t_prefix);
+  t.prefix_off = reinterpret_cast<const int64_t*>(w);
+  t.out = reinterpret_cast<uint32_t*>(w + o_out);
+  c->t_n = n;
+  c->t_ran = false;
+  return KAD_OK;
+}
+
+int kad_trigger_run(kad_ctx* c) {
+  if (!c) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->t_suffix_len < 0 || c->t_n < 0) return fail(c, KAD_ESTATE, "upload the trigger suffix and prefixes first");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipEventRecord(c->tev[0], c->stream));
+  HIPCHK(c, launch_trigger_summary(c->td, c->stream));
+  HIPCHK(c, hipEventRecord(c->tev[1], c->stream));
+  HIPCHK(c, launch_trigger_objects(c->td, c->stream));
+  HIPCHK(c, hipEventRecord(c->tev[2], c->stream));
+  c->t_ran = true;
+  return KAD_OK;
+}
+
+int kad_trigger_timing(kad_ctx* c, float ms[2]) {
+  if (!c || !ms) return KAD_EINVAL;
+  if (!c->t_ran) return fail(c, KAD_ESTATE, "no trigger run");
+  HIPCHK(c, hipEventSynchronize(c->tev[2]));
+  HIPCHK(c, hipEventElapsedTime(&ms[0], c->tev[0], c->tev[2]));
+  HIPCHK(c, hipEventElapsedTime(&ms[1], c->tev[0], c->tev[1]));
+  return KAD_OK;
+}
+
+int kad_trigger_download(kad_ctx* c, uint32_t* out_hash) {
+  if (!c) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->t_ran) return fail(c, KAD_ESTATE, "no trigger run");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->t_n > 0 && out_hash)
+    HIPCHK(c, hipMemcpyAsync(out_hash, c->td.out, (size_t)c->t_n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KAD_OK;
+}
+
+int kad_trigger_hashes(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix, const uint8_t* suffix,
+                       size_t suffix_len, uint32_t* out_hash) {
+  int r = kad_trigger_suffix_upload(c, suffix, suffix_len);
+  if (!r) r = kad_trigger_prefixes_upload(c, n, prefix_off, prefix);
+  if (!r) r = kad_trigger_run(c);
+  if (!r) r = kad_trigger_download(c, out_hash);
+  return r;
 }
 
 }  // extern "C"

@@ -94,6 +94,22 @@ struct PlanRowsDev {
   int64_t *out_plan, *out_overflow;
 };
 
+// Scheduling-trigger hash pipeline (kad_trigger.hip): device buffers of one run.
+struct TriggerDev {
+  int n;                          // objects
+  const uint8_t* prefix;          // per-object bytes (CSR by prefix_off)
+  const int64_t* prefix_off;      // [n+1]
+  const uint32_t* suffix;         // shared cluster part (4-B aligned)
+  int64_t suffix_len;             // bytes
+  uint32_t* tables;               // [trigger_table_count][256] segment / composed tables
+  uint32_t* powers;               // [trigger_table_count] p^len of each table's bytes
+  uint32_t* out;                  // [n]
+};
+int64_t trigger_segment_len(int64_t suffix_len);
+int64_t trigger_table_count(int64_t suffix_len);
+hipError_t launch_trigger_summary(const TriggerDev& t, hipStream_t st);
+hipError_t launch_trigger_objects(const TriggerDev& t, hipStream_t st);
+
 // bytes of per-wave scratch for the filter/score/select kernel at C clusters
 size_t select_wave_bytes(int C);
 size_t plan_wave_bytes(int K);

@@ -75,6 +75,12 @@ def load_library(path: str = LIB_PATH):
     L.kad_select_rows.argtypes = [P, I, P, P, P, U32, P, P, P]
     L.kad_plan_rows.argtypes = [P, I, P, P, P, P, P, P, P, P, P, P, P, P]
     L.kad_debug_scores.argtypes = [P, P, P, P]
+    L.kad_trigger_suffix_upload.argtypes = [P, P, SZ]
+    L.kad_trigger_prefixes_upload.argtypes = [P, I, P, P]
+    L.kad_trigger_run.argtypes = [P]
+    L.kad_trigger_timing.argtypes = [P, P]
+    L.kad_trigger_download.argtypes = [P, P]
+    L.kad_trigger_hashes.argtypes = [P, I, P, P, P, SZ, P]
     _lib = L
     return L
 
@@ -203,6 +209,64 @@ class Context:
             a, b = off[r], off[r + 1]
             out.append((plan[a:b].tolist(), [None if o < 0 else int(o) for o in over[a:b].tolist()]))
         return out
+
+
+    # ------------------------------------------------ scheduling-trigger hashes
+    def trigger_suffix_upload(self, suffix: bytes):
+        buf = np.frombuffer(suffix, np.uint8) if suffix else np.zeros(1, np.uint8)
+        self._chk(self.L.kad_trigger_suffix_upload(self.h, _p(buf), len(suffix)))
+
+    def trigger_prefixes_upload(self, prefixes: Sequence[bytes]):
+        off = np.zeros(len(prefixes) + 1, np.int64)
+        off[1:] = np.cumsum([len(p) for p in prefixes])
+        data = np.frombuffer(b"".join(prefixes) or b"\0", np.uint8)
+        self._chk(self.L.kad_trigger_prefixes_upload(self.h, len(prefixes), _p(off), _p(data)))
+        self._trig_n = len(prefixes)
+
+    def trigger_run(self):
+        self._chk(self.L.kad_trigger_run(self.h))
+
+    def trigger_timing(self):
+        ms = (ctypes.c_float * 2)()
+        self._chk(self.L.kad_trigger_timing(self.h, ms))
+        return float(ms[0]), float(ms[1])
+
+    def trigger_download(self) -> np.ndarray:
+        out = np.zeros(max(1, self._trig_n), np.uint32)
+        self._chk(self.L.kad_trigger_download(self.h, _p(out)))
+        return out[:self._trig_n]
+
+
+class TriggerHasher:
+    """Scheduler.computeSchedulingTriggerHash for a batch of objects (schedulingtriggers.go:106-147).
+
+    The cluster part of the trigger JSON is built once per cluster list
+    (:meth:`set_clusters`), each object's part on the host, and the FNV-1 over
+    object part ‖ cluster part runs on the GPU (``kad_trigger_*``). Returns the
+    decimal strings the reference writes to the
+    ``kubeadmiral.io/scheduling-trigger-hash`` annotation.
+    """
+
+    def __init__(self, ctx: Optional[Context] = None, device: int = 0):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self.suffix: Optional[bytes] = None
+
+    def set_clusters(self, clusters: List[T.FederatedCluster]) -> bytes:
+        from .objects import trigger_suffix
+
+        self.suffix = trigger_suffix(clusters)
+        self.ctx.trigger_suffix_upload(self.suffix)
+        return self.suffix
+
+    def hashes(self, type_config, objs: Sequence[dict], policies: Sequence) -> List[str]:
+        from .objects import format_trigger_hash, trigger_prefix
+
+        if self.suffix is None:
+            raise RuntimeError("set_clusters first")
+        self.ctx.trigger_prefixes_upload([trigger_prefix(type_config, o, p) for o, p in zip(objs, policies)])
+        self.ctx.trigger_run()
+        h = self.ctx.trigger_download()
+        return [format_trigger_hash(x) for x in h.tolist()]
 
 
 class BatchScheduler:

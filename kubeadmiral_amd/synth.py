@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from typing import List, Optional, Tuple
 
+import json
+
 import numpy as np
 
 from . import framework as F
@@ -333,3 +335,63 @@ FUZZ_PROFILES = [
 def fuzz_framework(i: int) -> F.Framework:
     ep = FUZZ_PROFILES[i % len(FUZZ_PROFILES)]
     return F.Framework(ep if ep is not None else F.default_enabled_plugins())
+
+
+# ------------------------------------------------------------ scheduling-trigger workload (§8(f) f4)
+TRIGGER_SIZES = {"t1": (1000, 16), "t2": (100_000, 256)}
+
+
+def _api_pool(n: int):
+    base = [("apps", "v1", "Deployment", "deployments"), ("apps", "v1", "StatefulSet", "statefulsets"),
+            ("apps", "v1", "DaemonSet", "daemonsets"), ("batch", "v1", "Job", "jobs"),
+            ("batch", "v1", "CronJob", "cronjobs"), ("", "v1", "ConfigMap", "configmaps"),
+            ("", "v1", "Secret", "secrets"), ("", "v1", "Service", "services"),
+            ("networking.k8s.io", "v1", "Ingress", "ingresses")]
+    out = [T.APIResource(g, v, k, p, "Namespaced") for g, v, k, p in base]
+    i = 0
+    while len(out) < n:
+        out.append(T.APIResource(f"crd{i // 4}.example.com", f"v{1 + i % 2}", f"Kind{i}", f"kind{i}s",
+                                 "Cluster" if i % 5 == 0 else "Namespaced"))
+        i += 1
+    return out[:n]
+
+
+def gen_trigger_workload(rng: np.random.Generator, W: int, C: int, n_policies: int = 64, n_api: int = 64):
+    """Joined clusters as the trigger hash sees them (labels, taints, ~n_api API resources each) and W
+    federated Deployments: a policy out of ``n_policies`` (some with auto migration), replicas 1-100,
+    10 % with scheduling annotations. Returns (type_config, clusters, objects, policies)."""
+    from . import objects as O
+
+    clusters = gen_clusters(rng, C)
+    pool = _api_pool(n_api)
+    for c in clusters:
+        keep = rng.random(len(pool)) < 0.9
+        api = [pool[i] for i in np.nonzero(keep)[0]]
+        rng.shuffle(api)
+        c.api_resource_types = api
+    pols = [O.PropagationPolicy(f"policy-{i}", "default", int(rng.integers(1, 20)), O.PropagationPolicySpec(
+        scheduling_mode=T.SCHEDULING_MODE_DIVIDE,
+        auto_migration=O.AutoMigration() if i % 4 == 0 else None)) for i in range(n_policies)]
+    ftc = O.FederatedTypeConfig("apps", "v1", "Deployment", "deployments", "Namespaced", "spec.replicas")
+    objs, opols = [], []
+    for w in range(W):
+        p = pols[int(rng.integers(0, n_policies))]
+        ann = {O.PROPAGATION_POLICY_NAME_LABEL: p.name}
+        annotations = {"kubectl.kubernetes.io/last-applied-configuration": "{}"}
+        r = rng.random()
+        if r < 0.05:
+            annotations[O.MAX_CLUSTERS_ANNOTATIONS] = str(int(rng.integers(1, 8)))
+        elif r < 0.10:
+            annotations[O.PLACEMENTS_ANNOTATIONS] = json.dumps(
+                [{"cluster": clusters[int(rng.integers(0, C))].name, "preferences": {"weight": int(rng.integers(1, 9))}}])
+        if p.spec.auto_migration is not None and rng.random() < 0.5:
+            annotations[O.AUTO_MIGRATION_INFO_ANNOTATION] = json.dumps(
+                {"estimatedCapacity": {clusters[int(rng.integers(0, C))].name: int(rng.integers(0, 50))}})
+        objs.append({"apiVersion": "types.kubeadmiral.io/v1alpha1", "kind": "FederatedDeployment",
+                     "metadata": {"name": f"app-{w}", "namespace": "default", "labels": ann,
+                                  "annotations": annotations},
+                     "spec": {"template": {"apiVersion": "apps/v1", "kind": "Deployment",
+                                           "metadata": {"name": f"app-{w}", "namespace": "default"},
+                                           "spec": {"replicas": int(rng.integers(1, 101))}}}})
+        opols.append(p)
+    return ftc, clusters, objs, opols

@@ -75,6 +75,7 @@ class Toleration:
     operator: str = ""
     value: str = ""
     effect: str = ""
+    toleration_seconds: Optional[int] = None  # not read by the scheduling path
 
     def to_json(self):
         d = {}
@@ -82,11 +83,14 @@ class Toleration:
             v = getattr(self, k)
             if v:
                 d[k] = v
+        if self.toleration_seconds is not None:
+            d["tolerationSeconds"] = self.toleration_seconds
         return d
 
     @staticmethod
     def from_json(d):
-        return Toleration(d.get("key", ""), d.get("operator", ""), d.get("value", ""), d.get("effect", ""))
+        return Toleration(d.get("key", ""), d.get("operator", ""), d.get("value", ""), d.get("effect", ""),
+                          d.get("tolerationSeconds"))
 
 
 @dataclass
@@ -94,13 +98,21 @@ class APIResource:
     group: str = ""
     version: str = ""
     kind: str = ""
+    plural_name: str = ""   # read by the scheduling-trigger hash only
+    scope: str = ""
 
     def to_json(self):
-        return {"group": self.group, "version": self.version, "kind": self.kind}
+        d = {"group": self.group, "version": self.version, "kind": self.kind}
+        if self.plural_name:
+            d["pluralName"] = self.plural_name
+        if self.scope:
+            d["scope"] = self.scope
+        return d
 
     @staticmethod
     def from_json(d):
-        return APIResource(d.get("group", ""), d.get("version", ""), d.get("kind", ""))
+        return APIResource(d.get("group", ""), d.get("version", ""), d.get("kind", ""), d.get("pluralName", ""),
+                           d.get("scope", ""))
 
 
 @dataclass

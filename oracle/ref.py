@@ -33,6 +33,8 @@ def lib():
         L.kad_ref_schedule.restype = ctypes.c_int
         L.kad_ref_select_row.argtypes = [ctypes.c_int, P, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32, P]
         L.kad_ref_select_row.restype = ctypes.c_int
+        L.kad_ref_trigger_hashes.argtypes = [ctypes.c_int, P, P, P, ctypes.c_int64, P, ctypes.c_int]
+        L.kad_ref_trigger_hashes.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -70,3 +72,16 @@ def select_row(scores, max_clusters=None, flags=0):
     if k < 0:
         return None
     return out[:k].tolist()
+
+
+def trigger_hashes(prefixes, suffix: bytes, n_threads=1):
+    """FNV-1 32 of prefix_i ‖ suffix per object, each end to end (schedulingtriggers.go:141-145)."""
+    off = np.zeros(len(prefixes) + 1, np.int64)
+    off[1:] = np.cumsum([len(p) for p in prefixes])
+    pre = np.frombuffer(b"".join(prefixes) or b"\0", np.uint8)
+    suf = np.frombuffer(suffix or b"\0", np.uint8)
+    out = np.zeros(max(1, len(prefixes)), np.uint32)
+    rc = lib().kad_ref_trigger_hashes(len(prefixes), _p(off), _p(pre), _p(suf), len(suffix), _p(out), n_threads)
+    if rc != 0:
+        raise RuntimeError(f"kad_ref_trigger_hashes failed: {rc}")
+    return out[:len(prefixes)]
