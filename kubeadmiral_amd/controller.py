@@ -1,0 +1,168 @@
+"""Batched reconcile: the scheduler controller's per-object loop, one GPU pass per batch.
+
+``Scheduler.reconcile`` (pkg/controllers/scheduler/scheduler.go:240-309) runs
+per federated object on ``--worker-count`` goroutines: look up the policy and
+profile (``prepareToSchedule``, :311-443), compute the scheduling-trigger hash
+and skip the object if it is unchanged (:394-421), build the SchedulingUnit and
+call ``ScheduleAlgorithm.Schedule`` (``schedule``, :445-521), then write the
+result back (``applySchedulingResult``, :632-695). :class:`BatchReconciler`
+takes a whole batch of objects through the same steps with the two hot
+stages batched on the GPU — every object's trigger hash in one
+``kad_trigger_run`` and every SchedulingUnit of one framework in one
+``kad_schedule`` — and returns, per object, what the reference's reconcile
+would have done (worker status, whether it scheduled, whether the object
+changed). Objects are mutated in place exactly as the reference mutates its
+deep copy before ``Update``.
+
+Out of scope (no API server here): pending-controller bookkeeping
+(``pendingcontrollers``), events, the ``Update`` call itself, webhook plugins
+(rejected by :class:`~kubeadmiral_amd.framework.Framework`), deletion
+timestamps. Policies and profiles are looked up in the dicts the caller passes
+(the informer caches of the reference).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import framework as F
+from . import objects as O
+from . import types as T
+from .runtime import BatchScheduler, Context, TriggerHasher
+
+STATUS_ALL_OK = "AllOK"   # worker.StatusAllOK
+STATUS_ERROR = "Error"    # worker.StatusError
+
+
+@dataclass
+class ReconcileOutcome:
+    status: str                                  # STATUS_ALL_OK / STATUS_ERROR
+    stage: str = ""                              # where the reconcile ended (see BatchReconciler.reconcile)
+    scheduled: bool = False                      # a result was computed and applied
+    modified: bool = False                       # applySchedulingResult changed the object
+    result: Optional[T.ScheduleResult] = None
+    error: str = ""
+
+
+class BatchReconciler:
+    """Scheduler.reconcile for a batch of federated objects of one FederatedTypeConfig."""
+
+    def __init__(self, type_config: O.FederatedTypeConfig, ctx: Optional[Context] = None, device: int = 0):
+        self.type_config = type_config
+        self.ctx = ctx if ctx is not None else Context(device)
+        self.hasher = TriggerHasher(self.ctx)
+        self.scheduler = BatchScheduler(self.ctx)
+        self._clusters_key = None
+
+    def _framework(self, profile: Optional[dict]) -> F.Framework:
+        """createFramework (scheduler.go:492, profile.go:52-82): default plugins + the profile's changes."""
+        return F.Framework(F.apply_profile(F.default_enabled_plugins(), profile))
+
+    def reconcile(self, objs: Sequence[dict], policies: Dict[Tuple[str, str], O.PropagationPolicy],
+                  clusters: List[T.FederatedCluster], profiles: Optional[Dict[str, Optional[dict]]] = None
+                  ) -> List[ReconcileOutcome]:
+        """Reconcile every object against the joined ``clusters``.
+
+        ``policies`` maps (namespace, name) → policy ("" namespace for
+        ClusterPropagationPolicies); ``profiles`` maps SchedulingProfile name →
+        its ``spec.plugins`` dict (None = no changes). Stages recorded in
+        ``ReconcileOutcome.stage``: ``policy-not-found``, ``profile-not-found``,
+        ``trigger-error``, ``unchanged`` (trigger hash equal), ``no-scheduling``,
+        ``unit-error``, ``framework-error``, ``schedule-error``, ``apply-error``,
+        ``scheduled``.
+        """
+        profiles = profiles or {}
+        out: List[Optional[ReconcileOutcome]] = [None] * len(objs)
+        ctx_pol: List[Optional[O.PropagationPolicy]] = [None] * len(objs)
+        ctx_prof: List[Optional[str]] = [None] * len(objs)
+
+        # prepareToSchedule :349-392 — policy and profile lookup
+        live = []
+        for i, obj in enumerate(objs):
+            key = O.matched_policy_key(obj, self.type_config.namespaced)
+            if key is not None:
+                pol = policies.get(key)
+                if pol is None:
+                    out[i] = ReconcileOutcome(STATUS_ALL_OK, "policy-not-found")
+                    continue
+                ctx_pol[i] = pol
+                name = pol.spec.scheduling_profile
+                if name:
+                    if name not in profiles:
+                        out[i] = ReconcileOutcome(STATUS_ALL_OK, "profile-not-found")
+                        continue
+                    ctx_prof[i] = name
+            live.append(i)
+
+        # :394-421 — trigger hashes for the whole batch in one GPU pass
+        key = id(clusters), len(clusters)
+        if key != self._clusters_key:
+            self.hasher.set_clusters(clusters)
+            self._clusters_key = key
+        hashed, prefixes = [], []
+        for i in live:
+            try:
+                prefixes.append(O.trigger_prefix(self.type_config, objs[i], ctx_pol[i]))
+                hashed.append(i)
+            except O.ObjectError as e:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "trigger-error", error=str(e))
+        self.ctx.trigger_prefixes_upload(prefixes)
+        self.ctx.trigger_run()
+        hashes = self.ctx.trigger_download()
+        to_schedule = []
+        for i, h in zip(hashed, hashes.tolist()):
+            changed = O.add_annotation(objs[i], O.SCHEDULING_TRIGGER_HASH_ANNOTATION, O.format_trigger_hash(h))
+            if not changed:
+                out[i] = ReconcileOutcome(STATUS_ALL_OK, "unchanged")
+            elif (O.get_annotations(objs[i]) or {}).get(O.NO_SCHEDULING_ANNOTATION, ""):
+                out[i] = ReconcileOutcome(STATUS_ALL_OK, "no-scheduling")
+            else:
+                to_schedule.append(i)
+
+        # schedule :445-521 — units grouped by framework, one GPU batch per framework
+        results: Dict[int, T.ScheduleResult] = {}
+        groups: Dict[Optional[str], List[Tuple[int, T.SchedulingUnit]]] = {}
+        for i in to_schedule:
+            if ctx_pol[i] is None:
+                results[i] = T.ScheduleResult({})  # :454-467 no policy: schedule to no clusters
+                continue
+            try:
+                su = O.scheduling_unit_for_fed_object(self.type_config, objs[i], ctx_pol[i])
+            except (O.ObjectError, O.GoPanic) as e:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "unit-error", error=str(e))
+                continue
+            groups.setdefault(ctx_prof[i], []).append((i, su))
+        for prof_name, members in groups.items():
+            try:
+                fwk = self._framework(profiles.get(prof_name) if prof_name else None)
+            except F.FrameworkError as e:
+                for i, _ in members:
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "framework-error", error=str(e))
+                continue
+            res = self.scheduler.schedule(fwk, [su for _, su in members], clusters)
+            for (i, _), r in zip(members, res):
+                if isinstance(r, T.ScheduleError):
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "schedule-error", error=str(r))
+                else:
+                    results[i] = r
+
+        # reconcile :291-308 + persistSchedulingResult → applySchedulingResult
+        for i, r in results.items():
+            pol = ctx_pol[i]
+            follower = False
+            threshold = None
+            try:
+                if pol is not None:
+                    follower = not pol.spec.disable_follower_scheduling
+                    am = pol.spec.auto_migration
+                    if am is not None:
+                        if am.when.pod_unschedulable_for is None:
+                            raise O.GoPanic("invalid memory address or nil pointer dereference")  # :302
+                        threshold = O.parse_duration(am.when.pod_unschedulable_for)
+                modified = O.apply_scheduling_result(self.type_config, objs[i], r, follower, threshold)
+            except (O.ObjectError, O.GoPanic) as e:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=r, error=str(e))
+                continue
+            out[i] = ReconcileOutcome(STATUS_ALL_OK, "scheduled", True, modified, r)
+        return out  # type: ignore[return-value]

@@ -1,0 +1,91 @@
+"""BatchReconciler (trigger hashes + packer + schedule + apply, on the GPU) == per-object CPU path.
+
+The expected outcome of every object is built the reference's way, one object
+at a time: trigger hash from oracle/triggers.py, SchedulingUnit from the
+packer, Schedule from the C oracle (oracle/kad_ref.c), result applied to a
+copy of the object. Then a second reconcile must find every trigger hash
+unchanged (scheduler.go:407-410), and a cluster label change must reschedule.
+"""
+
+import copy
+
+import numpy as np
+import pytest
+
+from kubeadmiral_amd import framework as F
+from kubeadmiral_amd import objects as O
+from kubeadmiral_amd import pack, synth
+from kubeadmiral_amd import types as T
+from kubeadmiral_amd.results import to_schedule_result
+from oracle import ref
+from oracle import triggers as OT
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected(ftc, objs, pols_by_key, clusters):
+    objs = copy.deepcopy(objs)
+    fwk = F.Framework()
+    snap = pack.Snapshot(clusters)
+    outs = []
+    for obj in objs:
+        key = O.matched_policy_key(obj, True)
+        pol = pols_by_key.get(key) if key else None
+        if key is not None and pol is None:
+            outs.append(("policy-not-found", None))
+            continue
+        ann = O.get_annotations(obj) or {}
+        h = OT.trigger_hash(ann, O.get_replica_count(ftc, obj),
+                            None if pol is None else (pol.name, pol.generation, pol.spec.auto_migration is not None),
+                            clusters)
+        O.add_annotation(obj, O.SCHEDULING_TRIGGER_HASH_ANNOTATION, h)
+        if pol is None:
+            r = T.ScheduleResult({})
+        else:
+            su = O.scheduling_unit_for_fed_object(ftc, obj, pol)
+            batch = pack.Batch(snap, fwk, [su])
+            r = to_schedule_result(ref.schedule(snap, batch, fwk), 0, su, snap.names)
+            if isinstance(r, T.ScheduleError):
+                outs.append(("schedule-error", None))
+                continue
+        thr = None
+        if pol is not None and pol.spec.auto_migration is not None:
+            thr = O.parse_duration(pol.spec.auto_migration.when.pod_unschedulable_for)
+        follower = pol is not None and not pol.spec.disable_follower_scheduling
+        O.apply_scheduling_result(ftc, obj, r, follower, thr)
+        outs.append(("scheduled", r))
+    return objs, outs
+
+
+def test_batch_reconcile_matches_per_object_path():
+    from kubeadmiral_amd.controller import BatchReconciler
+
+    ftc, clusters, objs, pols = synth.gen_trigger_workload(np.random.default_rng(5), 400, 16, n_policies=8)
+    by_key = {}
+    for p in pols:
+        if p.spec.auto_migration is not None:
+            p.spec.auto_migration.when.pod_unschedulable_for = "2m"
+        by_key[(p.namespace, p.name)] = p
+    # a few objects without a policy label, and one whose policy is missing
+    for o in objs[:5]:
+        del o["metadata"]["labels"][O.PROPAGATION_POLICY_NAME_LABEL]
+    objs[5]["metadata"]["labels"][O.PROPAGATION_POLICY_NAME_LABEL] = "missing"
+    want_objs, want = _expected(ftc, objs, by_key, clusters)
+
+    rec = BatchReconciler(ftc)
+    got = rec.reconcile(objs, by_key, clusters)
+    for i, (g, (stage, r)) in enumerate(zip(got, want)):
+        assert g.stage == stage, i
+        if stage == "scheduled":
+            assert g.result == r, i
+    assert objs == want_objs
+
+    # nothing changed: every scheduled object is skipped on the trigger hash
+    again = rec.reconcile(objs, by_key, clusters)
+    assert [g.stage for g in again] == ["policy-not-found" if s == "policy-not-found" else "unchanged"
+                                        for s, _ in want]
+    # a cluster label change is a scheduling trigger
+    clusters2 = copy.deepcopy(clusters)
+    clusters2[0].labels = dict(clusters2[0].labels or {}, extra="1")
+    third = rec.reconcile(objs, by_key, clusters2)
+    assert all(g.stage in ("scheduled", "policy-not-found") for g in third)
