@@ -42,9 +42,11 @@ WORKLOAD_DESC = {
     "t1": "scheduling-trigger hashes: 1k federated Deployments x 16 joined clusters",
     "t2": "scheduling-trigger hashes: 100k federated Deployments x 256 joined clusters (~1.6 MB cluster part)",
 }
-# VALU issue bound of one FNV-1 step per lane (v_mul_lo_u32 at quarter rate + one v_bitop3/v_xor):
-# 20 SIMD cycles per 64 steps → 3.2 steps/cycle/SIMD × 4 SIMDs × 256 CUs × 2.4 GHz
-FNV_STEP_PEAK = 3.2 * 4 * 256 * 2.4e9
+# Issue bound of one FNV-1 step per lane: the inner loop is one v_mul_lo_u32 (quarter rate: 16 SIMD cycles per
+# wave64 instruction) + one v_bitop3_b32 per byte. The round-1 t2 run measured 3.64 steps/cycle/SIMD, above the
+# 3.2 of issuing both back to back, so the bitop overlaps the multiply: the bound is the multiply alone,
+# 4 steps/cycle/SIMD × 4 SIMDs × 256 CUs × 2.4 GHz.
+FNV_STEP_PEAK = 4.0 * 4 * 256 * 2.4e9
 
 
 def log(*a):
