@@ -135,9 +135,35 @@ typedef struct kad_snapshot_header {
   int32_t n_scalar;      /* S  */
   int32_t reserved0;
   uint64_t total_bytes;
-  uint64_t fingerprint; /* batches carry it: packed against this snapshot  */
+  uint64_t fingerprint; /* vocabulary fingerprint (cluster names in order and
+                           the interned label / taint / API-resource / scalar
+                           ids a batch is packed against); batches carry it */
   uint64_t off[KAD_S_NARRAYS];
 } kad_snapshot_header;
+
+/* ----------------------------------------------- snapshot delta blob
+ * Cluster informer updates (scheduler.go:157-177) that change existing
+ * clusters without growing the vocabulary — resources (the common case:
+ * status collection), a label to an already-interned value, a known taint —
+ * are applied to the resident snapshot in place: the delta carries the
+ * changed clusters' columns of every snapshot array, so batches packed
+ * against the snapshot stay valid. Anything else (cluster join/leave, a new
+ * label value, taint, API resource or scalar name) needs a full upload.
+ * Layout: header, i32 idx[n_changed] (snapshot positions, strictly
+ * increasing), then for each snapshot array a its rows for the changed
+ * clusters, element [r][j] at off[a] + (r*n_changed + j)*elem_size(a), rows
+ * and element sizes as in the snapshot (1 / S / GW / TW / K rows).          */
+#define KAD_DELTA_MAGIC 0x4441444Bu /* "KADD" */
+typedef struct kad_snapshot_delta_header {
+  uint32_t magic;
+  uint32_t abi_version;
+  int32_t n_clusters;   /* must equal the resident snapshot's C            */
+  int32_t n_changed;    /* clusters rewritten                              */
+  uint64_t total_bytes;
+  uint64_t fingerprint; /* must equal the resident snapshot's fingerprint  */
+  uint64_t idx_off;     /* i32[n_changed]                                  */
+  uint64_t off[KAD_S_NARRAYS];
+} kad_snapshot_delta_header;
 
 /* --------------------------------------------------------- batch blob
  * W scheduling units; CSR arrays are indexed by *_OFF[w] .. *_OFF[w+1].    */
@@ -290,6 +316,11 @@ int kad_abi_version(void);
  * kad_schedule.                                                              */
 int kad_snapshot_upload(kad_ctx* ctx, const void* blob, size_t nbytes);
 int kad_snapshot_upload_device(kad_ctx* ctx, const void* dev_blob, size_t nbytes);
+/* Apply a kad_snapshot_delta blob to the resident snapshot (one H2D of the
+ * delta + one scatter kernel, ordered on the ctx stream after any schedule
+ * already issued). The resident batch stays valid.  ← cluster update events
+ * (scheduler.go:157-177) that re-enqueue objects against changed clusters. */
+int kad_snapshot_update(kad_ctx* ctx, const void* delta, size_t nbytes);
 int kad_batch_upload(kad_ctx* ctx, const void* blob, size_t nbytes);
 
 /* Run the pipeline for the resident batch; asynchronous on the ctx stream. */

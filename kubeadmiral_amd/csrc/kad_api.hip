@@ -51,6 +51,9 @@ struct kad_ctx {
   size_t scratch_bytes = 0;
   bool have_snapshot = false, have_batch = false, ran = false;
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
+  std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
+  void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
+  size_t delta_cap = 0;
   bool batch_defer = false;    // some unit uses a feature the lean kernel defers
   // scheduling-trigger hashes (kad_trigger_*)
   void* t_suffix = nullptr;
@@ -137,7 +140,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_sw, c->d_cw, c->d_defer,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -188,6 +191,30 @@ static int check_snapshot_header(kad_ctx* c, const kad_snapshot_header& h, size_
   return 0;
 }
 
+static const int kResArrays[4] = {KAD_S_ALLOC_CPU, KAD_S_ALLOC_MEM, KAD_S_USED_CPU, KAD_S_USED_MEM};
+
+static bool res_negative(const std::vector<int64_t>& v) {
+  bool neg = false;
+  for (int64_t x : v) neg |= x < 0 || x >= (1ll << 46);
+  return neg;
+}
+
+// rows and element size of snapshot array a (include/kad_sched.h, enum kad_snapshot_array)
+static void snapshot_array_shape(const kad_snapshot_header& h, int a, int64_t* rows, int* esz) {
+  *rows = 1;
+  *esz = 8;
+  switch (a) {
+    case KAD_S_ALLOC_SCALAR: case KAD_S_USED_SCALAR: *rows = h.n_scalar; break;
+    case KAD_S_GVK: *rows = h.n_gvk_words; break;
+    case KAD_S_TAINT_NSNE: case KAD_S_TAINT_NE: case KAD_S_TAINT_PNS: *rows = h.n_taint_words; break;
+    case KAD_S_LABEL_VAL: *rows = h.n_label_keys; *esz = 4; break;
+    case KAD_S_LABEL_INT: *rows = h.n_label_keys; break;
+    case KAD_S_LABEL_INT_OK: *rows = h.n_label_keys; *esz = 1; break;
+    case KAD_S_NAME_FNV: case KAD_S_CFLAGS: *esz = 4; break;
+    default: break;
+  }
+}
+
 int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   if (!c || !blob) return KAD_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -200,11 +227,12 @@ int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->snap_hdr = h;
   if (int r = bind_snapshot(c, h)) return r;
-  c->snap_negative = false;
-  for (int a : {KAD_S_ALLOC_CPU, KAD_S_ALLOC_MEM, KAD_S_USED_CPU, KAD_S_USED_MEM}) {
-    const int64_t* v = at<int64_t>(blob, h.off, a);
-    for (int i = 0; i < h.n_clusters; i++) c->snap_negative |= v[i] < 0 || v[i] >= (1ll << 46);
+  c->h_res.assign((size_t)4 * h.n_clusters, 0);
+  {
+    for (int q = 0; q < 4; q++)
+      if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
   }
+  c->snap_negative = res_negative(c->h_res);
   c->have_snapshot = true;
   c->have_batch = false;
   return KAD_OK;
@@ -222,17 +250,72 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->snap_hdr = h;
   if (int r = bind_snapshot(c, h)) return r;
-  c->snap_negative = false;
+  c->h_res.assign((size_t)4 * h.n_clusters, 0);
   {
-    std::vector<int64_t> v((size_t)h.n_clusters);
-    for (int a : {KAD_S_ALLOC_CPU, KAD_S_ALLOC_MEM, KAD_S_USED_CPU, KAD_S_USED_MEM}) {
+    for (int q = 0; q < 4; q++)
       if (h.n_clusters)
-        HIPCHK(c, hipMemcpy(v.data(), static_cast<const char*>(dev_blob) + h.off[a], v.size() * 8, hipMemcpyDeviceToHost));
-      for (int64_t x : v) c->snap_negative |= x < 0 || x >= (1ll << 46);
-    }
+        HIPCHK(c, hipMemcpy(c->h_res.data() + (size_t)q * h.n_clusters, static_cast<const char*>(dev_blob) + h.off[kResArrays[q]],
+                            (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
   }
+  c->snap_negative = res_negative(c->h_res);
   c->have_snapshot = true;
   c->have_batch = false;
+  return KAD_OK;
+}
+
+int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
+  if (!c || !delta) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot uploaded");
+  kad_snapshot_delta_header h;
+  if (nbytes < sizeof(h)) return fail(c, KAD_EINVAL, "delta too small");
+  std::memcpy(&h, delta, sizeof(h));
+  const kad_snapshot_header& sh = c->snap_hdr;
+  if (h.magic != KAD_DELTA_MAGIC) return fail(c, KAD_EINVAL, "bad delta magic");
+  if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "delta ABI version mismatch");
+  if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "delta size mismatch");
+  if (h.n_clusters != sh.n_clusters || h.fingerprint != sh.fingerprint)
+    return fail(c, KAD_EINVAL, "delta was packed against a different snapshot vocabulary");
+  const int n = h.n_changed, C = sh.n_clusters;
+  if (n < 0 || n > C) return fail(c, KAD_EINVAL, "bad n_changed");
+  if (n == 0) return KAD_OK;
+  if (h.idx_off > nbytes || (h.idx_off & 3) || h.idx_off + (uint64_t)n * 4 > nbytes)
+    return fail(c, KAD_EINVAL, "bad delta index offset");
+  const int32_t* idx = reinterpret_cast<const int32_t*>(static_cast<const char*>(delta) + h.idx_off);
+  for (int j = 0; j < n; j++)
+    if (idx[j] < 0 || idx[j] >= C || (j && idx[j] <= idx[j - 1]))
+      return fail(c, KAD_EINVAL, "delta cluster indices must be strictly increasing snapshot positions");
+  DeltaDev d{};
+  d.n = n;
+  d.C = C;
+  d.start[0] = 0;
+  for (int a = 0; a < KAD_S_NARRAYS; a++) {
+    int64_t rows;
+    int esz;
+    snapshot_array_shape(sh, a, &rows, &esz);
+    const uint64_t len = (uint64_t)rows * n * esz;
+    if (h.off[a] > nbytes || (h.off[a] % esz) || h.off[a] + len > nbytes)
+      return fail(c, KAD_EINVAL, "bad delta array offset");
+    d.s_off[a] = sh.off[a];
+    d.d_off[a] = h.off[a];
+    d.esz[a] = esz;
+    d.start[a + 1] = d.start[a] + rows * n;
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int r = grow(c, &c->d_delta, &c->delta_cap, nbytes)) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_delta, delta, nbytes, hipMemcpyHostToDevice, c->stream));
+  d.snap = static_cast<uint8_t*>(c->d_snap);
+  d.delta = static_cast<const uint8_t*>(c->d_delta);
+  d.idx = reinterpret_cast<const int32_t*>(d.delta + h.idx_off);
+  HIPCHK(c, launch_snapshot_delta(d, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's delta buffer is free on return
+  {
+    for (int q = 0; q < 4; q++) {
+      const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
+      for (int j = 0; j < n; j++) c->h_res[(size_t)q * C + idx[j]] = v[j];
+    }
+  }
+  c->snap_negative = res_negative(c->h_res);
   return KAD_OK;
 }
 

@@ -132,4 +132,17 @@ hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t*
 hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, void* global_scratch, size_t scratch_bytes,
                             hipStream_t st);
 
+// kad_snapshot_update: scatter the changed clusters' columns of every snapshot
+// array from a resident delta blob into the resident snapshot blob.
+struct DeltaDev {
+  uint8_t* snap;
+  const uint8_t* delta;
+  const int32_t* idx;  // [n] snapshot positions of the changed clusters
+  int n, C;
+  uint64_t s_off[KAD_S_NARRAYS], d_off[KAD_S_NARRAYS];
+  int32_t esz[KAD_S_NARRAYS];
+  int64_t start[KAD_S_NARRAYS + 1];  // prefix of rows(a) * n: element ranges per array
+};
+hipError_t launch_snapshot_delta(const DeltaDev& d, hipStream_t st);
+
 }  // namespace kad

@@ -115,11 +115,24 @@ def _csr(rows: List[list], dtype) -> tuple:
 
 # ===================================================================== snapshot
 class Snapshot:
-    """A packed cluster snapshot plus the host-side vocabularies the batch packer needs."""
+    """A packed cluster snapshot plus the host-side vocabularies the batch packer needs.
+
+    Two passes over the clusters: :meth:`_intern` assigns vocabulary ids (label
+    keys / values, taints by occurrence, API resources, scalar resource names,
+    in cluster order), :meth:`_columns` computes one cluster's column of every
+    snapshot array against that vocabulary. :meth:`update` reuses the second
+    pass for cluster update events that fit the existing vocabulary.
+    """
+
+    # snapshot arrays in enum kad_snapshot_array order: (dtype, rows attribute or None = 1 row)
+    ARRAYS = [(np.int64, None), (np.int64, None), (np.int64, None), (np.int64, None), (np.int64, "S"),
+              (np.int64, "S"), (np.int64, None), (np.int64, None), (np.uint64, "GW"), (np.uint64, "TW"),
+              (np.uint64, "TW"), (np.uint64, "TW"), (np.int32, "K"), (np.int64, "K"), (np.uint8, "K"),
+              (np.uint32, None), (np.uint32, None)]
 
     def __init__(self, clusters: List[T.FederatedCluster]):
         C = len(clusters)
-        self.clusters = clusters
+        self.clusters = list(clusters)
         self.names = [c.name for c in clusters]
         self.name_id: Dict[str, int] = {}
         for i, n in enumerate(self.names):
@@ -127,116 +140,189 @@ class Snapshot:
                 raise ValueError(f"duplicate cluster name {n!r} in snapshot")
             self.name_id[n] = i
         self.C = C
-
-        alloc_cpu = np.zeros(C, np.int64)
-        alloc_mem = np.zeros(C, np.int64)
-        used_cpu = np.zeros(C, np.int64)
-        used_mem = np.zeros(C, np.int64)
-        alloc_cores = np.zeros(C, np.int64)
-        avail_cores = np.zeros(C, np.int64)
-        cflags = np.zeros(C, np.uint32)
-        name_fnv = np.zeros(C, np.uint32)
-        scal_alloc: List[dict] = []
-        scal_used: List[dict] = []
         self.scalar_id: Dict[str, int] = {}
         self.gvk_id: Dict[tuple, int] = {}
         self.taint_id: Dict[tuple, int] = {}
         self.taint_defs: List[T.Taint] = []
         self.label_key_id: Dict[str, int] = {}
         self.label_vals: List[Dict[str, int]] = []
-        cl_taints, cl_gvk = [], []
-
+        for c in clusters:
+            self._intern(c)
+        self.S = len(self.scalar_id)
+        self.GW = _words(len(self.gvk_id))
+        self.TW = _words(len(self.taint_defs))
+        self.K = len(self.label_vals)
+        arrays = [np.zeros((self._rows(r), C) if r else C, dt) for dt, r in self.ARRAYS]
         for i, c in enumerate(clusters):
-            a = _Resource.new(c.allocatable)
-            u = _Resource.new(c.allocatable)
-            if u.sub(c.available):
-                cflags[i] |= 1
-            alloc_cpu[i], alloc_mem[i] = a.milli_cpu, a.memory
-            used_cpu[i], used_mem[i] = u.milli_cpu, u.memory
-            scal_alloc.append(a.scalar or {})
-            scal_used.append(u.scalar or {})
-            for n in list(a.scalar or {}) + list(u.scalar or {}):
-                self.scalar_id.setdefault(n, len(self.scalar_id))
-            # rsp.go:286-325: cpu defaults to "0" and is summed with the listed quantity
-            alloc_cores[i] = k8s.value(k8s.quantity("0") + k8s.quantity(c.allocatable["cpu"])) \
-                if c.allocatable and "cpu" in c.allocatable else 0
-            avail_cores[i] = k8s.value(k8s.quantity("0") + k8s.quantity(c.available["cpu"])) \
-                if c.available and "cpu" in c.available else 0
-            name_fnv[i] = k8s.fnv1_32(c.name.encode())
-            ids = []
-            for r in c.api_resource_types:
-                ids.append(self.gvk_id.setdefault((r.group, r.version, r.kind), len(self.gvk_id)))
-            cl_gvk.append(ids)
-            seen: Dict[tuple, int] = {}
-            tids = []
-            for t in c.taints:
-                base = (t.key, t.value, t.effect)
-                occ = seen.get(base, 0)
-                seen[base] = occ + 1
-                key = base + (occ,)
-                if key not in self.taint_id:
-                    self.taint_id[key] = len(self.taint_defs)
-                    self.taint_defs.append(t)
-                tids.append((self.taint_id[key], t.effect))
-            cl_taints.append(tids)
-            for k, v in (c.labels or {}).items():
-                kid = self.label_key_id.get(k)
-                if kid is None:
-                    kid = self.label_key_id[k] = len(self.label_vals)
-                    self.label_vals.append({})
-                self.label_vals[kid].setdefault(v, len(self.label_vals[kid]))
-
-        S = len(self.scalar_id)
-        alloc_s = np.zeros((S, C), np.int64)
-        used_s = np.zeros((S, C), np.int64)
-        for i in range(C):
-            for n, v in scal_alloc[i].items():
-                alloc_s[self.scalar_id[n], i] = v
-            for n, v in scal_used[i].items():
-                used_s[self.scalar_id[n], i] = v
-        GW = _words(len(self.gvk_id))
-        gvk = np.zeros((GW, C), np.uint64)
-        for i, ids in enumerate(cl_gvk):
-            for g in ids:
-                gvk[g // 64, i] |= np.uint64(1 << (g % 64))
-        TW = _words(len(self.taint_defs))
-        nsne = np.zeros((TW, C), np.uint64)
-        ne = np.zeros((TW, C), np.uint64)
-        pns = np.zeros((TW, C), np.uint64)
-        for i, tids in enumerate(cl_taints):
-            for tid, eff in tids:
-                bit = np.uint64(1 << (tid % 64))
-                if eff in (T.TAINT_NO_SCHEDULE, T.TAINT_NO_EXECUTE):
-                    nsne[tid // 64, i] |= bit
-                if eff == T.TAINT_NO_EXECUTE:
-                    ne[tid // 64, i] |= bit
-                if eff == T.TAINT_PREFER_NO_SCHEDULE:
-                    pns[tid // 64, i] |= bit
-        K = len(self.label_vals)
-        lval = np.full((K, C), -1, np.int32)
-        lint = np.zeros((K, C), np.int64)
-        lok = np.zeros((K, C), np.uint8)
-        for i, c in enumerate(clusters):
-            for k, v in (c.labels or {}).items():
-                kid = self.label_key_id[k]
-                lval[kid, i] = self.label_vals[kid][v]
-                iv, ok = k8s.parse_int64(v)
-                if ok:
-                    lint[kid, i] = iv
-                    lok[kid, i] = 1
-        self.TW, self.GW, self.K, self.S = TW, GW, K, S
-        arrays = [alloc_cpu, alloc_mem, used_cpu, used_mem, alloc_s, used_s, alloc_cores, avail_cores, gvk, nsne,
-                  ne, pns, lval, lint, lok, name_fnv, cflags]
-        h = hashlib.blake2b(digest_size=8)
-        for a in arrays:
-            h.update(np.ascontiguousarray(a).tobytes())
-        self.fingerprint = int.from_bytes(h.digest(), "little")
+            for a, col in zip(arrays, self._columns(c)):
+                a[..., i] = col
+        self.fingerprint = self._vocab_fingerprint()
         hdr = SnapshotHeader()
         hdr.magic, hdr.abi_version = SNAPSHOT_MAGIC, ABI_VERSION
-        hdr.n_clusters, hdr.n_gvk_words, hdr.n_taint_words, hdr.n_label_keys, hdr.n_scalar = C, GW, TW, K, S
+        hdr.n_clusters, hdr.n_gvk_words, hdr.n_taint_words, hdr.n_label_keys, hdr.n_scalar = \
+            C, self.GW, self.TW, self.K, self.S
         hdr.fingerprint = self.fingerprint
         self.blob = _assemble(hdr, arrays)
-        self.arrays = arrays
+        self.offsets = list(hdr.off)
+        # the arrays live inside the blob from here on: update() writes through these views
+        self.arrays = [self.blob[o:o + a.nbytes].view(a.dtype).reshape(a.shape) for o, a in zip(self.offsets, arrays)]
+
+    def _rows(self, attr: Optional[str]) -> int:
+        return 1 if attr is None else getattr(self, attr)
+
+    def _intern(self, c: T.FederatedCluster) -> None:
+        a = _Resource.new(c.allocatable)
+        u = _Resource.new(c.allocatable)
+        u.sub(c.available)
+        for n in list(a.scalar or {}) + list(u.scalar or {}):
+            self.scalar_id.setdefault(n, len(self.scalar_id))
+        for r in c.api_resource_types:
+            self.gvk_id.setdefault((r.group, r.version, r.kind), len(self.gvk_id))
+        seen: Dict[tuple, int] = {}
+        for t in c.taints:
+            base = (t.key, t.value, t.effect)
+            occ = seen.get(base, 0)
+            seen[base] = occ + 1
+            key = base + (occ,)
+            if key not in self.taint_id:
+                self.taint_id[key] = len(self.taint_defs)
+                self.taint_defs.append(t)
+        for k, v in (c.labels or {}).items():
+            kid = self.label_key_id.get(k)
+            if kid is None:
+                kid = self.label_key_id[k] = len(self.label_vals)
+                self.label_vals.append({})
+            self.label_vals[kid].setdefault(v, len(self.label_vals[kid]))
+
+    def _columns(self, c: T.FederatedCluster) -> Optional[list]:
+        """Cluster ``c``'s column of every snapshot array, or None if it needs a vocabulary entry not interned."""
+        a = _Resource.new(c.allocatable)
+        u = _Resource.new(c.allocatable)
+        cflags = 1 if u.sub(c.available) else 0
+        S, GW, TW, K = self.S, self.GW, self.TW, self.K
+        alloc_s, used_s = np.zeros(S, np.int64), np.zeros(S, np.int64)
+        for m, dst in ((a.scalar or {}, alloc_s), (u.scalar or {}, used_s)):
+            for n, v in m.items():
+                sid = self.scalar_id.get(n)
+                if sid is None:
+                    return None
+                dst[sid] = v
+        # rsp.go:286-325: cpu defaults to "0" and is summed with the listed quantity
+        alloc_cores = k8s.value(k8s.quantity("0") + k8s.quantity(c.allocatable["cpu"])) \
+            if c.allocatable and "cpu" in c.allocatable else 0
+        avail_cores = k8s.value(k8s.quantity("0") + k8s.quantity(c.available["cpu"])) \
+            if c.available and "cpu" in c.available else 0
+        gvk = np.zeros(GW, np.uint64)
+        for r in c.api_resource_types:
+            g = self.gvk_id.get((r.group, r.version, r.kind))
+            if g is None:
+                return None
+            gvk[g // 64] |= np.uint64(1 << (g % 64))
+        nsne, ne, pns = np.zeros(TW, np.uint64), np.zeros(TW, np.uint64), np.zeros(TW, np.uint64)
+        seen: Dict[tuple, int] = {}
+        for t in c.taints:
+            base = (t.key, t.value, t.effect)
+            occ = seen.get(base, 0)
+            seen[base] = occ + 1
+            tid = self.taint_id.get(base + (occ,))
+            if tid is None:
+                return None
+            bit = np.uint64(1 << (tid % 64))
+            if t.effect in (T.TAINT_NO_SCHEDULE, T.TAINT_NO_EXECUTE):
+                nsne[tid // 64] |= bit
+            if t.effect == T.TAINT_NO_EXECUTE:
+                ne[tid // 64] |= bit
+            if t.effect == T.TAINT_PREFER_NO_SCHEDULE:
+                pns[tid // 64] |= bit
+        lval, lint, lok = np.full(K, -1, np.int32), np.zeros(K, np.int64), np.zeros(K, np.uint8)
+        for k, v in (c.labels or {}).items():
+            kid = self.label_key_id.get(k)
+            if kid is None or v not in self.label_vals[kid]:
+                return None
+            lval[kid] = self.label_vals[kid][v]
+            iv, ok = k8s.parse_int64(v)
+            if ok:
+                lint[kid] = iv
+                lok[kid] = 1
+        return [a.milli_cpu, a.memory, u.milli_cpu, u.memory, alloc_s, used_s, alloc_cores, avail_cores, gvk, nsne,
+                ne, pns, lval, lint, lok, k8s.fnv1_32(c.name.encode()), cflags]
+
+    def _vocab_fingerprint(self) -> int:
+        h = hashlib.blake2b(digest_size=8)
+        h.update(repr((self.C, self.names, list(self.scalar_id), list(self.gvk_id), list(self.taint_id),
+                       list(self.label_key_id), [list(v) for v in self.label_vals])).encode())
+        return int.from_bytes(h.digest(), "little")
+
+    def update(self, clusters: List[T.FederatedCluster]) -> Optional["SnapshotDelta"]:
+        """Apply cluster update events in place; returns the delta for ``kad_snapshot_update``.
+
+        ``clusters`` is the new cluster list. Returns None — the caller repacks
+        (``Snapshot(clusters)``) and re-uploads — when the names or their order
+        changed (join / leave) or a changed cluster needs a vocabulary entry
+        that is not interned yet. Otherwise the changed clusters' columns are
+        written into this snapshot's blob and the same columns come back as a
+        delta blob; the vocabulary (and with it every packed batch) stays valid.
+        """
+        if len(clusters) != self.C or any(c.name != n for c, n in zip(clusters, self.names)):
+            return None
+        changed, cols = [], []
+        for i, (old, new) in enumerate(zip(self.clusters, clusters)):
+            if old is new or old == new:
+                continue
+            col = self._columns(new)
+            if col is None:
+                return None
+            changed.append(i)
+            cols.append(col)
+        for i, col in zip(changed, cols):
+            for a, v in zip(self.arrays, col):
+                a[..., i] = v
+        self.clusters = list(clusters)
+        return SnapshotDelta(self, changed, cols)
+
+
+DELTA_MAGIC = 0x4441444B
+
+
+class SnapshotDeltaHeader(ctypes.Structure):
+    _fields_ = [("magic", ctypes.c_uint32), ("abi_version", ctypes.c_uint32), ("n_clusters", ctypes.c_int32),
+                ("n_changed", ctypes.c_int32), ("total_bytes", ctypes.c_uint64), ("fingerprint", ctypes.c_uint64),
+                ("idx_off", ctypes.c_uint64), ("off", ctypes.c_uint64 * S_NARRAYS)]
+
+
+class SnapshotDelta:
+    """A kad_snapshot_delta blob: the changed clusters' columns of every snapshot array ([rows][n_changed])."""
+
+    def __init__(self, snap: Snapshot, changed: List[int], cols: List[list]):
+        n = len(changed)
+        self.changed = changed
+        arrays = [np.array(changed, np.int32)]
+        for k, (dt, r) in enumerate(Snapshot.ARRAYS):
+            rows = snap._rows(r)
+            m = np.zeros((rows, n) if r else n, dt)
+            for j, col in enumerate(cols):
+                m[..., j] = col[k]
+            arrays.append(m)
+        hdr = SnapshotDeltaHeader()
+        hdr.magic, hdr.abi_version, hdr.n_clusters, hdr.n_changed = DELTA_MAGIC, ABI_VERSION, snap.C, n
+        hdr.fingerprint = snap.fingerprint
+        # _assemble fills a header's `off` array; lay the index array out first, then the snapshot arrays
+        pos = (ctypes.sizeof(hdr) + ALIGN - 1) // ALIGN * ALIGN
+        offs = []
+        for a in arrays:
+            offs.append(pos)
+            pos += (a.nbytes + ALIGN - 1) // ALIGN * ALIGN
+        blob = np.zeros(max(pos, ALIGN), np.uint8)
+        for o, a in zip(offs, arrays):
+            if a.nbytes:
+                blob[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        hdr.idx_off = offs[0]
+        for k, o in enumerate(offs[1:]):
+            hdr.off[k] = o
+        hdr.total_bytes = len(blob)
+        hb = bytes(hdr)
+        blob[:len(hb)] = np.frombuffer(hb, np.uint8)
+        self.blob = blob
 
 
 class _Resource:

@@ -19,7 +19,7 @@ import numpy as np
 
 from . import types as T
 from .framework import Framework
-from .pack import Batch, Snapshot
+from .pack import Batch, Snapshot, SnapshotDelta
 from .results import BatchResult, to_schedule_result
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -66,6 +66,7 @@ def load_library(path: str = LIB_PATH):
     L.kad_last_error.restype = ctypes.c_char_p
     L.kad_snapshot_upload.argtypes = [P, P, SZ]
     L.kad_snapshot_upload_device.argtypes = [P, P, SZ]
+    L.kad_snapshot_update.argtypes = [P, P, SZ]
     L.kad_batch_upload.argtypes = [P, P, SZ]
     L.kad_schedule.argtypes = [P, P]
     L.kad_sync.argtypes = [P]
@@ -124,6 +125,10 @@ class Context:
     def upload_snapshot_device(self, dev_ptr: int, nbytes: int, snap: Optional[Snapshot] = None):
         self._chk(self.L.kad_snapshot_upload_device(self.h, ctypes.c_void_p(dev_ptr), nbytes))
         self.snap = snap
+
+    def update_snapshot(self, delta: SnapshotDelta):
+        """kad_snapshot_update: patch the resident snapshot; the resident batch stays valid."""
+        self._chk(self.L.kad_snapshot_update(self.h, _p(delta.blob), delta.blob.nbytes))
 
     def upload_batch(self, batch: Batch):
         self._chk(self.L.kad_batch_upload(self.h, _p(batch.blob), batch.blob.nbytes))
@@ -274,17 +279,33 @@ class BatchScheduler:
 
     def __init__(self, ctx: Optional[Context] = None, device: int = 0):
         self.ctx = ctx if ctx is not None else Context(device)
-        self._snap_key = None
+        self._clusters: Optional[List[T.FederatedCluster]] = None
+        self.full_uploads = 0   # snapshot (re)packs + uploads
+        self.delta_updates = 0  # in-place kad_snapshot_update calls
 
     def set_clusters(self, clusters: List[T.FederatedCluster]) -> Snapshot:
+        """Make ``clusters`` the resident snapshot: an in-place delta when only existing clusters changed
+        within the interned vocabulary (cluster status / label / taint events, scheduler.go:157-177), else a
+        repack and full upload (join, leave, new label value / taint / API resource)."""
+        snap = self.ctx.snap
+        if snap is not None:
+            delta = snap.update(clusters)
+            if delta is not None:
+                if delta.changed:
+                    self.ctx.update_snapshot(delta)
+                    self.delta_updates += 1
+                self._clusters = clusters
+                return snap
         snap = Snapshot(clusters)
         self.ctx.upload_snapshot(snap)
+        self.full_uploads += 1
+        self._clusters = clusters
         return snap
 
     def schedule(self, fwk: Framework, units: List[T.SchedulingUnit], clusters: List[T.FederatedCluster]
                  ) -> List[Union[T.ScheduleResult, T.ScheduleError]]:
         snap = self.ctx.snap
-        if snap is None or snap.clusters is not clusters:
+        if snap is None or self._clusters is not clusters:
             snap = self.set_clusters(clusters)
         batch = Batch(snap, fwk, units)
         res = self.ctx.run(fwk, batch)

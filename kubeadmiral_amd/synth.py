@@ -16,13 +16,14 @@ shapes and distributions of SURVEY.md §8(d):
 
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import json
 
 import numpy as np
 
 from . import framework as F
+from . import k8s
 from . import types as T
 
 GI = 1 << 30
@@ -395,3 +396,45 @@ def gen_trigger_workload(rng: np.random.Generator, W: int, C: int, n_policies: i
                                            "spec": {"replicas": int(rng.integers(1, 101))}}}})
         opols.append(p)
     return ftc, clusters, objs, opols
+
+
+# ------------------------------------------------------- cluster update events
+def mutate_clusters(rng: np.random.Generator, clusters: List[T.FederatedCluster], n_changed: int,
+                    structural: bool = True) -> Tuple[List[T.FederatedCluster], List[int]]:
+    """A cluster informer update: ``n_changed`` clusters get new status resources (the periodic status
+    collection) and, with ``structural``, label values / taints / API resources drawn from what the other
+    clusters already carry (so the snapshot vocabulary does not grow). Returns (new list, changed positions)."""
+    import copy
+
+    vals: Dict[str, list] = {}
+    taints, apis = {}, {}
+    for c in clusters:
+        for k, v in (c.labels or {}).items():
+            vals.setdefault(k, []).append(v)
+        for t in c.taints:
+            taints[(t.key, t.value, t.effect)] = t
+        for r in c.api_resource_types:
+            apis[(r.group, r.version, r.kind)] = r
+    taint_pool, api_pool = list(taints.values()), list(apis.values())
+    idx = sorted(int(i) for i in rng.choice(len(clusters), size=min(n_changed, len(clusters)), replace=False))
+    out = list(clusters)
+    for i in idx:
+        c = copy.deepcopy(clusters[i])
+        if c.allocatable and "cpu" in c.allocatable:
+            ac = k8s.milli_value(k8s.quantity(c.allocatable["cpu"]))
+            am = k8s.value(k8s.quantity(c.allocatable["memory"])) if "memory" in c.allocatable else 0
+            c.available = dict(c.available or {}, cpu=f"{int(ac * rng.random())}m", memory=str(int(am * rng.random())))
+            if "example.com/gpu" in c.allocatable:
+                c.available["example.com/gpu"] = str(int(rng.integers(0, int(c.allocatable["example.com/gpu"]) + 1)))
+        if structural:
+            if c.labels and rng.random() < 0.5:
+                k = sorted(c.labels)[int(rng.integers(0, len(c.labels)))]
+                c.labels = dict(c.labels)
+                c.labels[k] = vals[k][int(rng.integers(0, len(vals[k])))]
+            if taint_pool and rng.random() < 0.4:
+                nt = int(rng.integers(0, min(4, len(taint_pool)) + 1))
+                c.taints = [taint_pool[int(j)] for j in rng.choice(len(taint_pool), size=nt, replace=False)]
+            if api_pool and rng.random() < 0.3:
+                c.api_resource_types = [r for r in api_pool if rng.random() < 0.8]
+        out[i] = c
+    return out, idx
