@@ -118,6 +118,11 @@ def test_closed_scheduler_refuses_calls():
         cs.submit(F.Framework(), _unit("late"), [])
 
 
+def _norm(r):
+    """ScheduleErrors compare by error class (parity is on the class, not the message)."""
+    return ("error", r.stage) if isinstance(r, T.ScheduleError) else r
+
+
 @pytest.mark.gpu
 def test_gpu_worker_threads_match_oracle():
     from kubeadmiral_amd.results import to_schedule_result
@@ -129,6 +134,5 @@ def test_gpu_worker_threads_match_oracle():
     want = [to_schedule_result(want_b, w, su, snap.names) for w, su in enumerate(units)]
     with CoalescingScheduler(max_wait_s=0.005) as cs:
         got = _run_workers(cs, [(fwk, su, cl) for su in units], n_threads=8)
-    norm = [lambda r: ("error", r.stage) if isinstance(r, T.ScheduleError) else r][0]
-    assert [norm(r) for r in got] == [norm(r) for r in want]
+    assert [_norm(r) for r in got] == [_norm(r) for r in want]
     assert len(cs.batches) < len(units)
