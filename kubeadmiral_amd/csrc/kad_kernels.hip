@@ -76,57 +76,98 @@ size_t select_wave_bytes(int C) { return row_layout(C).bytes; }
 
 // ---------------------------------------------------------- predicate programs
 // labels.Requirement.Matches / fields one-term selectors (apimachinery v0.26.6)
-// for one interned requirement on cluster c. `p` is wave-uniform (scalar loads).
-__device__ __forceinline__ bool eval_req(const SnapDev& s, const int32_t* p, int c) {
-  const int w0 = ldc(p);
-  const int op = w0 & 0xff, n = w0 >> 8, key = ldc(p + 1);
-  switch (op) {
-    case KAD_OP_TRUE: return true;
-    case KAD_OP_FALSE: return false;
-    case KAD_OP_NAME_EQ: return c == key;
-    case KAD_OP_NAME_NE: return c != key;
-    default: break;
-  }
-  const size_t at = (size_t)key * s.C + c;
-  const int32_t v = s.lval[at];
-  switch (op) {
-    case KAD_OP_EXISTS: return v >= 0;
-    case KAD_OP_DNE: return v < 0;
-    case KAD_OP_EQ:
-    case KAD_OP_IN: {
-      bool hit = false;
-      for (int i = 0; i < n; i++) hit |= (ldc(p + 2 + i) == v);
-      return v >= 0 && hit;
-    }
-    case KAD_OP_NOTIN: {
-      bool hit = false;
-      for (int i = 0; i < n; i++) hit |= (ldc(p + 2 + i) == v);
-      return v < 0 || !hit;
-    }
-    case KAD_OP_GT:
-    case KAD_OP_LT: {
-      if (v < 0 || !s.lok[at]) return false;
-      const int64_t thr = (int64_t)(((uint64_t)(uint32_t)ldc(p + 3) << 32) | (uint32_t)ldc(p + 2));
-      const int64_t lv = s.lint[at];
-      return op == KAD_OP_GT ? lv > thr : lv < thr;
-    }
-  }
-  return false;
-}
-
+// per interned requirement and cluster: req_group / req_mask_kernel below.
 // Requirement × cluster bitmask rows: M[r][ch] bit l = requirement r holds on
 // cluster 64*ch + l. Every distinct requirement of the batch is evaluated once
 // per cluster here, instead of once per (unit, cluster) pair.
-__global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b) {
+// One wave per (requirement, group of G consecutive chunks): the requirement
+// is decoded once (scalar loads), each chunk is one coalesced label-row load +
+// compares + ballot, the group's words are gathered in lanes (lane j = chunk
+// g0 + j) and written with one coalesced store. (One wave per (requirement,
+// chunk) made C5 — 50k requirements × 157 chunks — wave-dispatch bound.)
+template <int OPC>  // 0: lval only (IN/NOTIN/EQ/EXISTS/DNE), 1: Gt/Lt
+__device__ __forceinline__ uint64_t req_group(const SnapDev& s, const int32_t* p, int op, int n, int key, int g0,
+                                              int ng) {
+  const int lane = lane_id();
+  uint64_t acc = 0;
+  const int32_t* lv = s.lval + (size_t)key * s.C;
+  int64_t thr = 0;
+  if (OPC == 1) thr = (int64_t)(((uint64_t)(uint32_t)ldc(p + 3) << 32) | (uint32_t)ldc(p + 2));
+  for (int j0 = 0; j0 < ng; j0 += 4) {
+    int32_t v[4];
+    int64_t li[4];
+    uint8_t ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // four chunks' loads in flight
+      const int c = (g0 + j0 + u) * WAVE + lane;
+      const uint32_t cc = (j0 + u < ng && c < s.C) ? (uint32_t)c : 0u;
+      v[u] = ldg(lv, cc);
+      if (OPC == 1) {
+        ok[u] = ldg(s.lok + (size_t)key * s.C, cc);
+        li[u] = ldg(s.lint + (size_t)key * s.C, cc);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = (g0 + j0 + u) * WAVE + lane;
+      bool r;
+      if (OPC == 1) {
+        r = v[u] >= 0 && ok[u] && (op == KAD_OP_GT ? li[u] > thr : li[u] < thr);
+      } else if (op == KAD_OP_EXISTS) {
+        r = v[u] >= 0;
+      } else if (op == KAD_OP_DNE) {
+        r = v[u] < 0;
+      } else {
+        bool hit = false;
+        for (int i = 0; i < n; i++) hit |= (ldc(p + 2 + i) == v[u]);
+        r = op == KAD_OP_NOTIN ? (v[u] < 0 || !hit) : (v[u] >= 0 && hit);
+      }
+      const uint64_t m = ballot(r && c < s.C);
+      acc = lane == j0 + u ? m : acc;
+    }
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, int G) {
   const int lane = lane_id();
   const int nch = (s.C + 63) >> 6;
-  const long g = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= (long)b.NR * nch) return;
-  const int r = (int)(g / nch), ch = (int)(g % nch);
-  const int c = ch * WAVE + lane;
-  const bool v = c < s.C && eval_req(s, b.req + ldc(b.req_off + r), c);
-  const uint64_t m = ballot(v);
-  if (lane == 0) b.req_mask[g] = m;
+  const int ngrp = (nch + G - 1) / G;
+  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= (long)b.NR * ngrp) return;
+  const int r = (int)(gw / ngrp), g0 = (int)(gw % ngrp) * G;
+  const int ng = nch - g0 < G ? nch - g0 : G;
+  const int32_t* p = b.req + ldc(b.req_off + r);
+  const int w0 = ldc(p);
+  const int op = w0 & 0xff, n = w0 >> 8, key = ldc(p + 1);
+  uint64_t acc = 0;
+  switch (op) {
+    case KAD_OP_TRUE:
+    case KAD_OP_FALSE:
+    case KAD_OP_NAME_EQ:
+    case KAD_OP_NAME_NE:
+      for (int j = 0; j < ng; ++j) {
+        const int c = (g0 + j) * WAVE + lane;
+        const bool v = op == KAD_OP_TRUE || (op == KAD_OP_NAME_EQ && c == key) || (op == KAD_OP_NAME_NE && c != key);
+        const uint64_t m = ballot(v && c < s.C);
+        acc = lane == j ? m : acc;
+      }
+      break;
+    case KAD_OP_GT:
+    case KAD_OP_LT:
+      acc = req_group<1>(s, p, op, n, key, g0, ng);
+      break;
+    case KAD_OP_IN:
+    case KAD_OP_NOTIN:
+    case KAD_OP_EQ:
+    case KAD_OP_EXISTS:
+    case KAD_OP_DNE:
+      acc = req_group<0>(s, p, op, n, key, g0, ng);
+      break;
+    default:
+      break;
+  }
+  if (lane < ng) b.req_mask[(size_t)r * nch + g0 + lane] = acc;
 }
 
 // A unit's program (filter / score words) held in VGPR lanes: word i < 64 is
@@ -1627,10 +1668,15 @@ static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st) {
   (void)hipGetLastError();
-  const long waves = (long)b.NR * ((s.C + 63) >> 6);
+  const int nch = (s.C + 63) >> 6;
+  // chunks per wave: enough waves to fill the chip (~32k), at most 64 (one lane per chunk word)
+  const long pairs = (long)b.NR * nch;
+  int G = 1;
+  while (G < 64 && pairs / (2 * G) >= 32768) G *= 2;
+  const long waves = (long)b.NR * ((nch + G - 1) / G);
   if (waves == 0) return hipSuccess;
   const long grid = (waves + 3) / 4;
-  hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b);
+  hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, G);
   return hipGetLastError();
 }
 
