@@ -1162,6 +1162,28 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) t32[q] = (int)t[q];
         int lo32 = mn32, hi32 = mx32;
+        if (Q >= 2 && (uint32_t)mx32 - (uint32_t)mn32 < 128u) {
+          // totals within 128 of each other (the usual case: sums of 0..100
+          // plugin scores): LDS histogram in descending bin order, one
+          // prefix sum over the wave, the k-th largest from one ballot —
+          // instead of a ballot-count bisection step per bit of the range
+          uint32_t* hist = key;  // 128 u32; the replay rewrites key[] afterwards
+          *(uint2*)(hist + 2 * lane) = make_uint2(0u, 0u);
+          wave_sync();
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if ((vm[q] >> lane) & 1) atomicAdd(hist + (127 - (t32[q] - mn32)), 1u);
+          wave_sync();
+          const uint2 hh = *(const uint2*)(hist + 2 * lane);  // bins 127-2l, 126-2l
+          const int pre = wave_incl_sum_i32((int)(hh.x + hh.y));  // #(total >= mn + 126 - 2l)
+          const int kk = (int)k;
+          const int l0 = (int)__builtin_ctzll(ballot(pre >= kk));
+          const int pl = __builtin_amdgcn_readlane(pre, l0);
+          const int h1 = __builtin_amdgcn_readlane((int)hh.y, l0);
+          lo32 = mn32 + (pl - h1 >= kk ? 127 - 2 * l0 : 126 - 2 * l0);
+          hi32 = lo32;
+          wave_sync();
+        }
         if (nq == 1) {  // one position per lane: one ballot per step
           while (lo32 < hi32) {
             const uint32_t d = (uint32_t)hi32 - (uint32_t)lo32;
