@@ -198,6 +198,17 @@ static bool res_negative(const std::vector<int64_t>& v) {
   for (int64_t x : v) neg |= x < 0 || x >= (1ll << 46);
   return neg;
 }
+// every cluster has 1 <= allocatable < 2^46 and 0 <= used <= allocatable for cpu and
+// memory: the lean kernel's exact-f64 resource path applies (SnapDev::clean)
+static int res_clean(const std::vector<int64_t>& v) {
+  const size_t C = v.size() / 4;
+  for (size_t c = 0; c < C; c++)
+    for (int r = 0; r < 2; r++) {
+      const int64_t a = v[r * C + c], u = v[(2 + r) * C + c];
+      if (a < 1 || a >= (1ll << 46) || u < 0 || u > a) return 0;
+    }
+  return 1;
+}
 
 // rows and element size of snapshot array a (include/kad_sched.h, enum kad_snapshot_array)
 static void snapshot_array_shape(const kad_snapshot_header& h, int a, int64_t* rows, int* esz) {
@@ -233,6 +244,7 @@ int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
       if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
   }
   c->snap_negative = res_negative(c->h_res);
+  c->sd.clean = res_clean(c->h_res);
   c->have_snapshot = true;
   c->have_batch = false;
   return KAD_OK;
@@ -258,6 +270,7 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
                             (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
   }
   c->snap_negative = res_negative(c->h_res);
+  c->sd.clean = res_clean(c->h_res);
   c->have_snapshot = true;
   c->have_batch = false;
   return KAD_OK;
@@ -316,6 +329,7 @@ int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
     }
   }
   c->snap_negative = res_negative(c->h_res);
+  c->sd.clean = res_clean(c->h_res);
   return KAD_OK;
 }
 

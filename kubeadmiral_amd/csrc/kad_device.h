@@ -10,6 +10,7 @@ namespace kad {
 
 struct SnapDev {
   int C, GW, TW, K, S;
+  int clean;  // host: every cluster's cpu/mem fit the lean kernel's exact-f64 path (kad_api.hip res_clean)
   const int64_t *alloc_cpu, *alloc_mem, *used_cpu, *used_mem, *alloc_s, *used_s, *alloc_cores, *avail_cores;
   const uint64_t *gvk, *nsne, *ne, *pns;
   const int32_t* lval;

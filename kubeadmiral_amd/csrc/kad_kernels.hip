@@ -14,6 +14,8 @@
 // in LDS (per-wave region) when it fits, else in a per-wave global scratch slab.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "kad_device.h"
 #include "kad_plan.h"
 #include "kad_select.h"
@@ -273,9 +275,25 @@ __device__ __forceinline__ int64_t alloc_score(int64_t req, int64_t cap, bool mo
   const int64_t num = wmul(most ? req : wsub(cap, req), 100);
   return go_div(num, cap);
 }
+// floor(100 x / cap) for integer-valued 0 <= x <= cap, 1 <= cap < 2^46 (the
+// lean kernel's clean-snapshot path): the f32 estimate x * (100/cap) is within
+// 1e-4 of the quotient (<= 100), so one exact f64 correction (100x and q*cap
+// are integers < 2^53) gives the exact Go integer quotient
+__device__ __forceinline__ int quot100(double x, double cap, float inv100) {
+  int q = (int)((float)x * inv100);
+  const double r = __builtin_fma(-(double)q, cap, x * 100.0);
+  q += (int)(r >= cap) - (int)(r < 0.0);
+  return q;
+}
 __device__ __forceinline__ int64_t least_requested(int64_t req, int64_t cap) { return alloc_score(req, cap, false); }
 __device__ __forceinline__ int64_t most_requested(int64_t req, int64_t cap) { return alloc_score(req, cap, true); }
 // balanced_allocation.go:45-88 — IEEE float64, no contraction (-ffp-contract=off)
+__device__ __forceinline__ int64_t balanced_d(double cf, double mf) {
+  if (cf >= 1 || mf >= 1) return 0;
+  const double diff = fabs(cf - mf);
+  const double one_minus = 1 - diff;
+  return go_f2i(one_minus * 100.0);
+}
 __device__ __forceinline__ int64_t balanced(int64_t rc, int64_t cc, int64_t rm, int64_t cm) {
   const double cf = cc == 0 ? 1.0 : (double)rc / (double)cc;
   const double mf = cm == 0 ? 1.0 : (double)rm / (double)cm;
@@ -779,8 +797,19 @@ __device__ __forceinline__ void lean_defer(int w) {
   }
 }
 
-template <int NCH>
+// CL (clean snapshot, host-checked SnapDev::clean, NCH > 0): resources as exact
+// f64 columns, every total in [-2^28, 2^28] (units with wide affinity weights
+// or requests outside [0, 2^46) are deferred), so totals live in 32 bits
+template <typename TT>
+__device__ __forceinline__ TT tadd(TT a, int64_t b) {
+  if constexpr (sizeof(TT) == 8)
+    return wadd(a, b);
+  else
+    return a + (TT)b;
+}
+template <int NCH, bool CL>
 __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
+  using TT = typename std::conditional<CL, int, int64_t>::type;
   (void)args;  // read through largs()
   constexpr int Q = lean_qmax(NCH);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -825,21 +854,37 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   uint64_t* c_gv = (uint64_t*)(cache + 5 * Cp);
   uint64_t* c_ne = nullptr;
   uint64_t* c_pn = nullptr;
+  float2* c_iv = nullptr;
+  // clean snapshot (host-checked, SnapDev::clean): the resource columns are
+  // cached as exact f64 capacity / available (alloc - used) plus f32 100/cap,
+  // and fit / Least / Most / Balanced run in f64 compares and one correction
+  constexpr bool clean = CL && NCH > 0;
   {
     LArgs a = largs();
     int nx = 6;
     if (a->cache_ne) c_ne = (uint64_t*)(cache + (nx++) * Cp);
     if (a->cache_pn) c_pn = (uint64_t*)(cache + (nx++) * Cp);
+    if (clean) c_iv = (float2*)(cache + (nx++) * Cp);
   }
   if constexpr (NCH > 0) {
     LArgs a = largs();
     for (int c = threadIdx.x; c < Cp; c += blockDim.x) {
       const bool in = c < C;
       const uint32_t cl = in ? (uint32_t)c : 0u;
-      c_ac[c] = in ? ldg(a->s.alloc_cpu, cl) : 0;
-      c_uc[c] = in ? ldg(a->s.used_cpu, cl) : 0;
-      c_am[c] = in ? ldg(a->s.alloc_mem, cl) : 0;
-      c_um[c] = in ? ldg(a->s.used_mem, cl) : 0;
+      const int64_t ac = in ? ldg(a->s.alloc_cpu, cl) : 1, uc = in ? ldg(a->s.used_cpu, cl) : 0;
+      const int64_t am = in ? ldg(a->s.alloc_mem, cl) : 1, um = in ? ldg(a->s.used_mem, cl) : 0;
+      if (clean) {
+        c_ac[c] = __builtin_bit_cast(int64_t, (double)ac);
+        c_uc[c] = __builtin_bit_cast(int64_t, (double)(ac - uc));
+        c_am[c] = __builtin_bit_cast(int64_t, (double)am);
+        c_um[c] = __builtin_bit_cast(int64_t, (double)(am - um));
+        c_iv[c] = make_float2((float)(100.0 / (double)ac), (float)(100.0 / (double)am));
+      } else {
+        c_ac[c] = in ? ac : 0;
+        c_uc[c] = uc;
+        c_am[c] = in ? am : 0;
+        c_um[c] = um;
+      }
       c_ns[c] = in ? ldg(a->s.nsne, cl) : 0;
       c_gv[c] = in ? ldg(a->s.gvk, cl) : 0;
       if (c_ne) c_ne[c] = in ? ldg(a->s.ne, cl) : 0;
@@ -869,7 +914,15 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     w = (int)(W * gw / G) - 1;
     wend = (int)(W * (gw + 1) / G);
   }
-  uint32_t rvA = 0, svv = ~0u;
+  // the next batch's records are loaded one batch ahead (nrvA/nsvv): the
+  // wait at a batch start then only covers the previous unit's stores
+  uint32_t rvA = 0, svv = ~0u, nrvA = 0, nsvv = ~0u;
+  auto fetch = [&](int wb) {
+    const int nb = (wb + LEAN_BATCH < wend ? wb + LEAN_BATCH : wend) - wb;
+    nrvA = lane < nb * 16 ? ldg((const uint32_t*)(recs + wb), (uint32_t)lane) : 0u;
+    if (NCH > 0 && f_sw) nsvv = lane < nb * 2 * nch ? ldg((const uint32_t*)(sws + (size_t)wb * nch), (uint32_t)lane) : ~0u;
+  };
+  fetch(w + 1);
   int w1 = w + 1, u = 0;
   KAD_PACC;
   for (;;) {
@@ -878,9 +931,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     if (w >= wend) break;
     if (w >= w1) {  // next batch
       w1 = w + LEAN_BATCH < wend ? w + LEAN_BATCH : wend;
-      const int nb = w1 - w;
-      rvA = lane < nb * 16 ? ldg((const uint32_t*)(recs + w), (uint32_t)lane) : 0u;
-      if (NCH > 0 && f_sw) svv = lane < nb * 2 * nch ? ldg((const uint32_t*)(sws + (size_t)w * nch), (uint32_t)lane) : ~0u;
+      rvA = nrvA;
+      svv = nsvv;
+      fetch(w1);
       u = 0;
     }
     KAD_PT(t0);
@@ -902,10 +955,12 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       lean_status(w, KAD_ST_STICKY);
       continue;
     }
-    if (fc & REC_FULL) {
-      lean_defer(w);
+    if ((fc & REC_FULL) ||
+        (clean && ((uint64_t)rqc >= (1ull << 46) || (uint64_t)rqm >= (1ull << 46) || (fc & KAD_W_WIDE_SCORES)))) {
+      lean_defer(w);  // (requests outside [0, 2^46) and wide weights set the host's batch_defer)
       continue;
     }
+    const double rqcd = (double)rqc, rqmd = (double)rqm;  // exact on the clean path
     const int spo = (int)fld(3);
     const int64_t mc = fld64(8), ooff = fld64(10);
     const uint64_t tolp0 = (uint64_t)fld64(14);
@@ -945,9 +1000,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       int64_t acpu, ucpu, amem, umem;
       uint64_t ns0, ne0, pn0, gv0, sw0, cw0;
       if constexpr (NCH > 0) {
-        acpu = c_ac[c];
-        ucpu = c_uc[c];
-        amem = c_am[c];
+        acpu = clean ? 0 : c_ac[c];
+        ucpu = c_uc[c];  // clean: available cpu as f64
+        amem = clean ? 0 : c_am[c];
         umem = c_um[c];
         ns0 = c_ns[c];
         ne0 = use_cur ? c_ne[c] : 0ull;
@@ -995,7 +1050,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       }
       const uint64_t m_taint = ballot(tok);      // taint_toleration.go:50-77
       const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
-      const uint64_t m_fit = ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));  // fit.go:73-134
+      // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64)
+      const uint64_t m_fit = clean ? ballot((__builtin_bit_cast(double, ucpu) >= rqcd) & (__builtin_bit_cast(double, umem) >= rqmd))
+                                   : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
       m &= f_sw ? sw0 : ~0ull;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
       m &= f_taint ? m_taint : ~0ull;
       m &= f_api ? (gvc >= 0 ? m_api : 0ull) : ~0ull;
@@ -1036,7 +1093,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 
     // ---------------- scores of positions 64q + lane (RunScorePlugins, framework.go:139-181)
     const int nq = (n + 63) >> 6;
-    int64_t t[Q];
+    TT t[Q];
     uint32_t cid[Q];
     int ttv[Q];
     int ttmax = 0;
@@ -1050,7 +1107,19 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       const bool v = p < n;
       cid[q] = v ? idx[p] : 0u;
       const uint32_t cq = cid[q];
-      if (s_res) {
+      if (s_res && clean) {
+        // x = cap - req = available - request (exact); req > cap <=> x < 0 (score 0)
+        const double capc = __builtin_bit_cast(double, c_ac[cq]), capm = __builtin_bit_cast(double, c_am[cq]);
+        const double xc = __builtin_bit_cast(double, c_uc[cq]) - rqcd, xm = __builtin_bit_cast(double, c_um[cq]) - rqmd;
+        const float2 iv = c_iv[cq];
+        int x = 0;
+        if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
+          x += ((xc < 0.0 ? 0 : quot100(xc, capc, iv.x)) + (xm < 0.0 ? 0 : quot100(xm, capm, iv.y))) >> 1;
+        if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+          x += ((xc < 0.0 ? 0 : quot100(capc - xc, capc, iv.x)) + (xm < 0.0 ? 0 : quot100(capm - xm, capm, iv.y))) >> 1;
+        if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x += (int)balanced_d((capc - xc) / capc, (capm - xm) / capm);
+        t[q] = (TT)x;
+      } else if (s_res) {
         int64_t cc, cm, uc, um;
         if constexpr (NCH > 0) {
           cc = c_ac[cq];
@@ -1096,24 +1165,34 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       ttmax = wave_max_u_i32(ttmax);
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        if (q < nq) t[q] = wadd(t[q], ttmax == 0 ? 100 : 100 - (int64_t)small_quot(100 * ttv[q], ttmax));
+        if (q < nq) t[q] = tadd(t[q], ttmax == 0 ? 100 : 100 - (int64_t)small_quot(100 * ttv[q], ttmax));
     }
     if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {  // cluster_affinity.go:96-140 + DefaultNormalizeScore(100, false)
       LArgs a = largs();
       const int32_t* sp = a->b.sprog + spo;
       if (ldc(sp) > 0) {  // units without preferred terms score 0 everywhere
-        int64_t afs[Q];
-        int64_t amax = 0;
+        TT afs[Q];  // CL: |raw| <= sum |weight| <= 2^20 (wider units are deferred)
+        TT amax = 0;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           afs[q] = 0;
-          if (q < nq && q * 64 + lane < n) afs[q] = affinity_score(a->b.req_mask, sp, nch, (int)cid[q]);
+          if (q < nq && q * 64 + lane < n) afs[q] = (TT)affinity_score(a->b.req_mask, sp, nch, (int)cid[q]);
           amax = afs[q] > amax ? afs[q] : amax;
         }
-        amax = wave_max_u_i64(amax);
+        if constexpr (CL) {
+          amax = wave_max_u_i32(amax);
 #pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if (q < nq) t[q] = wadd(t[q], amax == 0 ? afs[q] : div_fast(wmul(100, afs[q]), amax));
+          for (int q = 0; q < Q; ++q)
+            if (q < nq) {
+              const int num = 100 * afs[q];
+              t[q] += amax == 0 ? afs[q] : (num >= 0 && num < (1 << 24) ? (int)small_quot(num, amax) : num / amax);
+            }
+        } else {
+          amax = wave_max_u_i64(amax);
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (q < nq) t[q] = wadd(t[q], amax == 0 ? afs[q] : div_fast(wmul(100, afs[q]), amax));
+        }
       }
     }
     KAD_PT(t2);
@@ -1140,7 +1219,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     } else if (k > 0) {
       // lanes holding a total, per position chunk
       uint64_t vm[Q];
-      int64_t mn = I64_MAX, mx = I64_MIN;
+      TT mn = CL ? (TT)INT32_MAX : (TT)I64_MAX, mx = CL ? (TT)INT32_MIN : (TT)I64_MIN;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int r = n - q * 64;
@@ -1711,9 +1790,9 @@ hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bo
   return hipGetLastError();
 }
 
-template <int NCH>
+template <int NCH, bool CL>
 static void launch_lean(const LeanArgs& A, int grid, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL(schedule_lean_kernel<NCH>, dim3(grid), dim3(64 * A.waves_per_block), lds, st, A);
+  hipLaunchKernelGGL((schedule_lean_kernel<NCH, CL>), dim3(grid), dim3(64 * A.waves_per_block), lds, st, A);
 }
 
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
@@ -1730,7 +1809,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     // many times the resident wave count
     const int cache_ne = (p.filter_mask & (1u << KAD_PL_TAINT_TOLERATION)) && (b.flags_or & KAD_W_HAS_CURRENT);
     const int cache_pn = (p.score_mask >> KAD_PL_TAINT_TOLERATION) & 1;
-    const size_t lds = lb * wpb + (nch <= 4 ? lean_cache_bytes(s.C, 6 + cache_ne + cache_pn) : 0);
+    const size_t lds = lb * wpb + (nch <= 4 ? lean_cache_bytes(s.C, 6 + cache_ne + cache_pn + ((s.clean && nch >= 1 && nch <= 4) ? 1 : 0)) : 0);
     // one wave per resident slot: contiguous equal shares, no tail of late blocks
     static int n_cu = 0;
     if (n_cu == 0) {
@@ -1739,13 +1818,16 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     }
     int per_cu = 0;
     hipError_t oe;
+    const bool cl = s.clean && nch >= 1 && nch <= 4;
+#define KAD_OCC(N, B) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<N, B>, 64 * wpb, lds)
     switch (nch) {
-      case 1: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<1>, 64 * wpb, lds); break;
-      case 2: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<2>, 64 * wpb, lds); break;
-      case 3: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<3>, 64 * wpb, lds); break;
-      case 4: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<4>, 64 * wpb, lds); break;
-      default: oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<0>, 64 * wpb, lds); break;
+      case 1: oe = cl ? KAD_OCC(1, true) : KAD_OCC(1, false); break;
+      case 2: oe = cl ? KAD_OCC(2, true) : KAD_OCC(2, false); break;
+      case 3: oe = cl ? KAD_OCC(3, true) : KAD_OCC(3, false); break;
+      case 4: oe = cl ? KAD_OCC(4, true) : KAD_OCC(4, false); break;
+      default: oe = KAD_OCC(0, false); break;
     }
+#undef KAD_OCC
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     if (getenv("KAD_LEAN_BLOCKS_PER_CU")) per_cu = atoi(getenv("KAD_LEAN_BLOCKS_PER_CU"));
     long grid = (long)n_cu * per_cu;
@@ -1753,11 +1835,11 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (grid > need) grid = need;
     const LeanArgs A{s, b, o, p, (int)lb, wpb, LEAN_BATCH, cache_ne, cache_pn};
     switch (nch) {
-      case 1: launch_lean<1>(A, (int)grid, lds, st); break;
-      case 2: launch_lean<2>(A, (int)grid, lds, st); break;
-      case 3: launch_lean<3>(A, (int)grid, lds, st); break;
-      case 4: launch_lean<4>(A, (int)grid, lds, st); break;
-      default: launch_lean<0>(A, (int)grid, lds, st); break;
+      case 1: cl ? launch_lean<1, true>(A, (int)grid, lds, st) : launch_lean<1, false>(A, (int)grid, lds, st); break;
+      case 2: cl ? launch_lean<2, true>(A, (int)grid, lds, st) : launch_lean<2, false>(A, (int)grid, lds, st); break;
+      case 3: cl ? launch_lean<3, true>(A, (int)grid, lds, st) : launch_lean<3, false>(A, (int)grid, lds, st); break;
+      case 4: cl ? launch_lean<4, true>(A, (int)grid, lds, st) : launch_lean<4, false>(A, (int)grid, lds, st); break;
+      default: launch_lean<0, false>(A, (int)grid, lds, st); break;
     }
     if (hipError_t e = hipGetLastError()) return e;
     // nothing can be deferred (host-checked: every unit and cluster is in the

@@ -270,3 +270,35 @@ def test_ties_straddle_many_feasible(ctx):
     snap, batch, res = run(ctx, clusters, units, fwk)
     assert (res.flags & 1).mean() > 0.5  # most rows straddle
     assert_same(res, c_oracle(snap, batch, fwk), "tie-heavy 256")
+
+
+# ------------------------------------------------- clean-snapshot f64 path
+def snapshot_is_clean(snap):
+    """Host restatement of kad_api.hip res_clean: 1 <= alloc < 2^46, 0 <= used <= alloc (cpu, memory)."""
+    h = pack.header_of(snap.blob, pack.SnapshotHeader)
+    C = len(snap.names)
+    a = [pack.array_of(snap.blob, h, i, np.int64, C) for i in (pack.S_ALLOC_CPU, pack.S_ALLOC_MEM)]
+    u = [pack.array_of(snap.blob, h, i, np.int64, C) for i in (pack.S_USED_CPU, pack.S_USED_MEM)]
+    return all(((x >= 1) & (x < (1 << 46)) & (y >= 0) & (y <= x)).all() for x, y in zip(a, u))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_clean_snapshot_gpu_equals_c_oracle(ctx, seed):
+    """Snapshots whose cpu/memory satisfy SnapDev::clean at C = 16..256 (lean kernel
+    instantiations NCH = 1..4 with the f64 resource columns), every fuzz profile
+    (Least/Most/Balanced, taint and affinity scores), requests incl. zero and > capacity."""
+    rng = np.random.default_rng(9000 + seed)
+    C = [16, 64, 70, 130, 200, 256][seed % 6]
+    clusters, units = synth.gen_fuzz(9000 + seed, W=90, C=C)
+    for c in clusters:
+        r = rng.random()
+        if r < 0.3:  # large exact capacities near the 2^46 bound
+            am = int(rng.integers(1 << 40, (1 << 46) - 1))
+            c.allocatable["memory"] = str(am)
+            c.available["memory"] = str(int(rng.integers(0, am + 1)))
+        elif r < 0.5:  # fully used / fully free
+            c.available["cpu"] = c.allocatable["cpu"] if rng.random() < 0.5 else "0"
+    fwk = synth.fuzz_framework(seed) if seed % 3 else F.Framework(F.default_enabled_plugins())
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert snapshot_is_clean(snap), "fixture must exercise the clean path"
+    assert_same(res, c_oracle(snap, batch, fwk), f"clean fuzz seed {seed} C={C}")
