@@ -994,84 +994,95 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       p_ne = ldg(a->s.ne, cl);
       p_gv = ldg(a->s.gvk, cl);
     }
+    // the chunk loop twice: FAST (no CurrentClusters, one taint word) has no
+    // uniform branch inside, so the cache reads of every chunk issue together
+    auto filter_chunks = [&](auto fast_t) {
+      constexpr bool FAST = decltype(fast_t)::value;
+      const bool ucur = !FAST && use_cur;
 #pragma unroll
-    for (int ch = 0; ch < NC; ++ch) {
-      const int c = ch * WAVE + lane;
-      int64_t acpu, ucpu, amem, umem;
-      uint64_t ns0, ne0, pn0, gv0, sw0, cw0;
-      if constexpr (NCH > 0) {
-        acpu = clean ? 0 : c_ac[c];
-        ucpu = c_uc[c];  // clean: available cpu as f64
-        amem = clean ? 0 : c_am[c];
-        umem = c_um[c];
-        ns0 = c_ns[c];
-        ne0 = use_cur ? c_ne[c] : 0ull;
-        pn0 = 0;
-        gv0 = c_gv[c];
-        sw0 = swc[ch];
-        cw0 = use_cur ? ldc(largs()->b.cw + (size_t)w * nch + ch) : 0ull;
-      } else {
-        acpu = p_ac;
-        ucpu = p_uc;
-        amem = p_am;
-        umem = p_um;
-        ns0 = p_ns;
-        ne0 = p_ne;
-        gv0 = p_gv;
-        pn0 = 0;
-        if (ch + 1 < NC) {
+      for (int ch = 0; ch < NC; ++ch) {
+        const int c = ch * WAVE + lane;
+        int64_t acpu, ucpu, amem, umem;
+        uint64_t ns0, ne0, pn0, gv0, sw0, cw0;
+        if constexpr (NCH > 0) {
+          acpu = clean ? 0 : c_ac[c];
+          ucpu = c_uc[c];  // clean: available cpu as f64
+          amem = clean ? 0 : c_am[c];
+          umem = c_um[c];
+          ns0 = c_ns[c];
+          ne0 = ucur ? c_ne[c] : 0ull;
+          pn0 = 0;
+          gv0 = c_gv[c];
+          sw0 = swc[ch];
+          cw0 = ucur ? ldc(largs()->b.cw + (size_t)w * nch + ch) : 0ull;
+        } else {
+          acpu = p_ac;
+          ucpu = p_uc;
+          amem = p_am;
+          umem = p_um;
+          ns0 = p_ns;
+          ne0 = p_ne;
+          gv0 = p_gv;
+          pn0 = 0;
+          if (ch + 1 < NC) {
+            LArgs a = largs();
+            const int cn = c + WAVE;
+            const uint32_t cl = cn < C ? (uint32_t)cn : 0u;
+            p_ac = ldg(a->s.alloc_cpu, cl);
+            p_uc = ldg(a->s.used_cpu, cl);
+            p_am = ldg(a->s.alloc_mem, cl);
+            p_um = ldg(a->s.used_mem, cl);
+            p_ns = ldg(a->s.nsne, cl);
+            p_ne = ldg(a->s.ne, cl);
+            p_gv = ldg(a->s.gvk, cl);
+          }
+          if (ch > 0 && (ch & 63) == 0) load_words(ch);
+          sw0 = readlane64(dsw, ch & 63);
+          cw0 = readlane64(dcw, ch & 63);
+        }
+        // each filter as a lane mask (v_cmp → SGPR pair), combined with scalar
+        // ANDs under uniform selects (no branches inside the unrolled loop)
+        const int rem = C - ch * WAVE;
+        uint64_t m = rem >= WAVE ? ~0ull : ((1ull << rem) - 1);
+        const bool sch = ucur && ((cw0 >> lane) & 1);
+        const uint64_t x = sch ? ne0 : ns0;
+        bool tok = (x & ~tolc) == 0;
+        for (int tw = 1; tw < (FAST ? 1 : TWs); ++tw) {  // more than 64 taint ids (C5): words 1.. from global
           LArgs a = largs();
-          const int cn = c + WAVE;
-          const uint32_t cl = cn < C ? (uint32_t)cn : 0u;
-          p_ac = ldg(a->s.alloc_cpu, cl);
-          p_uc = ldg(a->s.used_cpu, cl);
-          p_am = ldg(a->s.alloc_mem, cl);
-          p_um = ldg(a->s.used_mem, cl);
-          p_ns = ldg(a->s.nsne, cl);
-          p_ne = ldg(a->s.ne, cl);
-          p_gv = ldg(a->s.gvk, cl);
+          const uint32_t cl = c < C ? (uint32_t)c : 0u;
+          const uint64_t xt = sch ? ldg(a->s.ne, (uint32_t)(tw * C) + cl) : ldg(a->s.nsne, (uint32_t)(tw * C) + cl);
+          tok &= (xt & ~ldc(a->b.tol_all + (size_t)tsc * TWs + tw)) == 0;
         }
-        if (ch > 0 && (ch & 63) == 0) load_words(ch);
-        sw0 = readlane64(dsw, ch & 63);
-        cw0 = readlane64(dcw, ch & 63);
-      }
-      // each filter as a lane mask (v_cmp → SGPR pair), combined with scalar
-      // ANDs under uniform selects (no branches inside the unrolled loop)
-      const int rem = C - ch * WAVE;
-      uint64_t m = rem >= WAVE ? ~0ull : ((1ull << rem) - 1);
-      const bool sch = use_cur && ((cw0 >> lane) & 1);
-      const uint64_t x = sch ? ne0 : ns0;
-      bool tok = (x & ~tolc) == 0;
-      for (int tw = 1; tw < TWs; ++tw) {  // more than 64 taint ids (C5): words 1.. from global
-        LArgs a = largs();
-        const uint32_t cl = c < C ? (uint32_t)c : 0u;
-        const uint64_t xt = sch ? ldg(a->s.ne, (uint32_t)(tw * C) + cl) : ldg(a->s.nsne, (uint32_t)(tw * C) + cl);
-        tok &= (xt & ~ldc(a->b.tol_all + (size_t)tsc * TWs + tw)) == 0;
-      }
-      const uint64_t m_taint = ballot(tok);      // taint_toleration.go:50-77
-      const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
-      // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64)
-      const uint64_t m_fit = clean ? ballot((__builtin_bit_cast(double, ucpu) >= rqcd) & (__builtin_bit_cast(double, umem) >= rqmd))
-                                   : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
-      m &= f_sw ? sw0 : ~0ull;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
-      m &= f_taint ? m_taint : ~0ull;
-      m &= f_api ? (gvc >= 0 ? m_api : 0ull) : ~0ull;
-      m &= fit_on ? m_fit : ~0ull;
-      (void)pn0;
-      if constexpr (NCH > 0) {
-        mk[ch] = m;  // compaction after every chunk's mask: no LDS store between the cache reads
-      } else {
-        if ((m >> lane) & 1) {
-          const int pos = n + mbcnt(m);
-          if (pos < P) idx[pos] = (uint16_t)c;  // more than P feasible: the unit is deferred
+        const uint64_t m_taint = ballot(tok);      // taint_toleration.go:50-77
+        const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
+        // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64)
+        const uint64_t m_fit = clean ? ballot(__builtin_bit_cast(double, ucpu) >= rqcd) & ballot(__builtin_bit_cast(double, umem) >= rqmd)
+                                     : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
+        m &= f_sw ? sw0 : ~0ull;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
+        m &= f_taint ? m_taint : ~0ull;
+        m &= f_api ? (gvc >= 0 ? m_api : 0ull) : ~0ull;
+        m &= fit_on ? m_fit : ~0ull;
+        (void)pn0;
+        if constexpr (NCH > 0) {
+          mk[ch] = m;  // compaction after every chunk's mask: no LDS store between the cache reads
+        } else {
+          if ((m >> lane) & 1) {
+            const int pos = n + mbcnt(m);
+            if (pos < P) idx[pos] = (uint16_t)c;  // more than P feasible: the unit is deferred
+          }
+          n += popc64(m);
         }
-        n += popc64(m);
       }
-    }
+    };
+    if (!use_cur && TWs == 1)
+      filter_chunks(std::true_type{});
+    else
+      filter_chunks(std::false_type{});
     if constexpr (NCH > 0) {
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        if ((mk[ch] >> lane) & 1) idx[n + mbcnt(mk[ch])] = (uint16_t)(ch * WAVE + lane);
+        // every lane stores (no exec branch): infeasible lanes into pid[], rewritten before use
+        idx[((mk[ch] >> lane) & 1) ? n + mbcnt(mk[ch]) : P + lane] = (uint16_t)(ch * WAVE + lane);
         n += popc64(mk[ch]);
       }
     }
