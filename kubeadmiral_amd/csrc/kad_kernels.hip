@@ -1123,11 +1123,13 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         const double capc = __builtin_bit_cast(double, c_ac[cq]), capm = __builtin_bit_cast(double, c_am[cq]);
         const double xc = __builtin_bit_cast(double, c_uc[cq]) - rqcd, xm = __builtin_bit_cast(double, c_um[cq]) - rqmd;
         const float2 iv = c_iv[cq];
+        // branch-free: quotients of max(x, 0) (= 0 when x <= 0), masked to 0 where req > cap
+        const double xcp = fmax(xc, 0.0), xmp = fmax(xm, 0.0);
+        const int okc = -(int)(xc >= 0.0), okm = -(int)(xm >= 0.0);
         int x = 0;
-        if (sm & BIT(KAD_PL_LEAST_ALLOCATED))
-          x += ((xc < 0.0 ? 0 : quot100(xc, capc, iv.x)) + (xm < 0.0 ? 0 : quot100(xm, capm, iv.y))) >> 1;
+        if (sm & BIT(KAD_PL_LEAST_ALLOCATED)) x += (quot100(xcp, capc, iv.x) + quot100(xmp, capm, iv.y)) >> 1;
         if (sm & BIT(KAD_PL_MOST_ALLOCATED))
-          x += ((xc < 0.0 ? 0 : quot100(capc - xc, capc, iv.x)) + (xm < 0.0 ? 0 : quot100(capm - xm, capm, iv.y))) >> 1;
+          x += ((quot100(capc - xcp, capc, iv.x) & okc) + (quot100(capm - xmp, capm, iv.y) & okm)) >> 1;
         if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x += (int)balanced_d((capc - xc) / capc, (capm - xm) / capm);
         t[q] = (TT)x;
       } else if (s_res) {
