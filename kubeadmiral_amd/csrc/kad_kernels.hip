@@ -87,7 +87,9 @@ size_t select_wave_bytes(int C) { return row_layout(C).bytes; }
 // compares + ballot, the group's words are gathered in lanes (lane j = chunk
 // g0 + j) and written with one coalesced store. (One wave per (requirement,
 // chunk) made C5 — 50k requirements × 157 chunks — wave-dispatch bound.)
-template <int OPC>  // 0: lval only (IN/NOTIN/EQ/EXISTS/DNE), 1: Gt/Lt
+// U: chunk loads in flight (1 when every wave owns one chunk, G == 1: C2's
+// 1.5k requirements x 4 chunks, where the extra dummy loads only lengthen the chain)
+template <int OPC, int U>  // OPC 0: lval only (IN/NOTIN/EQ/EXISTS/DNE), 1: Gt/Lt
 __device__ __forceinline__ uint64_t req_group(const SnapDev& s, const int32_t* p, int op, int n, int key, int g0,
                                               int ng) {
   const int lane = lane_id();
@@ -95,12 +97,12 @@ __device__ __forceinline__ uint64_t req_group(const SnapDev& s, const int32_t* p
   const int32_t* lv = s.lval + (size_t)key * s.C;
   int64_t thr = 0;
   if (OPC == 1) thr = (int64_t)(((uint64_t)(uint32_t)ldc(p + 3) << 32) | (uint32_t)ldc(p + 2));
-  for (int j0 = 0; j0 < ng; j0 += 4) {
-    int32_t v[4];
-    int64_t li[4];
-    uint8_t ok[4];
+  for (int j0 = 0; j0 < ng; j0 += U) {
+    int32_t v[U];
+    int64_t li[U];
+    uint8_t ok[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // four chunks' loads in flight
+    for (int u = 0; u < U; ++u) {  // U chunks' loads in flight
       const int c = (g0 + j0 + u) * WAVE + lane;
       const uint32_t cc = (j0 + u < ng && c < s.C) ? (uint32_t)c : 0u;
       v[u] = ldg(lv, cc);
@@ -110,7 +112,7 @@ __device__ __forceinline__ uint64_t req_group(const SnapDev& s, const int32_t* p
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int c = (g0 + j0 + u) * WAVE + lane;
       bool r;
       if (OPC == 1) {
@@ -157,14 +159,14 @@ __global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, in
       break;
     case KAD_OP_GT:
     case KAD_OP_LT:
-      acc = req_group<1>(s, p, op, n, key, g0, ng);
+      acc = G == 1 ? req_group<1, 1>(s, p, op, n, key, g0, ng) : req_group<1, 4>(s, p, op, n, key, g0, ng);
       break;
     case KAD_OP_IN:
     case KAD_OP_NOTIN:
     case KAD_OP_EQ:
     case KAD_OP_EXISTS:
     case KAD_OP_DNE:
-      acc = req_group<0>(s, p, op, n, key, g0, ng);
+      acc = G == 1 ? req_group<0, 1>(s, p, op, n, key, g0, ng) : req_group<0, 4>(s, p, op, n, key, g0, ng);
       break;
     default:
       break;
