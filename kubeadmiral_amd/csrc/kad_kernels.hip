@@ -810,7 +810,7 @@ __device__ __forceinline__ TT tadd(TT a, int64_t b) {
     return a + (TT)b;
 }
 template <int NCH, bool CL>
-__global__ __launch_bounds__(CL ? 512 : 256, CL ? 8 : 6) void schedule_lean_kernel(LeanArgs args) {
+__global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   using TT = typename std::conditional<CL, int, int64_t>::type;
   (void)args;  // read through largs()
   constexpr int Q = lean_qmax(NCH);
@@ -1818,8 +1818,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
   if (fast_path(s.C)) {
     const int nch = (s.C + 63) >> 6;
     const size_t lb = lean_layout(s.C, lean_qmax(nch <= 4 ? nch : 0)).bytes;
-    const bool cl = s.clean && nch >= 1 && nch <= 4;
-    const int wpb = cl ? 8 : 4;  // clean kernel: 8 waves/SIMD in 4 blocks of 8 waves sharing one cluster cache
+    const int wpb = 4;
     // runs of consecutive units per wave: long enough to amortise the
     // register-resident cluster attributes, short enough that the grid is
     // many times the resident wave count
@@ -1834,6 +1833,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     }
     int per_cu = 0;
     hipError_t oe;
+    const bool cl = s.clean && nch >= 1 && nch <= 4;
 #define KAD_OCC(N, B) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<N, B>, 64 * wpb, lds)
     switch (nch) {
       case 1: oe = cl ? KAD_OCC(1, true) : KAD_OCC(1, false); break;
