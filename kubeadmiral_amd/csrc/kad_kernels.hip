@@ -968,6 +968,8 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     const uint64_t tolp0 = (uint64_t)fld64(14);
     const bool use_cur = f_taint && (fc & KAD_W_HAS_CURRENT);
     const bool fit_on = f_fit && (fc & KAD_W_FIT_NONZERO);
+    const uint64_t o_sw = f_sw ? 0ull : ~0ull, o_taint = f_taint ? 0ull : ~0ull, o_fit = fit_on ? 0ull : ~0ull;
+    const uint64_t o_api = f_api ? 0ull : ~0ull, a_api = gvc >= 0 ? ~0ull : 0ull;  // no GVK id: no cluster has it
     uint64_t dsw = ~0ull, dcw = 0;  // dynamic-NCH path: words of chunks 64g..64g+63 in lanes
     auto load_words = [&](int ch0) {
       LArgs a = largs();
@@ -1060,10 +1062,8 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64)
         const uint64_t m_fit = clean ? ballot(__builtin_bit_cast(double, ucpu) >= rqcd) & ballot(__builtin_bit_cast(double, umem) >= rqmd)
                                      : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
-        m &= f_sw ? sw0 : ~0ull;  // ClusterAffinity ∧ PlacementFilter (prep_kernel)
-        m &= f_taint ? m_taint : ~0ull;
-        m &= f_api ? (gvc >= 0 ? m_api : 0ull) : ~0ull;
-        m &= fit_on ? m_fit : ~0ull;
+        // disabled filters OR in an all-ones mask (per-unit constants: two SALU ops per filter)
+        m &= (sw0 | o_sw) & (m_taint | o_taint) & ((m_api & a_api) | o_api) & (m_fit | o_fit);
         (void)pn0;
         if constexpr (NCH > 0) {
           mk[ch] = m;  // compaction after every chunk's mask: no LDS store between the cache reads
