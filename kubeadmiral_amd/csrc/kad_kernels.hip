@@ -1215,14 +1215,14 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 
     // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
     LArgs ad = largs();
-    int64_t k = n;
+    int k = n;  // <= n <= 64 * Q: 32-bit counts
     if (ad->p.select_plugin == KAD_PL_MAX_CLUSTER) {
       const bool hm = fc & KAD_W_HAS_MAX_CLUSTERS;
       if (hm && mc < 0) {
         lean_status(w, KAD_ST_ERR_SELECT);
         continue;
       }
-      if (hm && mc < k) k = mc;
+      if (hm && mc < k) k = (int)mc;
     }
     uint64_t sel[Q];
     uint32_t rflags = 0;
@@ -1323,7 +1323,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         }
       }
       uint64_t gm[Q], em[Q];
-      int64_t g = 0, e = 0;
+      int g = 0, e = 0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         gm[q] = ballot(t[q] > lo) & vm[q];
@@ -1331,7 +1331,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         g += popc64(gm[q]);
         e += popc64(em[q]);
       }
-      const int64_t need = k - g;
+      const int need = k - g;
       if (need == e) {  // the cut takes every tie: no sort needed
 #pragma unroll
         for (int q = 0; q < Q; ++q) sel[q] = gm[q] | em[q];
