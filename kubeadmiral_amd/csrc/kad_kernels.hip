@@ -723,25 +723,26 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
 }
 
 // ================================================= lean schedule kernel
-// schedule_lean_kernel<NCH> — the common case, used whenever C fits the
+// schedule_lean_kernel<NCH, CL> — the common case, used whenever C fits the
 // per-wave LDS budget (fast_path). Each wave owns a run of consecutive units.
 // For NCH > 0 (C <= 64*NCH) the block first copies the cluster attributes the
 // path reads (fit resources, taint words, GVK word) into an LDS cache shared
-// by its waves, and a unit's fixed fields and static filter words arrive
-// through scalar loads issued one unit ahead: the common path issues NO
-// vector load after the prologue, so no s_waitcnt vmcnt ever waits behind the
-// previous unit's output stores (gfx9 counts stores and loads in one in-order
-// counter), and the cache costs no VGPRs (occupancy).
+// by its waves; a unit's record and static filter words arrive in VGPRs with
+// one vector load per 4-unit batch (issued a batch ahead) and are read with
+// v_readlane. CL (clean snapshot, SnapDev::clean, NCH > 0): the resource
+// columns are cached as exact f64 (capacity, available) + f32 100/cap and
+// every total fits 32 bits (see quot100).
 // The feasible list is compacted into LDS (snapshot order = the reference's
 // feasible list, generic_scheduler.go:152-169); then each lane owns
 // positions lane + 64q (q < QMAX), and scores, normalisation and MaxCluster's
 // first-k set are computed in registers:
-//   * the k-th largest total T by ballot bisection over [min, max];
+//   * the k-th largest total T from an LDS histogram when the totals span
+//     < 128 (one wave prefix sum), else by ballot bisection over [min, max];
 //   * cut takes every tie (k - #(>T) == #(==T)): selection = {total >= T};
 //   * n <= 12: Go's pdqsort is one stable insertionSort, so the selection is
 //     {> T} plus the first k - #(>T) ties in input order;
-//   * otherwise the restricted pdqsort replay (kad_select.h) on registers
-//     (keys as u32 offsets from the row minimum; LDS for wider rows).
+//   * otherwise the restricted pdqsort replay (kad_select.h PdqWave) on u32
+//     keys (total - row minimum) in the wave's LDS region.
 // Units routed REC_FULL by prep, or (NCH == 0) with more than 64*QMAX
 // feasible clusters, go to the defer list and schedule_kernel afterwards.
 constexpr int LEAN_QMAX_DYN = 4;
