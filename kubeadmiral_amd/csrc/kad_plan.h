@@ -121,6 +121,22 @@ __device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const i
     const uint32_t he = lane < m ? ws.hash[e] : 0u;
     int rank = 0;
     bool tie = false;
+    if (!ballot(lane < m && (we < 0 || we > 0x7FFFFFFF))) {
+      // every weight in [0, 2^31): (weight desc, hash asc) as one ascending u64
+      // key, so each step is two readlanes and one 64-bit compare per order
+      const uint64_t ke = ((uint64_t)(uint32_t)(0x7FFFFFFF - (int)we) << 32) | he;
+      for (int j = 0; j < m; j++) {
+        const int f = __builtin_amdgcn_readlane(e, j);
+        const uint64_t kf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ke >> 32), j) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ke, j);
+        rank += kf < ke || (kf == ke && f < e);
+        tie |= (j != lane && kf == ke);
+      }
+      wsync<GSCR>();
+      if (lane < m) ws.ord[rank] = e;
+      wsync<GSCR>();
+      return ballot(lane < m && tie) != 0;
+    }
     for (int j = 0; j < m; j++) {
       const int f = __builtin_amdgcn_readlane(e, j);
       const int64_t wf = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)we >> 32), j)
