@@ -51,6 +51,33 @@ __device__ __forceinline__ Clamp wave_scan_clamp(Clamp v) {
   v = clamp_compose(dpp_clamp<0x143, 0xc>(v), v);
   return v;
 }
+// The same scan in 32 bits when the row is narrow (clamp_narrow: R and every
+// |s| < 2^24, t in {0, -inf} — partial sums stay within 2^30 over 64 lanes, so
+// no value wraps in either width and the results are identical): half the DPP
+// moves and 32-bit compose. -inf is INT32_MIN in the narrow form.
+constexpr int NEG32 = INT32_MIN;
+__device__ __forceinline__ bool clamp_narrow(Clamp f, int64_t R) {
+  return R >= 0 && R < (1ll << 24) && !ballot(f.s <= -(1ll << 24) || f.s >= (1ll << 24));
+}
+#define KAD_CLAMP32_STEP(CTRL, RM)                                        \
+  {                                                                       \
+    const int ps = dpp32<CTRL, RM>(0, s), pt = dpp32<CTRL, RM>(NEG32, t); \
+    const int at = pt == NEG32 ? NEG32 : pt - s;                          \
+    t = at > t ? at : t;                                                  \
+    s = ps + s;                                                           \
+  }
+__device__ __forceinline__ Clamp wave_scan_clamp_n(Clamp v, bool narrow) {
+  if (!narrow) return wave_scan_clamp(v);
+  int s = (int)v.s, t = v.t == NEG_INF ? NEG32 : (int)v.t;
+  KAD_CLAMP32_STEP(0x111, 0xf)
+  KAD_CLAMP32_STEP(0x112, 0xf)
+  KAD_CLAMP32_STEP(0x114, 0xf)
+  KAD_CLAMP32_STEP(0x118, 0xf)
+  KAD_CLAMP32_STEP(0x142, 0xa)
+  KAD_CLAMP32_STEP(0x143, 0xc)
+  return Clamp{(int64_t)s, t == NEG32 ? NEG_INF : (int64_t)t};
+}
+#undef KAD_CLAMP32_STEP
 // exclusive value: the inclusive scan shifted one lane up (wave_shr:1); lane 0 gets the identity
 __device__ __forceinline__ Clamp wave_shr1_clamp(Clamp v) {
   Clamp o;
@@ -198,7 +225,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
     } else {
       f = {Mn, NEG_INF};
     }
-    Clamp inc = wave_scan_clamp(f);
+    Clamp inc = wave_scan_clamp_n(f, clamp_narrow(f, R));
     Clamp exc = wave_shr1_clamp(inc);
     int64_t Ri = clamp_apply(exc, R);
     if (v) {
@@ -250,7 +277,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
       int64_t V = U == I64_MAX ? I64_MAX : wsub(U, start);
       int64_t mm = ee < V ? ee : V;
       Clamp f = !v ? Clamp{0, NEG_INF} : (mm >= 0 ? Clamp{mm, 0} : Clamp{mm, NEG_INF});
-      Clamp inc = wave_scan_clamp(f);
+      Clamp inc = wave_scan_clamp_n(f, clamp_narrow(f, R));
       Clamp exc = wave_shr1_clamp(inc);
       int64_t Ri = clamp_apply(exc, R);
       bool full = false;
