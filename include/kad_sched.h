@@ -329,6 +329,10 @@ int kad_sync(kad_ctx* ctx);
 /* Device time of the last kad_schedule, from HIP events on the ctx stream:
  * ms[0] = whole pipeline, ms[1] = filter/score/select kernel, ms[2] = planner. */
 int kad_last_timing(kad_ctx* ctx, float ms[3]);
+/* Record those events in later kad_schedule calls (default on). Off, the
+ * stream carries only the kernels (no marker packets between passes) and
+ * kad_last_timing returns KAD_ESTATE.  No reference counterpart (instrumentation). */
+int kad_set_timing(kad_ctx* ctx, int on);
 int kad_results_download(kad_ctx* ctx, const kad_result_view* out);
 
 /* All in one: upload batch, schedule, download (blocking). */

@@ -50,6 +50,9 @@ struct kad_ctx {
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   bool have_snapshot = false, have_batch = false, ran = false;
+  // HIP event records around the stages (kad_set_timing); timed = the last
+  // kad_schedule recorded them
+  bool timing = true, timed = false;
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
   std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
   void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
@@ -512,18 +515,20 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   OutDev o = out_dev(c);
   o.dbg_feas = dbg_feas;
   o.dbg_total = dbg_total;
-  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  const bool tm = c->timing;
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
   c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total;
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream));
-  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())
     HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, c->d_plan_rows, (int)c->plan_rows.size(), c->batch_hdr.max_row_slots,
                           c->d_scratch, c->scratch_bytes, c->stream));
-  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   c->ran = true;
+  c->timed = tm;
   return KAD_OK;
 }
 
@@ -540,10 +545,18 @@ int kad_sync(kad_ctx* c) {
   return KAD_OK;
 }
 
+int kad_set_timing(kad_ctx* c, int on) {
+  if (!c) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->timing = on != 0;
+  return KAD_OK;
+}
+
 int kad_last_timing(kad_ctx* c, float ms[3]) {
   if (!c || !ms) return KAD_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
+  if (!c->timed) return fail(c, KAD_ESTATE, "the last kad_schedule ran with timing off");
   HIPCHK(c, hipEventSynchronize(c->ev[2]));
   HIPCHK(c, hipEventElapsedTime(&ms[0], c->ev[0], c->ev[2]));
   HIPCHK(c, hipEventElapsedTime(&ms[1], c->ev[0], c->ev[1]));

@@ -71,6 +71,7 @@ def load_library(path: str = LIB_PATH):
     L.kad_schedule.argtypes = [P, P]
     L.kad_sync.argtypes = [P]
     L.kad_last_timing.argtypes = [P, P]
+    L.kad_set_timing.argtypes = [P, I]
     L.kad_results_download.argtypes = [P, P]
     L.kad_schedule_batch.argtypes = [P, P, P, SZ, P]
     L.kad_select_rows.argtypes = [P, I, P, P, P, U32, P, P, P]
@@ -140,6 +141,10 @@ class Context:
 
     def sync(self):
         self._chk(self.L.kad_sync(self.h))
+
+    def set_timing(self, on: bool):
+        """kad_set_timing: HIP event records around the stages of later schedule() calls."""
+        self._chk(self.L.kad_set_timing(self.h, 1 if on else 0))
 
     def timing(self):
         ms = (ctypes.c_float * 3)()

@@ -174,6 +174,19 @@ def test_c2_full_size(ctx):
     ctx.schedule(fwk)
     res2 = ctx.download()
     assert_same(res2, res, "c2 rerun")
+    # timing off (bench's timed region): same bytes, and no event times to read
+    ctx.set_timing(False)
+    try:
+        ctx.schedule(fwk)
+        ctx.sync()
+        assert_same(ctx.download(), res, "c2 timing off")
+        with pytest.raises(Exception, match="timing off"):
+            ctx.timing()
+    finally:
+        ctx.set_timing(True)
+    ctx.schedule(fwk)
+    ctx.sync()
+    assert ctx.timing()[1] > 0
 
 
 def test_c4_subset(ctx):
