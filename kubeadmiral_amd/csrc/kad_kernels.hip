@@ -1508,17 +1508,22 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
   for (int r = gw; r < n_rows; r += r_stride) {
     KAD_PT(t0);
     const int w = rows[r];
-    if (o.status[w] != KAD_ST_OK) continue;
+    // every per-unit scalar is loaded before the status test so the loads
+    // issue together (one memory round trip instead of three dependent ones;
+    // w < W, so each index is in bounds whatever the status)
+    const int st = o.status[w];
     const int K = o.count[w];
-    if (K <= 0) continue;
     const uint32_t f = b.flags[w];
-    PlanWs ws = plan_ws(region, K);
     const int64_t off = b.out_off[w];
     const int p0 = b.pref_off[w], p1 = b.pref_off[w + 1];
     const int c0 = b.cur_off[w], c1 = b.cur_off[w + 1];
-    const uint8_t* key = b.key + b.key_off[w];
-    const int klen = b.key_off[w + 1] - b.key_off[w];
-    const int64_t total = (f & KAD_W_HAS_DESIRED) ? b.desired[w] : 0;
+    const int ko0 = b.key_off[w], ko1 = b.key_off[w + 1];
+    const int64_t desired = b.desired[w];
+    if (st != KAD_ST_OK || K <= 0) continue;
+    PlanWs ws = plan_ws(region, K);
+    const uint8_t* key = b.key + ko0;
+    const int klen = ko1 - ko0;
+    const int64_t total = (f & KAD_W_HAS_DESIRED) ? desired : 0;
     // preferences (rsp.go:99-126)
     if (use_tbl) {
       for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = (uint16_t)(j - p0 + 1);
@@ -1556,16 +1561,18 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
         uint32_t fl = 0;
         int64_t wt = 0, mn = 0, mx = 0, cp = 0;
         if (pi >= 0) {
+          // all five columns in one round trip (pi is in bounds), flags select after
           const uint32_t pf = b.pref_fl[pi];
-          if (pf & KAD_PREF_HAS_WEIGHT) wt = b.pref_w[pi];
+          const int64_t pw = b.pref_w[pi], pmx = b.pref_max[pi], pcp = b.pref_cap[pi];
           mn = b.pref_min[pi];
+          if (pf & KAD_PREF_HAS_WEIGHT) wt = pw;
           if (pf & KAD_PREF_HAS_MAX) {
             fl |= EF_HAS_MAX;
-            mx = b.pref_max[pi];
+            mx = pmx;
           }
           if (pf & KAD_PREF_HAS_CAP) {
             fl |= EF_HAS_CAP;
-            cp = b.pref_cap[pi];
+            cp = pcp;
           }
         }
         ws.w[i] = wt;
