@@ -691,29 +691,37 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   }
   if (g >= (uint32_t)b.W * per) return;
   const uint32_t w = g / per, ch = g - w * per;
+  // every per-unit load is issued up front by every lane (w < W, the four
+  // lanes of a unit share its cache lines), so the record lanes' chain and the
+  // affinity chain below overlap instead of running one after the other
   const uint32_t f = b.flags[w];
   const uint32_t fm = p.filter_mask;
+  const int32_t gvk = b.gvk[w], tolset = b.tolset[w], sprog = b.sprog_off[w];
+  const int64_t rqc = b.req_cpu[w], rqm = b.req_mem[w], maxc = b.maxc[w], desired = b.desired[w];
+  const int64_t oo = b.out_off[w];
+  const int32_t so0 = b.sreq_off[w], so1 = b.sreq_off[w + 1];
+  const int32_t fpo = b.fprog_off[w];
+  const uint64_t tol0 = b.tol_all[(size_t)tolset * b.TW], tolp0 = b.tol_pns[(size_t)tolset * b.TW];
   if (ch == 0) {
     UnitRec r;
     bool full = force_full != 0;
-    if ((fm & (1u << KAD_PL_API_RESOURCES)) && b.gvk[w] >= 64) full = true;
-    if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && b.sreq_off[w] < b.sreq_off[w + 1])
-      full = true;
-    r.flags = f | (((f & KAD_W_HAS_DESIRED) && b.desired[w] > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
-    r.gvk = b.gvk[w];
-    r.tolset = b.tolset[w];
-    r.sprog_off = b.sprog_off[w];
-    r.req_cpu = b.req_cpu[w];
-    r.req_mem = b.req_mem[w];
-    r.maxc = b.maxc[w];
-    r.out_off = b.out_off[w];
-    r.tol0 = b.tol_all[(size_t)r.tolset * b.TW];
-    r.tolp0 = b.tol_pns[(size_t)r.tolset * b.TW];
+    if ((fm & (1u << KAD_PL_API_RESOURCES)) && gvk >= 64) full = true;
+    if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && so0 < so1) full = true;
+    r.flags = f | (((f & KAD_W_HAS_DESIRED) && desired > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
+    r.gvk = gvk;
+    r.tolset = tolset;
+    r.sprog_off = sprog;
+    r.req_cpu = rqc;
+    r.req_mem = rqm;
+    r.maxc = maxc;
+    r.out_off = oo;
+    r.tol0 = tol0;
+    r.tolp0 = tolp0;
     b.rec[w] = r;
   }
   if (ch < nch && !(f & KAD_W_STICKY)) {
     uint64_t m = ~0ull;
-    if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) m = affinity_word(b.req_mask, b.fprog + b.fprog_off[w], nch, ch);
+    if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) m = affinity_word(b.req_mask, b.fprog + fpo, nch, ch);
     if ((fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT))
       m &= id_list_word(b.place, b.place_off[w], b.place_off[w + 1], ch);
     b.sw[g] = m;
