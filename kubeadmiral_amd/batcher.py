@@ -9,7 +9,7 @@ once per object from each of ``--worker-count`` reconcile goroutines
 gathers the calls that arrive together (up to ``max_batch`` units, or until
 ``max_wait_s`` after the first one) and runs them as one
 :class:`~kubeadmiral_amd.runtime.BatchScheduler` batch per (framework,
-cluster list) pair. Between batches the cluster list may change: the
+cluster-list content) pair. Between batches the cluster list may change: the
 BatchScheduler applies it as an in-place snapshot delta when it can.
 """
 
@@ -96,10 +96,17 @@ class CoalescingScheduler:
             items, stop = self._gather(first)
             self.batches.append(len(items))
             # one batch per (framework, cluster list): a batch is packed against one snapshot and one profile
+            # grouped by cluster-list CONTENT: the reference lists clusters afresh on every reconcile
+            # (scheduler.go:334), so equal lists arrive as distinct objects; fingerprinted once per list
+            # object of the window (the items keep those objects alive)
             groups: Dict[tuple, list] = {}
+            fps: Dict[int, bytes] = {}
             for it in items:
                 fwk, _, clusters, _ = it
-                groups.setdefault((bytes(fwk.to_c()), id(clusters)), []).append(it)
+                fp = fps.get(id(clusters))
+                if fp is None:
+                    fp = fps[id(clusters)] = T.clusters_fingerprint(clusters)
+                groups.setdefault((bytes(fwk.to_c()), fp), []).append(it)
             for members in groups.values():
                 fwk, clusters = members[0][0], members[0][2]
                 live = [m for m in members if m[3].set_running_or_notify_cancel()]

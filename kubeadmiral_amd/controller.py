@@ -96,7 +96,7 @@ class BatchReconciler:
             live.append(i)
 
         # :394-421 — trigger hashes for the whole batch in one GPU pass
-        key = id(clusters), len(clusters)
+        key = T.clusters_fingerprint(clusters)  # content (labels, taints, API resources), not the list object
         if key != self._clusters_key:
             self.hasher.set_clusters(clusters)
             self._clusters_key = key

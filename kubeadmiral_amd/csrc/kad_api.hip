@@ -52,7 +52,7 @@ struct kad_ctx {
   bool have_snapshot = false, have_batch = false, ran = false;
   // HIP event records around the stages (kad_set_timing); timed = the last
   // kad_schedule recorded them
-  bool timing = true, timed = false;
+  bool timing = false, timed = false;
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
   std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
   void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
@@ -106,6 +106,193 @@ static int to_dev(kad_ctx* c, const T* h, size_t n, T** d, std::vector<void*>& o
   HIPCHK(c, hipMalloc((void**)d, (n ? n : 1) * sizeof(T)));
   owned.push_back(*d);
   if (n && h) HIPCHK(c, hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+// ------------------------------------------------------ batch validation
+// A batch blob may come from any packer (the Go port INTEGRATION.md proposes),
+// so before anything is copied to the device every array is checked to lie in
+// the blob, every CSR offset array to be monotone and to end inside its data
+// array, every id the kernels index with to be in range, and every predicate
+// program to be well formed — the kernels then read only inside the blob.
+namespace {
+struct BatchCheck {
+  kad_ctx* c;
+  const char* base;
+  size_t nbytes;
+  const kad_batch_header& h;
+  // array a holds count elements of esz bytes inside the blob
+  bool extent(int a, uint64_t count, int esz, const char* what) {
+    const uint64_t o = h.off[a];
+    if (o > nbytes || (o % (uint64_t)esz) || count > (nbytes - o) / (uint64_t)esz) {
+      fail(c, KAD_EINVAL, std::string("batch array ") + what + " lies outside the blob");
+      return false;
+    }
+    return true;
+  }
+  template <class T>
+  const T* arr(int a) const { return reinterpret_cast<const T*>(base + h.off[a]); }
+  // CSR offsets off_a[0..n]: 0-based, non-decreasing; the data array d has off[n] elements of esz bytes
+  bool csr(int off_a, int n, int data_a, int esz, const char* what, int64_t* total) {
+    if (!extent(off_a, (uint64_t)n + 1, 4, what)) return false;
+    const int32_t* o = arr<int32_t>(off_a);
+    if (o[0] != 0) return fail(c, KAD_EINVAL, std::string(what) + " offsets must start at 0"), false;
+    for (int i = 0; i < n; i++)
+      if (o[i + 1] < o[i]) return fail(c, KAD_EINVAL, std::string(what) + " offsets must be non-decreasing"), false;
+    *total = o[n];
+    return data_a < 0 || extent(data_a, (uint64_t)o[n], esz, what);
+  }
+  // each row's ids in [lo, hi), ascending (strictly when unique)
+  bool sorted_ids(int off_a, int ids_a, int n, int lo, int hi, bool unique, const char* what) {
+    const int32_t* o = arr<int32_t>(off_a);
+    const int32_t* v = arr<int32_t>(ids_a);
+    for (int w = 0; w < n; w++)
+      for (int j = o[w]; j < o[w + 1]; j++) {
+        if (v[j] < lo || v[j] >= hi) return fail(c, KAD_EINVAL, std::string(what) + " id out of range"), false;
+        if (j > o[w] && (unique ? v[j] <= v[j - 1] : v[j] < v[j - 1]))
+          return fail(c, KAD_EINVAL, std::string(what) + " ids must be ascending"), false;
+      }
+    return true;
+  }
+};
+}  // namespace
+
+static int validate_batch(kad_ctx* c, const void* blob, size_t nbytes, const kad_batch_header& h) {
+  const kad_snapshot_header& sh = c->snap_hdr;
+  const int W = h.n_units, C = sh.n_clusters, TW = h.n_taint_words, NT = h.n_tolsets, NR = h.n_reqs;
+  if (W < 0 || NT < 0 || NR < 0 || (W > 0 && NT < 1)) return fail(c, KAD_EINVAL, "bad batch counts");
+  for (int i = 0; i < KAD_B_NARRAYS; i++)
+    if (h.off[i] > nbytes || (h.off[i] & 7)) return fail(c, KAD_EINVAL, "bad batch array offset");
+  BatchCheck k{c, static_cast<const char*>(blob), nbytes, h};
+  const uint64_t Wu = (uint64_t)W;
+  if (!k.extent(KAD_B_FLAGS, Wu, 4, "flags") || !k.extent(KAD_B_GVK, Wu, 4, "gvk") ||
+      !k.extent(KAD_B_REQ_CPU, Wu, 8, "req_cpu") || !k.extent(KAD_B_REQ_MEM, Wu, 8, "req_mem") ||
+      !k.extent(KAD_B_DESIRED, Wu, 8, "desired") || !k.extent(KAD_B_MAX_CLUSTERS, Wu, 8, "max_clusters") ||
+      !k.extent(KAD_B_TOLSET, Wu, 4, "tolset") || !k.extent(KAD_B_TOL_ALL, (uint64_t)NT * TW, 8, "tol_all") ||
+      !k.extent(KAD_B_TOL_PNS, (uint64_t)NT * TW, 8, "tol_pns") || !k.extent(KAD_B_OUT_OFF, Wu + 1, 8, "out_off"))
+    return KAD_EINVAL;
+  int64_t n_s, n_f, n_sp, n_pl, n_cur, n_pref, n_key, n_req;
+  if (!k.csr(KAD_B_SREQ_OFF, W, KAD_B_SREQ_ID, 4, "sreq", &n_s) || !k.extent(KAD_B_SREQ_VAL, n_s, 8, "sreq_val") ||
+      !k.csr(KAD_B_FPROG_OFF, W, KAD_B_FPROG, 4, "fprog", &n_f) ||
+      !k.csr(KAD_B_SPROG_OFF, W, KAD_B_SPROG, 4, "sprog", &n_sp) ||
+      !k.csr(KAD_B_PLACE_OFF, W, KAD_B_PLACE, 4, "place", &n_pl) ||
+      !k.csr(KAD_B_CUR_OFF, W, KAD_B_CUR_ID, 4, "cur", &n_cur) || !k.extent(KAD_B_CUR_REP, n_cur, 8, "cur_rep") ||
+      !k.csr(KAD_B_PREF_OFF, W, KAD_B_PREF_ID, 4, "pref", &n_pref) ||
+      !k.extent(KAD_B_PREF_W, n_pref, 8, "pref_w") || !k.extent(KAD_B_PREF_MIN, n_pref, 8, "pref_min") ||
+      !k.extent(KAD_B_PREF_MAX, n_pref, 8, "pref_max") || !k.extent(KAD_B_PREF_CAP, n_pref, 8, "pref_cap") ||
+      !k.extent(KAD_B_PREF_FLAGS, n_pref, 4, "pref_flags") || !k.csr(KAD_B_KEY_OFF, W, KAD_B_KEY, 1, "key", &n_key) ||
+      !k.csr(KAD_B_REQ_OFF, NR, KAD_B_REQ, 4, "req", &n_req))
+    return KAD_EINVAL;
+  if (!k.sorted_ids(KAD_B_PLACE_OFF, KAD_B_PLACE, W, 0, C, true, "placement") ||
+      !k.sorted_ids(KAD_B_CUR_OFF, KAD_B_CUR_ID, W, 0, C, true, "current cluster") ||
+      !k.sorted_ids(KAD_B_PREF_OFF, KAD_B_PREF_ID, W, 0, C, true, "preference"))
+    return KAD_EINVAL;
+  const uint32_t* fl = k.arr<uint32_t>(KAD_B_FLAGS);
+  const int32_t* gv = k.arr<int32_t>(KAD_B_GVK);
+  const int32_t* ts = k.arr<int32_t>(KAD_B_TOLSET);
+  const int64_t* mc = k.arr<int64_t>(KAD_B_MAX_CLUSTERS);
+  const int64_t* oo = k.arr<int64_t>(KAD_B_OUT_OFF);
+  const int32_t* sid = k.arr<int32_t>(KAD_B_SREQ_ID);
+  const int32_t* po = k.arr<int32_t>(KAD_B_PLACE_OFF);
+  for (int64_t j = 0; j < n_s; j++)
+    if (sid[j] < -1 || sid[j] >= sh.n_scalar) return fail(c, KAD_EINVAL, "scalar request id out of range");
+  // output slot ranges must hold every pair the kernels can write for the packed
+  // profile: min(C, MaxClusters, |ClusterNames|) (pack.py Batch), 0 when sticky
+  if (oo[0] != 0 || oo[W] != h.n_out_slots) return fail(c, KAD_EINVAL, "out_off must run from 0 to n_out_slots");
+  const bool sel_max = h.packed_select_plugin == KAD_PL_MAX_CLUSTER;
+  const bool place_on = h.packed_filter_mask & (1u << KAD_PL_PLACEMENT_FILTER);
+  for (int w = 0; w < W; w++) {
+    if (gv[w] < -1 || gv[w] >= 64 * sh.n_gvk_words) return fail(c, KAD_EINVAL, "gvk id out of range");
+    if (ts[w] < 0 || ts[w] >= NT) return fail(c, KAD_EINVAL, "toleration-set id out of range");
+    const int64_t len = oo[w + 1] - oo[w];
+    if (len < 0 || len > h.max_row_slots) return fail(c, KAD_EINVAL, "output slot range exceeds max_row_slots");
+    int64_t bound = C;
+    if (sel_max && (fl[w] & KAD_W_HAS_MAX_CLUSTERS) && mc[w] >= 0 && mc[w] < bound) bound = mc[w];
+    if (place_on && (fl[w] & KAD_W_HAS_PLACEMENT) && po[w + 1] - po[w] < bound) bound = po[w + 1] - po[w];
+    if (fl[w] & KAD_W_STICKY) bound = 0;
+    if (len < bound) return fail(c, KAD_EINVAL, "output slot range smaller than the unit's selection bound");
+  }
+  if (h.max_row_slots < 0 || h.max_row_slots > (C > 0 ? C : 1)) return fail(c, KAD_EINVAL, "bad max_row_slots");
+  // requirement table: [op | n << 8, key, payload...]
+  const int32_t* ro = k.arr<int32_t>(KAD_B_REQ_OFF);
+  const int32_t* rq = k.arr<int32_t>(KAD_B_REQ);
+  for (int r = 0; r < NR; r++) {
+    const int len = ro[r + 1] - ro[r];
+    if (len < 2) return fail(c, KAD_EINVAL, "requirement shorter than two words");
+    const int32_t* p = rq + ro[r];
+    const int op = p[0] & 0xff, n = (int)((uint32_t)p[0] >> 8), key = p[1];
+    if (len != 2 + n) return fail(c, KAD_EINVAL, "requirement payload length mismatch");
+    switch (op) {
+      case KAD_OP_IN: case KAD_OP_NOTIN: case KAD_OP_EQ:
+        if (key < 0 || key >= sh.n_label_keys || n < 1) return fail(c, KAD_EINVAL, "bad label requirement");
+        break;
+      case KAD_OP_EXISTS: case KAD_OP_DNE:
+        if (key < 0 || key >= sh.n_label_keys || n != 0) return fail(c, KAD_EINVAL, "bad label requirement");
+        break;
+      case KAD_OP_GT: case KAD_OP_LT:
+        if (key < 0 || key >= sh.n_label_keys || n != 2) return fail(c, KAD_EINVAL, "bad Gt/Lt requirement");
+        break;
+      case KAD_OP_NAME_EQ: case KAD_OP_NAME_NE:
+        if (key < -1 || key >= C) return fail(c, KAD_EINVAL, "bad field requirement");
+        break;
+      case KAD_OP_TRUE: case KAD_OP_FALSE:
+        break;
+      default:
+        return fail(c, KAD_EINVAL, "unknown requirement op");
+    }
+  }
+  // programs: every requirement id in range, structure consumes exactly the unit's words
+  const int32_t* fo = k.arr<int32_t>(KAD_B_FPROG_OFF);
+  const int32_t* fp = k.arr<int32_t>(KAD_B_FPROG);
+  const int32_t* spo = k.arr<int32_t>(KAD_B_SPROG_OFF);
+  const int32_t* sp = k.arr<int32_t>(KAD_B_SPROG);
+  auto ids_ok = [&](const int32_t* p, int at, int n, int len) {
+    if (n < 0 || at + n > len) return false;
+    for (int i = 0; i < n; i++)
+      if (p[at + i] < 0 || p[at + i] >= NR) return false;
+    return true;
+  };
+  for (int w = 0; w < W; w++) {
+    const int32_t* p = fp + fo[w];
+    const int len = fo[w + 1] - fo[w];
+    bool ok = len >= 2;
+    int pc = 0;
+    if (ok) {
+      const int n_sel = p[pc++];
+      ok = ids_ok(p, pc, n_sel, len);
+      pc += ok ? n_sel : 0;
+      ok = ok && pc < len;
+      if (ok && p[pc++]) {
+        ok = pc < len;
+        const int n_terms = ok ? p[pc++] : 0;
+        ok = ok && n_terms >= 0;
+        for (int t = 0; ok && t < n_terms; t++) {
+          ok = pc + 3 <= len;
+          if (!ok) break;
+          const int ne = p[pc + 1], nf = p[pc + 2];
+          ok = ne >= 0 && nf >= 0 && ids_ok(p, pc + 3, ne + nf, len);
+          pc += 3 + (ok ? ne + nf : 0);
+        }
+      }
+    }
+    if (!ok || pc != len) return fail(c, KAD_EINVAL, "malformed filter program of unit " + std::to_string(w));
+    p = sp + spo[w];
+    const int sl = spo[w + 1] - spo[w];
+    ok = sl >= 1;
+    pc = 0;
+    if (ok) {
+      const int n_terms = p[pc++];
+      ok = n_terms >= 0;
+      for (int t = 0; ok && t < n_terms; t++) {
+        ok = pc + 2 <= sl;
+        if (!ok) break;
+        const int ne = p[pc + 1];
+        ok = ids_ok(p, pc + 2, ne, sl);
+        pc += 2 + (ok ? ne : 0);
+      }
+    }
+    if (!ok || pc != sl) return fail(c, KAD_EINVAL, "malformed score program of unit " + std::to_string(w));
+  }
   return 0;
 }
 
@@ -185,14 +372,6 @@ static int bind_snapshot(kad_ctx* c, const kad_snapshot_header& h) {
   return 0;
 }
 
-static int check_snapshot_header(kad_ctx* c, const kad_snapshot_header& h, size_t nbytes) {
-  if (nbytes < sizeof(h) || h.magic != KAD_SNAPSHOT_MAGIC) return fail(c, KAD_EINVAL, "bad snapshot magic");
-  if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "snapshot ABI version mismatch");
-  if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "snapshot size mismatch");
-  for (int i = 0; i < KAD_S_NARRAYS; i++)
-    if (h.off[i] > nbytes || (h.off[i] & 7)) return fail(c, KAD_EINVAL, "bad snapshot array offset");
-  return 0;
-}
 
 static const int kResArrays[4] = {KAD_S_ALLOC_CPU, KAD_S_ALLOC_MEM, KAD_S_USED_CPU, KAD_S_USED_MEM};
 
@@ -227,6 +406,26 @@ static void snapshot_array_shape(const kad_snapshot_header& h, int a, int64_t* r
     case KAD_S_NAME_FNV: case KAD_S_CFLAGS: *esz = 4; break;
     default: break;
   }
+}
+
+// every array of the snapshot lies inside the blob: rows(a) * C elements of its size at an aligned offset
+static int check_snapshot_header(kad_ctx* c, const kad_snapshot_header& h, size_t nbytes) {
+  if (nbytes < sizeof(h) || h.magic != KAD_SNAPSHOT_MAGIC) return fail(c, KAD_EINVAL, "bad snapshot magic");
+  if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "snapshot ABI version mismatch");
+  if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "snapshot size mismatch");
+  if (h.n_clusters < 0 || h.n_clusters > 65535) return fail(c, KAD_EINVAL, "n_clusters must be in [0, 65535]");
+  // the kernels read GVK and taint word 0 of every cluster
+  if (h.n_gvk_words < 1 || h.n_taint_words < 1 || h.n_label_keys < 0 || h.n_scalar < 0)
+    return fail(c, KAD_EINVAL, "snapshot needs n_gvk_words >= 1, n_taint_words >= 1, n_label_keys >= 0, n_scalar >= 0");
+  for (int i = 0; i < KAD_S_NARRAYS; i++) {
+    int64_t rows;
+    int esz;
+    snapshot_array_shape(h, i, &rows, &esz);
+    const uint64_t len = (uint64_t)rows * (uint64_t)h.n_clusters * (uint64_t)esz;
+    if (h.off[i] > nbytes || (h.off[i] & 7) || len > nbytes - h.off[i])
+      return fail(c, KAD_EINVAL, "snapshot array " + std::to_string(i) + " lies outside the blob");
+  }
+  return 0;
 }
 
 int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
@@ -336,9 +535,10 @@ int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
   return KAD_OK;
 }
 
-int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
-  if (!c || !blob) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
+  // any failed upload leaves no batch resident (validation failed, or device buffers half-written)
+  c->have_batch = false;
+  c->ran = false;
   if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot uploaded");
   kad_batch_header h;
   if (nbytes < sizeof(h)) return fail(c, KAD_EINVAL, "batch too small");
@@ -349,8 +549,7 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   if (h.snapshot_fingerprint != c->snap_hdr.fingerprint || h.n_clusters != c->snap_hdr.n_clusters ||
       h.n_taint_words != c->snap_hdr.n_taint_words)
     return fail(c, KAD_EINVAL, "batch was packed against a different snapshot");
-  for (int i = 0; i < KAD_B_NARRAYS; i++)
-    if (h.off[i] > nbytes || (h.off[i] & 7)) return fail(c, KAD_EINVAL, "bad batch array offset");
+  if (int r = validate_batch(c, blob, nbytes, h)) return r;
   HIPCHK(c, hipSetDevice(c->device));
   if (int r = grow(c, &c->d_batch, &c->batch_cap, nbytes)) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_batch, blob, nbytes, hipMemcpyHostToDevice, c->stream));
@@ -478,6 +677,12 @@ int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   return KAD_OK;
 }
 
+int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
+  if (!c || !blob) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return batch_upload_locked(c, blob, nbytes);
+}
+
 static int validate_profile(kad_ctx* c, const kad_profile* p) {
   if (!p) return fail(c, KAD_EINVAL, "null profile");
   const uint32_t filters = (1u << KAD_PL_API_RESOURCES) | (1u << KAD_PL_TAINT_TOLERATION) |
@@ -564,9 +769,7 @@ int kad_last_timing(kad_ctx* c, float ms[3]) {
   return KAD_OK;
 }
 
-int kad_results_download(kad_ctx* c, const kad_result_view* out) {
-  if (!c || !out) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+static int results_download_locked(kad_ctx* c, const kad_result_view* out) {
   if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
   HIPCHK(c, hipSetDevice(c->device));
   const size_t W = c->batch_hdr.n_units;
@@ -584,10 +787,20 @@ int kad_results_download(kad_ctx* c, const kad_result_view* out) {
   return KAD_OK;
 }
 
+int kad_results_download(kad_ctx* c, const kad_result_view* out) {
+  if (!c || !out) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return results_download_locked(c, out);
+}
+
+// One critical section from upload to download: worker goroutines sharing the
+// ctx cannot interleave and schedule / download each other's batches.
 int kad_schedule_batch(kad_ctx* c, const kad_profile* p, const void* blob, size_t nbytes, const kad_result_view* out) {
-  if (int r = kad_batch_upload(c, blob, nbytes)) return r;
-  if (int r = kad_schedule(c, p)) return r;
-  return kad_results_download(c, out);
+  if (!c || !blob || !out) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (int r = batch_upload_locked(c, blob, nbytes)) return r;
+  if (int r = schedule_locked(c, p, nullptr, nullptr)) return r;
+  return results_download_locked(c, out);
 }
 
 int kad_debug_phase_counters(uint64_t* out, int reset) { return kad::debug_phase_counters(out, reset); }
@@ -720,9 +933,7 @@ int kad_plan_rows(kad_ctx* c, int n_rows, const int32_t* row_off, const uint32_t
 }
 
 /* ------------------------------------------------ scheduling-trigger hashes */
-int kad_trigger_suffix_upload(kad_ctx* c, const uint8_t* suffix, size_t nbytes) {
-  if (!c || (!suffix && nbytes)) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+static int trigger_suffix_upload_locked(kad_ctx* c, const uint8_t* suffix, size_t nbytes) {
   HIPCHK(c, hipSetDevice(c->device));
   int r = grow(c, &c->t_suffix, &c->t_suffix_cap, ((nbytes + 63) & ~(size_t)63) + 64);
   if (r) return r;
@@ -743,11 +954,9 @@ int kad_trigger_suffix_upload(kad_ctx* c, const uint8_t* suffix, size_t nbytes) 
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-int kad_trigger_prefixes_upload(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix) {
-  if (!c || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
+static int trigger_prefixes_upload_locked(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix) {
   for (int i = 0; i < n; i++)
     if (prefix_off[i + 1] < prefix_off[i]) return fail(c, KAD_EINVAL, "prefix_off must be non-decreasing");
-  std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(c, hipSetDevice(c->device));
   const size_t nbytes = (size_t)prefix_off[n];
   int r = grow(c, &c->t_prefix, &c->t_prefix_cap, nbytes + 64);
@@ -770,9 +979,7 @@ int kad_trigger_prefixes_upload(kad_ctx* c, int n, const int64_t* prefix_off, co
   return KAD_OK;
 }
 
-int kad_trigger_run(kad_ctx* c) {
-  if (!c) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+static int trigger_run_locked(kad_ctx* c) {
   if (c->t_suffix_len < 0 || c->t_n < 0) return fail(c, KAD_ESTATE, "upload the trigger suffix and prefixes first");
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipEventRecord(c->tev[0], c->stream));
@@ -786,6 +993,7 @@ int kad_trigger_run(kad_ctx* c) {
 
 int kad_trigger_timing(kad_ctx* c, float ms[2]) {
   if (!c || !ms) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
   if (!c->t_ran) return fail(c, KAD_ESTATE, "no trigger run");
   HIPCHK(c, hipEventSynchronize(c->tev[2]));
   HIPCHK(c, hipEventElapsedTime(&ms[0], c->tev[0], c->tev[2]));
@@ -793,9 +1001,7 @@ int kad_trigger_timing(kad_ctx* c, float ms[2]) {
   return KAD_OK;
 }
 
-int kad_trigger_download(kad_ctx* c, uint32_t* out_hash) {
-  if (!c) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
+static int trigger_download_locked(kad_ctx* c, uint32_t* out_hash) {
   if (!c->t_ran) return fail(c, KAD_ESTATE, "no trigger run");
   HIPCHK(c, hipSetDevice(c->device));
   if (c->t_n > 0 && out_hash)
@@ -804,12 +1010,39 @@ int kad_trigger_download(kad_ctx* c, uint32_t* out_hash) {
   return KAD_OK;
 }
 
+int kad_trigger_suffix_upload(kad_ctx* c, const uint8_t* suffix, size_t nbytes) {
+  if (!c || (!suffix && nbytes)) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return trigger_suffix_upload_locked(c, suffix, nbytes);
+}
+
+int kad_trigger_prefixes_upload(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix) {
+  if (!c || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return trigger_prefixes_upload_locked(c, n, prefix_off, prefix);
+}
+
+int kad_trigger_run(kad_ctx* c) {
+  if (!c) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return trigger_run_locked(c);
+}
+
+int kad_trigger_download(kad_ctx* c, uint32_t* out_hash) {
+  if (!c) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  return trigger_download_locked(c, out_hash);
+}
+
+// one critical section (see kad_schedule_batch)
 int kad_trigger_hashes(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix, const uint8_t* suffix,
                        size_t suffix_len, uint32_t* out_hash) {
-  int r = kad_trigger_suffix_upload(c, suffix, suffix_len);
-  if (!r) r = kad_trigger_prefixes_upload(c, n, prefix_off, prefix);
-  if (!r) r = kad_trigger_run(c);
-  if (!r) r = kad_trigger_download(c, out_hash);
+  if (!c || (!suffix && suffix_len) || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  int r = trigger_suffix_upload_locked(c, suffix, suffix_len);
+  if (!r) r = trigger_prefixes_upload_locked(c, n, prefix_off, prefix);
+  if (!r) r = trigger_run_locked(c);
+  if (!r) r = trigger_download_locked(c, out_hash);
   return r;
 }
 

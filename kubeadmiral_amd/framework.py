@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Callable, Dict, FrozenSet, List, Mapping, Optional
 
 APIResources = "APIResources"
 TaintToleration = "TaintToleration"
@@ -100,27 +100,62 @@ class KadProfile(ctypes.Structure):
                 ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 3)]
 
 
+EXTENSION_POINTS = ("FilterPlugin", "ScorePlugin", "SelectPlugin", "ReplicasPlugin")
+# what each in-tree plugin implements (plugins/*: which framework interfaces the type satisfies)
+IN_TREE_REGISTRY: Dict[str, Callable[[], FrozenSet[str]]] = {
+    n: (lambda n=n: frozenset(p for p, kinds in zip(EXTENSION_POINTS, (FILTER_PLUGINS, SCORE_PLUGINS, SELECT_PLUGINS,
+                                                                      REPLICAS_PLUGINS)) if n in kinds))
+    for n in sorted(IN_TREE)
+}
+
+
+def new_framework(registry: Mapping[str, Callable[[], FrozenSet[str]]], enabled: EnabledPlugins) -> Dict[str, List[str]]:
+    """runtime.NewFramework (framework/runtime/framework.go:45-95) over a registry of plugin factories.
+
+    A factory returns the set of extension-point interfaces its plugin implements (the Go plugin's type).
+    Every enabled plugin is constructed exactly once; plugins that are registered but not enabled are never
+    constructed (IsPluginEnabled, pkg/apis/core/types.go:28-43). Each extension point is then filled in
+    order, failing like addPlugins (:72-99): "<Point> <name> does not exist", "plugin <name> does not
+    implement <Point>", "plugin <name> already registered as <Point>". Returns the plugin lists per point.
+    """
+    built = {name: factory() for name, factory in registry.items() if enabled.is_plugin_enabled(name)}
+    out: Dict[str, List[str]] = {}
+    for point, names in zip(EXTENSION_POINTS, (enabled.filter_plugins, enabled.score_plugins,
+                                               enabled.select_plugins, enabled.replicas_plugins)):
+        seen: List[str] = []
+        for n in names:
+            if n not in built:
+                raise FrameworkError(f"{point} {n} does not exist")
+            if point not in built[n]:
+                raise FrameworkError(f"plugin {n} does not implement {point}")
+            if n in seen:
+                raise FrameworkError(f"plugin {n} already registered as {point}")
+            seen.append(n)
+        out[point] = seen
+    return out
+
+
 class Framework:
-    """Validated framework = the device profile (kad_profile)."""
+    """Validated framework = the device profile (kad_profile).
+
+    ``registry``: None = the in-tree registry (profile.go:39-50); a set of names = the in-tree plugins
+    among them plus, for any other name, a registered out-of-tree (webhook) plugin; or a mapping
+    name → factory as :func:`new_framework` takes. Construction fails where ``runtime.NewFramework``
+    does; a valid framework that enables an out-of-tree plugin raises :class:`UnsupportedPlugin` (the
+    device runs only in-tree plugins, so such profiles keep the Go path).
+    """
 
     def __init__(self, enabled: Optional[EnabledPlugins] = None, registry=None, flags: int = 0):
         enabled = enabled if enabled is not None else default_enabled_plugins()
-        registry = set(IN_TREE if registry is None else registry)
-        for point, names, kinds in (("FilterPlugin", enabled.filter_plugins, FILTER_PLUGINS),
-                                    ("ScorePlugin", enabled.score_plugins, SCORE_PLUGINS),
-                                    ("SelectPlugin", enabled.select_plugins, SELECT_PLUGINS),
-                                    ("ReplicasPlugin", enabled.replicas_plugins, REPLICAS_PLUGINS)):
-            seen = set()
+        if registry is None:
+            registry = IN_TREE_REGISTRY
+        elif not isinstance(registry, Mapping):  # names: out-of-tree ones implement every point (webhook adapter)
+            registry = {n: IN_TREE_REGISTRY.get(n, lambda: frozenset(EXTENSION_POINTS)) for n in registry}
+        lists = new_framework(registry, enabled)
+        for names in lists.values():
             for n in names:
-                if n not in registry:
-                    raise FrameworkError(f"{point} {n} does not exist")
                 if n not in IN_TREE:
                     raise UnsupportedPlugin(f"plugin {n} is not an in-tree plugin")
-                if n not in kinds:
-                    raise FrameworkError(f"plugin {n} does not implement {point}")
-                if n in seen:
-                    raise FrameworkError(f"plugin {n} already registered as {point}")
-                seen.add(n)
         self.enabled = enabled
         self.flags = flags
 

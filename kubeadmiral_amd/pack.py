@@ -133,6 +133,7 @@ class Snapshot:
     def __init__(self, clusters: List[T.FederatedCluster]):
         C = len(clusters)
         self.clusters = list(clusters)
+        self.keys = [T.cluster_key(c) for c in clusters]  # content identity per cluster (diff)
         self.names = [c.name for c in clusters]
         self.name_id: Dict[str, int] = {}
         for i, n in enumerate(self.names):
@@ -253,32 +254,49 @@ class Snapshot:
                        list(self.label_key_id), [list(v) for v in self.label_vals])).encode())
         return int.from_bytes(h.digest(), "little")
 
-    def update(self, clusters: List[T.FederatedCluster]) -> Optional["SnapshotDelta"]:
-        """Apply cluster update events in place; returns the delta for ``kad_snapshot_update``.
+    def diff(self, clusters: List[T.FederatedCluster]) -> Optional["SnapshotDelta"]:
+        """The delta from this snapshot to ``clusters`` (cluster update events), without applying it.
 
-        ``clusters`` is the new cluster list. Returns None — the caller repacks
-        (``Snapshot(clusters)``) and re-uploads — when the names or their order
-        changed (join / leave) or a changed cluster needs a vocabulary entry
-        that is not interned yet. Otherwise the changed clusters' columns are
-        written into this snapshot's blob and the same columns come back as a
-        delta blob; the vocabulary (and with it every packed batch) stays valid.
+        Returns None — the caller repacks (``Snapshot(clusters)``) and re-uploads
+        — when the names or their order changed (join / leave) or a changed
+        cluster needs a vocabulary entry that is not interned yet. Otherwise a
+        delta blob of the changed clusters' columns (compared by
+        :func:`types.cluster_key`: resourceVersion, else content) for
+        ``kad_snapshot_update``; the vocabulary (and with it every packed
+        batch) stays valid. :meth:`commit` writes it into this snapshot once
+        the device has taken it.
         """
         if len(clusters) != self.C or any(c.name != n for c, n in zip(clusters, self.names)):
             return None
-        changed, cols = [], []
-        for i, (old, new) in enumerate(zip(self.clusters, clusters)):
-            if old is new or old == new:
+        changed, cols, keys = [], [], []
+        for i, new in enumerate(clusters):
+            k = T.cluster_key(new)
+            if k == self.keys[i]:
                 continue
             col = self._columns(new)
             if col is None:
                 return None
             changed.append(i)
             cols.append(col)
-        for i, col in zip(changed, cols):
+            keys.append(k)
+        d = SnapshotDelta(self, changed, cols)
+        d.clusters, d.keys = list(clusters), keys
+        return d
+
+    def commit(self, delta: "SnapshotDelta") -> None:
+        """Apply a delta from :meth:`diff` to the host copy (blob columns, cluster list, keys)."""
+        for i, col, k in zip(delta.changed, delta.cols, delta.keys):
             for a, v in zip(self.arrays, col):
                 a[..., i] = v
-        self.clusters = list(clusters)
-        return SnapshotDelta(self, changed, cols)
+            self.keys[i] = k
+        self.clusters = delta.clusters
+
+    def update(self, clusters: List[T.FederatedCluster]) -> Optional["SnapshotDelta"]:
+        """:meth:`diff` + :meth:`commit` on the host copy; returns the delta (None: repack)."""
+        d = self.diff(clusters)
+        if d is not None:
+            self.commit(d)
+        return d
 
 
 DELTA_MAGIC = 0x4441444B
@@ -296,6 +314,9 @@ class SnapshotDelta:
     def __init__(self, snap: Snapshot, changed: List[int], cols: List[list]):
         n = len(changed)
         self.changed = changed
+        self.cols = cols
+        self.clusters: List[T.FederatedCluster] = []
+        self.keys: list = []
         arrays = [np.array(changed, np.int32)]
         for k, (dt, r) in enumerate(Snapshot.ARRAYS):
             rows = snap._rows(r)

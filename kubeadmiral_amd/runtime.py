@@ -158,6 +158,17 @@ class Context:
         self._chk(self.L.kad_results_download(self.h, ctypes.byref(v)))
         return res
 
+    def schedule_batch(self, fwk: Framework, batch: Batch) -> BatchResult:
+        """kad_schedule_batch: upload, schedule and download under one hold of the context lock."""
+        res = BatchResult.empty(batch)
+        v = ResultView(res.status.ctypes.data, res.count.ctypes.data, res.flags.ctypes.data, res.cluster.ctypes.data,
+                       res.replicas.ctypes.data)
+        prof = fwk.to_c()
+        self._chk(self.L.kad_schedule_batch(self.h, ctypes.byref(prof), _p(batch.blob), batch.blob.nbytes,
+                                            ctypes.byref(v)))
+        self.batch = batch
+        return res
+
     def run(self, fwk: Framework, batch: Batch) -> BatchResult:
         self.upload_batch(batch)
         self.schedule(fwk)
@@ -280,11 +291,18 @@ class TriggerHasher:
 
 
 class BatchScheduler:
-    """Batch ScheduleAlgorithm on the GPU (generic_scheduler.go:37-44 semantics per unit)."""
+    """Batch ScheduleAlgorithm on the GPU (generic_scheduler.go:37-44 semantics per unit).
+
+    The resident snapshot follows the cluster list of every call: each call
+    diffs the list against it by content (``types.cluster_key``), so a new
+    list, replaced elements or elements edited in place are all picked up —
+    the library keeps no caller pointers. Host columns are committed only
+    after the device accepted the delta; a failed device update forces a full
+    re-upload on the next call.
+    """
 
     def __init__(self, ctx: Optional[Context] = None, device: int = 0):
         self.ctx = ctx if ctx is not None else Context(device)
-        self._clusters: Optional[List[T.FederatedCluster]] = None
         self.full_uploads = 0   # snapshot (re)packs + uploads
         self.delta_updates = 0  # in-place kad_snapshot_update calls
 
@@ -294,24 +312,25 @@ class BatchScheduler:
         repack and full upload (join, leave, new label value / taint / API resource)."""
         snap = self.ctx.snap
         if snap is not None:
-            delta = snap.update(clusters)
+            delta = snap.diff(clusters)
             if delta is not None:
                 if delta.changed:
-                    self.ctx.update_snapshot(delta)
+                    try:
+                        self.ctx.update_snapshot(delta)
+                    except BaseException:
+                        self.ctx.snap = None  # device state unknown: the next call re-uploads in full
+                        raise
                     self.delta_updates += 1
-                self._clusters = clusters
+                snap.commit(delta)
                 return snap
         snap = Snapshot(clusters)
         self.ctx.upload_snapshot(snap)
         self.full_uploads += 1
-        self._clusters = clusters
         return snap
 
     def schedule(self, fwk: Framework, units: List[T.SchedulingUnit], clusters: List[T.FederatedCluster]
                  ) -> List[Union[T.ScheduleResult, T.ScheduleError]]:
-        snap = self.ctx.snap
-        if snap is None or self._clusters is not clusters:
-            snap = self.set_clusters(clusters)
+        snap = self.set_clusters(clusters)
         batch = Batch(snap, fwk, units)
         res = self.ctx.run(fwk, batch)
         return [to_schedule_result(res, w, su, snap.names) for w, su in enumerate(units)]

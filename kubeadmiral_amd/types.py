@@ -29,8 +29,9 @@ in the reference) uses its Go field names.
 
 from __future__ import annotations
 
+import hashlib
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Set, Tuple
+from typing import Dict, List, Optional, Sequence, Set, Tuple
 
 # pkg/apis/core/v1alpha1/types_propagationpolicy.go (SchedulingMode constants)
 SCHEDULING_MODE_DUPLICATE = "Duplicate"
@@ -131,9 +132,12 @@ class FederatedCluster:
     api_resource_types: List[APIResource] = field(default_factory=list)
     allocatable: Optional[Dict[str, str]] = None
     available: Optional[Dict[str, str]] = None
+    resource_version: str = ""  # metadata.resourceVersion ("" = unknown: content is compared instead)
 
     def to_json(self):
         meta = {"name": self.name}
+        if self.resource_version:
+            meta["resourceVersion"] = self.resource_version
         if self.labels is not None:
             meta["labels"] = dict(self.labels)
         spec = {}
@@ -164,7 +168,24 @@ class FederatedCluster:
             api_resource_types=[APIResource.from_json(r) for r in (status.get("apiResourceTypes") or [])],
             allocatable=res.get("allocatable"),
             available=res.get("available"),
+            resource_version=meta.get("resourceVersion", "") or "",
         )
+
+
+def cluster_key(c: FederatedCluster):
+    """What identifies a cluster object's content: (name, resourceVersion) when it carries one — the API
+    server bumps resourceVersion on every change, and informer-cache objects are never mutated in place —
+    else the whole content (so a list whose elements were replaced or edited in place is still seen)."""
+    return ("rv", c.name, c.resource_version) if c.resource_version else repr(c)
+
+
+def clusters_fingerprint(clusters: Sequence[FederatedCluster]) -> bytes:
+    """Content fingerprint of a cluster list, in order (the order is part of the snapshot)."""
+    h = hashlib.blake2b(digest_size=16)
+    for c in clusters:
+        h.update(repr(cluster_key(c)).encode())
+        h.update(b"\0")
+    return h.digest()
 
 
 @dataclass

@@ -26,7 +26,7 @@ class Recorder:
         self.fail_batches = fail_batches
 
     def schedule(self, fwk, units, clusters):
-        self.calls.append((bytes(fwk.to_c()), id(clusters), [u.name for u in units]))
+        self.calls.append((bytes(fwk.to_c()), T.clusters_fingerprint(clusters), [u.name for u in units]))
         if self.fail_batches:
             raise RuntimeError("device lost")
         return [T.ScheduleError("score", "boom") if u.name.startswith("bad")
@@ -74,15 +74,51 @@ def test_batches_split_by_framework_and_cluster_list():
     rec = Recorder()
     f1 = F.Framework()
     f2 = F.Framework(F.EnabledPlugins([F.APIResources], [], [F.MaxCluster], [F.ClusterCapacityWeight]))
-    cl_a, cl_b = [], []
+    cl_a, cl_b = [T.FederatedCluster("a")], [T.FederatedCluster("b")]
     jobs = [(f1 if i % 2 else f2, _unit(f"u{i}"), cl_a if i % 3 else cl_b) for i in range(120)]
     with CoalescingScheduler(rec, max_wait_s=0.05) as cs:
         _run_workers(cs, jobs, n_threads=4)
-    for prof, cid, names in rec.calls:
+    for prof, fp, names in rec.calls:
         idx = [int(n[1:]) for n in names]
         assert len({bytes((f1 if i % 2 else f2).to_c()) for i in idx}) == 1
         assert {bytes((f1 if i % 2 else f2).to_c()) for i in idx} == {prof}
-        assert {id(cl_a if i % 3 else cl_b) for i in idx} == {cid}
+        assert {T.clusters_fingerprint(cl_a if i % 3 else cl_b) for i in idx} == {fp}
+
+
+def test_equal_content_lists_share_a_batch():
+    """The reference lists clusters afresh per reconcile (scheduler.go:334): every call brings its own
+    list object. Equal content → one group per window; a changed label → its own group."""
+    rec = Recorder()
+    fwk = F.Framework()
+    base = [T.FederatedCluster(f"c{i}", labels={"k": "v"}) for i in range(4)]
+    changed = [T.FederatedCluster(f"c{i}", labels={"k": "w" if i == 2 else "v"}) for i in range(4)]
+    cs = CoalescingScheduler(rec, max_wait_s=0.5, max_batch=64)
+    futs = [cs.submit(fwk, _unit(f"u{i}"), [T.FederatedCluster(c.name, labels=dict(c.labels)) for c in base])
+            for i in range(40)]
+    futs += [cs.submit(fwk, _unit(f"x{i}"), list(changed)) for i in range(8)]
+    for f in futs:
+        f.result(timeout=10)
+    cs.close()
+    assert sum(cs.batches) == 48
+    by_fp = {}
+    for _, fp, names in rec.calls:
+        by_fp.setdefault(fp, []).extend(names)
+    assert sorted(by_fp[T.clusters_fingerprint(base)]) == sorted(f"u{i}" for i in range(40))
+    assert sorted(by_fp[T.clusters_fingerprint(changed)]) == sorted(f"x{i}" for i in range(8))
+    assert len(rec.calls) <= 2 * len(cs.batches)
+
+
+def test_resource_version_identifies_content():
+    a = T.FederatedCluster("c0", labels={"k": "v"}, resource_version="7")
+    b = T.FederatedCluster("c0", labels={"k": "other"}, resource_version="7")
+    assert T.clusters_fingerprint([a]) == T.clusters_fingerprint([b])  # same RV: the API server's promise
+    b.resource_version = "8"
+    assert T.clusters_fingerprint([a]) != T.clusters_fingerprint([b])
+    c = T.FederatedCluster("c0", labels={"k": "v"})
+    d = T.FederatedCluster("c0", labels={"k": "v"})
+    assert T.clusters_fingerprint([c]) == T.clusters_fingerprint([d])
+    d.labels["k"] = "w"  # edited in place, no RV: content decides
+    assert T.clusters_fingerprint([c]) != T.clusters_fingerprint([d])
 
 
 def test_unit_errors_raise_per_call_and_batch_failures_reach_every_caller():
@@ -132,7 +168,10 @@ def test_gpu_worker_threads_match_oracle():
     snap = pack.Snapshot(cl)
     want_b = ref.schedule(snap, pack.Batch(snap, fwk, units), fwk, n_threads=min(8, os.cpu_count() or 1))
     want = [to_schedule_result(want_b, w, su, snap.names) for w, su in enumerate(units)]
+    # every call brings its own copy of the cluster list, as the reference's reconcile does (scheduler.go:334)
     with CoalescingScheduler(max_wait_s=0.005) as cs:
-        got = _run_workers(cs, [(fwk, su, cl) for su in units], n_threads=8)
+        got = _run_workers(cs, [(fwk, su, list(cl)) for su in units], n_threads=8)
+        uploads = cs.scheduler.full_uploads
     assert [_norm(r) for r in got] == [_norm(r) for r in want]
-    assert len(cs.batches) < len(units)
+    assert len(cs.batches) < len(units) // 4  # coalesced across distinct but equal lists
+    assert uploads == 1  # the resident snapshot is reused: equal content, no repack

@@ -1,0 +1,155 @@
+"""The C ABI a Go shim binds (include/kad_sched.h), exercised through ctypes on the GPU.
+
+* ``kad_schedule_batch`` — the one scheduling entry the Go shim calls — against the C oracle, alone and
+  from 8 threads sharing one ``kad_ctx`` with batches of different sizes (the lock is held from upload
+  to download, so no thread can schedule or download another's batch).
+* ``kad_snapshot_upload_device`` — the snapshot taken from a device buffer (the RCCL-broadcast path of
+  bench.py) — then scheduled and compared with the oracle.
+* ``kad_batch_upload`` rejects malformed blobs (array extents, CSR offsets, ids, programs, output slot
+  bounds) with KAD_EINVAL before any device access, and the context keeps working afterwards.
+"""
+
+import threading
+
+import numpy as np
+import pytest
+
+from gpu_util import assert_same, c_oracle
+from kubeadmiral_amd import pack, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from kubeadmiral_amd import build, runtime
+    build.build()
+    c = runtime.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_schedule_batch_equals_oracle(ctx, seed):
+    clusters, units = synth.gen_fuzz(3000 + seed, W=90)
+    fwk = synth.fuzz_framework(seed)
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, units)
+    ctx.upload_snapshot(snap)
+    assert_same(ctx.schedule_batch(fwk, batch), c_oracle(snap, batch, fwk), f"kad_schedule_batch seed {seed}")
+
+
+def test_schedule_batch_empty(ctx):
+    clusters, _ = synth.gen_fuzz(1, W=1, C=8)
+    fwk = synth.fuzz_framework(1)
+    snap = pack.Snapshot(clusters)
+    ctx.upload_snapshot(snap)
+    res = ctx.schedule_batch(fwk, pack.Batch(snap, fwk, []))
+    assert len(res.status) == 0
+
+
+def test_schedule_batch_threads_share_one_ctx(ctx):
+    """8 threads, one kad_ctx, batches of 7..400 units each, interleaved: every result is its own batch's."""
+    clusters, _ = synth.gen_fuzz(77, W=1, C=120)
+    snap = pack.Snapshot(clusters)
+    ctx.upload_snapshot(snap)
+    jobs = []
+    for t in range(8):
+        # fuzz units name clusters "cluster-NNNNN", which the shared snapshot also has
+        _, units = synth.gen_fuzz(7000 + t, W=[7, 400, 33, 250, 90, 1, 310, 64][t], C=120)
+        fwk = synth.fuzz_framework(t)
+        batch = pack.Batch(snap, fwk, units)
+        jobs.append((fwk, batch, c_oracle(snap, batch, fwk)))
+    errors = []
+    start = threading.Barrier(8)
+
+    def work(i):
+        fwk, batch, want = jobs[i]
+        start.wait()
+        try:
+            for _ in range(6):
+                assert_same(ctx.schedule_batch(fwk, batch), want, f"thread {i}")
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[0]
+
+
+def test_snapshot_upload_device(ctx):
+    """Snapshot blob in device memory (as after bench.py's RCCL broadcast) → kad_snapshot_upload_device."""
+    import torch
+
+    clusters, units, fwk = synth.make_config("c2", W=3000, C=256, seed=21)
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, units)
+    buf = torch.from_numpy(snap.blob.copy()).to("cuda:0")
+    torch.cuda.synchronize()
+    ctx.upload_snapshot_device(buf.data_ptr(), snap.blob.nbytes, snap)
+    got = ctx.run(fwk, batch)
+    assert_same(got, c_oracle(snap, batch, fwk), "snapshot from device memory")
+    # a corrupted device header is rejected
+    bad = buf.clone()
+    bad[0] ^= 0xFF
+    torch.cuda.synchronize()
+    from kubeadmiral_amd.runtime import KadError
+    with pytest.raises(KadError, match="KAD_EINVAL"):
+        ctx.upload_snapshot_device(bad.data_ptr(), snap.blob.nbytes, snap)
+
+
+def _mutations(batch):
+    """(name, blob) pairs, each with one defect the validator must catch."""
+    h = pack.header_of(batch.blob, pack.BatchHeader)
+
+    def arr(i, dt):
+        return batch.blob[h.off[i]:].view(dt)
+
+    out = []
+
+    def mut(name, f):
+        b = batch.blob.copy()
+        f(b)
+        out.append((name, b))
+
+    W = batch.W
+    o = h.off
+    mut("tolset out of range", lambda b: b[o[pack.B_TOLSET]:].view(np.int32).__setitem__(0, h.n_tolsets))
+    mut("gvk out of range", lambda b: b[o[pack.B_GVK]:].view(np.int32).__setitem__(1, 1 << 20))
+    mut("fprog offsets not monotone",
+        lambda b: b[o[pack.B_FPROG_OFF]:].view(np.int32).__setitem__(1, int(arr(pack.B_FPROG_OFF, np.int32)[2]) + 1))
+    mut("fprog end past its array",
+        lambda b: b[o[pack.B_FPROG_OFF]:].view(np.int32).__setitem__(W, 1 << 28))
+    mut("requirement id past NR", lambda b: b[o[pack.B_FPROG]:].view(np.int32).__setitem__(1, h.n_reqs + 5)
+        if arr(pack.B_FPROG, np.int32)[0] > 0 else b[o[pack.B_FPROG]:].view(np.int32).__setitem__(0, 3))
+    mut("requirement key past K", lambda b: b[o[pack.B_REQ]:].view(np.int32).__setitem__(1, 1 << 20))
+    mut("unknown requirement op", lambda b: b[o[pack.B_REQ]:].view(np.int32).__setitem__(0, 0x7f))
+    mut("output slot range too small", lambda b: b[o[pack.B_OUT_OFF]:].view(np.int64).__setitem__(
+        1, int(arr(pack.B_OUT_OFF, np.int64)[0])))
+    mut("array offset past the blob",
+        lambda b: b.view(np.uint64).__setitem__(pack.BatchHeader.off.offset // 8 + pack.B_PREF_CAP, b.nbytes + 8))
+    mut("negative unit count", lambda b: b.view(np.int32).__setitem__(pack.BatchHeader.n_units.offset // 4, -3))
+    return out
+
+
+def test_malformed_batches_are_rejected(ctx):
+    from kubeadmiral_amd.runtime import KadError
+
+    clusters, units, fwk = synth.make_config("c5", W=200, C=300, seed=23)
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, units)
+    ctx.upload_snapshot(snap)
+    for name, blob in _mutations(batch):
+        bad = pack.Batch.__new__(pack.Batch)
+        bad.__dict__.update(batch.__dict__)
+        bad.blob = blob
+        with pytest.raises(KadError, match="KAD_EINVAL"):
+            ctx.upload_batch(bad)
+            pytest.fail(f"accepted: {name}")
+        with pytest.raises(KadError, match="KAD_ESTATE"):  # a rejected upload leaves no batch resident
+            ctx.schedule(fwk)
+    # the context still works
+    assert_same(ctx.run(fwk, batch), c_oracle(snap, batch, fwk), "after rejected blobs")

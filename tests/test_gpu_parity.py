@@ -174,19 +174,18 @@ def test_c2_full_size(ctx):
     ctx.schedule(fwk)
     res2 = ctx.download()
     assert_same(res2, res, "c2 rerun")
-    # timing off (bench's timed region): same bytes, and no event times to read
-    ctx.set_timing(False)
+    # timing is off by default (production callers pay no event records): no event times to read
+    with pytest.raises(Exception, match="timing off"):
+        ctx.timing()
+    # timing on (bench's per-kernel times): same bytes, and the stage times are there
+    ctx.set_timing(True)
     try:
         ctx.schedule(fwk)
         ctx.sync()
-        assert_same(ctx.download(), res, "c2 timing off")
-        with pytest.raises(Exception, match="timing off"):
-            ctx.timing()
+        assert_same(ctx.download(), res, "c2 timing on")
+        assert ctx.timing()[1] > 0
     finally:
-        ctx.set_timing(True)
-    ctx.schedule(fwk)
-    ctx.sync()
-    assert ctx.timing()[1] > 0
+        ctx.set_timing(False)
 
 
 def test_c4_subset(ctx):
@@ -199,6 +198,56 @@ def test_c5_subset(ctx):
     clusters, units, fwk = synth.make_config("c5", W=1500, C=2000)
     snap, batch, res = run(ctx, clusters, units, fwk)
     assert_same(res, c_oracle(snap, batch, fwk), "c5 1.5k x 2k")
+
+
+def test_c3_clusters_1000(ctx):
+    """C3's defining cluster count (C = 1000, 16 chunks: the lean kernel's wide rows, feasible lists beyond
+    256 positions) on 20k units of the C3 generator (seed 0xC3), against the C oracle."""
+    clusters, units, fwk = synth.make_config("c3", W=20_000)
+    assert len(clusters) == 1000
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert (res.status == pack.ST_OK).mean() > 0.5
+    assert (res.flags & pack.RF_TIE_STRADDLE).mean() > 0.05  # MaxCluster ties cut: pdqsort replays
+    assert_same(res, c_oracle(snap, batch, fwk), "c3 20k x 1000")
+
+
+def test_c3_default_set_divide_subrun(ctx):
+    """'a parity sub-run with the full default plugin set in Divide mode' (C = 1000)."""
+    rng = np.random.default_rng(synth.SEEDS["c3"] + 1)
+    clusters = synth.gen_clusters(rng, 1000)
+    units = synth.gen_units_c2(rng, 20_000, mode=T.SCHEDULING_MODE_DIVIDE)
+    for i, su in enumerate(units):  # half static weights, half dynamic (rsp.go:69)
+        if i % 2 == 0:
+            su.weights = {clusters[int(j)].name: int(rng.integers(0, 10)) for j in rng.integers(0, 1000, 24)}
+        su.avoid_disruption = bool(i % 3 == 0)
+    fwk = F.Framework(F.default_enabled_plugins())
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert (res.status == pack.ST_OK).mean() > 0.5
+    assert (res.replicas[:batch.n_out_slots] > 0).any()
+    assert_same(res, c_oracle(snap, batch, fwk), "c3 default-set Divide 20k x 1000")
+
+
+def test_c5_clusters_10000(ctx):
+    """C5's defining cluster count (C = 10 000: rows past the LDS budget, global-scratch replays, 256
+    taint ids in 4 words, 64 label keys) on 1 000 units of the C5 generator, against the C oracle."""
+    clusters, units, fwk = synth.make_config("c5", W=1000, C=10_000)
+    assert len(clusters) == 10_000
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert snap.TW == 4
+    assert_same(res, c_oracle(snap, batch, fwk), "c5 1k x 10000")
+
+
+@pytest.mark.parametrize("cfg,W,C", [("c2", 200, 256), ("c3", 60, 1000), ("c4", 100, 512), ("c5", 16, 10_000)])
+def test_config_shaped_gpu_equals_python_oracle(ctx, cfg, W, C):
+    """The object-level Python oracle (pinned by the reference's golden vectors) on samples of each
+    config's own generator: pins the packer at config shape, not only through the C oracle."""
+    from test_c_oracle import py_results, same
+    clusters, units, fwk = synth.make_config(cfg, W=W, C=C)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    want = py_results(fwk, units, clusters)
+    for w, su in enumerate(units):
+        got = to_schedule_result(res, w, su, snap.names)
+        assert same(got, want[w]), (cfg, w, got, want[w])
 
 
 def test_large_c_global_scratch(ctx):

@@ -89,3 +89,27 @@ def test_batch_reconcile_matches_per_object_path():
     clusters2[0].labels = dict(clusters2[0].labels or {}, extra="1")
     third = rec.reconcile(objs, by_key, clusters2)
     assert all(g.stage in ("scheduled", "policy-not-found") for g in third)
+
+
+def test_same_length_list_with_changed_label_reschedules():
+    """A NEW list object of the same length whose only change is a cluster label: the trigger hash must
+    change (schedulingtriggers.go:132-134 hashes cluster labels), so every object is rescheduled."""
+    from kubeadmiral_amd.controller import BatchReconciler
+
+    ftc, clusters, objs, pols = synth.gen_trigger_workload(np.random.default_rng(6), 120, 16, n_policies=4)
+    by_key = {}
+    for p in pols:
+        if p.spec.auto_migration is not None:
+            p.spec.auto_migration.when.pod_unschedulable_for = "2m"
+        by_key[(p.namespace, p.name)] = p
+    rec = BatchReconciler(ftc)
+    rec.reconcile(objs, by_key, clusters)
+    same = [copy.deepcopy(c) for c in clusters]  # equal content, new objects
+    assert all(g.stage == "unchanged" for g in rec.reconcile(objs, by_key, same))
+    relabeled = [copy.deepcopy(c) for c in clusters]
+    k = sorted(relabeled[5].labels)[0]
+    relabeled[5].labels[k] = relabeled[5].labels[k] + "x"
+    assert all(g.stage != "unchanged" for g in rec.reconcile(objs, by_key, relabeled))
+    # and in place on the very same list object
+    relabeled[6].taints = relabeled[6].taints + [T.Taint("new", "t", T.TAINT_PREFER_NO_SCHEDULE)]
+    assert all(g.stage != "unchanged" for g in rec.reconcile(objs, by_key, relabeled))

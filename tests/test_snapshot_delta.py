@@ -108,6 +108,62 @@ def test_vocabulary_growth_and_membership_need_a_full_upload():
     assert np.array_equal(before, snap.blob)  # a refused update leaves the snapshot untouched
 
 
+def test_in_place_edits_and_replaced_elements_are_seen():
+    """The same list object, an element replaced and another edited in place: both columns change."""
+    cl, _, _ = synth.make_config("c2", W=1, C=40, seed=11)
+    snap = pack.Snapshot(cl)
+    import copy
+
+    cl2 = list(cl)
+    snap2 = pack.Snapshot(cl2)
+    cl2[3] = copy.deepcopy(cl2[3])
+    cl2[3].available = dict(cl2[3].available, cpu="0")
+    cl2[7].available["memory"] = "0"  # edited in place (shared with ``cl``)
+    d = snap2.diff(cl2)
+    assert d is not None and d.changed == [3, 7]
+    assert snap2.diff(cl2).changed == [3, 7]  # not committed yet: still pending
+    snap2.commit(d)
+    assert snap2.diff(cl2).changed == []
+    assert np.array_equal(snap2.blob, pack.Snapshot(cl2).blob)
+    del snap
+
+
+def test_failed_device_update_is_not_committed():
+    """BatchScheduler commits host columns only after kad_snapshot_update succeeded; after a failure the
+    next call re-uploads the whole snapshot."""
+    from kubeadmiral_amd.runtime import BatchScheduler
+
+    class FakeCtx:
+        def __init__(self):
+            self.snap, self.fail, self.uploads, self.updates = None, False, 0, 0
+
+        def upload_snapshot(self, snap):
+            self.snap = snap
+            self.uploads += 1
+
+        def update_snapshot(self, delta):
+            if self.fail:
+                raise RuntimeError("device update failed")
+            self.updates += 1
+
+    ctx = FakeCtx()
+    bs = BatchScheduler(ctx)
+    cl, _, _ = synth.make_config("c1", W=1, seed=12)
+    snap = bs.set_clusters(cl)
+    before = snap.blob.copy()
+    new, _ = synth.mutate_clusters(np.random.default_rng(3), cl, 4, structural=False)
+    ctx.fail = True
+    with pytest.raises(RuntimeError):
+        bs.set_clusters(new)
+    assert np.array_equal(before, snap.blob)  # host copy unchanged
+    ctx.fail = False
+    bs.set_clusters(new)
+    assert ctx.uploads == 2 and ctx.updates == 0  # full re-upload after the failure
+    newer, _ = synth.mutate_clusters(np.random.default_rng(4), new, 3, structural=False)
+    bs.set_clusters(newer)
+    assert ctx.updates == 1 and np.array_equal(ctx.snap.blob, pack.Snapshot(newer).blob)
+
+
 def test_delta_header_layout():
     cl, _, _ = synth.make_config("c5", W=1, C=64, seed=6)
     snap = pack.Snapshot(cl)
