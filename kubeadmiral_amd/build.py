@@ -16,7 +16,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libkad.so")
-SOURCES = ["kad_kernels.hip", "kad_trigger.hip", "kad_delta.hip", "kad_api.hip"]
+SOURCES = ["kad_kernels.hip", "kad_trigger.hip", "kad_delta.hip", "kad_api.hip", "kad_pack.cpp"]
 HEADERS = ["kad_device.h", "kad_wave.h", "kad_select.h", "kad_plan.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KAD_OFFLOAD_ARCH", "gfx950")
@@ -24,7 +24,7 @@ ARCH = os.environ.get("KAD_OFFLOAD_ARCH", "gfx950")
 
 def _inputs():
     return [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [
-        os.path.join(os.path.dirname(HERE), "include", "kad_sched.h")]
+        os.path.join(os.path.dirname(HERE), "include", h) for h in ("kad_sched.h", "kad_pack.h")]
 
 
 def up_to_date() -> bool:
@@ -40,7 +40,7 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) 
         return LIB
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
            "-fno-fast-math", "-Wall", "-Wno-unused-function", "-o", out + ".tmp"]
-    cmd += list(extra)
+    cmd += ["-pthread"] + list(extra)
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)

@@ -1,0 +1,419 @@
+"""Columnar SchedulingUnits and the native packer (include/kad_pack.h).
+
+``SUColumns`` is the batch a cgo shim hands to ``kad_pack_batch``: every field
+of ``framework.SchedulingUnit`` (``pkg/controllers/scheduler/framework/
+types.go:33-69``) as flat arrays, maps and lists as CSR ranges, strings as ids
+into one string table. ``NativePacker(snap).pack(fwk, cols)`` runs the C++
+packer in libkad.so and returns a :class:`NativeBatch`, which the runtime
+uploads like a ``pack.Batch`` — its blob is byte-identical to the Python
+packer's for the same units (``tests/test_native_pack.py``).
+
+``from_units`` converts ``types.SchedulingUnit`` objects (the Python mirror of
+the reference's type) into columns; ``to_units`` converts back (tests use it to
+run the object-level oracle on natively packed batches). ``gen_units_c2_columns``
+(in ``synth``) generates the C2/C3 workload directly as columns.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import types as T
+from .framework import Framework
+
+# include/kad_pack.h KAD_SU_*
+SU_DUPLICATE = 1 << 0
+SU_STICKY = 1 << 1
+SU_AVOID_DISRUPTION = 1 << 2
+SU_HAS_DESIRED = 1 << 3
+SU_HAS_MAX_CLUSTERS = 1 << 4
+SU_HAS_AUTO_MIGRATION = 1 << 5
+SU_KEEP_UNSCHED = 1 << 6
+SU_HAS_CLUSTER_AFFINITY = 1 << 7
+SU_HAS_REQUIRED = 1 << 8
+
+I32, I64, U8, U32 = np.int32, np.int64, np.uint8, np.uint32
+
+# kad_su_columns fields after (n_units, str) in declaration order; n_reqs sits before rq_key
+FIELDS = [("group", I32), ("version", I32), ("kind", I32), ("namespace_", I32), ("name", I32), ("flags", U32),
+          ("desired", I64), ("max_clusters", I64), ("req_cpu", I64), ("req_mem", I64), ("req_eph", I64),
+          ("scalar_off", I32), ("scalar_name", I32), ("scalar_val", I64),
+          ("tol_off", I32), ("tol_key", I32), ("tol_op", I32), ("tol_value", I32), ("tol_effect", I32),
+          ("sel_off", I32), ("sel_key", I32), ("sel_value", I32),
+          ("rq_key", I32), ("rq_op", I32), ("rq_val_off", I32), ("rq_val", I32),
+          ("rterm_off", I32), ("rt_req", I32), ("rt_n_expr", I32), ("rt_n_field", I32),
+          ("pterm_off", I32), ("pt_weight", I32), ("pt_req", I32), ("pt_n_expr", I32),
+          ("place_off", I32), ("place_name", I32),
+          ("cur_off", I32), ("cur_name", I32), ("cur_rep", I64), ("cur_has_rep", U8),
+          ("wt_off", I32), ("wt_name", I32), ("wt_val", I64),
+          ("min_off", I32), ("min_name", I32), ("min_val", I64),
+          ("max_off", I32), ("max_name", I32), ("max_val", I64),
+          ("cap_off", I32), ("cap_name", I32), ("cap_val", I64)]
+DTYPES = dict(FIELDS)
+CSR_GROUPS = ["scalar", "tol", "sel", "rterm", "pterm", "place", "cur", "wt", "min", "max", "cap"]
+
+
+class StringTable:
+    """Strings by id: ``bytes[off[i]:off[i+1]]``. ``id()`` interns (dedup)."""
+
+    def __init__(self):
+        self._ids: Dict[str, int] = {}
+        self._parts: List[bytes] = []
+
+    def id(self, s: str) -> int:
+        i = self._ids.get(s)
+        if i is None:
+            i = self._ids[s] = len(self._parts)
+            self._parts.append(s.encode())
+        return i
+
+    def arrays(self):
+        off = np.zeros(len(self._parts) + 1, I64)
+        if self._parts:
+            off[1:] = np.cumsum([len(p) for p in self._parts])
+        data = np.frombuffer(b"".join(self._parts) or b"\0", U8).copy()
+        return off, data
+
+
+class SUColumns:
+    """A batch of SchedulingUnits as columns (kad_su_columns); arrays are contiguous numpy."""
+
+    def __init__(self, n_units: int, str_off: np.ndarray, str_data: np.ndarray, cols: Dict[str, np.ndarray]):
+        self.n_units = n_units
+        self.str_off = np.ascontiguousarray(str_off, I64)
+        self.str_data = np.ascontiguousarray(str_data, U8)
+        self.cols = {k: np.ascontiguousarray(cols[k], dt) for k, dt in FIELDS}
+
+    def __getitem__(self, k) -> np.ndarray:
+        return self.cols[k]
+
+    @property
+    def n_reqs(self) -> int:
+        return len(self.cols["rq_key"])
+
+    def strings(self) -> List[str]:
+        b = self.str_data.tobytes()
+        o = self.str_off
+        return [b[o[i]:o[i + 1]].decode() for i in range(len(o) - 1)]
+
+
+def _csr_off(lengths) -> np.ndarray:
+    off = np.zeros(len(lengths) + 1, I32)
+    if len(lengths):
+        off[1:] = np.cumsum(lengths)
+    return off
+
+
+# ------------------------------------------------------------------ objects → columns
+def from_units(units: Sequence[T.SchedulingUnit], st: Optional[StringTable] = None) -> SUColumns:
+    """SchedulingUnit objects → columns (what a Go shim fills from []SchedulingUnit)."""
+    st = st or StringTable()
+    c: Dict[str, list] = {k: [] for k, _ in FIELDS}
+    lens: Dict[str, list] = {k: [] for k in CSR_GROUPS}
+    rq_val_off = [0]
+    sid = st.id
+
+    def add_req(r: T.ClusterSelectorRequirement) -> None:
+        c["rq_key"].append(sid(r.key))
+        c["rq_op"].append(sid(r.operator))
+        for v in r.values or []:
+            c["rq_val"].append(sid(v))
+        rq_val_off.append(len(c["rq_val"]))
+
+    for su in units:
+        f = 0
+        if su.scheduling_mode == T.SCHEDULING_MODE_DUPLICATE:
+            f |= SU_DUPLICATE
+        if su.sticky_cluster:
+            f |= SU_STICKY
+        if su.avoid_disruption:
+            f |= SU_AVOID_DISRUPTION
+        if su.desired_replicas is not None:
+            f |= SU_HAS_DESIRED
+        c["desired"].append(su.desired_replicas if su.desired_replicas is not None else 0)
+        mc = 0
+        if su.max_clusters is not None:
+            f |= SU_HAS_MAX_CLUSTERS
+            mc = max(min(su.max_clusters, (1 << 63) - 1), -(1 << 63))
+        c["max_clusters"].append(mc)
+        am = su.auto_migration
+        if am is not None:
+            f |= SU_HAS_AUTO_MIGRATION
+            if am.keep_unschedulable_replicas:
+                f |= SU_KEEP_UNSCHED
+        ca = su.affinity.cluster_affinity if su.affinity is not None else None
+        if ca is not None:
+            f |= SU_HAS_CLUSTER_AFFINITY
+            if ca.required is not None:
+                f |= SU_HAS_REQUIRED
+        c["flags"].append(f)
+        for k, v in (("group", su.group), ("version", su.version), ("kind", su.kind),
+                     ("namespace_", su.namespace), ("name", su.name)):
+            c[k].append(sid(v))
+        rr = su.resource_request
+        c["req_cpu"].append(rr.milli_cpu)
+        c["req_mem"].append(rr.memory)
+        c["req_eph"].append(rr.ephemeral_storage)
+        sc = rr.scalar_resources or {}
+        lens["scalar"].append(len(sc))
+        for n, v in sc.items():
+            c["scalar_name"].append(sid(n))
+            c["scalar_val"].append(v)
+        tols = su.tolerations or []
+        lens["tol"].append(len(tols))
+        for t in tols:
+            c["tol_key"].append(sid(t.key))
+            c["tol_op"].append(sid(t.operator))
+            c["tol_value"].append(sid(t.value))
+            c["tol_effect"].append(sid(t.effect))
+        sel = su.cluster_selector or {}
+        lens["sel"].append(len(sel))
+        for k, v in sel.items():
+            c["sel_key"].append(sid(k))
+            c["sel_value"].append(sid(v))
+        terms = (ca.required.cluster_selector_terms or []) if (ca is not None and ca.required is not None) else []
+        lens["rterm"].append(len(terms))
+        for t in terms:
+            c["rt_req"].append(len(c["rq_key"]))
+            exprs, fields = t.match_expressions or [], t.match_fields or []
+            c["rt_n_expr"].append(len(exprs))
+            c["rt_n_field"].append(len(fields))
+            for r in exprs:
+                add_req(r)
+            for r in fields:
+                add_req(r)
+        prefs = (ca.preferred or []) if ca is not None else []
+        lens["pterm"].append(len(prefs))
+        for p in prefs:
+            exprs = p.preference.match_expressions or []
+            c["pt_weight"].append(p.weight)
+            c["pt_req"].append(len(c["rq_key"]))
+            c["pt_n_expr"].append(len(exprs))
+            for r in exprs:
+                add_req(r)
+        names = su.cluster_names or set()
+        lens["place"].append(len(names))
+        for n in sorted(names):
+            c["place_name"].append(sid(n))
+        cur = su.current_clusters or {}
+        lens["cur"].append(len(cur))
+        for n, r in cur.items():
+            c["cur_name"].append(sid(n))
+            c["cur_rep"].append(r if r is not None else 0)
+            c["cur_has_rep"].append(0 if r is None else 1)
+        for key, m in (("wt", su.weights), ("min", su.min_replicas), ("max", su.max_replicas),
+                       ("cap", am.estimated_capacity if am is not None else None)):
+            m = m or {}
+            lens[key].append(len(m))
+            for n, v in m.items():
+                c[key + "_name"].append(sid(n))
+                c[key + "_val"].append(v)
+
+    cols = {k: (np.asarray(c[k], dtype=dt) if c[k] else np.zeros(0, dt)) for k, dt in FIELDS}
+    for k in CSR_GROUPS:
+        cols[k + "_off"] = _csr_off(lens[k])
+    cols["rq_val_off"] = np.asarray(rq_val_off, I32)
+    off, data = st.arrays()
+    return SUColumns(len(units), off, data, cols)
+
+
+# ------------------------------------------------------------------ columns → objects
+def to_units(cols: SUColumns) -> List[T.SchedulingUnit]:
+    """Columns → SchedulingUnit objects (for the object-level oracle in tests)."""
+    S = cols.strings()
+    C = cols.cols
+    out = []
+
+    def rng(k, w):
+        o = C[k + "_off"]
+        return range(int(o[w]), int(o[w + 1]))
+
+    def req(i):
+        a, b = int(C["rq_val_off"][i]), int(C["rq_val_off"][i + 1])
+        return T.ClusterSelectorRequirement(S[C["rq_key"][i]], S[C["rq_op"][i]], [S[v] for v in C["rq_val"][a:b]])
+
+    for w in range(cols.n_units):
+        f = int(C["flags"][w])
+        ca = None
+        if f & SU_HAS_CLUSTER_AFFINITY:
+            required = None
+            if f & SU_HAS_REQUIRED:
+                terms = []
+                for t in rng("rterm", w):
+                    r0, ne, nf = int(C["rt_req"][t]), int(C["rt_n_expr"][t]), int(C["rt_n_field"][t])
+                    terms.append(T.ClusterSelectorTerm([req(i) for i in range(r0, r0 + ne)] or None,
+                                                       [req(i) for i in range(r0 + ne, r0 + ne + nf)] or None))
+                required = T.ClusterSelector(terms)
+            prefs = [T.PreferredSchedulingTerm(int(C["pt_weight"][t]), T.ClusterSelectorTerm(
+                [req(i) for i in range(int(C["pt_req"][t]), int(C["pt_req"][t]) + int(C["pt_n_expr"][t]))] or None))
+                for t in rng("pterm", w)]
+            ca = T.ClusterAffinity(required, prefs or None)
+        am = None
+        if f & SU_HAS_AUTO_MIGRATION:
+            cap = {S[C["cap_name"][i]]: int(C["cap_val"][i]) for i in rng("cap", w)}
+            am = T.AutoMigrationSpec(cap or None, bool(f & SU_KEEP_UNSCHED))
+        out.append(T.SchedulingUnit(
+            group=S[C["group"][w]], version=S[C["version"][w]], kind=S[C["kind"][w]],
+            namespace=S[C["namespace_"][w]], name=S[C["name"][w]],
+            desired_replicas=int(C["desired"][w]) if f & SU_HAS_DESIRED else None,
+            resource_request=T.Resource(int(C["req_cpu"][w]), int(C["req_mem"][w]), int(C["req_eph"][w]),
+                                        {S[C["scalar_name"][i]]: int(C["scalar_val"][i]) for i in rng("scalar", w)}
+                                        or None),
+            current_clusters={S[C["cur_name"][i]]: (int(C["cur_rep"][i]) if C["cur_has_rep"][i] else None)
+                              for i in rng("cur", w)} or None,
+            auto_migration=am,
+            scheduling_mode=T.SCHEDULING_MODE_DUPLICATE if f & SU_DUPLICATE else T.SCHEDULING_MODE_DIVIDE,
+            sticky_cluster=bool(f & SU_STICKY), avoid_disruption=bool(f & SU_AVOID_DISRUPTION),
+            cluster_selector={S[C["sel_key"][i]]: S[C["sel_value"][i]] for i in rng("sel", w)} or None,
+            cluster_names={S[C["place_name"][i]] for i in rng("place", w)} or None,
+            affinity=T.Affinity(ca) if ca is not None else None,
+            tolerations=[T.Toleration(S[C["tol_key"][i]], S[C["tol_op"][i]], S[C["tol_value"][i]],
+                                      S[C["tol_effect"][i]]) for i in rng("tol", w)] or None,
+            max_clusters=int(C["max_clusters"][w]) if f & SU_HAS_MAX_CLUSTERS else None,
+            min_replicas={S[C["min_name"][i]]: int(C["min_val"][i]) for i in rng("min", w)} or None,
+            max_replicas={S[C["max_name"][i]]: int(C["max_val"][i]) for i in rng("max", w)} or None,
+            weights={S[C["wt_name"][i]]: int(C["wt_val"][i]) for i in rng("wt", w)} or None))
+    return out
+
+
+# ------------------------------------------------------------------ ctypes mirror of kad_pack.h
+class KadStrs(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("off", ctypes.c_void_p), ("bytes", ctypes.c_void_p)]
+
+
+class KadPackVocab(ctypes.Structure):
+    _fields_ = [("cluster_names", KadStrs), ("scalar_names", KadStrs), ("gvk_group", KadStrs),
+                ("gvk_version", KadStrs), ("gvk_kind", KadStrs), ("label_keys", KadStrs),
+                ("label_val_off", ctypes.c_void_p), ("label_vals", KadStrs), ("taint_key", KadStrs),
+                ("taint_value", KadStrs), ("taint_effect", KadStrs), ("n_taint_words", ctypes.c_int32),
+                ("fingerprint", ctypes.c_uint64)]
+
+
+def _su_fields():
+    f = [("n_units", ctypes.c_int32), ("str", KadStrs)]
+    for k, _ in FIELDS:
+        if k == "rq_key":
+            f.append(("n_reqs", ctypes.c_int32))
+        f.append((k, ctypes.c_void_p))
+    return f
+
+
+class KadSUColumns(ctypes.Structure):
+    _fields_ = _su_fields()
+
+
+class KadPackStats(ctypes.Structure):
+    _fields_ = [("n_reqs", ctypes.c_void_p), ("n_tols", ctypes.c_void_p), ("n_distinct_reqs", ctypes.c_int32),
+                ("n_tolsets", ctypes.c_int32)]
+
+
+def _strs(strings: Sequence[str], keep: list) -> KadStrs:
+    parts = [s.encode() for s in strings]
+    off = np.zeros(len(parts) + 1, I64)
+    if parts:
+        off[1:] = np.cumsum([len(p) for p in parts])
+    data = np.frombuffer(b"".join(parts) or b"\0", U8).copy()
+    keep += [off, data]
+    return KadStrs(len(parts), off.ctypes.data, data.ctypes.data)
+
+
+class NativeBatch:
+    """A batch blob from the native packer; duck-types ``pack.Batch`` for the runtime and bench."""
+
+    def __init__(self, snap, fwk: Framework, blob: np.ndarray, n_reqs: np.ndarray, n_tols: np.ndarray,
+                 n_distinct_reqs: int, n_tolsets: int):
+        from .pack import B_FLAGS, B_OUT_OFF, BatchHeader, array_of, header_of
+
+        self.snap, self.fwk, self.blob = snap, fwk, blob
+        h = header_of(blob, BatchHeader)
+        self.W = int(h.n_units)
+        self.n_out_slots = int(h.n_out_slots)
+        self.out_off = array_of(blob, h, B_OUT_OFF, np.int64, self.W + 1)
+        self.flags = array_of(blob, h, B_FLAGS, np.uint32, self.W)
+        self.n_reqs, self.n_tols = n_reqs, n_tols
+        self.n_distinct_reqs, self.n_tolsets = n_distinct_reqs, n_tolsets
+        self.units = None
+
+
+class NativePacker:
+    """kad_packer for one pack.Snapshot's vocabulary."""
+
+    def __init__(self, snap):
+        from .runtime import load_library
+
+        self.L = L = load_library()
+        P = ctypes.c_void_p
+        L.kad_packer_create.argtypes = [P, ctypes.POINTER(P)]
+        L.kad_packer_destroy.argtypes = [P]
+        L.kad_packer_error.argtypes = [P]
+        L.kad_packer_error.restype = ctypes.c_char_p
+        L.kad_pack_batch.argtypes = [P, P, P, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), P]
+        L.kad_packer_take.argtypes = [P, P, ctypes.c_size_t]
+        self.snap = snap
+        keep: list = []
+        gvks = sorted(snap.gvk_id, key=snap.gvk_id.get)
+        keys = sorted(snap.label_key_id, key=snap.label_key_id.get)
+        vals, voff = [], [0]
+        for k in keys:
+            d = snap.label_vals[snap.label_key_id[k]]
+            vals += sorted(d, key=d.get)
+            voff.append(len(vals))
+        voff_a = np.asarray(voff, I32)
+        keep.append(voff_a)
+        v = KadPackVocab()
+        v.cluster_names = _strs(snap.names, keep)
+        v.scalar_names = _strs(sorted(snap.scalar_id, key=snap.scalar_id.get), keep)
+        v.gvk_group = _strs([g[0] for g in gvks], keep)
+        v.gvk_version = _strs([g[1] for g in gvks], keep)
+        v.gvk_kind = _strs([g[2] for g in gvks], keep)
+        v.label_keys = _strs(keys, keep)
+        v.label_val_off = voff_a.ctypes.data
+        v.label_vals = _strs(vals, keep)
+        v.taint_key = _strs([t.key for t in snap.taint_defs], keep)
+        v.taint_value = _strs([t.value for t in snap.taint_defs], keep)
+        v.taint_effect = _strs([t.effect for t in snap.taint_defs], keep)
+        v.n_taint_words = snap.TW
+        v.fingerprint = snap.fingerprint
+        h = ctypes.c_void_p()
+        rc = L.kad_packer_create(ctypes.byref(v), ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"kad_packer_create failed ({rc})")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.kad_packer_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def pack(self, fwk: Framework, cols: SUColumns, threads: int = 0) -> NativeBatch:
+        su = KadSUColumns()
+        su.n_units = cols.n_units
+        su.str = KadStrs(len(cols.str_off) - 1, cols.str_off.ctypes.data, cols.str_data.ctypes.data)
+        for k, _ in FIELDS:
+            setattr(su, k, cols.cols[k].ctypes.data)
+        su.n_reqs = cols.n_reqs
+        W = cols.n_units
+        nr = np.zeros(max(1, W), I32)
+        nt = np.zeros(max(1, W), I32)
+        st = KadPackStats(nr.ctypes.data, nt.ctypes.data, 0, 0)
+        prof = fwk.to_c()
+        n = ctypes.c_size_t()
+        rc = self.L.kad_pack_batch(self.h, ctypes.byref(prof), ctypes.byref(su), threads, ctypes.byref(n),
+                                   ctypes.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"kad_pack_batch: {self.L.kad_packer_error(self.h).decode()}")
+        blob = np.empty(n.value, U8)
+        rc = self.L.kad_packer_take(self.h, blob.ctypes.data, blob.nbytes)
+        if rc != 0:
+            raise RuntimeError(f"kad_packer_take: {self.L.kad_packer_error(self.h).decode()}")
+        return NativeBatch(self.snap, fwk, blob, nr[:W].astype(np.int64), nt[:W].astype(np.int64),
+                           int(st.n_distinct_reqs), int(st.n_tolsets))

@@ -46,6 +46,8 @@ struct kad_ctx {
   size_t cw_cap = 0;
   void* d_defer = nullptr;  // i32[W + 2]: defer_n, work_n, then the defer list
   size_t defer_cap = 0;
+  void* d_wq = nullptr;     // u32[8 * 32]: schedule_wide_kernel work heads
+  size_t wq_cap = 0;
   // scratch (per-wave slabs for rows that do not fit LDS)
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -55,6 +57,9 @@ struct kad_ctx {
   bool timing = false, timed = false;
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
   std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
+  std::vector<uint64_t> h_ns0; // host shadow of NoSchedule|NoExecute taint word 0 [C] (SnapDev::present_taints)
+  void* d_slices = nullptr;    // SnapDev::slices [3][64][nch]
+  size_t slices_cap = 0;
   void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
   size_t delta_cap = 0;
   bool batch_defer = false;    // some unit uses a feature the lean kernel defers
@@ -330,7 +335,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -428,6 +433,22 @@ static int check_snapshot_header(kad_ctx* c, const kad_snapshot_header& h, size_
   return 0;
 }
 
+// state derived from the resident snapshot: clean / negative ranges (host shadows) and, with one taint
+// word, the per-id cluster slices prep_kernel folds the taint and API filters from (SnapDev::fold)
+static int refresh_derived(kad_ctx* c) {
+  c->snap_negative = res_negative(c->h_res);
+  c->sd.clean = res_clean(c->h_res);
+  uint64_t present = 0;
+  for (uint64_t x : c->h_ns0) present |= x;
+  c->sd.present_taints = present;
+  c->sd.fold = c->sd.TW == 1;
+  const size_t nch = (size_t)((c->sd.C + 63) / 64);
+  if (int r = grow(c, &c->d_slices, &c->slices_cap, 3 * 64 * (nch ? nch : 1) * 8)) return r;
+  c->sd.slices = static_cast<const uint64_t*>(c->d_slices);
+  HIPCHK(c, launch_slices(c->sd, static_cast<uint64_t*>(c->d_slices), c->stream));
+  return 0;
+}
+
 int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   if (!c || !blob) return KAD_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
@@ -445,8 +466,8 @@ int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
     for (int q = 0; q < 4; q++)
       if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
   }
-  c->snap_negative = res_negative(c->h_res);
-  c->sd.clean = res_clean(c->h_res);
+  c->h_ns0.assign(at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE), at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + h.n_clusters);
+  if (int r = refresh_derived(c)) return r;
   c->have_snapshot = true;
   c->have_batch = false;
   return KAD_OK;
@@ -465,14 +486,15 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
   c->snap_hdr = h;
   if (int r = bind_snapshot(c, h)) return r;
   c->h_res.assign((size_t)4 * h.n_clusters, 0);
-  {
+  c->h_ns0.assign((size_t)h.n_clusters, 0);
+  if (h.n_clusters) {
     for (int q = 0; q < 4; q++)
-      if (h.n_clusters)
-        HIPCHK(c, hipMemcpy(c->h_res.data() + (size_t)q * h.n_clusters, static_cast<const char*>(dev_blob) + h.off[kResArrays[q]],
-                            (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(c->h_res.data() + (size_t)q * h.n_clusters, static_cast<const char*>(dev_blob) + h.off[kResArrays[q]],
+                          (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(c->h_ns0.data(), static_cast<const char*>(dev_blob) + h.off[KAD_S_TAINT_NSNE],
+                        (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
   }
-  c->snap_negative = res_negative(c->h_res);
-  c->sd.clean = res_clean(c->h_res);
+  if (int r = refresh_derived(c)) return r;
   c->have_snapshot = true;
   c->have_batch = false;
   return KAD_OK;
@@ -529,9 +551,11 @@ int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
       const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
       for (int j = 0; j < n; j++) c->h_res[(size_t)q * C + idx[j]] = v[j];
     }
+    const uint64_t* ns = at<uint64_t>(delta, h.off, KAD_S_TAINT_NSNE);  // row 0 of [TW][n_changed]
+    for (int j = 0; j < n; j++) c->h_ns0[idx[j]] = ns[j];
   }
-  c->snap_negative = res_negative(c->h_res);
-  c->sd.clean = res_clean(c->h_res);
+  if (int r = refresh_derived(c)) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return KAD_OK;
 }
 
@@ -623,6 +647,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_defer, &c->defer_cap, ((size_t)W + 2) * 4)) return r;
+  if (int r = grow(c, &c->d_wq, &c->wq_cap, 8 * 32 * 4)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->batch_hdr = h;
   const char* base = static_cast<const char*>(c->d_batch);
@@ -672,6 +697,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   b.defer_n = static_cast<int32_t*>(c->d_defer);
   b.work_n = b.defer_n + 1;
   b.defer = b.defer_n + 2;
+  b.wq = static_cast<uint32_t*>(c->d_wq);
   c->have_batch = true;
   c->ran = false;
   return KAD_OK;
@@ -723,7 +749,7 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   const bool tm = c->timing;
   if (tm) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
-  c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total;
+  c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total || wide_path(c->sd);
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream));

@@ -11,6 +11,12 @@ namespace kad {
 struct SnapDev {
   int C, GW, TW, K, S;
   int clean;  // host: every cluster's cpu/mem fit the lean kernel's exact-f64 path (kad_api.hip res_clean)
+  // TW == 1: prep_kernel folds TaintToleration's and APIResources' filters into each unit's static
+  // filter words from per-id cluster bitmask slices ([3][64][nch]: NoSchedule|NoExecute taint id t,
+  // NoExecute taint id t, GVK id g), so the schedule kernels only test resource fit per lane
+  int fold;
+  uint64_t present_taints;    // OR of every cluster's NoSchedule|NoExecute word 0 (host shadow)
+  const uint64_t* slices;
   const int64_t *alloc_cpu, *alloc_mem, *used_cpu, *used_mem, *alloc_s, *used_s, *alloc_cores, *avail_cores;
   const uint64_t *gvk, *nsne, *ne, *pns;
   const int32_t* lval;
@@ -47,6 +53,7 @@ struct BatchDev {
   int32_t* defer;           // [W] units the lean kernel hands to schedule_kernel
   int32_t* defer_n;         // [1] length of defer
   int32_t* work_n;          // [1] lean kernel work queue: next batch of LEAN_BATCH units
+  uint32_t* wq;             // [8 * 32] schedule_wide_kernel work heads (reset by prep_kernel)
 };
 
 // Per-unit record, rebuilt by prep_kernel at every kad_schedule: the fixed-size
@@ -119,9 +126,13 @@ size_t plan_wave_bytes(int K);
 int debug_phase_counters(uint64_t* out, int reset);
 
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st);
+// per-id cluster bitmask slices of the snapshot (SnapDev::slices), rebuilt at upload / update
+hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st);
 // true if the batch runs on schedule_lean_kernel (+ schedule_kernel over its
 // defer list); then launch_prep must run between launch_req_masks and launch_schedule.
 bool fast_path(int C);
+// true if launch_schedule runs schedule_wide_kernel for this snapshot (clean, 5..16 chunks)
+bool wide_path(const SnapDev& s);
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st);
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p,
                            void* global_scratch, size_t scratch_bytes, hipStream_t st);

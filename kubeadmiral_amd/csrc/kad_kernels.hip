@@ -681,6 +681,42 @@ __device__ uint64_t id_list_word(const int32_t* ids, int lo, int hi, uint32_t ch
   return m;
 }
 
+// cluster bitmask of id t in table tbl (0: NoSchedule|NoExecute taints, 1: NoExecute taints, 2: GVKs),
+// chunk ch: one wave per (tbl, t, ch), lane = cluster
+__global__ __launch_bounds__(256) void slice_kernel(SnapDev s, uint64_t* out) {
+  const int lane = lane_id();
+  const int nch = (s.C + 63) >> 6;
+  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= 3L * 64 * nch) return;
+  const int ch = (int)(gw % nch), t = (int)((gw / nch) % 64), tbl = (int)(gw / (64L * nch));
+  const int c = ch * WAVE + lane;
+  const uint32_t cl = c < s.C ? (uint32_t)c : 0u;
+  const uint64_t word = tbl == 0 ? ldg(s.nsne, cl) : (tbl == 1 ? ldg(s.ne, cl) : ldg(s.gvk, cl));
+  const uint64_t m = ballot(c < s.C && ((word >> t) & 1));
+  if (lane == 0) out[((size_t)tbl * 64 + t) * nch + ch] = m;
+}
+
+// TaintToleration.Filter (taint_toleration.go:44-89) and APIResources.Filter (apiresources.go:25-43) of
+// unit w on chunk ch from the slices (TW == 1): clusters with a NoSchedule|NoExecute taint the unit does
+// not tolerate are out — only NoExecute ones on its CurrentClusters (cw) — and clusters without its GVK
+__device__ __forceinline__ uint64_t folded_word(const SnapDev& s, uint32_t fm, uint32_t f, int gvk, uint64_t tol,
+                                                uint64_t cw, uint32_t nch, uint32_t ch) {
+  uint64_t m = ~0ull;
+  if (fm & (1u << KAD_PL_TAINT_TOLERATION)) {
+    const bool cur = f & KAD_W_HAS_CURRENT;
+    uint64_t bad_ns = 0, bad_ne = 0;
+    for (uint64_t r = s.present_taints & ~tol; r; r &= r - 1) {
+      const int t = (int)__builtin_ctzll(r);
+      bad_ns |= s.slices[(size_t)t * nch + ch];
+      if (cur) bad_ne |= s.slices[((size_t)64 + t) * nch + ch];
+    }
+    m = cur ? ((cw & ~bad_ne) | (~cw & ~bad_ns)) : ~bad_ns;
+  }
+  if (fm & (1u << KAD_PL_API_RESOURCES)) m &= (gvk >= 0 && gvk < 64) ? s.slices[((size_t)128 + gvk) * nch + ch] : 0ull;
+  return m;
+}
+
+constexpr int WQ_HEADS_PREP = 8, WQ_STRIDE_PREP = 32;  // = WQ_HEADS, WQ_STRIDE (schedule_wide_kernel)
 __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
   const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
   const uint32_t per = nch > 0 ? nch : 1u;
@@ -689,6 +725,7 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
     *b.defer_n = 0;
     *b.work_n = 0;
   }
+  if (g < (uint32_t)WQ_HEADS_PREP) b.wq[g * WQ_STRIDE_PREP] = 0u;  // schedule_wide_kernel's work heads
   if (g >= (uint32_t)b.W * per) return;
   const uint32_t w = g / per, ch = g - w * per;
   // every per-unit load is issued up front by every lane (w < W, the four
@@ -724,9 +761,13 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
     if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) m = affinity_word(b.req_mask, b.fprog + fpo, nch, ch);
     if ((fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT))
       m &= id_list_word(b.place, b.place_off[w], b.place_off[w + 1], ch);
+    uint64_t cw = 0;
+    if ((fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT)) {
+      cw = id_list_word(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch);
+      b.cw[g] = cw;
+    }
+    if (s.fold) m &= folded_word(s, fm, f, gvk, tol0, cw, nch, ch);
     b.sw[g] = m;
-    if ((fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT))
-      b.cw[g] = id_list_word(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch);
   }
 }
 
@@ -849,7 +890,10 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   uint16_t* posr = (uint16_t*)(region + L.posr);
   uint16_t* inv = posl;  // ranks after the replay
   const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
-  const bool f_sw = fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER));
+  // static filter words carry ClusterAffinity + PlacementFilter, and with SnapDev::fold also TaintToleration
+  // + APIResources (prep_kernel)
+  const bool fold = largs()->s.fold;
+  const bool f_sw = (fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER))) || (fold && (f_taint || f_api));
   const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
   const bool s_res =
       sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
@@ -1009,8 +1053,11 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     }
     // the chunk loop twice: FAST (no CurrentClusters, one taint word) has no
     // uniform branch inside, so the cache reads of every chunk issue together
-    auto filter_chunks = [&](auto fast_t) {
-      constexpr bool FAST = decltype(fast_t)::value;
+    // MODE 2 (FOLD): taint and API filters already in the static words (prep_kernel, SnapDev::fold);
+    // 1 (FAST): one taint word, no CurrentClusters; 0: general
+    auto filter_chunks = [&](auto mode_t) {
+      constexpr int MODE = decltype(mode_t)::value;
+      constexpr bool FAST = MODE >= 1, FOLD = MODE == 2;
       const bool ucur = !FAST && use_cur;
 #pragma unroll
       for (int ch = 0; ch < NC; ++ch) {
@@ -1022,10 +1069,10 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           ucpu = c_uc[c];  // clean: available cpu as f64
           amem = clean ? 0 : c_am[c];
           umem = c_um[c];
-          ns0 = c_ns[c];
+          ns0 = FOLD ? 0ull : c_ns[c];
           ne0 = ucur ? c_ne[c] : 0ull;
           pn0 = 0;
-          gv0 = c_gv[c];
+          gv0 = FOLD ? 0ull : c_gv[c];
           sw0 = swc[ch];
           cw0 = ucur ? ldc(largs()->b.cw + (size_t)w * nch + ch) : 0ull;
         } else {
@@ -1066,13 +1113,18 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           const uint64_t xt = sch ? ldg(a->s.ne, (uint32_t)(tw * C) + cl) : ldg(a->s.nsne, (uint32_t)(tw * C) + cl);
           tok &= (xt & ~ldc(a->b.tol_all + (size_t)tsc * TWs + tw)) == 0;
         }
-        const uint64_t m_taint = ballot(tok);      // taint_toleration.go:50-77
-        const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
         // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64)
         const uint64_t m_fit = clean ? ballot(__builtin_bit_cast(double, ucpu) >= rqcd) & ballot(__builtin_bit_cast(double, umem) >= rqmd)
                                      : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
-        // disabled filters OR in an all-ones mask (per-unit constants: two SALU ops per filter)
-        m &= (sw0 | o_sw) & (m_taint | o_taint) & ((m_api & a_api) | o_api) & (m_fit | o_fit);
+        if constexpr (FOLD) {
+          (void)tok;
+          m &= (sw0 | o_sw) & (m_fit | o_fit);
+        } else {
+          const uint64_t m_taint = ballot(tok);      // taint_toleration.go:50-77
+          const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
+          // disabled filters OR in an all-ones mask (per-unit constants: two SALU ops per filter)
+          m &= (sw0 | o_sw) & (m_taint | o_taint) & ((m_api & a_api) | o_api) & (m_fit | o_fit);
+        }
         (void)pn0;
         if constexpr (NCH > 0) {
           mk[ch] = m;  // compaction after every chunk's mask: no LDS store between the cache reads
@@ -1085,10 +1137,12 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         }
       }
     };
-    if (!use_cur && TWs == 1)
-      filter_chunks(std::true_type{});
+    if (fold)
+      filter_chunks(std::integral_constant<int, 2>{});
+    else if (!use_cur && TWs == 1)
+      filter_chunks(std::integral_constant<int, 1>{});
     else
-      filter_chunks(std::false_type{});
+      filter_chunks(std::integral_constant<int, 0>{});
     if constexpr (NCH > 0) {
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
@@ -1413,6 +1467,569 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     wave_sync();
     KAD_PT(t4);
     KAD_PADD(3, t4 - t3);
+  }
+  KAD_PFLUSH_LEAN;
+}
+
+// ================================================== wide schedule kernel
+// schedule_wide_kernel<NCH> — 256 < C <= 64*NCH (C3: 1 000 clusters, 16
+// chunks) on a clean snapshot. The lean kernel's register-resident positions
+// do not scale to feasible lists of several hundred clusters (C3: 20 % of the
+// units have n > 256), so here:
+//   * one 1024-thread workgroup per CU (persistent grid = #CUs): ONE block-
+//     shared LDS copy of the cluster attributes (C = 1000: ~56 KB) serves 16
+//     waves, and each wave's region (positions, replay scratch: 6 KB at
+//     P = 512) fits beside it in the 160 KB LDS;
+//   * units are dequeued dynamically: 8 work heads (one per contiguous eighth
+//     of the batch, a wave starts at head blockIdx % 8 — the round-robin XCD
+//     of its block, for locality only) hand out WQ_BATCH units per returning
+//     atomicAdd, one batch ahead of use; an exhausted head sends the wave to
+//     the next one, so every wave runs until the whole batch is drained (no
+//     static-share tail);
+//   * each unit's 64-B record and static filter words arrive in ONE VGPR,
+//     loaded one unit ahead (lanes 0-15: UnitRec, lanes 16..16+2*nch: sw);
+//   * filter per 64-cluster chunk: two ds_read_b128 (available cpu/mem as
+//     exact f64; NS|NE taint word + GVK word) → lane masks ANDed in SALU →
+//     compaction into the wave's position list (u16 cluster ids);
+//   * scores and totals for positions 64q + lane (q < WIDE_Q) in registers,
+//     normalisation by DPP wave max; MaxCluster's k-th largest total by LDS
+//     histogram (span < 128) or ballot bisection; the same tie rules as the
+//     lean kernel (all ties / n <= 12 insertionSort / PdqWave replay).
+// Units with more than WIDE_P feasible clusters, REC_FULL units and requests
+// outside the exact-f64 range go to the defer list (schedule_kernel).
+constexpr int WIDE_Q = 8;
+constexpr int WIDE_P = WIDE_Q * 64;
+constexpr int WIDE_MAX_NCH = 16;
+constexpr int WQ_BATCH = 4;          // units per dequeue
+constexpr int WQ_HEADS = WQ_HEADS_PREP;    // work heads, one 128-B line each
+constexpr int WQ_STRIDE = WQ_STRIDE_PREP;  // u32 words between heads
+constexpr int WIDE_THREADS = 1024;
+
+struct WideLayout {
+  size_t key, idx, pid, posl, posr, bytes;
+};
+__host__ __device__ inline WideLayout wide_layout() {
+  WideLayout L;
+  L.key = 0;                      // u32[P] replay keys / histogram
+  L.idx = L.key + 4 * WIDE_P;     // u16[P] position -> cluster id
+  L.pid = L.idx + 2 * WIDE_P;     // u16[P] replay: original position
+  L.posl = L.pid + 2 * WIDE_P;    // u16[P] replay scratch, then ranks
+  L.posr = L.posl + 2 * WIDE_P;   // u16[P]
+  L.bytes = L.posr + 2 * WIDE_P;
+  return L;
+}
+// block-shared cluster cache: av (f64 x2), tg (u64 x2: NS|NE taints, GVK word),
+// cap (f64 x2), iv (f32 x2), [ne u64], [pn u64]
+__host__ __device__ inline size_t wide_cache_bytes(int C, int cache_ne, int cache_pn) {
+  const size_t Cp = (size_t)((C + 63) & ~63);
+  return Cp * (16 + 16 + 16 + 8 + 8 * cache_ne + 8 * cache_pn);
+}
+
+struct WideArgs {
+  SnapDev s;
+  BatchDev b;
+  OutDev o;
+  ProfDev p;
+  int waves_per_block;
+  int cache_ne, cache_pn;
+};
+typedef const __attribute__((address_space(4))) WideArgs* WArgs;
+__device__ __forceinline__ WArgs wargs() {
+  return (WArgs)opq((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
+}
+
+// Work queue: WQ_HEADS heads, head x hands out the batches of the x-th
+// contiguous eighth of the units. A ticket is one returning atomicAdd on a
+// head (issued by lane 0); it is resolved into a batch one batch later, so
+// the atomic's latency hides behind a unit's work. A drained head sends the
+// wave to the next head that is not drained (synchronous retries: only at the
+// end of the queue). Every wave ends once all heads are drained.
+struct WorkTicket {
+  int x;        // head of the pending ticket
+  uint32_t i;   // its atomicAdd result (lane 0)
+  uint32_t drained;
+};
+__device__ __forceinline__ void wq_issue(uint32_t* heads, WorkTicket& t) {
+  if (lane_id() == 0) t.i = atomicAdd(heads + t.x * WQ_STRIDE, 1u);
+}
+// the batch [first, first + count) of a ticket; count 0 = queue drained
+__device__ __forceinline__ int2 wq_resolve(uint32_t* heads, int W, WorkTicket& t) {
+  int first = 0, count = 0;
+  if (lane_id() == 0) {
+    for (int tries = 0; tries < WQ_HEADS; ++tries) {
+      const int x = t.x;
+      const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
+      const int nb = (s1 - s0 + WQ_BATCH - 1) / WQ_BATCH;
+      if ((int)t.i < nb) {
+        first = s0 + (int)t.i * WQ_BATCH;
+        count = (s1 - first) < WQ_BATCH ? (s1 - first) : WQ_BATCH;
+        break;
+      }
+      t.drained |= 1u << x;
+      int nx = -1;
+      for (int u = 1; u < WQ_HEADS; ++u) {
+        const int y = (x + u) & (WQ_HEADS - 1);
+        if (!((t.drained >> y) & 1)) {
+          nx = y;
+          break;
+        }
+      }
+      if (nx < 0) break;
+      t.x = nx;
+      t.i = atomicAdd(heads + nx * WQ_STRIDE, 1u);
+    }
+  }
+  first = __builtin_amdgcn_readfirstlane(__shfl(first, 0));
+  count = __builtin_amdgcn_readfirstlane(__shfl(count, 0));
+  return make_int2(first, count);
+}
+
+__device__ __forceinline__ void wide_status(int w, int32_t st) {
+  if (lane_id() == 0) {
+    WArgs a = wargs();
+    a->o.status[w] = st;
+    a->o.count[w] = 0;
+    a->o.flags[w] = 0;
+  }
+}
+__device__ __forceinline__ void wide_defer(int w) {
+  if (lane_id() == 0) {
+    WArgs a = wargs();
+    const int slot = atomicAdd(a->b.defer_n, 1);
+    a->b.defer[slot] = w;
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs args) {
+  (void)args;  // read through wargs()
+  constexpr int Q = WIDE_Q;
+  constexpr int P = WIDE_P;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int C, W, TWs;
+  uint32_t fm, sm;
+  {
+    WArgs a = wargs();
+    C = a->s.C;
+    TWs = a->s.TW;
+    W = a->b.W;
+    fm = a->p.filter_mask;
+    sm = a->p.score_mask;
+  }
+  const int nch = (C + 63) >> 6;
+  const int Cp = nch * 64;
+  const WideLayout L = wide_layout();
+  const int nwaves = blockDim.x >> 6;
+  char* region = smem + (size_t)wv * L.bytes;
+  uint32_t* key = (uint32_t*)(region + L.key);
+  uint16_t* idx = (uint16_t*)(region + L.idx);
+  uint16_t* pid = (uint16_t*)(region + L.pid);
+  uint16_t* posl = (uint16_t*)(region + L.posl);
+  uint16_t* posr = (uint16_t*)(region + L.posr);
+  uint16_t* inv = posl;
+  char* cache = smem + (size_t)nwaves * L.bytes;
+  double2* c_av = (double2*)cache;
+  ulonglong2* c_tg = (ulonglong2*)(cache + (size_t)16 * Cp);
+  double2* c_cap = (double2*)(cache + (size_t)32 * Cp);
+  float2* c_iv = (float2*)(cache + (size_t)48 * Cp);
+  uint64_t* c_ne = nullptr;
+  uint64_t* c_pn = nullptr;
+  {
+    WArgs a = wargs();
+    size_t o = (size_t)56 * Cp;
+    if (a->cache_ne) {
+      c_ne = (uint64_t*)(cache + o);
+      o += (size_t)8 * Cp;
+    }
+    if (a->cache_pn) c_pn = (uint64_t*)(cache + o);
+  }
+  const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
+  const bool fold = wargs()->s.fold;  // taint + API filters in the static words (prep_kernel)
+  const bool f_sw = (fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER))) || (fold && (f_taint || f_api));
+  const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
+  const bool s_res =
+      sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
+  const bool s_tt = sm & BIT(KAD_PL_TAINT_TOLERATION);
+  {
+    WArgs a = wargs();
+    for (int c = threadIdx.x; c < Cp; c += blockDim.x) {
+      const bool in = c < C;
+      const uint32_t cl = in ? (uint32_t)c : 0u;
+      const int64_t ac = in ? ldg(a->s.alloc_cpu, cl) : 1, uc = in ? ldg(a->s.used_cpu, cl) : 0;
+      const int64_t am = in ? ldg(a->s.alloc_mem, cl) : 1, um = in ? ldg(a->s.used_mem, cl) : 0;
+      c_av[c] = make_double2((double)(ac - uc), (double)(am - um));
+      c_cap[c] = make_double2((double)ac, (double)am);
+      c_iv[c] = make_float2((float)(100.0 / (double)ac), (float)(100.0 / (double)am));
+      c_tg[c] = make_ulonglong2(in ? ldg(a->s.nsne, cl) : 0ull, in ? ldg(a->s.gvk, cl) : 0ull);
+      if (c_ne) c_ne[c] = in ? ldg(a->s.ne, cl) : 0;
+      if (c_pn) c_pn[c] = in ? ldg(a->s.pns, cl) : 0;
+    }
+    __syncthreads();
+  }
+
+  uint32_t* heads;
+  const UnitRec* recs;
+  const uint64_t* sws;
+  {
+    WArgs a = wargs();
+    heads = a->b.wq;
+    recs = a->b.rec;
+    sws = a->b.sw;
+  }
+  WorkTicket tk{(int)(blockIdx.x & (WQ_HEADS - 1)), 0u, 0u};
+  // one VGPR per unit: lanes 0-15 its UnitRec dwords, lanes 16..16+2*nch its static filter words
+  auto fetch = [&](int w) -> uint32_t {
+    if (w < 0) return 0u;
+    if (lane < 16) return ldg((const uint32_t*)(recs + w), (uint32_t)lane);
+    if (f_sw && lane < 16 + 2 * nch) return ldg((const uint32_t*)(sws + (size_t)w * nch), (uint32_t)(lane - 16));
+    return ~0u;
+  };
+  wq_issue(heads, tk);
+  int2 cb = wq_resolve(heads, W, tk);
+  if (cb.y > 0) wq_issue(heads, tk);  // the next batch's ticket, resolved when this batch ends
+  int w = cb.y > 0 ? cb.x : -1;
+  uint32_t cur = fetch(w);
+  int bend = cb.x + cb.y;
+  KAD_PACC;
+  while (w >= 0) {
+    // the next unit: within this batch, else the head of the next batch
+    int wn = -1;
+    if (w + 1 < bend) {
+      wn = w + 1;
+    } else {
+      const int2 nb = wq_resolve(heads, W, tk);
+      if (nb.y > 0) {
+        wn = nb.x;
+        bend = nb.x + nb.y;
+        wq_issue(heads, tk);  // resolved one batch later
+      }
+    }
+    const uint32_t nxt = fetch(wn);
+    KAD_PT(t0);
+
+    auto fld = [&](int d) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)cur, d); };
+    auto fld64 = [&](int d) -> int64_t { return (int64_t)(((uint64_t)fld(d + 1) << 32) | fld(d)); };
+    const uint32_t fc = fld(0);
+    const int gvc = (int)fld(1);
+    const int tsc = (int)fld(2);
+    const int64_t rqc = fld64(4), rqm = fld64(6);
+    const uint64_t tolc = (uint64_t)fld64(12);
+    do {  // one unit; `break` = done with it
+      if (fc & KAD_W_STICKY) {  // generic_scheduler.go:101-104
+        wide_status(w, KAD_ST_STICKY);
+        break;
+      }
+      if ((fc & REC_FULL) || (uint64_t)rqc >= (1ull << 46) || (uint64_t)rqm >= (1ull << 46) ||
+          (fc & KAD_W_WIDE_SCORES)) {
+        wide_defer(w);
+        break;
+      }
+      const double rqcd = (double)rqc, rqmd = (double)rqm;  // exact: 0 <= request < 2^46
+      const int spo = (int)fld(3);
+      const int64_t mc = fld64(8), ooff = fld64(10);
+      const uint64_t tolp0 = (uint64_t)fld64(14);
+      const bool use_cur = f_taint && (fc & KAD_W_HAS_CURRENT);
+      const bool fit_on = f_fit && (fc & KAD_W_FIT_NONZERO);
+      const uint64_t o_sw = f_sw ? 0ull : ~0ull, o_taint = f_taint ? 0ull : ~0ull, o_fit = fit_on ? 0ull : ~0ull;
+      const uint64_t o_api = f_api ? 0ull : ~0ull, a_api = gvc >= 0 ? ~0ull : 0ull;
+
+      // ---------------- filters → compacted feasible list (findClustersThatFitWorkload, :152-169)
+      int n = 0;
+      // the chunk loop twice: FAST (one taint word, no CurrentClusters) has no branch inside a
+      // 4-chunk group, so the 8 LDS reads of a group issue together; compaction stores are
+      // exec-free (infeasible lanes and overflow positions write into pid[], rewritten before use)
+      // MODE 2 (FOLD): taint + API already in the static words; 1 (FAST): one taint word, no
+      // CurrentClusters; 0: general
+      auto filter_chunks = [&](auto mode_t) {
+        constexpr int MODE = decltype(mode_t)::value;
+        constexpr bool FAST = MODE >= 1, FOLD = MODE == 2;
+#pragma unroll 1
+        for (int g = 0; g < nch; g += 4) {
+          uint64_t mk[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ch = g + j;
+            const int c = ch * WAVE + lane;
+            const int rem = C - ch * WAVE;
+            uint64_t m = rem >= WAVE ? ~0ull : (rem > 0 ? ((1ull << rem) - 1) : 0ull);
+            const int cc = c < Cp ? c : 0;
+            const double2 av = c_av[cc];
+            const ulonglong2 tg = FOLD ? make_ulonglong2(0ull, 0ull) : c_tg[cc];
+            const uint64_t sw0 = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)cur, 17 + 2 * ch)) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)cur, 16 + 2 * ch);
+            bool tok;
+            if constexpr (FAST) {
+              tok = (tg.x & ~tolc) == 0;
+            } else {
+              WArgs a = wargs();
+              const bool sch = use_cur && ch < nch && ((ldc(a->b.cw + (size_t)w * nch + ch) >> lane) & 1);
+              tok = ((sch ? c_ne[cc] : tg.x) & ~tolc) == 0;
+              for (int tw = 1; tw < TWs; ++tw) {  // more than 64 taint ids: words 1.. from global
+                const uint32_t cl = c < C ? (uint32_t)c : 0u;
+                const uint64_t xt = sch ? ldg(a->s.ne, (uint32_t)(tw * C) + cl) : ldg(a->s.nsne, (uint32_t)(tw * C) + cl);
+                tok &= (xt & ~ldc(a->b.tol_all + (size_t)tsc * TWs + tw)) == 0;
+              }
+            }
+            // fit.go:73-134 on exact f64: available - request >= 0
+            const uint64_t m_fit = ballot(av.x >= rqcd) & ballot(av.y >= rqmd);
+            if constexpr (FOLD) {
+              (void)tok;
+              m &= (sw0 | o_sw) & (m_fit | o_fit);
+            } else {
+              const uint64_t m_taint = ballot(tok);                    // taint_toleration.go:50-77
+              const uint64_t m_api = ballot((tg.y >> (gvc & 63)) & 1);  // apiresources.go:25-43
+              m &= (sw0 | o_sw) & (m_taint | o_taint) & ((m_api & a_api) | o_api) & (m_fit | o_fit);
+            }
+            mk[j] = m;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int pos = n + mbcnt(mk[j]);
+            idx[(((mk[j] >> lane) & 1) && pos < P) ? pos : P + lane] = (uint16_t)((g + j) * WAVE + lane);
+            n += popc64(mk[j]);
+          }
+        }
+      };
+      if (fold)
+        filter_chunks(std::integral_constant<int, 2>{});
+      else if (!use_cur && TWs == 1)
+        filter_chunks(std::integral_constant<int, 1>{});
+      else
+        filter_chunks(std::integral_constant<int, 0>{});
+      KAD_PT(t1);
+      KAD_PADD(0, t1 - t0);
+      if (n == 0) {  // generic_scheduler.go:112-114
+        wide_status(w, KAD_ST_NO_FEASIBLE);
+        break;
+      }
+      if (n > P) {
+        wide_defer(w);
+        break;
+      }
+      if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && (fc & KAD_W_SCORE_ERROR)) {  // framework.go:149-159
+        wide_status(w, KAD_ST_ERR_SCORE);
+        break;
+      }
+      wave_sync();
+
+      // ---------------- scores of positions 64q + lane (RunScorePlugins, framework.go:139-181)
+      const int nq = (n + 63) >> 6;
+      int t[Q];
+      uint32_t cid[Q];
+      int ttv[Q];
+      int ttmax = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        t[q] = 0;
+        cid[q] = 0;
+        ttv[q] = 0;
+        if (q >= nq) continue;
+        const int p = q * 64 + lane;
+        const bool v = p < n;
+        cid[q] = v ? idx[p] : 0u;
+        const uint32_t cq = cid[q];
+        if (s_res) {
+          // x = cap - req = available - request (exact); req > cap <=> x < 0 (score 0)
+          const double2 cap = c_cap[cq], av = c_av[cq];
+          const double xc = av.x - rqcd, xm = av.y - rqmd;
+          const float2 iv = c_iv[cq];
+          const double xcp = fmax(xc, 0.0), xmp = fmax(xm, 0.0);
+          const int okc = -(int)(xc >= 0.0), okm = -(int)(xm >= 0.0);
+          int x = 0;
+          if (sm & BIT(KAD_PL_LEAST_ALLOCATED)) x += (quot100(xcp, cap.x, iv.x) + quot100(xmp, cap.y, iv.y)) >> 1;
+          if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+            x += ((quot100(cap.x - xcp, cap.x, iv.x) & okc) + (quot100(cap.y - xmp, cap.y, iv.y) & okm)) >> 1;
+          if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x += (int)balanced_d((cap.x - xc) / cap.x, (cap.y - xm) / cap.y);
+          t[q] = x;
+        }
+        if (s_tt) {  // taint_toleration.go:91-118: PreferNoSchedule taints not tolerated
+          int tc = popc64(c_pn[cq] & ~tolp0);
+          for (int tw = 1; tw < TWs; ++tw) {
+            WArgs a = wargs();
+            tc += popc64(ldg(a->s.pns, (uint32_t)(tw * C) + cq) & ~ldc(a->b.tol_pns + (size_t)tsc * TWs + tw));
+          }
+          ttv[q] = v ? tc : 0;
+          ttmax = ttv[q] > ttmax ? ttv[q] : ttmax;
+        }
+      }
+      if (s_tt) {  // DefaultNormalizeScore(100, reverse=true), framework/util.go:455-483
+        ttmax = wave_max_u_i32(ttmax);
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (q < nq) t[q] += ttmax == 0 ? 100 : 100 - (int)small_quot(100 * ttv[q], ttmax);
+      }
+      if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {  // cluster_affinity.go:96-140 + DefaultNormalizeScore(100, false)
+        WArgs a = wargs();
+        const int32_t* sp = a->b.sprog + spo;
+        if (ldc(sp) > 0) {
+          int afs[Q];  // |raw| <= sum |weight| <= 2^20 (wider units are deferred)
+          int amax = 0;
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            afs[q] = 0;
+            if (q < nq && q * 64 + lane < n) afs[q] = (int)affinity_score(a->b.req_mask, sp, nch, (int)cid[q]);
+            amax = afs[q] > amax ? afs[q] : amax;
+          }
+          amax = wave_max_u_i32(amax);
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (q < nq) {
+              const int num = 100 * afs[q];
+              t[q] += amax == 0 ? afs[q] : (num >= 0 && num < (1 << 24) ? (int)small_quot(num, amax) : num / amax);
+            }
+        }
+      }
+
+      KAD_PT(t2);
+      KAD_PADD(1, t2 - t1);
+      // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
+      WArgs ad = wargs();
+      int k = n;
+      if (ad->p.select_plugin == KAD_PL_MAX_CLUSTER) {
+        const bool hm = fc & KAD_W_HAS_MAX_CLUSTERS;
+        if (hm && mc < 0) {
+          wide_status(w, KAD_ST_ERR_SELECT);
+          break;
+        }
+        if (hm && mc < k) k = (int)mc;
+      }
+      // selection rule for the output pass: 0 all, 1 total >= T, 2 first ties (n <= 12), 3 replay ranks
+      int mode = 0, T = 0, need = 0;
+      uint32_t rflags = 0;
+      if (k < n && k > 0) {
+        int mn = INT32_MAX, mx = INT32_MIN;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (q < nq && q * 64 + lane < n) {
+            mn = t[q] < mn ? t[q] : mn;
+            mx = t[q] > mx ? t[q] : mx;
+          }
+        int mn32, mx32;
+        wave_minmax_u_i32(mn, mx, mn32, mx32);
+        int lo32 = mn32, hi32 = mx32;
+        if ((uint32_t)mx32 - (uint32_t)mn32 < 128u) {
+          // LDS histogram in descending bin order + one wave prefix sum: the k-th largest total
+          uint32_t* hist = key;
+          *(uint2*)(hist + 2 * lane) = make_uint2(0u, 0u);
+          wave_sync();
+#pragma unroll
+          for (int q = 0; q < Q; ++q)
+            if (q < nq && q * 64 + lane < n) atomicAdd(hist + (127 - (t[q] - mn32)), 1u);
+          wave_sync();
+          const uint2 hh = *(const uint2*)(hist + 2 * lane);  // bins 127-2l, 126-2l
+          const int pre = wave_incl_sum_i32((int)(hh.x + hh.y));
+          const int l0 = (int)__builtin_ctzll(ballot(pre >= k));
+          const int pl = __builtin_amdgcn_readlane(pre, l0);
+          const int h1 = __builtin_amdgcn_readlane((int)hh.y, l0);
+          lo32 = mn32 + (pl - h1 >= k ? 127 - 2 * l0 : 126 - 2 * l0);
+          wave_sync();
+        } else {
+          while (lo32 < hi32) {  // the largest T with #(total >= T) >= k
+            const uint32_t d = (uint32_t)hi32 - (uint32_t)lo32;
+            const int mid = (int)((uint32_t)lo32 + (d >> 1) + (d & 1));
+            int cnt = 0;
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq) cnt += popc64(ballot(q * 64 + lane < n && t[q] >= mid));
+            if (cnt >= k)
+              lo32 = mid;
+            else
+              hi32 = mid - 1;
+          }
+        }
+        T = lo32;
+        int gcount = 0, e = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (q < nq) {
+            const bool v = q * 64 + lane < n;
+            gcount += popc64(ballot(v && t[q] > T));
+            e += popc64(ballot(v && t[q] == T));
+          }
+        need = k - gcount;
+        if (need == e) {  // the cut takes every tie: no sort needed
+          mode = 1;
+        } else {
+          rflags = KAD_RF_TIE_STRADDLE;
+          if (n <= 12) {  // pdqsort_func: a single (stable) insertionSort
+            mode = 2;
+          } else {
+            // restricted pdqsort replay, wave-parallel, on u32 keys total - min (order-preserving)
+            const int xs_b = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
+            const int xs_c = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq && q * 64 + lane < n) {
+                key[q * 64 + lane] = (uint32_t)(t[q] - mn32);
+                pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
+              }
+            wave_sync();
+            PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
+            pw.select(n, k);
+            for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
+            wave_sync();
+            mode = 3;
+          }
+        }
+      } else if (k <= 0) {
+        mode = -1;  // nothing selected
+      }
+
+      KAD_PT(t3);
+      KAD_PADD(2, t3 - t2);
+      if (rflags) {
+        KAD_PADD(4, 1);
+        KAD_PADD(5, t3 - t2);
+      }
+      // ---------------- output, ascending cluster id (= ascending position)
+      {
+        WArgs ae = wargs();
+        const bool dup = fc & KAD_W_DUPLICATE;
+        const bool replicas =
+            !dup && ae->p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (fc & REC_DESIRED_POS) && k > 0;
+        int base = 0;
+        if ((dup || replicas) && mode >= 0) {
+          int32_t* oc = ae->o.cluster + ooff;
+          int64_t* orp = ae->o.replicas + ooff;
+          int eq_before = 0;  // mode 2: ties at T in earlier positions (q = 0 only: n <= 12)
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            if (q >= nq) continue;
+            const int p = q * 64 + lane;
+            const bool v = p < n;
+            bool s;
+            if (mode == 0)
+              s = v;
+            else if (mode == 1)
+              s = v && t[q] >= T;
+            else if (mode == 2)
+              s = v && (t[q] > T || (t[q] == T && mbcnt(ballot(v && t[q] == T)) + eq_before < need));
+            else
+              s = v && inv[p] < k;
+            const uint64_t sel = ballot(s);
+            if (s) {
+              const uint32_t at = (uint32_t)(base + mbcnt(sel));
+              stg(oc, at, (int32_t)cid[q]);
+              stg(orp, at, (int64_t)(dup ? -1 : 0));
+            }
+            base += popc64(sel);
+          }
+          (void)eq_before;
+        }
+        if (lane == 0) {
+          ae->o.status[w] = KAD_ST_OK;
+          ae->o.count[w] = base;  // Divide without replicas plugin: empty map
+          ae->o.flags[w] = rflags;
+        }
+      }
+      wave_sync();
+      KAD_PT(t4);
+      KAD_PADD(3, t4 - t3);
+    } while (false);
+    cur = nxt;
+    w = wn;
   }
   KAD_PFLUSH_LEAN;
 }
@@ -1812,6 +2429,15 @@ hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st)
   return hipGetLastError();
 }
 
+hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st) {
+  (void)hipGetLastError();
+  const int nch = (s.C + 63) >> 6;
+  const long waves = 3L * 64 * nch;
+  if (waves == 0) return hipSuccess;
+  hipLaunchKernelGGL(slice_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, slices);
+  return hipGetLastError();
+}
+
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
@@ -1826,11 +2452,77 @@ static void launch_lean(const LeanArgs& A, int grid, size_t lds, hipStream_t st)
   hipLaunchKernelGGL((schedule_lean_kernel<NCH, CL>), dim3(grid), dim3(64 * A.waves_per_block), lds, st, A);
 }
 
+static int n_cus() {
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+  }
+  return n_cu;
+}
+
+// the wide kernel takes clean snapshots with WIDE_MIN_NCH <= nch <= WIDE_MAX_NCH
+// (KAD_WIDE_MIN_NCH overrides the lower bound, for A/B runs of C <= 256)
+static bool use_wide(const SnapDev& s) {
+  static int min_nch = -1;
+  if (min_nch < 0) min_nch = getenv("KAD_WIDE_MIN_NCH") ? atoi(getenv("KAD_WIDE_MIN_NCH")) : 5;
+  const int nch = (s.C + 63) >> 6;
+  return s.clean && nch >= min_nch && nch >= 1 && nch <= WIDE_MAX_NCH;
+}
+bool wide_path(const SnapDev& s) { return use_wide(s); }
+
+static hipError_t launch_defer_pass(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
+                                    size_t scr_bytes, hipStream_t st) {
+  const size_t wb = row_layout(s.C).bytes;
+  if (wb <= (size_t)LDS_BUDGET) {
+    int wpb2 = (int)(LDS_BUDGET / wb);
+    wpb2 = wpb2 > 4 ? 4 : (wpb2 < 1 ? 1 : wpb2);
+    long waves2 = b.W < 256 * 16 ? b.W : 256 * 16;
+    const int grid2 = (int)((waves2 + wpb2 - 1) / wpb2);
+    const SchedArgs A2{s, b, o, p, nullptr, (int)wb, wpb2, grid2 * wpb2, b.defer, b.defer_n};
+    hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid2), dim3(64 * wpb2), wb * wpb2, st, A2);
+  } else {  // rows too large for LDS: per-wave global scratch slabs
+    size_t slots = scr_bytes / wb;
+    if (slots < 1) return hipErrorInvalidValue;
+    if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
+    if (slots > (size_t)b.W) slots = b.W;
+    const SchedArgs A2{s, b, o, p, (char*)gscr, (int)wb, 1, (int)slots, b.defer, b.defer_n};
+    hipLaunchKernelGGL(schedule_kernel<true>, dim3((int)slots), dim3(64), 0, st, A2);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
                            size_t scr_bytes, hipStream_t st) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (b.W == 0) return hipSuccess;
   const size_t wb = row_layout(s.C).bytes;
+  if (use_wide(s)) {
+    const int cache_ne = (p.filter_mask & (1u << KAD_PL_TAINT_TOLERATION)) && (b.flags_or & KAD_W_HAS_CURRENT);
+    const int cache_pn = (p.score_mask >> KAD_PL_TAINT_TOLERATION) & 1;
+    const size_t cache = wide_cache_bytes(s.C, cache_ne, cache_pn);
+    const size_t per_wave = wide_layout().bytes;
+    const size_t lds_max = 160 * 1024;
+    int wpb = (int)((lds_max - cache) / per_wave);
+    wpb = wpb > WIDE_THREADS / 64 ? WIDE_THREADS / 64 : wpb;
+    if (wpb < 1) return hipErrorInvalidValue;
+    const size_t lds = cache + (size_t)wpb * per_wave;
+    static bool attr = false;
+    if (!attr) {
+      if (hipError_t e = hipFuncSetAttribute((const void*)schedule_wide_kernel<WIDE_MAX_NCH>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max))
+        return e;
+      attr = true;
+    }
+    long grid = n_cus();
+    const long need = ((long)b.W + wpb - 1) / wpb;
+    if (grid > need) grid = need;
+    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn};
+    hipLaunchKernelGGL(schedule_wide_kernel<WIDE_MAX_NCH>, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
+    if (hipError_t e = hipGetLastError()) return e;
+    // feasible lists longer than WIDE_P positions can come from any unit: the defer pass always runs
+    return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);
+  }
   if (fast_path(s.C)) {
     const int nch = (s.C + 63) >> 6;
     const size_t lb = lean_layout(s.C, lean_qmax(nch <= 4 ? nch : 0)).bytes;
@@ -1842,11 +2534,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const int cache_pn = (p.score_mask >> KAD_PL_TAINT_TOLERATION) & 1;
     const size_t lds = lb * wpb + (nch <= 4 ? lean_cache_bytes(s.C, 6 + cache_ne + cache_pn + ((s.clean && nch >= 1 && nch <= 4) ? 1 : 0)) : 0);
     // one wave per resident slot: contiguous equal shares, no tail of late blocks
-    static int n_cu = 0;
-    if (n_cu == 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-    }
+    const int n_cu = n_cus();
     int per_cu = 0;
     hipError_t oe;
     const bool cl = s.clean && nch >= 1 && nch <= 4;
@@ -1878,22 +2566,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (nch <= 4 && !b.may_defer) return hipSuccess;
     // the defer list: its length is only known on the device, so the grid
     // strides over it (waves past its end exit at once)
-    if (wb <= (size_t)LDS_BUDGET) {
-      int wpb2 = (int)(LDS_BUDGET / wb);
-      wpb2 = wpb2 > 4 ? 4 : (wpb2 < 1 ? 1 : wpb2);
-      long waves2 = b.W < 256 * 16 ? b.W : 256 * 16;
-      const int grid2 = (int)((waves2 + wpb2 - 1) / wpb2);
-      const SchedArgs A2{s, b, o, p, nullptr, (int)wb, wpb2, grid2 * wpb2, b.defer, b.defer_n};
-      hipLaunchKernelGGL(schedule_kernel<false>, dim3(grid2), dim3(64 * wpb2), wb * wpb2, st, A2);
-    } else {  // rows too large for LDS: per-wave global scratch slabs
-      size_t slots = scr_bytes / wb;
-      if (slots < 1) return hipErrorInvalidValue;
-      if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
-      if (slots > (size_t)b.W) slots = b.W;
-      const SchedArgs A2{s, b, o, p, (char*)gscr, (int)wb, 1, (int)slots, b.defer, b.defer_n};
-      hipLaunchKernelGGL(schedule_kernel<true>, dim3((int)slots), dim3(64), 0, st, A2);
-    }
-    return hipGetLastError();
+    return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);
   }
   if (wb <= (size_t)LDS_BUDGET) {
     int wpb = (int)(LDS_BUDGET / wb);

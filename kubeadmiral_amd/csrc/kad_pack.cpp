@@ -1,0 +1,815 @@
+// Native batch packer (include/kad_pack.h): columnar SchedulingUnits → the
+// kad_sched.h batch blob, byte-identical to kubeadmiral_amd/pack.py Batch.
+//
+// Passes (W units, R requirement-table entries, NT toleration sets):
+//   1. per requirement entry, in parallel: labels.NewRequirement validation
+//      (apimachinery v0.26.6 labels/selector.go) and the requirement words of
+//      both uses (label expression, metadata.name field selector);
+//   2. serial, in unit order: interning — requirement words → batch-wide ids
+//      and toleration lists → toleration-set ids, in exactly the order pack.py
+//      assigns them (first use), so the blob is byte-identical;
+//   3. per unit, in parallel: flags, fixed columns and the length of every
+//      CSR row; serial prefix sums lay out the blob;
+//   4. per unit, in parallel: the CSR rows written in place (programs,
+//      placement / current / preference lists sorted by snapshot id, Key()
+//      bytes); per toleration set: tolerated-taint masks
+//      (Toleration.ToleratesTaint, k8s.io/api v0.26.6).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kad_pack.h"
+
+namespace {
+
+using sv = std::string_view;
+
+constexpr int ALIGN = 256;
+constexpr int OP_IN = 1, OP_NOTIN = 2, OP_EXISTS = 3, OP_DNE = 4, OP_GT = 5, OP_LT = 6, OP_EQ = 7, OP_TRUE = 8,
+              OP_FALSE = 9, OP_NAME_EQ = 10, OP_NAME_NE = 11;
+
+struct Strs {
+  const int64_t* off = nullptr;
+  const uint8_t* bytes = nullptr;
+  int32_t n = 0;
+  sv operator[](int i) const {
+    return sv(reinterpret_cast<const char*>(bytes) + off[i], (size_t)(off[i + 1] - off[i]));
+  }
+};
+Strs strs(const kad_strs& s) { return Strs{s.off, s.bytes, s.n}; }
+
+// ------------------------------------------------ apimachinery / k8s.io/api
+bool dns1123_subdomain(sv s) {  // [a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*
+  if (s.empty()) return false;
+  size_t i = 0;
+  while (true) {
+    size_t j = i;
+    while (j < s.size() && s[j] != '.') j++;
+    if (j == i) return false;
+    auto alnum = [](char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); };
+    if (!alnum(s[i]) || !alnum(s[j - 1])) return false;
+    for (size_t k = i; k < j; k++)
+      if (!alnum(s[k]) && s[k] != '-') return false;
+    if (j == s.size()) return true;
+    i = j + 1;
+  }
+}
+bool alnum_any(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
+bool qname_part(sv s) {  // ([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9], 1..63
+  if (s.empty() || s.size() > 63) return false;
+  if (!alnum_any(s.front()) || !alnum_any(s.back())) return false;
+  for (char c : s)
+    if (!alnum_any(c) && c != '-' && c != '_' && c != '.') return false;
+  return true;
+}
+bool is_qualified_name(sv v) {  // validation.IsQualifiedName
+  const size_t a = v.find('/');
+  if (a == sv::npos) return qname_part(v);
+  if (v.find('/', a + 1) != sv::npos) return false;
+  const sv prefix = v.substr(0, a), name = v.substr(a + 1);
+  if (prefix.empty() || prefix.size() > 253 || !dns1123_subdomain(prefix)) return false;
+  return qname_part(name);
+}
+bool is_valid_label_value(sv v) {  // validation.IsValidLabelValue (empty allowed)
+  return v.empty() || qname_part(v);
+}
+bool parse_int64(sv s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i == s.size()) return false;
+  uint64_t v = 0;
+  const uint64_t lim = neg ? (uint64_t)1 << 63 : ((uint64_t)1 << 63) - 1;
+  for (; i < s.size(); i++) {
+    const char c = s[i];
+    if (c < '0' || c > '9') return false;
+    const uint64_t d = (uint64_t)(c - '0');
+    if (v > (lim - d) / 10) return false;
+    v = v * 10 + d;
+  }
+  *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+  return true;
+}
+int label_op(sv op) {
+  if (op == "In") return OP_IN;
+  if (op == "NotIn") return OP_NOTIN;
+  if (op == "Exists") return OP_EXISTS;
+  if (op == "DoesNotExist") return OP_DNE;
+  if (op == "Gt") return OP_GT;
+  if (op == "Lt") return OP_LT;
+  return 0;
+}
+
+template <class F>
+void parallel_for(int n, int threads, F f) {
+  if (n <= 0) return;
+  if (threads <= 1 || n < 2048) {
+    f(0, n);
+    return;
+  }
+  const int T = std::min(threads, (n + 1023) / 1024);
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (int t = 0; t < T; t++) {
+    const int a = (int)((int64_t)n * t / T), b = (int)((int64_t)n * (t + 1) / T);
+    th.emplace_back([=, &f] { f(a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+struct WordsHash {
+  size_t operator()(const std::vector<int32_t>& v) const {
+    uint64_t h = 1469598103934665603ull;
+    for (int32_t x : v) h = (h ^ (uint32_t)x) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
+
+size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
+
+}  // namespace
+
+struct kad_packer {
+  using Map = std::unordered_map<sv, int>;
+  std::string err;
+  int C = 0, TW = 1;
+  uint64_t fingerprint = 0;
+  // vocabulary strings are owned here (a deque never moves its elements: the views stay valid)
+  std::deque<std::string> own;
+  Map name_id, scalar_id, label_key_id, gvk_id;
+  std::vector<Map> label_vals;
+  std::vector<std::string> taint_key, taint_value, taint_effect;
+  std::vector<uint8_t> out;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+  sv keep(std::string s) {
+    own.push_back(std::move(s));
+    return sv(own.back());
+  }
+  static void gvk_key(std::string& s, sv g, sv v, sv k) {
+    s.clear();
+    s.append(g).push_back('\0');
+    s.append(v).push_back('\0');
+    s.append(k);
+  }
+  static int find(const Map& m, sv s) {
+    auto it = m.find(s);
+    return it == m.end() ? -1 : it->second;
+  }
+
+  // label_req / eq_req / field_req of pack.py _Compiler
+  void label_words(sv key, int op, const int32_t* vals, int nv, const Strs& S, std::vector<int32_t>& w) const {
+    w.clear();
+    const int kid = find(label_key_id, key);
+    if (kid < 0) {
+      w = {(op == OP_NOTIN || op == OP_DNE) ? OP_TRUE : OP_FALSE, -1};
+      return;
+    }
+    if (op == OP_IN || op == OP_NOTIN) {
+      std::vector<int32_t> ids;
+      const auto& vocab = label_vals[kid];
+      for (int i = 0; i < nv; i++) {
+          auto it = vocab.find(S[vals[i]]);
+        if (it != vocab.end()) ids.push_back(it->second);
+      }
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      if (ids.empty()) {
+        w = {op == OP_IN ? OP_FALSE : OP_TRUE, -1};
+        return;
+      }
+      w.push_back(op | ((int32_t)ids.size() << 8));
+      w.push_back(kid);
+      w.insert(w.end(), ids.begin(), ids.end());
+      return;
+    }
+    if (op == OP_EXISTS || op == OP_DNE) {
+      w = {op, kid};
+      return;
+    }
+    int64_t thr = 0;
+    parse_int64(S[vals[0]], &thr);
+    const uint64_t u = (uint64_t)thr;
+    w = {op | (2 << 8), kid, (int32_t)(uint32_t)(u & 0xFFFFFFFFu), (int32_t)(uint32_t)(u >> 32)};
+  }
+  void eq_words(sv key, sv value, std::vector<int32_t>& w) const {
+    const int kid = find(label_key_id, key);
+    if (kid < 0) {
+      w = {OP_FALSE, -1};
+      return;
+    }
+    auto it = label_vals[kid].find(value);
+    if (it == label_vals[kid].end()) {
+      w = {OP_FALSE, -1};
+      return;
+    }
+    w = {OP_EQ | (1 << 8), kid, it->second};
+  }
+  void field_words(sv key, sv op, sv v, std::vector<int32_t>& w) const {
+    const bool eq = op == "In";
+    if (key == "metadata.name") {
+      w = {eq ? OP_NAME_EQ : OP_NAME_NE, find(name_id, v)};
+      return;
+    }
+    const bool hit = v.empty();  // fields.Set.Get of a missing key reads as ""
+    w = {hit == eq ? OP_TRUE : OP_FALSE, -1};
+  }
+};
+
+extern "C" {
+
+int kad_packer_create(const kad_pack_vocab* v, kad_packer** out) {
+  if (!v || !out) return KAD_EINVAL;
+  auto* p = new kad_packer();
+  const Strs names = strs(v->cluster_names), sc = strs(v->scalar_names), gg = strs(v->gvk_group),
+             gv = strs(v->gvk_version), gk = strs(v->gvk_kind), lk = strs(v->label_keys), lv = strs(v->label_vals),
+             tk = strs(v->taint_key), tv = strs(v->taint_value), te = strs(v->taint_effect);
+  p->C = names.n;
+  p->TW = v->n_taint_words;
+  p->fingerprint = v->fingerprint;
+  for (int i = 0; i < names.n; i++) p->name_id.emplace(p->keep(std::string(names[i])), i);
+  for (int i = 0; i < sc.n; i++) p->scalar_id.emplace(p->keep(std::string(sc[i])), i);
+  std::string key;
+  for (int i = 0; i < gg.n; i++) {
+    kad_packer::gvk_key(key, gg[i], gv[i], gk[i]);
+    p->gvk_id.emplace(p->keep(key), i);
+  }
+  p->label_vals.resize(lk.n);
+  for (int k = 0; k < lk.n; k++) {
+    p->label_key_id.emplace(p->keep(std::string(lk[k])), k);
+    for (int j = v->label_val_off[k]; j < v->label_val_off[k + 1]; j++)
+      p->label_vals[k].emplace(p->keep(std::string(lv[j])), j - v->label_val_off[k]);
+  }
+  for (int i = 0; i < tk.n; i++) {
+    p->taint_key.emplace_back(tk[i]);
+    p->taint_value.emplace_back(tv[i]);
+    p->taint_effect.emplace_back(te[i]);
+  }
+  if (p->TW < 1 || (int64_t)p->TW * 64 < tk.n) {
+    delete p;
+    return KAD_EINVAL;
+  }
+  *out = p;
+  return KAD_OK;
+}
+
+int kad_packer_destroy(kad_packer* p) {
+  delete p;
+  return KAD_OK;
+}
+
+const char* kad_packer_error(kad_packer* p) { return p ? p->err.c_str() : "null packer"; }
+
+int kad_packer_take(kad_packer* p, void* dst, size_t cap) {
+  if (!p || (!dst && !p->out.empty())) return KAD_EINVAL;
+  if (cap < p->out.size()) return p->fail(KAD_EINVAL, "destination smaller than the packed blob");
+  if (!p->out.empty()) std::memcpy(dst, p->out.data(), p->out.size());
+  std::vector<uint8_t>().swap(p->out);
+  return KAD_OK;
+}
+
+int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns* su, int threads, size_t* nbytes,
+                   kad_pack_stats* stats) {
+  if (!P || !prof || !su || !nbytes) return KAD_EINVAL;
+  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  const int W = su->n_units;
+  if (W < 0) return P->fail(KAD_EINVAL, "n_units < 0");
+  const Strs S{su->str.off, su->str.bytes, su->str.n};
+  const int C = P->C, TW = P->TW;
+  const bool select_max = prof->select_plugin == KAD_PL_MAX_CLUSTER;
+  const bool place_on = prof->filter_mask & (1u << KAD_PL_PLACEMENT_FILTER);
+  const int R = su->n_reqs;
+  static const bool tm = getenv("KAD_PACK_TIMING") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kad_pack] %-10s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
+    t_prev = t;
+  };
+
+  // ---- 1. requirement entries: validity and words of both uses
+  std::vector<uint8_t> valid(R), fvalid(R);
+  std::vector<std::vector<int32_t>> ewords(R), fwords(R);
+  parallel_for(R, threads, [&](int a, int b) {
+    std::vector<int32_t> tmp;
+    for (int r = a; r < b; r++) {
+      const sv key = S[su->rq_key[r]], ops = S[su->rq_op[r]];
+      const int v0 = su->rq_val_off[r], nv = su->rq_val_off[r + 1] - v0;
+      const int32_t* vals = su->rq_val + v0;
+      const int op = label_op(ops);
+      bool ok = op != 0 && is_qualified_name(key);
+      if (ok && (op == OP_IN || op == OP_NOTIN)) ok = nv > 0;
+      if (ok && (op == OP_EXISTS || op == OP_DNE)) ok = nv == 0;
+      if (ok && (op == OP_GT || op == OP_LT)) {
+        int64_t x;
+        ok = nv == 1 && parse_int64(S[vals[0]], &x);
+      }
+      for (int i = 0; ok && i < nv; i++) ok = is_valid_label_value(S[vals[i]]);
+      valid[r] = ok;
+      if (ok) P->label_words(key, op, vals, nv, S, ewords[r]);
+      fvalid[r] = (ops == "In" || ops == "NotIn") && nv == 1;
+      if (fvalid[r]) P->field_words(key, ops, S[vals[0]], fwords[r]);
+    }
+  });
+
+  lap("reqs");
+  // ---- 2. interning in unit order (pack.py _Compiler.intern / tol_key)
+  std::unordered_map<std::vector<int32_t>, int32_t, WordsHash> req_id;
+  std::vector<const std::vector<int32_t>*> reqs;  // by batch-wide id
+  std::vector<std::vector<int32_t>> sel_words_store;
+  std::vector<int32_t> egid(R, -1), fgid(R, -1);
+  const int64_t n_sel_total = W ? su->sel_off[W] : 0;
+  std::vector<int32_t> sgid((size_t)n_sel_total);
+  sel_words_store.reserve((size_t)n_sel_total);
+  std::vector<int32_t> tolset(W);
+  std::unordered_map<std::string, int32_t> tol_key;
+  std::vector<int> tol_rows;  // first unit of each toleration set
+  auto intern = [&](const std::vector<int32_t>& w) -> int32_t {
+    auto it = req_id.find(w);
+    if (it != req_id.end()) return it->second;
+    const int32_t id = (int32_t)reqs.size();
+    auto r = req_id.emplace(w, id);
+    reqs.push_back(&r.first->first);
+    return id;
+  };
+  {
+    std::vector<int32_t> tmp;
+    std::string key;
+    for (int w = 0; w < W; w++) {
+      // toleration list → set id
+      key.clear();
+      for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++) {
+        for (const int32_t s : {su->tol_key[t], su->tol_op[t], su->tol_value[t], su->tol_effect[t]}) {
+          const sv x = S[s];
+          const uint32_t n = (uint32_t)x.size();
+          key.append(reinterpret_cast<const char*>(&n), 4).append(x);
+        }
+      }
+      auto it = tol_key.find(key);
+      if (it == tol_key.end()) {
+        it = tol_key.emplace(key, (int32_t)tol_rows.size()).first;
+        tol_rows.push_back(w);
+      }
+      tolset[w] = it->second;
+      // filter program: ClusterSelector entries, then required terms
+      for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) {
+        P->eq_words(S[su->sel_key[e]], S[su->sel_value[e]], tmp);
+        sgid[e] = intern(tmp);
+      }
+      const uint32_t f = su->flags[w];
+      if ((f & KAD_SU_HAS_CLUSTER_AFFINITY) && (f & KAD_SU_HAS_REQUIRED)) {
+        for (int t = su->rterm_off[w]; t < su->rterm_off[w + 1]; t++) {
+          const int e0 = su->rt_req[t], e1 = e0 + su->rt_n_expr[t];
+          bool ok = true;
+          for (int e = e0; e < e1; e++) ok = ok && valid[e];
+          if (e1 > e0 && ok)
+            for (int e = e0; e < e1; e++)
+              if (egid[e] < 0) egid[e] = intern(ewords[e]);
+          const int g0 = e1, g1 = e1 + su->rt_n_field[t];
+          bool fok = true;
+          for (int e = g0; e < g1; e++) fok = fok && fvalid[e];
+          if (g1 > g0 && fok)
+            for (int e = g0; e < g1; e++)
+              if (fgid[e] < 0) fgid[e] = intern(fwords[e]);
+        }
+      }
+      // score program: preferred terms
+      if (f & KAD_SU_HAS_CLUSTER_AFFINITY) {
+        for (int t = su->pterm_off[w]; t < su->pterm_off[w + 1]; t++) {
+          if (su->pt_weight[t] == 0) continue;
+          const int e0 = su->pt_req[t], e1 = e0 + su->pt_n_expr[t];
+          if (e1 == e0) continue;
+          bool ok = true;
+          for (int e = e0; e < e1; e++) ok = ok && valid[e];
+          if (!ok) continue;
+          for (int e = e0; e < e1; e++)
+            if (egid[e] < 0) egid[e] = intern(ewords[e]);
+        }
+      }
+    }
+  }
+  const int NR = (int)reqs.size();
+  const int NT = std::max(1, (int)tol_rows.size());
+  lap("intern");
+
+  // ---- 3. per-unit columns and CSR row lengths
+  std::vector<uint32_t> flags(W);
+  std::vector<int32_t> gvk(W), n_sreq(W), n_fp(W), n_sp(W), n_place(W), n_cur(W), n_pref(W), n_key(W), nr(W);
+  std::vector<int64_t> maxc(W), desired(W), out_len(W);
+  // cluster names → snapshot ids, once per map / set entry
+  auto resolve = [&](const int32_t* off, const int32_t* names, std::vector<int32_t>& ids) {
+    const int n = W ? off[W] : 0;
+    ids.resize(n);
+    parallel_for(n, threads, [&](int a, int b) {
+      for (int i = a; i < b; i++) ids[i] = kad_packer::find(P->name_id, S[names[i]]);
+    });
+  };
+  std::vector<int32_t> place_c, cur_c, wt_c, min_c, max_c, cap_c;
+  resolve(su->place_off, su->place_name, place_c);
+  resolve(su->cur_off, su->cur_name, cur_c);
+  resolve(su->wt_off, su->wt_name, wt_c);
+  resolve(su->min_off, su->min_name, min_c);
+  resolve(su->max_off, su->max_name, max_c);
+  resolve(su->cap_off, su->cap_name, cap_c);
+  std::atomic<bool> bad_ids{false};
+  parallel_for(W, threads, [&](int a, int b) {
+    std::vector<int32_t> ids;
+    std::string gkey;
+    for (int w = a; w < b; w++) {
+      const uint32_t sf = su->flags[w];
+      uint32_t f = 0;
+      if (sf & KAD_SU_DUPLICATE) f |= KAD_W_DUPLICATE;
+      const int ncur_all = su->cur_off[w + 1] - su->cur_off[w];
+      if ((sf & KAD_SU_STICKY) && ncur_all > 0) f |= KAD_W_STICKY;
+      if (ncur_all > 0) f |= KAD_W_HAS_CURRENT;
+      if (sf & KAD_SU_AVOID_DISRUPTION) f |= KAD_W_AVOID_DISRUPTION;
+      const bool am = sf & KAD_SU_HAS_AUTO_MIGRATION;
+      if (am && (sf & KAD_SU_KEEP_UNSCHED)) f |= KAD_W_KEEP_UNSCHED;
+      desired[w] = 0;
+      if (sf & KAD_SU_HAS_DESIRED) {
+        f |= KAD_W_HAS_DESIRED;
+        desired[w] = su->desired[w];
+      }
+      maxc[w] = 0;
+      if (sf & KAD_SU_HAS_MAX_CLUSTERS) {
+        f |= KAD_W_HAS_MAX_CLUSTERS;
+        maxc[w] = su->max_clusters[w];
+      }
+      const int ns0 = su->scalar_off[w], ns1 = su->scalar_off[w + 1];
+      if (!(su->req_cpu[w] == 0 && su->req_mem[w] == 0 && su->req_eph[w] == 0 && ns1 == ns0)) f |= KAD_W_FIT_NONZERO;
+      int nsr = 0;
+      for (int i = ns0; i < ns1; i++) nsr += su->scalar_val[i] > 0;
+      n_sreq[w] = nsr;
+      kad_packer::gvk_key(gkey, S[su->group[w]], S[su->version[w]], S[su->kind[w]]);
+      gvk[w] = kad_packer::find(P->gvk_id, gkey);
+      // filter program length and R_w
+      int fl = 1 + (su->sel_off[w + 1] - su->sel_off[w]) + 1, rw = su->sel_off[w + 1] - su->sel_off[w];
+      const bool ca = sf & KAD_SU_HAS_CLUSTER_AFFINITY;
+      if (ca && (sf & KAD_SU_HAS_REQUIRED)) {
+        fl += 1;
+        for (int t = su->rterm_off[w]; t < su->rterm_off[w + 1]; t++) {
+          const int e0 = su->rt_req[t], e1 = e0 + su->rt_n_expr[t];
+          const int g0 = e1, g1 = e1 + su->rt_n_field[t];
+          bool ok = true, fok = true;
+          for (int e = e0; e < e1; e++) ok = ok && valid[e];
+          for (int e = g0; e < g1; e++) fok = fok && fvalid[e];
+          const int ne = (e1 > e0 && ok) ? e1 - e0 : 0, nf = (g1 > g0 && fok) ? g1 - g0 : 0;
+          fl += 3 + ne + nf;
+          rw += ne + nf;
+        }
+      }
+      n_fp[w] = fl;
+      // score program
+      int sl = 1;
+      bool serr = false;
+      int64_t wsum = 0;
+      if (ca) {
+        for (int t = su->pterm_off[w]; t < su->pterm_off[w + 1]; t++) {
+          if (su->pt_weight[t] == 0) continue;
+          const int e0 = su->pt_req[t], e1 = e0 + su->pt_n_expr[t];
+          if (e1 == e0) continue;
+          bool ok = true;
+          for (int e = e0; e < e1; e++) ok = ok && valid[e];
+          if (!ok) {
+            serr = true;
+            continue;
+          }
+          sl += 2 + (e1 - e0);
+          rw += e1 - e0;
+          wsum += su->pt_weight[t] < 0 ? -(int64_t)su->pt_weight[t] : su->pt_weight[t];
+        }
+      }
+      n_sp[w] = sl;
+      nr[w] = rw;
+      if (serr) f |= KAD_W_SCORE_ERROR;
+      if (wsum > (1 << 20)) f |= KAD_W_WIDE_SCORES;
+      // placement (a set: sorted unique snapshot ids)
+      const int np_all = su->place_off[w + 1] - su->place_off[w];
+      if (np_all > 0) f |= KAD_W_HAS_PLACEMENT;
+      ids.clear();
+      for (int i = su->place_off[w]; i < su->place_off[w + 1]; i++)
+        if (place_c[i] >= 0) ids.push_back(place_c[i]);
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      n_place[w] = (int)ids.size();
+      int ncur = 0;
+      for (int i = su->cur_off[w]; i < su->cur_off[w + 1]; i++) ncur += cur_c[i] >= 0;
+      n_cur[w] = ncur;
+      if (su->wt_off[w + 1] == su->wt_off[w]) f |= KAD_W_DYNAMIC_WEIGHTS;
+      // preferences: union of the Weights / Min / Max / EstimatedCapacity (>= 0) names in the snapshot
+      ids.clear();
+      for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++) ids.push_back(wt_c[i]);
+      for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++) ids.push_back(min_c[i]);
+      for (int i = su->max_off[w]; i < su->max_off[w + 1]; i++) ids.push_back(max_c[i]);
+      if (am)
+        for (int i = su->cap_off[w]; i < su->cap_off[w + 1]; i++)
+          if (su->cap_val[i] >= 0) ids.push_back(cap_c[i]);
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      n_pref[w] = (int)(ids.size() - (size_t)(!ids.empty() && ids[0] < 0));
+      const size_t ln = S[su->name[w]].size(), lns = S[su->namespace_[w]].size();
+      n_key[w] = (int)(lns ? lns + 1 + ln : ln);
+      int64_t bound = C;
+      if (select_max && (sf & KAD_SU_HAS_MAX_CLUSTERS) && maxc[w] >= 0 && maxc[w] < bound) bound = maxc[w];
+      if (place_on && (f & KAD_W_HAS_PLACEMENT) && n_place[w] < bound) bound = n_place[w];
+      if (f & KAD_W_STICKY) bound = 0;
+      out_len[w] = bound;
+      flags[w] = f;
+    }
+  });
+  if (bad_ids) return P->fail(KAD_EINVAL, "bad string id");
+  lap("units");
+
+  // ---- layout (pack.py _assemble: header, then 256-B aligned arrays in enum order)
+  auto csr_off = [&](const std::vector<int32_t>& len, std::vector<int32_t>& off) -> bool {
+    off.assign((size_t)W + 1, 0);
+    int64_t acc = 0;
+    for (int w = 0; w < W; w++) {
+      acc += len[w];
+      if (acc >= ((int64_t)1 << 31)) return false;
+      off[w + 1] = (int32_t)acc;
+    }
+    return true;
+  };
+  std::vector<int32_t> o_sreq, o_fp, o_sp, o_place, o_cur, o_pref, o_key;
+  if (!csr_off(n_sreq, o_sreq) || !csr_off(n_fp, o_fp) || !csr_off(n_sp, o_sp) || !csr_off(n_place, o_place) ||
+      !csr_off(n_cur, o_cur) || !csr_off(n_pref, o_pref) || !csr_off(n_key, o_key))
+    return P->fail(KAD_EINVAL, "CSR array exceeds 2^31 entries; split the batch");
+  std::vector<int64_t> o_out((size_t)W + 1, 0);
+  int64_t max_row = 0;
+  for (int w = 0; w < W; w++) {
+    o_out[w + 1] = o_out[w] + out_len[w];
+    max_row = std::max(max_row, out_len[w]);
+  }
+  std::vector<int32_t> req_off((size_t)NR + 1, 0);
+  for (int r = 0; r < NR; r++) req_off[r + 1] = req_off[r] + (int32_t)reqs[r]->size();
+  const size_t nS = (size_t)o_sreq[W], nF = (size_t)o_fp[W], nSP = (size_t)o_sp[W], nPL = (size_t)o_place[W],
+               nC = (size_t)o_cur[W], nP = (size_t)o_pref[W], nK = (size_t)o_key[W], nRQ = (size_t)req_off[NR];
+  const size_t sizes[KAD_B_NARRAYS] = {
+      4 * (size_t)W, 4 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 4 * (size_t)W,
+      8 * (size_t)NT * TW, 8 * (size_t)NT * TW,
+      4 * ((size_t)W + 1), 4 * nS, 8 * nS,
+      4 * ((size_t)W + 1), 4 * nF, 4 * ((size_t)W + 1), 4 * nSP,
+      4 * ((size_t)W + 1), 4 * nPL, 4 * ((size_t)W + 1), 4 * nC, 8 * nC,
+      4 * ((size_t)W + 1), 4 * nP, 8 * nP, 8 * nP, 8 * nP, 8 * nP, 4 * nP,
+      4 * ((size_t)W + 1), nK, 8 * ((size_t)W + 1), 4 * ((size_t)NR + 1), 4 * nRQ};
+  kad_batch_header h;
+  std::memset(&h, 0, sizeof(h));
+  size_t pos = align_up(sizeof(h));
+  for (int i = 0; i < KAD_B_NARRAYS; i++) {
+    h.off[i] = pos;
+    pos += align_up(sizes[i]);
+  }
+  const size_t total = std::max(pos, (size_t)ALIGN);
+  h.magic = KAD_BATCH_MAGIC;
+  h.abi_version = KAD_ABI_VERSION;
+  h.n_units = W;
+  h.n_clusters = C;
+  h.n_taint_words = TW;
+  h.n_tolsets = NT;
+  h.n_out_slots = o_out[W];
+  h.max_row_slots = (int32_t)max_row;
+  h.packed_filter_mask = prof->filter_mask;
+  h.packed_select_plugin = prof->select_plugin;
+  h.n_reqs = NR;
+  h.total_bytes = total;
+  h.snapshot_fingerprint = P->fingerprint;
+  std::vector<uint8_t>& blob = P->out;
+  blob.assign(total, 0);
+  std::memcpy(blob.data(), &h, sizeof(h));
+  uint8_t* base = blob.data();
+  auto A = [&](int i) { return base + h.off[i]; };
+  auto put = [&](int i, const void* src, size_t n) {
+    if (n) std::memcpy(A(i), src, n);
+  };
+  put(KAD_B_FLAGS, flags.data(), 4 * (size_t)W);
+  put(KAD_B_GVK, gvk.data(), 4 * (size_t)W);
+  put(KAD_B_REQ_CPU, su->req_cpu, 8 * (size_t)W);
+  put(KAD_B_REQ_MEM, su->req_mem, 8 * (size_t)W);
+  put(KAD_B_DESIRED, desired.data(), 8 * (size_t)W);
+  put(KAD_B_MAX_CLUSTERS, maxc.data(), 8 * (size_t)W);
+  put(KAD_B_TOLSET, tolset.data(), 4 * (size_t)W);
+  put(KAD_B_SREQ_OFF, o_sreq.data(), 4 * ((size_t)W + 1));
+  put(KAD_B_FPROG_OFF, o_fp.data(), 4 * ((size_t)W + 1));
+  put(KAD_B_SPROG_OFF, o_sp.data(), 4 * ((size_t)W + 1));
+  put(KAD_B_PLACE_OFF, o_place.data(), 4 * ((size_t)W + 1));
+  put(KAD_B_CUR_OFF, o_cur.data(), 4 * ((size_t)W + 1));
+  put(KAD_B_PREF_OFF, o_pref.data(), 4 * ((size_t)W + 1));
+  put(KAD_B_KEY_OFF, o_key.data(), 4 * ((size_t)W + 1));
+  put(KAD_B_OUT_OFF, o_out.data(), 8 * ((size_t)W + 1));
+  put(KAD_B_REQ_OFF, req_off.data(), 4 * ((size_t)NR + 1));
+  {
+    int32_t* rq = reinterpret_cast<int32_t*>(A(KAD_B_REQ));
+    for (int r = 0; r < NR; r++) std::memcpy(rq + req_off[r], reqs[r]->data(), 4 * reqs[r]->size());
+  }
+
+  lap("layout");
+  // ---- 4. CSR rows in place
+  int32_t* sreq_id = reinterpret_cast<int32_t*>(A(KAD_B_SREQ_ID));
+  int64_t* sreq_val = reinterpret_cast<int64_t*>(A(KAD_B_SREQ_VAL));
+  int32_t* fprog = reinterpret_cast<int32_t*>(A(KAD_B_FPROG));
+  int32_t* sprog = reinterpret_cast<int32_t*>(A(KAD_B_SPROG));
+  int32_t* place = reinterpret_cast<int32_t*>(A(KAD_B_PLACE));
+  int32_t* cur_id = reinterpret_cast<int32_t*>(A(KAD_B_CUR_ID));
+  int64_t* cur_rep = reinterpret_cast<int64_t*>(A(KAD_B_CUR_REP));
+  int32_t* pref_id = reinterpret_cast<int32_t*>(A(KAD_B_PREF_ID));
+  int64_t* pref_w = reinterpret_cast<int64_t*>(A(KAD_B_PREF_W));
+  int64_t* pref_min = reinterpret_cast<int64_t*>(A(KAD_B_PREF_MIN));
+  int64_t* pref_max = reinterpret_cast<int64_t*>(A(KAD_B_PREF_MAX));
+  int64_t* pref_cap = reinterpret_cast<int64_t*>(A(KAD_B_PREF_CAP));
+  uint32_t* pref_fl = reinterpret_cast<uint32_t*>(A(KAD_B_PREF_FLAGS));
+  uint8_t* keyb = A(KAD_B_KEY);
+  struct PrefEntry {
+    int32_t c, m, i;
+  };
+  parallel_for(W, threads, [&](int a, int b) {
+    std::vector<int32_t> ids;
+    std::vector<std::pair<int32_t, int64_t>> cl;
+    std::vector<PrefEntry> pe;
+    for (int w = a; w < b; w++) {
+      const uint32_t sf = su->flags[w];
+      // scalar requests with value > 0, in map order (snapshot id or -1)
+      int k = o_sreq[w];
+      for (int i = su->scalar_off[w]; i < su->scalar_off[w + 1]; i++)
+        if (su->scalar_val[i] > 0) {
+          sreq_id[k] = kad_packer::find(P->scalar_id, S[su->scalar_name[i]]);
+          sreq_val[k++] = su->scalar_val[i];
+        }
+      // filter program (kad_sched.h predicate programs)
+      int32_t* fp = fprog + o_fp[w];
+      int pc = 0;
+      fp[pc++] = su->sel_off[w + 1] - su->sel_off[w];
+      for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) fp[pc++] = sgid[e];
+      const bool ca = sf & KAD_SU_HAS_CLUSTER_AFFINITY;
+      if (!(ca && (sf & KAD_SU_HAS_REQUIRED))) {
+        fp[pc++] = 0;
+      } else {
+        fp[pc++] = 1;
+        fp[pc++] = su->rterm_off[w + 1] - su->rterm_off[w];
+        for (int t = su->rterm_off[w]; t < su->rterm_off[w + 1]; t++) {
+          const int e0 = su->rt_req[t], e1 = e0 + su->rt_n_expr[t];
+          const int g0 = e1, g1 = e1 + su->rt_n_field[t];
+          bool ok = true, fok = true;
+          for (int e = e0; e < e1; e++) ok = ok && valid[e];
+          for (int e = g0; e < g1; e++) fok = fok && fvalid[e];
+          int tf = 0;
+          if (e1 > e0) tf |= KAD_TERM_HAS_EXPR | (ok ? KAD_TERM_EXPR_VALID : 0);
+          if (g1 > g0) tf |= KAD_TERM_HAS_FIELD | (fok ? KAD_TERM_FIELD_VALID : 0);
+          const int ne = (e1 > e0 && ok) ? e1 - e0 : 0, nf = (g1 > g0 && fok) ? g1 - g0 : 0;
+          fp[pc++] = tf;
+          fp[pc++] = ne;
+          fp[pc++] = nf;
+          for (int e = 0; e < ne; e++) fp[pc++] = egid[e0 + e];
+          for (int e = 0; e < nf; e++) fp[pc++] = fgid[g0 + e];
+        }
+      }
+      // score program
+      int32_t* sp = sprog + o_sp[w];
+      int sc = 1, nt = 0;
+      if (ca) {
+        for (int t = su->pterm_off[w]; t < su->pterm_off[w + 1]; t++) {
+          if (su->pt_weight[t] == 0) continue;
+          const int e0 = su->pt_req[t], e1 = e0 + su->pt_n_expr[t];
+          if (e1 == e0) continue;
+          bool ok = true;
+          for (int e = e0; e < e1; e++) ok = ok && valid[e];
+          if (!ok) continue;
+          sp[sc++] = su->pt_weight[t];
+          sp[sc++] = e1 - e0;
+          for (int e = e0; e < e1; e++) sp[sc++] = egid[e];
+          nt++;
+        }
+      }
+      sp[0] = nt;
+      // placement
+      ids.clear();
+      for (int i = su->place_off[w]; i < su->place_off[w + 1]; i++)
+        if (place_c[i] >= 0) ids.push_back(place_c[i]);
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      if (!ids.empty()) std::memcpy(place + o_place[w], ids.data(), 4 * ids.size());
+      // current clusters (nil replicas → DesiredReplicas, rsp.go:119-126), by snapshot id
+      cl.clear();
+      const int64_t tot = (sf & KAD_SU_HAS_DESIRED) ? su->desired[w] : 0;
+      for (int i = su->cur_off[w]; i < su->cur_off[w + 1]; i++)
+        if (cur_c[i] >= 0) cl.emplace_back(cur_c[i], su->cur_has_rep[i] ? su->cur_rep[i] : tot);
+      std::sort(cl.begin(), cl.end());
+      for (size_t i = 0; i < cl.size(); i++) {
+        cur_id[o_cur[w] + i] = cl[i].first;
+        cur_rep[o_cur[w] + i] = cl[i].second;
+      }
+      // preferences sorted by snapshot id: (cluster, map, entry) triples, merged per cluster;
+      // a repeated map key keeps its last entry, as a Go map holds one
+      const bool am = sf & KAD_SU_HAS_AUTO_MIGRATION;
+      pe.clear();
+      for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++)
+        if (wt_c[i] >= 0) pe.push_back({wt_c[i], 0, i});
+      for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++)
+        if (min_c[i] >= 0) pe.push_back({min_c[i], 1, i});
+      for (int i = su->max_off[w]; i < su->max_off[w + 1]; i++)
+        if (max_c[i] >= 0) pe.push_back({max_c[i], 2, i});
+      if (am)
+        for (int i = su->cap_off[w]; i < su->cap_off[w + 1]; i++)
+          if (cap_c[i] >= 0 && su->cap_val[i] >= 0) pe.push_back({cap_c[i], 3, i});
+      std::sort(pe.begin(), pe.end(), [](const PrefEntry& x, const PrefEntry& y) {
+        return x.c != y.c ? x.c < y.c : (x.m != y.m ? x.m < y.m : x.i < y.i);
+      });
+      int j = o_pref[w];
+      for (size_t q = 0; q < pe.size();) {
+        const int c = pe[q].c;
+        int64_t wv = 0, mn = 0, mx = 0, cp = 0;
+        uint32_t fl = 0;
+        for (; q < pe.size() && pe[q].c == c; q++) {
+          const int i = pe[q].i;
+          switch (pe[q].m) {
+            case 0: wv = su->wt_val[i]; fl |= KAD_PREF_HAS_WEIGHT; break;
+            case 1: mn = su->min_val[i]; break;
+            case 2: mx = su->max_val[i]; fl |= KAD_PREF_HAS_MAX; break;
+            default: cp = su->cap_val[i]; fl |= KAD_PREF_HAS_CAP; break;
+          }
+        }
+        pref_id[j] = c;
+        pref_w[j] = wv;
+        pref_min[j] = mn;
+        pref_max[j] = mx;
+        pref_cap[j] = cp;
+        pref_fl[j] = fl;
+        j++;
+      }
+      // su.Key()
+      uint8_t* kb = keyb + o_key[w];
+      const sv nsp = S[su->namespace_[w]], nm = S[su->name[w]];
+      if (!nsp.empty()) {
+        std::memcpy(kb, nsp.data(), nsp.size());
+        kb[nsp.size()] = '/';
+        kb += nsp.size() + 1;
+      }
+      if (!nm.empty()) std::memcpy(kb, nm.data(), nm.size());
+    }
+  });
+
+  lap("rows");
+  // tolerated-taint masks per toleration set (framework/util.go:406-450 via Toleration.ToleratesTaint)
+  uint64_t* tol_all = reinterpret_cast<uint64_t*>(A(KAD_B_TOL_ALL));
+  uint64_t* tol_pns = reinterpret_cast<uint64_t*>(A(KAD_B_TOL_PNS));
+  const int ntaint = (int)P->taint_key.size();
+  parallel_for((int)tol_rows.size(), threads, [&](int a, int b) {
+    for (int r = a; r < b; r++) {
+      const int w = tol_rows[r];
+      for (int tid = 0; tid < ntaint; tid++) {
+        const std::string &tk = P->taint_key[tid], &tv = P->taint_value[tid], &te = P->taint_effect[tid];
+        bool all = false, pns = false;
+        for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++) {
+          const sv key = S[su->tol_key[t]], op = S[su->tol_op[t]], val = S[su->tol_value[t]], eff = S[su->tol_effect[t]];
+          bool ok;
+          if (!eff.empty() && eff != te)
+            ok = false;
+          else if (!key.empty() && key != tk)
+            ok = false;
+          else if (op.empty() || op == "Equal")
+            ok = val == tv;
+          else
+            ok = op == "Exists";
+          if (ok) {
+            all = true;
+            if (eff.empty() || eff == "PreferNoSchedule") pns = true;
+          }
+        }
+        const uint64_t bit = 1ull << (tid % 64);
+        if (all) tol_all[(size_t)r * TW + tid / 64] |= bit;
+        if (pns) tol_pns[(size_t)r * TW + tid / 64] |= bit;
+      }
+    }
+  });
+
+  lap("tolsets");
+  if (stats) {
+    if (stats->n_reqs) std::memcpy(stats->n_reqs, nr.data(), 4 * (size_t)W);
+    if (stats->n_tols)
+      for (int w = 0; w < W; w++) stats->n_tols[w] = su->tol_off[w + 1] - su->tol_off[w];
+    stats->n_distinct_reqs = NR;
+    stats->n_tolsets = NT;
+  }
+  *nbytes = total;
+  return KAD_OK;
+}
+
+}  // extern "C"

@@ -438,3 +438,86 @@ def mutate_clusters(rng: np.random.Generator, clusters: List[T.FederatedCluster]
                 c.api_resource_types = [r for r in api_pool if rng.random() < 0.8]
         out[i] = c
     return out, idx
+
+
+# ------------------------------------------------------------ columnar generator (native packer input)
+def gen_units_c2_columns(rng: np.random.Generator, W: int, n_keys=8, n_vals=8, n_taints=16,
+                         mode=T.SCHEDULING_MODE_DUPLICATE, prefix="su"):
+    """The C2/C3 workload of :func:`gen_units_c2` (same distributions, its own random stream) generated
+    directly as ``columns.SUColumns`` with numpy — the packer input a Go shim would hand over — so 1M-unit
+    batches (C3) are generated in about a second instead of minutes of Python objects."""
+    from . import columns as CO
+
+    st = CO.StringTable()
+    sid = st.id
+    key_ids = np.array([sid(f"key{k}") for k in range(n_keys)], np.int32)
+    val_ids = np.array([sid(f"val{v}") for v in range(n_vals)], np.int32)
+    op_ids = np.array([sid(o) for o in (T.OP_IN, T.OP_NOT_IN, T.OP_EXISTS)], np.int32)
+    nt5 = max(1, n_taints // 3)
+    tkey_ids = np.array([sid(f"taint-{i % nt5}") for i in range(max(1, n_taints))], np.int32)
+    tval_ids = np.array([sid(f"v{i}") for i in range(max(1, n_taints))], np.int32)
+    empty = sid("")
+    eff_ids = np.array([sid(e) for e in EFFECTS], np.int32)
+    equal_id, exists_id = sid(T.TOLERATION_OP_EQUAL), sid(T.TOLERATION_OP_EXISTS)
+    g, v, k, ns = sid("apps"), sid("v1"), sid("Deployment"), sid("default")
+    name0 = len(st._parts)
+    for w in range(W):
+        st._parts.append(f"{prefix}-{w}".encode())
+    str_off, str_data = st.arrays()
+
+    cols = {}
+    cols["group"] = np.full(W, g, np.int32)
+    cols["version"] = np.full(W, v, np.int32)
+    cols["kind"] = np.full(W, k, np.int32)
+    cols["namespace_"] = np.full(W, ns, np.int32)
+    cols["name"] = np.arange(name0, name0 + W, dtype=np.int32)
+    f = CO.SU_HAS_DESIRED | CO.SU_HAS_MAX_CLUSTERS | CO.SU_HAS_CLUSTER_AFFINITY | CO.SU_HAS_REQUIRED
+    if mode == T.SCHEDULING_MODE_DUPLICATE:
+        f |= CO.SU_DUPLICATE
+    cols["flags"] = np.full(W, f, np.uint32)
+    cols["req_cpu"] = rng.integers(0, 64_001, W).astype(np.int64)
+    cols["req_mem"] = rng.integers(0, 256 * GI + 1, W, dtype=np.int64)
+    cols["req_eph"] = np.zeros(W, np.int64)
+    cols["max_clusters"] = rng.integers(1, 17, W).astype(np.int64)
+    cols["desired"] = rng.integers(1, 101, W).astype(np.int64)
+    # ClusterSelector: half the units, one entry
+    has_sel = rng.random(W) < 0.5
+    ns_ = int(has_sel.sum())
+    cols["sel_off"] = CO._csr_off(has_sel.astype(np.int32))
+    cols["sel_key"] = key_ids[rng.integers(0, n_keys, ns_)]
+    cols["sel_value"] = val_ids[rng.integers(0, n_vals, ns_)]
+    # one required term of 1-2 In / NotIn / Exists expressions
+    n_expr = rng.integers(1, 3, W).astype(np.int32)
+    R = int(n_expr.sum())
+    cols["rterm_off"] = np.arange(W + 1, dtype=np.int32)
+    rt_req = np.zeros(W, np.int32)
+    rt_req[1:] = np.cumsum(n_expr)[:-1]
+    cols["rt_req"] = rt_req
+    cols["rt_n_expr"] = n_expr
+    cols["rt_n_field"] = np.zeros(W, np.int32)
+    op = rng.integers(0, 3, R)
+    cols["rq_key"] = key_ids[rng.integers(0, n_keys, R)]
+    cols["rq_op"] = op_ids[op]
+    nv = np.where(op == 2, 0, rng.integers(1, 4, R)).astype(np.int32)
+    cols["rq_val_off"] = CO._csr_off(nv)
+    cols["rq_val"] = val_ids[rng.integers(0, n_vals, int(nv.sum()))]
+    # tolerations: 0-3, half Equal (effect 70 %), half Exists (random effect 70 %)
+    n_tol = rng.integers(0, 4, W).astype(np.int32)
+    TT = int(n_tol.sum())
+    cols["tol_off"] = CO._csr_off(n_tol)
+    i = rng.integers(0, max(1, n_taints), TT)
+    r = rng.random(TT)
+    with_eff = rng.random(TT) < 0.7
+    eq = r < 0.5
+    cols["tol_key"] = tkey_ids[i]
+    cols["tol_op"] = np.where(eq, equal_id, exists_id).astype(np.int32)
+    cols["tol_value"] = np.where(eq, tval_ids[i], empty).astype(np.int32)
+    eff = np.where(eq, eff_ids[i % 3], eff_ids[rng.integers(0, 3, TT)])
+    cols["tol_effect"] = np.where(with_eff, eff, empty).astype(np.int32)
+    zero_off = np.zeros(W + 1, np.int32)
+    for grp in ("scalar", "pterm", "place", "cur", "wt", "min", "max", "cap"):
+        cols[grp + "_off"] = zero_off
+    for kname, dt in CO.FIELDS:
+        if kname not in cols:
+            cols[kname] = np.zeros(0, dt)
+    return CO.SUColumns(W, str_off, str_data, cols)

@@ -14,6 +14,11 @@ import threading
 import numpy as np
 import pytest
 
+try:  # torch's HIP runtime must initialise before libkad.so's in one process (bench.py's order too)
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - CPU-only environments without torch
+    torch = None
+
 from gpu_util import assert_same, c_oracle
 from kubeadmiral_amd import pack, synth
 
@@ -82,7 +87,6 @@ def test_schedule_batch_threads_share_one_ctx(ctx):
 
 def test_snapshot_upload_device(ctx):
     """Snapshot blob in device memory (as after bench.py's RCCL broadcast) → kad_snapshot_upload_device."""
-    import torch
 
     clusters, units, fwk = synth.make_config("c2", W=3000, C=256, seed=21)
     snap = pack.Snapshot(clusters)
