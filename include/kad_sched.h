@@ -333,7 +333,14 @@ int kad_last_timing(kad_ctx* ctx, float ms[3]);
  * stream carries only the kernels (no marker packets between passes) and
  * kad_last_timing returns KAD_ESTATE.  No reference counterpart (instrumentation). */
 int kad_set_timing(kad_ctx* ctx, int on);
+/* Per-stage device times of the last kad_schedule run with timing on (n <= 6 entries):
+ * ms[0] req_mask_kernel, [1] prep_kernel, [2] the main schedule kernel (lean / wide / full),
+ * [3] the defer pass, [4] the replica planner, [5] the whole pipeline. No reference counterpart. */
+int kad_stage_timing(kad_ctx* ctx, float* ms, int n);
 int kad_results_download(kad_ctx* ctx, const kad_result_view* out);
+/* The same results copied device-to-device into caller DEVICE buffers of the result view's sizes
+ * (e.g. the send buffers of an RCCL all-gather of placements across GPUs); blocking. */
+int kad_results_copy_device(kad_ctx* ctx, const kad_result_view* dev_out);
 
 /* All in one: upload batch, schedule, download (blocking). */
 int kad_schedule_batch(kad_ctx* ctx, const kad_profile* profile, const void* batch_blob, size_t nbytes,

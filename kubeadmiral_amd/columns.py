@@ -338,6 +338,14 @@ class NativeBatch:
         self.units = None
 
 
+def _from_blob(blob: np.ndarray, fwk: Framework) -> "NativeBatch":
+    """A received batch blob (e.g. sent by the packing rank) as a NativeBatch without pack statistics."""
+    return NativeBatch(None, fwk, blob, np.zeros(0, np.int64), np.zeros(0, np.int64), -1, -1)
+
+
+NativeBatch.from_blob = staticmethod(_from_blob)
+
+
 class NativePacker:
     """kad_packer for one pack.Snapshot's vocabulary."""
 

@@ -15,7 +15,9 @@ using namespace kad;
 struct kad_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // stage events: 0 start, 3 after req_mask, 4 after prep, 5 after the main schedule kernel, 1 after the
+  // defer pass, 2 after the planner
+  hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::mutex mu;
   std::string err;
   // snapshot
@@ -749,10 +751,13 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   const bool tm = c->timing;
   if (tm) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total || wide_path(c->sd);
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
-  HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream));
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[5], c->stream));  // re-recorded after the main kernel when it runs
+  HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream, tm ? c->ev[5] : nullptr));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())
     HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, c->d_plan_rows, (int)c->plan_rows.size(), c->batch_hdr.max_row_slots,
@@ -808,6 +813,39 @@ static int results_download_locked(kad_ctx* c, const kad_result_view* out) {
   if (S) {
     HIPCHK(c, hipMemcpyAsync(out->cluster, c->d_cluster, S * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(out->replicas, c->d_replicas, S * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KAD_OK;
+}
+
+int kad_stage_timing(kad_ctx* c, float* ms, int n) {
+  if (!c || !ms || n < 0) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
+  if (!c->timed) return fail(c, KAD_ESTATE, "the last kad_schedule ran with timing off");
+  HIPCHK(c, hipEventSynchronize(c->ev[2]));
+  const int pairs[6][2] = {{0, 3}, {3, 4}, {4, 5}, {5, 1}, {1, 2}, {0, 2}};
+  for (int i = 0; i < n && i < 6; i++) HIPCHK(c, hipEventElapsedTime(&ms[i], c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
+  return KAD_OK;
+}
+
+// device-to-device copy of the last results into caller device buffers (e.g. the send buffers of an
+// RCCL all-gather of placements); ordered on the ctx stream and synchronised before return
+int kad_results_copy_device(kad_ctx* c, const kad_result_view* dev_out) {
+  if (!c || !dev_out) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t W = c->batch_hdr.n_units;
+  const size_t S = c->batch_hdr.n_out_slots;
+  if (W) {
+    HIPCHK(c, hipMemcpyAsync(dev_out->status, c->d_status, W * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dev_out->count, c->d_count, W * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dev_out->flags, c->d_flags, W * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  if (S) {
+    HIPCHK(c, hipMemcpyAsync(dev_out->cluster, c->d_cluster, S * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dev_out->replicas, c->d_replicas, S * 8, hipMemcpyDeviceToDevice, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KAD_OK;

@@ -134,8 +134,9 @@ bool fast_path(int C);
 // true if launch_schedule runs schedule_wide_kernel for this snapshot (clean, 5..16 chunks)
 bool wide_path(const SnapDev& s);
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st);
+// after_main (optional): recorded between the main schedule kernel and the defer pass (stage timing)
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p,
-                           void* global_scratch, size_t scratch_bytes, hipStream_t st);
+                           void* global_scratch, size_t scratch_bytes, hipStream_t st, hipEvent_t after_main = nullptr);
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,
                        int n_rows, int kmax, void* global_scratch, size_t scratch_bytes, hipStream_t st);
 hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,

@@ -2493,7 +2493,7 @@ static hipError_t launch_defer_pass(const SnapDev& s, const BatchDev& b, const O
 }
 
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
-                           size_t scr_bytes, hipStream_t st) {
+                           size_t scr_bytes, hipStream_t st, hipEvent_t after_main) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (b.W == 0) return hipSuccess;
   const size_t wb = row_layout(s.C).bytes;
@@ -2520,6 +2520,8 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn};
     hipLaunchKernelGGL(schedule_wide_kernel<WIDE_MAX_NCH>, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
     if (hipError_t e = hipGetLastError()) return e;
+    if (after_main)
+      if (hipError_t e = hipEventRecord(after_main, st)) return e;
     // feasible lists longer than WIDE_P positions can come from any unit: the defer pass always runs
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);
   }
@@ -2561,6 +2563,8 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
       default: launch_lean<0, false>(A, (int)grid, lds, st); break;
     }
     if (hipError_t e = hipGetLastError()) return e;
+    if (after_main)
+      if (hipError_t e = hipEventRecord(after_main, st)) return e;
     // nothing can be deferred (host-checked: every unit and cluster is in the
     // lean kernel's range and every feasible list fits its registers)
     if (nch <= 4 && !b.may_defer) return hipSuccess;

@@ -44,10 +44,14 @@ _lib = None
 
 
 def declared_functions() -> List[str]:
-    """Names of the functions include/kad_sched.h declares."""
-    with open(HEADER) as f:
-        src = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(kad_\w+)\s*\(", src, re.M)))
+    """Names of the functions include/*.h declare (kad_sched.h, kad_pack.h)."""
+    import glob
+
+    names = set()
+    for h in sorted(glob.glob(os.path.join(os.path.dirname(HEADER), "*.h"))):
+        with open(h) as f:
+            names |= set(re.findall(r"^\s*(?:int|const char\*)\s+(kad_\w+)\s*\(", f.read(), re.M))
+    return sorted(names)
 
 
 def load_library(path: str = LIB_PATH):
@@ -73,6 +77,8 @@ def load_library(path: str = LIB_PATH):
     L.kad_last_timing.argtypes = [P, P]
     L.kad_set_timing.argtypes = [P, I]
     L.kad_results_download.argtypes = [P, P]
+    L.kad_results_copy_device.argtypes = [P, P]
+    L.kad_stage_timing.argtypes = [P, P, I]
     L.kad_schedule_batch.argtypes = [P, P, P, SZ, P]
     L.kad_select_rows.argtypes = [P, I, P, P, P, U32, P, P, P]
     L.kad_plan_rows.argtypes = [P, I, P, P, P, P, P, P, P, P, P, P, P, P]
@@ -123,6 +129,12 @@ class Context:
         self._chk(self.L.kad_snapshot_upload(self.h, _p(snap.blob), snap.blob.nbytes))
         self.snap = snap
 
+    def upload_snapshot_blob(self, blob: np.ndarray, snap: Optional[Snapshot] = None):
+        """kad_snapshot_upload of a packed snapshot blob (e.g. received from the packing rank)."""
+        blob = np.ascontiguousarray(blob, np.uint8)
+        self._chk(self.L.kad_snapshot_upload(self.h, _p(blob), blob.nbytes))
+        self.snap = snap
+
     def upload_snapshot_device(self, dev_ptr: int, nbytes: int, snap: Optional[Snapshot] = None):
         self._chk(self.L.kad_snapshot_upload_device(self.h, ctypes.c_void_p(dev_ptr), nbytes))
         self.snap = snap
@@ -150,6 +162,20 @@ class Context:
         ms = (ctypes.c_float * 3)()
         self._chk(self.L.kad_last_timing(self.h, ms))
         return float(ms[0]), float(ms[1]), float(ms[2])
+
+    STAGES = ("req_mask", "prep", "main", "defer", "planner", "total")
+
+    def stage_timing(self) -> dict:
+        """kad_stage_timing: device ms per stage of the last timed schedule()."""
+        ms = (ctypes.c_float * 6)()
+        self._chk(self.L.kad_stage_timing(self.h, ms, 6))
+        return {k: float(v) for k, v in zip(self.STAGES, ms)}
+
+    def copy_results_device(self, status_ptr: int, count_ptr: int, flags_ptr: int, cluster_ptr: int,
+                            replicas_ptr: int):
+        """kad_results_copy_device: results D2D into caller device buffers (e.g. torch tensors)."""
+        v = ResultView(status_ptr, count_ptr, flags_ptr, cluster_ptr, replicas_ptr)
+        self._chk(self.L.kad_results_copy_device(self.h, ctypes.byref(v)))
 
     def download(self) -> BatchResult:
         res = BatchResult.empty(self.batch)

@@ -18,7 +18,8 @@ import json
 import os
 from collections import defaultdict
 
-STAGE = ("req_mask_kernel", "prep_kernel", "schedule_lean_kernel", "schedule_kernel")
+STAGE = ("req_mask_kernel", "prep_kernel", "schedule_lean_kernel", "schedule_wide_kernel", "schedule_kernel")
+MAIN = ("schedule_wide_kernel", "schedule_lean_kernel")
 
 ap = argparse.ArgumentParser()
 ap.add_argument("out")
@@ -51,6 +52,14 @@ for k, d in res["kernels"].items():
         stage_bytes += d.get("hbm_bytes_corrected", 0.0)
         stage_ns += d.get("avg_ns", 0.0)
 res["stage"] = {"kernels": list(STAGE), "hbm_bytes_per_launch": stage_bytes, "avg_ns_sum": stage_ns}
+# the dominant kernel of the stage (bench.py's roofline kernel): traffic and instruction counts per launch
+main = {}
+for k, d in res["kernels"].items():
+    if any(m in k for m in MAIN) and d.get("avg_ns", 0) > main.get("avg_ns", 0):
+        main = dict(d, name=k)
+if main:
+    main["hbm_bytes_per_launch"] = main.get("hbm_bytes_corrected")
+res["main_kernel"] = main
 print(json.dumps(res, indent=1))
 if a.json:
     with open(a.json, "w") as f:
@@ -58,4 +67,4 @@ if a.json:
                    "hbm_bytes_per_launch": stage_bytes, "stage_avg_ns_sum": stage_ns,
                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; (2*FETCH_SIZE + WRITE_SIZE)"
                              " KiB per dispatch summed over the stage kernels (MI355X_MICROARCH.md HBM section)",
-                   "kernels": res["kernels"]}, f, indent=1)
+                   "main_kernel": res["main_kernel"], "kernels": res["kernels"]}, f, indent=1)
