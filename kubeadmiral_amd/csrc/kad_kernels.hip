@@ -767,6 +767,7 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
       b.cw[g] = cw;
     }
     if (s.fold) m &= folded_word(s, fm, f, gvk, tol0, cw, nch, ch);
+    if (ch == nch - 1 && (s.C & 63)) m &= (1ull << (s.C & 63)) - 1;  // clusters past C: never feasible
     b.sw[g] = m;
   }
 }
@@ -893,7 +894,8 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   // static filter words carry ClusterAffinity + PlacementFilter, and with SnapDev::fold also TaintToleration
   // + APIResources (prep_kernel)
   const bool fold = largs()->s.fold;
-  const bool f_sw = (fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER))) || (fold && (f_taint || f_api));
+  // the static words are always read: they also clear the last chunk's lanes past C (prep_kernel)
+  constexpr bool f_sw = true;
   const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
   const bool s_res =
       sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
@@ -1021,8 +1023,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     const uint64_t tolp0 = (uint64_t)fld64(14);
     const bool use_cur = f_taint && (fc & KAD_W_HAS_CURRENT);
     const bool fit_on = f_fit && (fc & KAD_W_FIT_NONZERO);
-    const uint64_t o_sw = f_sw ? 0ull : ~0ull, o_taint = f_taint ? 0ull : ~0ull, o_fit = fit_on ? 0ull : ~0ull;
+    const uint64_t o_sw = 0ull, o_taint = f_taint ? 0ull : ~0ull, o_fit = fit_on ? 0ull : ~0ull;
     const uint64_t o_api = f_api ? 0ull : ~0ull, a_api = gvc >= 0 ? ~0ull : 0ull;  // no GVK id: no cluster has it
+    const double fcpu = fit_on ? rqcd : -1.0, fmem = fit_on ? rqmd : -1.0;  // clean fit compare operands
     uint64_t dsw = ~0ull, dcw = 0;  // dynamic-NCH path: words of chunks 64g..64g+63 in lanes
     auto load_words = [&](int ch0) {
       LArgs a = largs();
@@ -1102,8 +1105,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         }
         // each filter as a lane mask (v_cmp → SGPR pair), combined with scalar
         // ANDs under uniform selects (no branches inside the unrolled loop)
-        const int rem = C - ch * WAVE;
-        uint64_t m = rem >= WAVE ? ~0ull : ((1ull << rem) - 1);
+        uint64_t m = ~0ull;  // lanes past C: cleared in the static word
         const bool sch = ucur && ((cw0 >> lane) & 1);
         const uint64_t x = sch ? ne0 : ns0;
         bool tok = (x & ~tolc) == 0;
@@ -1113,12 +1115,13 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           const uint64_t xt = sch ? ldg(a->s.ne, (uint32_t)(tw * C) + cl) : ldg(a->s.nsne, (uint32_t)(tw * C) + cl);
           tok &= (xt & ~ldc(a->b.tol_all + (size_t)tsc * TWs + tw)) == 0;
         }
-        // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64)
-        const uint64_t m_fit = clean ? ballot(__builtin_bit_cast(double, ucpu) >= rqcd) & ballot(__builtin_bit_cast(double, umem) >= rqmd)
+        // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64; with the filter
+        // off the compare is against -1, true everywhere)
+        const uint64_t m_fit = clean ? ballot(__builtin_bit_cast(double, ucpu) >= fcpu) & ballot(__builtin_bit_cast(double, umem) >= fmem)
                                      : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
         if constexpr (FOLD) {
           (void)tok;
-          m &= (sw0 | o_sw) & (m_fit | o_fit);
+          m &= sw0 & (clean ? m_fit : (m_fit | o_fit));
         } else {
           const uint64_t m_taint = ballot(tok);      // taint_toleration.go:50-77
           const uint64_t m_api = ballot((gv0 >> (gvc & 63)) & 1);  // apiresources.go:25-43
@@ -1647,7 +1650,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
   }
   const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
   const bool fold = wargs()->s.fold;  // taint + API filters in the static words (prep_kernel)
-  const bool f_sw = (fm & (BIT(KAD_PL_CLUSTER_AFFINITY) | BIT(KAD_PL_PLACEMENT_FILTER))) || (fold && (f_taint || f_api));
+  // the static words are always read: they also clear the last chunk's lanes past C (prep_kernel)
   const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
   const bool s_res =
       sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
@@ -1683,8 +1686,8 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
   auto fetch = [&](int w) -> uint32_t {
     if (w < 0) return 0u;
     if (lane < 16) return ldg((const uint32_t*)(recs + w), (uint32_t)lane);
-    if (f_sw && lane < 16 + 2 * nch) return ldg((const uint32_t*)(sws + (size_t)w * nch), (uint32_t)(lane - 16));
-    return ~0u;
+    if (lane < 16 + 2 * nch) return ldg((const uint32_t*)(sws + (size_t)w * nch), (uint32_t)(lane - 16));
+    return 0u;  // chunks past nch: nothing feasible
   };
   wq_issue(heads, tk);
   int2 cb = wq_resolve(heads, W, tk);
@@ -1732,8 +1735,9 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       const uint64_t tolp0 = (uint64_t)fld64(14);
       const bool use_cur = f_taint && (fc & KAD_W_HAS_CURRENT);
       const bool fit_on = f_fit && (fc & KAD_W_FIT_NONZERO);
-      const uint64_t o_sw = f_sw ? 0ull : ~0ull, o_taint = f_taint ? 0ull : ~0ull, o_fit = fit_on ? 0ull : ~0ull;
+      const uint64_t o_taint = f_taint ? 0ull : ~0ull;
       const uint64_t o_api = f_api ? 0ull : ~0ull, a_api = gvc >= 0 ? ~0ull : 0ull;
+      const double fcpu = fit_on ? rqcd : -1.0, fmem = fit_on ? rqmd : -1.0;  // fit off: compare against -1
 
       // ---------------- filters → compacted feasible list (findClustersThatFitWorkload, :152-169)
       int n = 0;
@@ -1745,15 +1749,16 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       auto filter_chunks = [&](auto mode_t) {
         constexpr int MODE = decltype(mode_t)::value;
         constexpr bool FAST = MODE >= 1, FOLD = MODE == 2;
-#pragma unroll 1
-        for (int g = 0; g < nch; g += 4) {
+        // FOLD: fully unrolled (constant readlane lanes for the static words); else one 4-chunk group per trip
+#pragma unroll
+        for (int g = 0; g < (FOLD ? NCH : nch); g += 4) {
+          if (FOLD && g >= nch) break;
           uint64_t mk[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int ch = g + j;
             const int c = ch * WAVE + lane;
-            const int rem = C - ch * WAVE;
-            uint64_t m = rem >= WAVE ? ~0ull : (rem > 0 ? ((1ull << rem) - 1) : 0ull);
+            uint64_t m = ~0ull;  // lanes past C and chunks past nch: cleared in the static words
             const int cc = c < Cp ? c : 0;
             const double2 av = c_av[cc];
             const ulonglong2 tg = FOLD ? make_ulonglong2(0ull, 0ull) : c_tg[cc];
@@ -1773,14 +1778,14 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
               }
             }
             // fit.go:73-134 on exact f64: available - request >= 0
-            const uint64_t m_fit = ballot(av.x >= rqcd) & ballot(av.y >= rqmd);
+            const uint64_t m_fit = ballot(av.x >= fcpu) & ballot(av.y >= fmem);
             if constexpr (FOLD) {
               (void)tok;
-              m &= (sw0 | o_sw) & (m_fit | o_fit);
+              m &= sw0 & m_fit;
             } else {
               const uint64_t m_taint = ballot(tok);                    // taint_toleration.go:50-77
               const uint64_t m_api = ballot((tg.y >> (gvc & 63)) & 1);  // apiresources.go:25-43
-              m &= (sw0 | o_sw) & (m_taint | o_taint) & ((m_api & a_api) | o_api) & (m_fit | o_fit);
+              m &= sw0 & (m_taint | o_taint) & ((m_api & a_api) | o_api) & m_fit;
             }
             mk[j] = m;
           }

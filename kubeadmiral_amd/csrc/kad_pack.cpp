@@ -15,6 +15,7 @@
 //      bytes); per toleration set: tolerated-taint masks
 //      (Toleration.ToleratesTaint, k8s.io/api v0.26.6).
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -22,6 +23,7 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -114,14 +116,16 @@ int label_op(sv op) {
   return 0;
 }
 
+// f(a, b) over [0, n) split into contiguous ranges on up to `threads` threads; `grain` = the fewest
+// items worth a thread of their own
 template <class F>
-void parallel_for(int n, int threads, F f) {
+void parallel_for(int n, int threads, F f, int grain = 1024) {
   if (n <= 0) return;
-  if (threads <= 1 || n < 2048) {
+  if (threads <= 1 || n < 2 * grain) {
     f(0, n);
     return;
   }
-  const int T = std::min(threads, (n + 1023) / 1024);
+  const int T = std::min(threads, (n + grain - 1) / grain);
   std::vector<std::thread> th;
   th.reserve(T);
   for (int t = 0; t < T; t++) {
@@ -153,7 +157,9 @@ struct kad_packer {
   Map name_id, scalar_id, label_key_id, gvk_id;
   std::vector<Map> label_vals;
   std::vector<std::string> taint_key, taint_value, taint_effect;
-  std::vector<uint8_t> out;
+  std::unique_ptr<uint8_t[]> out;  // the last packed blob (kad_packer_take)
+  size_t out_n = 0;
+  int take_threads = 1;
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -183,21 +189,20 @@ struct kad_packer {
       return;
     }
     if (op == OP_IN || op == OP_NOTIN) {
-      std::vector<int32_t> ids;
       const auto& vocab = label_vals[kid];
+      w.push_back(0);
+      w.push_back(kid);
       for (int i = 0; i < nv; i++) {
-          auto it = vocab.find(S[vals[i]]);
-        if (it != vocab.end()) ids.push_back(it->second);
+        auto it = vocab.find(S[vals[i]]);
+        if (it != vocab.end()) w.push_back(it->second);
       }
-      std::sort(ids.begin(), ids.end());
-      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-      if (ids.empty()) {
+      std::sort(w.begin() + 2, w.end());
+      w.erase(std::unique(w.begin() + 2, w.end()), w.end());
+      if (w.size() == 2) {
         w = {op == OP_IN ? OP_FALSE : OP_TRUE, -1};
         return;
       }
-      w.push_back(op | ((int32_t)ids.size() << 8));
-      w.push_back(kid);
-      w.insert(w.end(), ids.begin(), ids.end());
+      w[0] = op | ((int32_t)(w.size() - 2) << 8);
       return;
     }
     if (op == OP_EXISTS || op == OP_DNE) {
@@ -232,6 +237,63 @@ struct kad_packer {
     w = {hit == eq ? OP_TRUE : OP_FALSE, -1};
   }
 };
+
+// The columns come from another language's shim: every offset array must be monotone from 0, every
+// string id and requirement range in bounds, before any pass indexes with them.
+static int validate_columns(kad_packer* P, const kad_su_columns* su, int threads) {
+  const int W = su->n_units, NS = su->str.n, R = su->n_reqs;
+  if (NS < 0 || R < 0 || !su->str.off) return P->fail(KAD_EINVAL, "bad string table / requirement count");
+  if (su->str.off[0] != 0) return P->fail(KAD_EINVAL, "string offsets must start at 0");
+  for (int i = 0; i < NS; i++)
+    if (su->str.off[i + 1] < su->str.off[i]) return P->fail(KAD_EINVAL, "string offsets must be non-decreasing");
+  std::atomic<bool> bad{false};
+  auto ids_ok = [&](const int32_t* a, int64_t n) {
+    parallel_for((int)n, threads, [&](int lo, int hi) {
+      for (int i = lo; i < hi; i++)
+        if (a[i] < 0 || a[i] >= NS) bad = true;
+    });
+  };
+  auto csr = [&](const int32_t* off, int n, int64_t* total) -> bool {
+    if (!off || off[0] != 0) return false;
+    for (int i = 0; i < n; i++)
+      if (off[i + 1] < off[i]) return false;
+    *total = off[n];
+    return true;
+  };
+  ids_ok(su->group, W);
+  ids_ok(su->version, W);
+  ids_ok(su->kind, W);
+  ids_ok(su->namespace_, W);
+  ids_ok(su->name, W);
+  int64_t n;
+  struct G {
+    const int32_t* off;
+    std::vector<const int32_t*> ids;
+  };
+  const G groups[] = {{su->scalar_off, {su->scalar_name}}, {su->tol_off, {su->tol_key, su->tol_op, su->tol_value, su->tol_effect}},
+                      {su->sel_off, {su->sel_key, su->sel_value}}, {su->place_off, {su->place_name}},
+                      {su->cur_off, {su->cur_name}}, {su->wt_off, {su->wt_name}}, {su->min_off, {su->min_name}},
+                      {su->max_off, {su->max_name}}, {su->cap_off, {su->cap_name}}};
+  for (const G& g : groups) {
+    if (!csr(g.off, W, &n)) return P->fail(KAD_EINVAL, "a per-unit CSR offset array is not monotone from 0");
+    for (const int32_t* a : g.ids) ids_ok(a, n);
+  }
+  int64_t nrt, npt, nv;
+  if (!csr(su->rterm_off, W, &nrt) || !csr(su->pterm_off, W, &npt) || !csr(su->rq_val_off, R, &nv))
+    return P->fail(KAD_EINVAL, "term / requirement offsets are not monotone from 0");
+  ids_ok(su->rq_key, R);
+  ids_ok(su->rq_op, R);
+  ids_ok(su->rq_val, nv);
+  for (int64_t t = 0; t < nrt; t++)
+    if (su->rt_req[t] < 0 || su->rt_n_expr[t] < 0 || su->rt_n_field[t] < 0 ||
+        (int64_t)su->rt_req[t] + su->rt_n_expr[t] + su->rt_n_field[t] > R)
+      return P->fail(KAD_EINVAL, "required term outside the requirement table");
+  for (int64_t t = 0; t < npt; t++)
+    if (su->pt_req[t] < 0 || su->pt_n_expr[t] < 0 || (int64_t)su->pt_req[t] + su->pt_n_expr[t] > R)
+      return P->fail(KAD_EINVAL, "preferred term outside the requirement table");
+  if (bad) return P->fail(KAD_EINVAL, "string id out of range");
+  return 0;
+}
 
 extern "C" {
 
@@ -278,10 +340,18 @@ int kad_packer_destroy(kad_packer* p) {
 const char* kad_packer_error(kad_packer* p) { return p ? p->err.c_str() : "null packer"; }
 
 int kad_packer_take(kad_packer* p, void* dst, size_t cap) {
-  if (!p || (!dst && !p->out.empty())) return KAD_EINVAL;
-  if (cap < p->out.size()) return p->fail(KAD_EINVAL, "destination smaller than the packed blob");
-  if (!p->out.empty()) std::memcpy(dst, p->out.data(), p->out.size());
-  std::vector<uint8_t>().swap(p->out);
+  if (!p || (!dst && p->out_n)) return KAD_EINVAL;
+  if (cap < p->out_n) return p->fail(KAD_EINVAL, "destination smaller than the packed blob");
+  const size_t n = p->out_n, chunk = 4u << 20;
+  const int pieces = (int)((n + chunk - 1) / chunk);
+  parallel_for(pieces, p->take_threads, [&](int a, int b) {
+    for (int i = a; i < b; i++) {
+      const size_t o = (size_t)i * chunk;
+      std::memcpy(static_cast<uint8_t*>(dst) + o, p->out.get() + o, std::min(chunk, n - o));
+    }
+  }, 1);
+  p->out.reset();
+  p->out_n = 0;
   return KAD_OK;
 }
 
@@ -289,10 +359,12 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
                    kad_pack_stats* stats) {
   if (!P || !prof || !su || !nbytes) return KAD_EINVAL;
   if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  P->take_threads = threads;
   const int W = su->n_units;
   if (W < 0) return P->fail(KAD_EINVAL, "n_units < 0");
   const Strs S{su->str.off, su->str.bytes, su->str.n};
   const int C = P->C, TW = P->TW;
+  if (int r = validate_columns(P, su, threads)) return r;
   const bool select_max = prof->select_plugin == KAD_PL_MAX_CLUSTER;
   const bool place_on = prof->filter_mask & (1u << KAD_PL_PLACEMENT_FILTER);
   const int R = su->n_reqs;
@@ -305,9 +377,21 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
     t_prev = t;
   };
 
-  // ---- 1. requirement entries: validity and words of both uses
-  std::vector<uint8_t> valid(R), fvalid(R);
-  std::vector<std::vector<int32_t>> ewords(R), fwords(R);
+  // ---- 1. requirement entries (parallel): validity, expression words into one flat buffer (a slot of
+  // 2 + max(nv, 2) words per entry), field words only for entries a required term uses as a field
+  std::vector<uint8_t> valid(R), fvalid(R), is_field(R, 0);
+  std::vector<int64_t> eoff((size_t)R + 1, 0);
+  for (int r = 0; r < R; r++) eoff[r + 1] = eoff[r] + 2 + std::max(2, su->rq_val_off[r + 1] - su->rq_val_off[r]);
+  std::vector<int32_t> wbuf((size_t)eoff[R]), elen(R, 0), fw(2 * (size_t)R, 0);
+  {
+    const int nterms = W ? su->rterm_off[W] : 0;
+    parallel_for(nterms, threads, [&](int a, int b) {
+      for (int t = a; t < b; t++) {
+        const int g0 = su->rt_req[t] + su->rt_n_expr[t];
+        for (int e = g0; e < g0 + su->rt_n_field[t]; e++) is_field[e] = 1;
+      }
+    });
+  }
   parallel_for(R, threads, [&](int a, int b) {
     std::vector<int32_t> tmp;
     for (int r = a; r < b; r++) {
@@ -324,55 +408,122 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
       }
       for (int i = 0; ok && i < nv; i++) ok = is_valid_label_value(S[vals[i]]);
       valid[r] = ok;
-      if (ok) P->label_words(key, op, vals, nv, S, ewords[r]);
+      if (ok) {
+        P->label_words(key, op, vals, nv, S, tmp);
+        std::memcpy(wbuf.data() + eoff[r], tmp.data(), 4 * tmp.size());
+        elen[r] = (int32_t)tmp.size();
+      }
       fvalid[r] = (ops == "In" || ops == "NotIn") && nv == 1;
-      if (fvalid[r]) P->field_words(key, ops, S[vals[0]], fwords[r]);
+      if (fvalid[r] && is_field[r]) {
+        P->field_words(key, ops, S[vals[0]], tmp);
+        fw[2 * (size_t)r] = tmp[0];
+        fw[2 * (size_t)r + 1] = tmp[1];
+      }
     }
   });
+  // ClusterSelector entries (parallel): SelectorFromSet's Equals as (key id, value id), -1 = absent
+  const int64_t n_sel_total = W ? su->sel_off[W] : 0;
+  std::vector<int64_t> sel_code((size_t)n_sel_total);
+  parallel_for((int)n_sel_total, threads, [&](int a, int b) {
+    for (int e = a; e < b; e++) {
+      const int kid = kad_packer::find(P->label_key_id, S[su->sel_key[e]]);
+      int vid = -1;
+      if (kid >= 0) vid = kad_packer::find(P->label_vals[kid], S[su->sel_value[e]]);
+      sel_code[e] = (kid < 0 || vid < 0) ? -1 : (((int64_t)kid << 32) | (uint32_t)vid);
+    }
+  });
+  // toleration lists (parallel): a 64-bit content hash per unit, confirmed against the set's first unit
+  std::vector<uint64_t> tol_hash(W);
+  parallel_for(W, threads, [&](int a, int b) {
+    for (int w = a; w < b; w++) {
+      uint64_t h = 1469598103934665603ull;
+      for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++)
+        for (const int32_t s : {su->tol_key[t], su->tol_op[t], su->tol_value[t], su->tol_effect[t]}) {
+          for (char ch : S[s]) h = (h ^ (uint8_t)ch) * 1099511628211ull;
+          h = (h ^ 0x1ff) * 1099511628211ull;  // separator (not a byte value)
+        }
+      tol_hash[w] = h ^ (uint64_t)(su->tol_off[w + 1] - su->tol_off[w]);
+    }
+  });
+  auto same_tols = [&](int a, int b) {
+    const int na = su->tol_off[a + 1] - su->tol_off[a];
+    if (na != su->tol_off[b + 1] - su->tol_off[b]) return false;
+    for (int i = 0; i < na; i++) {
+      const int ta = su->tol_off[a] + i, tb = su->tol_off[b] + i;
+      if (S[su->tol_key[ta]] != S[su->tol_key[tb]] || S[su->tol_op[ta]] != S[su->tol_op[tb]] ||
+          S[su->tol_value[ta]] != S[su->tol_value[tb]] || S[su->tol_effect[ta]] != S[su->tol_effect[tb]])
+        return false;
+    }
+    return true;
+  };
 
   lap("reqs");
-  // ---- 2. interning in unit order (pack.py _Compiler.intern / tol_key)
-  std::unordered_map<std::vector<int32_t>, int32_t, WordsHash> req_id;
-  std::vector<const std::vector<int32_t>*> reqs;  // by batch-wide id
-  std::vector<std::vector<int32_t>> sel_words_store;
-  std::vector<int32_t> egid(R, -1), fgid(R, -1);
-  const int64_t n_sel_total = W ? su->sel_off[W] : 0;
-  std::vector<int32_t> sgid((size_t)n_sel_total);
-  sel_words_store.reserve((size_t)n_sel_total);
-  std::vector<int32_t> tolset(W);
-  std::unordered_map<std::string, int32_t> tol_key;
-  std::vector<int> tol_rows;  // first unit of each toleration set
-  auto intern = [&](const std::vector<int32_t>& w) -> int32_t {
+  // ---- 2. interning in unit order (pack.py _Compiler.intern / tol_key), keys are views of stable words
+  std::unordered_map<sv, int32_t> req_id;
+  std::vector<sv> reqs;  // by batch-wide id: the words as bytes
+  std::deque<std::array<int32_t, 3>> extra_words;  // selector words (stable addresses)
+  auto words_sv = [](const int32_t* p, size_t n) { return sv(reinterpret_cast<const char*>(p), 4 * n); };
+  auto intern = [&](sv w) -> int32_t {
     auto it = req_id.find(w);
     if (it != req_id.end()) return it->second;
     const int32_t id = (int32_t)reqs.size();
-    auto r = req_id.emplace(w, id);
-    reqs.push_back(&r.first->first);
+    req_id.emplace(w, id);
+    reqs.push_back(w);
     return id;
   };
+  static const int32_t kFalse[2] = {OP_FALSE, -1};
+  std::vector<int32_t> egid(R, -1), fgid(R, -1);
+  std::vector<int32_t> sgid((size_t)n_sel_total);
+  std::unordered_map<int64_t, int32_t> eq_gid;
+  std::vector<int32_t> tolset(W);
+  std::unordered_map<uint64_t, int32_t> tol_by_hash;
+  std::unordered_map<std::string, int32_t> tol_collide;  // exact fallback on a 64-bit hash collision
+  std::vector<int> tol_rows;  // first unit of each toleration set
   {
-    std::vector<int32_t> tmp;
     std::string key;
     for (int w = 0; w < W; w++) {
       // toleration list → set id
-      key.clear();
-      for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++) {
-        for (const int32_t s : {su->tol_key[t], su->tol_op[t], su->tol_value[t], su->tol_effect[t]}) {
-          const sv x = S[s];
-          const uint32_t n = (uint32_t)x.size();
-          key.append(reinterpret_cast<const char*>(&n), 4).append(x);
+      auto it = tol_by_hash.find(tol_hash[w]);
+      int32_t ts;
+      if (it == tol_by_hash.end()) {
+        ts = (int32_t)tol_rows.size();
+        tol_by_hash.emplace(tol_hash[w], ts);
+        tol_rows.push_back(w);
+      } else if (same_tols(tol_rows[it->second], w)) {
+        ts = it->second;
+      } else {
+        key.clear();
+        for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++)
+          for (const int32_t s2 : {su->tol_key[t], su->tol_op[t], su->tol_value[t], su->tol_effect[t]}) {
+            const sv x = S[s2];
+            const uint32_t n = (uint32_t)x.size();
+            key.append(reinterpret_cast<const char*>(&n), 4).append(x);
+          }
+        auto jt = tol_collide.find(key);
+        if (jt == tol_collide.end()) {
+          ts = (int32_t)tol_rows.size();
+          tol_collide.emplace(key, ts);
+          tol_rows.push_back(w);
+        } else {
+          ts = jt->second;
         }
       }
-      auto it = tol_key.find(key);
-      if (it == tol_key.end()) {
-        it = tol_key.emplace(key, (int32_t)tol_rows.size()).first;
-        tol_rows.push_back(w);
-      }
-      tolset[w] = it->second;
+      tolset[w] = ts;
       // filter program: ClusterSelector entries, then required terms
       for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) {
-        P->eq_words(S[su->sel_key[e]], S[su->sel_value[e]], tmp);
-        sgid[e] = intern(tmp);
+        const int64_t code = sel_code[e];
+        if (code < 0) {
+          sgid[e] = intern(words_sv(kFalse, 2));
+          continue;
+        }
+        auto jt = eq_gid.find(code);
+        if (jt != eq_gid.end()) {
+          sgid[e] = jt->second;
+          continue;
+        }
+        extra_words.push_back({OP_EQ | (1 << 8), (int32_t)(code >> 32), (int32_t)(uint32_t)code});
+        sgid[e] = intern(words_sv(extra_words.back().data(), 3));
+        eq_gid.emplace(code, sgid[e]);
       }
       const uint32_t f = su->flags[w];
       if ((f & KAD_SU_HAS_CLUSTER_AFFINITY) && (f & KAD_SU_HAS_REQUIRED)) {
@@ -382,13 +533,13 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
           for (int e = e0; e < e1; e++) ok = ok && valid[e];
           if (e1 > e0 && ok)
             for (int e = e0; e < e1; e++)
-              if (egid[e] < 0) egid[e] = intern(ewords[e]);
+              if (egid[e] < 0) egid[e] = intern(words_sv(wbuf.data() + eoff[e], elen[e]));
           const int g0 = e1, g1 = e1 + su->rt_n_field[t];
           bool fok = true;
           for (int e = g0; e < g1; e++) fok = fok && fvalid[e];
           if (g1 > g0 && fok)
             for (int e = g0; e < g1; e++)
-              if (fgid[e] < 0) fgid[e] = intern(fwords[e]);
+              if (fgid[e] < 0) fgid[e] = intern(words_sv(fw.data() + 2 * (size_t)e, 2));
         }
       }
       // score program: preferred terms
@@ -401,7 +552,7 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
           for (int e = e0; e < e1; e++) ok = ok && valid[e];
           if (!ok) continue;
           for (int e = e0; e < e1; e++)
-            if (egid[e] < 0) egid[e] = intern(ewords[e]);
+            if (egid[e] < 0) egid[e] = intern(words_sv(wbuf.data() + eoff[e], elen[e]));
         }
       }
     }
@@ -429,7 +580,6 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   resolve(su->min_off, su->min_name, min_c);
   resolve(su->max_off, su->max_name, max_c);
   resolve(su->cap_off, su->cap_name, cap_c);
-  std::atomic<bool> bad_ids{false};
   parallel_for(W, threads, [&](int a, int b) {
     std::vector<int32_t> ids;
     std::string gkey;
@@ -535,7 +685,6 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
       flags[w] = f;
     }
   });
-  if (bad_ids) return P->fail(KAD_EINVAL, "bad string id");
   lap("units");
 
   // ---- layout (pack.py _assemble: header, then 256-B aligned arrays in enum order)
@@ -560,7 +709,7 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
     max_row = std::max(max_row, out_len[w]);
   }
   std::vector<int32_t> req_off((size_t)NR + 1, 0);
-  for (int r = 0; r < NR; r++) req_off[r + 1] = req_off[r] + (int32_t)reqs[r]->size();
+  for (int r = 0; r < NR; r++) req_off[r + 1] = req_off[r] + (int32_t)(reqs[r].size() / 4);
   const size_t nS = (size_t)o_sreq[W], nF = (size_t)o_fp[W], nSP = (size_t)o_sp[W], nPL = (size_t)o_place[W],
                nC = (size_t)o_cur[W], nP = (size_t)o_pref[W], nK = (size_t)o_key[W], nRQ = (size_t)req_off[NR];
   const size_t sizes[KAD_B_NARRAYS] = {
@@ -592,10 +741,18 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   h.n_reqs = NR;
   h.total_bytes = total;
   h.snapshot_fingerprint = P->fingerprint;
-  std::vector<uint8_t>& blob = P->out;
-  blob.assign(total, 0);
-  std::memcpy(blob.data(), &h, sizeof(h));
-  uint8_t* base = blob.data();
+  P->out.reset(new uint8_t[total]);
+  P->out_n = total;
+  uint8_t* base = P->out.get();
+  // every array is written in full below except the OR-filled toleration masks; zero those, the header
+  // region and the alignment padding after each array (the blob must equal pack.py's byte for byte)
+  std::memset(base, 0, h.off[0]);
+  std::memcpy(base, &h, sizeof(h));
+  for (int i = 0; i < KAD_B_NARRAYS; i++) {
+    const size_t end = i + 1 < KAD_B_NARRAYS ? h.off[i + 1] : total;
+    const size_t used = (i == KAD_B_TOL_ALL || i == KAD_B_TOL_PNS) ? 0 : sizes[i];
+    std::memset(base + h.off[i] + used, 0, end - h.off[i] - used);
+  }
   auto A = [&](int i) { return base + h.off[i]; };
   auto put = [&](int i, const void* src, size_t n) {
     if (n) std::memcpy(A(i), src, n);
@@ -618,7 +775,7 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   put(KAD_B_REQ_OFF, req_off.data(), 4 * ((size_t)NR + 1));
   {
     int32_t* rq = reinterpret_cast<int32_t*>(A(KAD_B_REQ));
-    for (int r = 0; r < NR; r++) std::memcpy(rq + req_off[r], reqs[r]->data(), 4 * reqs[r]->size());
+    for (int r = 0; r < NR; r++) std::memcpy(rq + req_off[r], reqs[r].data(), reqs[r].size());
   }
 
   lap("layout");

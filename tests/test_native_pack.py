@@ -1,0 +1,121 @@
+"""Native batch packer (include/kad_pack.h, libkad.so kad_pack_batch) against the Python packer.
+
+The Python packer (kubeadmiral_amd/pack.py) is pinned to the object-level oracle by
+tests/test_c_oracle.py; the native packer must produce the SAME blob byte for byte
+(interning order, programs, CSR rows, toleration masks, output bounds) on every
+fuzz batch and on samples of every config's generator, for every fuzz profile.
+Host code only: runs on CPU (libkad.so loads without a GPU).
+"""
+
+import numpy as np
+import pytest
+
+from kubeadmiral_amd import columns as CO
+from kubeadmiral_amd import framework as F
+from kubeadmiral_amd import pack, synth
+from kubeadmiral_amd import types as T
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from kubeadmiral_amd import build
+    build.build()
+
+
+def _same(snap, fwk, units, threads=0):
+    want = pack.Batch(snap, fwk, units)
+    got = CO.NativePacker(snap).pack(fwk, CO.from_units(units), threads=threads)
+    assert got.blob.nbytes == want.blob.nbytes
+    if not np.array_equal(got.blob, want.blob):
+        hw, hg = pack.header_of(want.blob, pack.BatchHeader), pack.header_of(got.blob, pack.BatchHeader)
+        diff = [i for i in range(pack.B_NARRAYS)
+                if not np.array_equal(pack.array_of(want.blob, hw, i, np.uint8), pack.array_of(got.blob, hg, i, np.uint8))]
+        raise AssertionError(f"blobs differ in arrays {diff}")
+    assert np.array_equal(got.n_reqs, want.n_reqs) and np.array_equal(got.n_tols, want.n_tols)
+    assert got.n_distinct_reqs == want.n_distinct_reqs
+    return got
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_fuzz_blob_identical(seed):
+    clusters, units = synth.gen_fuzz(seed, W=70)
+    _same(pack.Snapshot(clusters), synth.fuzz_framework(seed), units, threads=1 + seed % 4)
+
+
+@pytest.mark.parametrize("cfg,W,C", [("c1", 600, 16), ("c2", 5000, 256), ("c3", 3000, 1000), ("c4", 2500, 512),
+                                     ("c5", 400, 2000)])
+def test_config_samples_blob_identical(cfg, W, C):
+    clusters, units, fwk = synth.make_config(cfg, W=W, C=C)
+    _same(pack.Snapshot(clusters), fwk, units)
+
+
+@pytest.mark.parametrize("prof", range(len(synth.FUZZ_PROFILES)))
+def test_profiles_change_output_bounds(prof):
+    clusters, units = synth.gen_fuzz(900 + prof, W=120, C=30)
+    _same(pack.Snapshot(clusters), synth.fuzz_framework(prof), units)
+
+
+def test_threads_do_not_change_the_blob():
+    clusters, units = synth.gen_fuzz(4242, W=6000, C=50)
+    snap = pack.Snapshot(clusters)
+    fwk = F.Framework()
+    cols = CO.from_units(units)
+    P = CO.NativePacker(snap)
+    blobs = [P.pack(fwk, cols, threads=t).blob for t in (1, 2, 3, 8)]
+    assert all(np.array_equal(blobs[0], b) for b in blobs[1:])
+
+
+def test_empty_batch():
+    clusters, _ = synth.gen_fuzz(3, W=1, C=10)
+    _same(pack.Snapshot(clusters), F.Framework(), [])
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_columns_round_trip(seed):
+    """from_units -> to_units loses nothing the scheduler reads: the objects it gives back pack (through
+    pack.py, the path pinned to the oracle) to the same blob as the originals, and a second round trip is
+    the identity on the columns."""
+    clusters, units = synth.gen_fuzz(seed, W=50)
+    snap, fwk = pack.Snapshot(clusters), synth.fuzz_framework(seed)
+    cols = CO.from_units(units)
+    back = CO.to_units(cols)
+    assert np.array_equal(pack.Batch(snap, fwk, back).blob, pack.Batch(snap, fwk, units).blob)
+    again = CO.from_units(back)
+    assert np.array_equal(again.str_off, cols.str_off) and np.array_equal(again.str_data, cols.str_data)
+    assert all(np.array_equal(again.cols[k], cols.cols[k]) for k in cols.cols)
+
+
+def test_columnar_generator_matches_its_objects():
+    """synth.gen_units_c2_columns (the bench's C2/C3 input) packs to the same blob natively and through
+    pack.py from the objects it describes, and has the C2 distributions."""
+    rng = np.random.default_rng(0xC3)
+    clusters = synth.gen_clusters(rng, 1000)
+    snap = pack.Snapshot(clusters)
+    fwk = synth.profile_for("c3")
+    cols = synth.gen_units_c2_columns(np.random.default_rng(7), 4000)
+    units = CO.to_units(cols)
+    got = CO.NativePacker(snap).pack(fwk, cols)
+    assert np.array_equal(got.blob, pack.Batch(snap, fwk, units).blob)
+    assert all(1 <= u.max_clusters <= 16 and 1 <= u.desired_replicas <= 100 for u in units)
+    assert 0.45 < np.mean([u.cluster_selector is not None for u in units]) < 0.55
+    assert all(len(u.affinity.cluster_affinity.required.cluster_selector_terms) == 1 for u in units)
+    assert {len(u.tolerations or []) for u in units} == {0, 1, 2, 3}
+
+
+def test_malformed_columns_are_rejected():
+    _, units = synth.gen_fuzz(5, W=20, C=12)
+    clusters, _ = synth.gen_fuzz(5, W=1, C=12)
+    snap = pack.Snapshot(clusters)
+    P = CO.NativePacker(snap)
+    good = CO.from_units(units)
+    P.pack(F.Framework(), good)
+    for field, idx, val in (("name", 0, 10 ** 6), ("tol_off", 1, -1), ("rq_key", 0, -7), ("rt_req", 0, 10 ** 6),
+                            ("sel_off", 0, 3)):
+        if len(good.cols[field]) <= idx:
+            continue
+        bad = CO.SUColumns(good.n_units, good.str_off, good.str_data, dict(good.cols))
+        bad.cols[field] = bad.cols[field].copy()
+        bad.cols[field][idx] = val
+        with pytest.raises(RuntimeError, match="kad_pack_batch"):
+            P.pack(F.Framework(), bad)
+    P.pack(F.Framework(), good)  # still usable
