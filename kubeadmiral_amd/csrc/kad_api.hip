@@ -60,7 +60,7 @@ struct kad_ctx {
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
   std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
   std::vector<uint64_t> h_ns0; // host shadow of NoSchedule|NoExecute taint word 0 [C] (SnapDev::present_taints)
-  void* d_slices = nullptr;    // SnapDev::slices [3][64][nch]
+  void* d_slices = nullptr;    // SnapDev::slices [3][64][nch], then SnapDev::taint_tab [2][8][256][nch]
   size_t slices_cap = 0;
   void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
   size_t delta_cap = 0;
@@ -445,8 +445,10 @@ static int refresh_derived(kad_ctx* c) {
   c->sd.present_taints = present;
   c->sd.fold = c->sd.TW == 1;
   const size_t nch = (size_t)((c->sd.C + 63) / 64);
-  if (int r = grow(c, &c->d_slices, &c->slices_cap, 3 * 64 * (nch ? nch : 1) * 8)) return r;
+  const size_t nc1 = nch ? nch : 1;
+  if (int r = grow(c, &c->d_slices, &c->slices_cap, (3 * 64 + 2 * 8 * 256) * nc1 * 8)) return r;
   c->sd.slices = static_cast<const uint64_t*>(c->d_slices);
+  c->sd.taint_tab = c->sd.slices + 3 * 64 * nc1;
   HIPCHK(c, launch_slices(c->sd, static_cast<uint64_t*>(c->d_slices), c->stream));
   return 0;
 }

@@ -17,6 +17,9 @@ struct SnapDev {
   int fold;
   uint64_t present_taints;    // OR of every cluster's NoSchedule|NoExecute word 0 (host shadow)
   const uint64_t* slices;
+  // [2][8][256][nch]: entry (tbl, g, sub, ch) = OR of the chunk-ch slices of taint ids 8g + b, b in sub,
+  // table tbl (0: NoSchedule|NoExecute, 1: NoExecute) — a unit's untolerated taints in 8 lookups
+  const uint64_t* taint_tab;
   const int64_t *alloc_cpu, *alloc_mem, *used_cpu, *used_mem, *alloc_s, *used_s, *alloc_cores, *avail_cores;
   const uint64_t *gvk, *nsne, *ne, *pns;
   const int32_t* lval;
@@ -126,7 +129,8 @@ size_t plan_wave_bytes(int K);
 int debug_phase_counters(uint64_t* out, int reset);
 
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st);
-// per-id cluster bitmask slices of the snapshot (SnapDev::slices), rebuilt at upload / update
+// per-id cluster bitmask slices of the snapshot (SnapDev::slices) and the taint table over them
+// (SnapDev::taint_tab), rebuilt at upload / update
 hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st);
 // true if the batch runs on schedule_lean_kernel (+ schedule_kernel over its
 // defer list); then launch_prep must run between launch_req_masks and launch_schedule.

@@ -618,12 +618,12 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
 }
 
 // ============================================================ prep kernel
-// One lane per (unit, 64-cluster chunk), every launch, before the lean
-// schedule kernel:
-//  * chunk 0's lane writes the unit's 64-B UnitRec, routing units that use a
+// One lane per (unit, PREP_CPL consecutive 64-cluster chunks), every launch,
+// before the schedule kernel:
+//  * the unit's first lane writes its 64-B UnitRec, routing units that use a
 //    feature the lean kernel leaves out (scalar resource requests, more than
 //    64 taint ids or GVKs, debug capture) to schedule_kernel (REC_FULL);
-//  * every lane writes the unit's static filter word for its chunk: the
+//  * every lane writes the unit's static filter words for its chunks: the
 //    ClusterAffinity filter (cluster_affinity.go:50-94,
 //    MatchClusterSelectorTerms clusterselector/util.go:97-132) evaluated over
 //    the requirement rows, ANDed with the PlacementFilter's ClusterNames
@@ -632,37 +632,66 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
 //    rule, taint_toleration.go:64-78).
 // This takes the program → requirement-row load chain off every unit's
 // critical path in the schedule kernel.
-__device__ uint64_t affinity_word(const uint64_t* rows, const int32_t* p, uint32_t nch, uint32_t ch) {
-  auto row = [&](int id) { return ldg(rows, (uint32_t)id * nch + ch); };
+// p(i): word i of the unit's filter program (prep_kernel stages the first words in LDS). The CPL
+// chunks ch0 .. ch0+CPL-1 are evaluated together (their row loads are independent); chunks past
+// nch read chunk nch-1 and are never stored.
+template <int CPL, class Prog>
+__device__ __forceinline__ void affinity_words(const uint64_t* rows, Prog p, uint32_t nch, uint32_t ch0,
+                                               uint64_t (&out)[CPL]) {
+  uint32_t cc[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; k++) cc[k] = ch0 + k < nch ? ch0 + k : nch - 1;
+  auto and_row = [&](uint64_t (&v)[CPL], int id) {
+    uint64_t r[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; k++) r[k] = ldg(rows, (uint32_t)id * nch + cc[k]);
+#pragma unroll
+    for (int k = 0; k < CPL; k++) v[k] &= r[k];
+  };
+  auto any = [](const uint64_t (&v)[CPL]) {
+    uint64_t o = 0;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) o |= v[k];
+    return o != 0;
+  };
   int pc = 0;
-  const int n_sel = p[pc++];
-  uint64_t m = ~0ull;  // SelectorFromSet: AND of the ClusterSelector entries
-  for (int i = 0; i < n_sel; i++) m &= row(p[pc + i]);
+  const int n_sel = p(pc++);
+  uint64_t m[CPL];  // SelectorFromSet: AND of the ClusterSelector entries
+#pragma unroll
+  for (int k = 0; k < CPL; k++) m[k] = ~0ull;
+  for (int i = 0; i < n_sel; i++) and_row(m, p(pc + i));
   pc += n_sel;
-  if (!p[pc++]) return m;  // Required == nil: Success
-  const int n_terms = p[pc++];
-  uint64_t matched = 0, undecided = m;
-  for (int t = 0; t < n_terms && undecided; t++) {
-    const int tf = p[pc], ne = p[pc + 1], nf = p[pc + 2];
+#pragma unroll
+  for (int k = 0; k < CPL; k++) out[k] = m[k];
+  if (!p(pc++)) return;  // Required == nil: Success
+  const int n_terms = p(pc++);
+  uint64_t matched[CPL], undecided[CPL], cand[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; k++) matched[k] = 0, undecided[k] = m[k];
+  for (int t = 0; t < n_terms && any(undecided); t++) {
+    const int tf = p(pc), ne = p(pc + 1), nf = p(pc + 2);
     const int at = pc + 3;
     pc += 3 + ne + nf;
     if (!(tf & (KAD_TERM_HAS_EXPR | KAD_TERM_HAS_FIELD))) continue;  // nil/empty term selects nothing
-    uint64_t cand = undecided;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) cand[k] = undecided[k];
     if (tf & KAD_TERM_HAS_EXPR) {
       if (!(tf & KAD_TERM_EXPR_VALID)) break;  // invalid selector reached: false for every undecided cluster
-      for (int i = 0; i < ne; i++) cand &= row(p[at + i]);
+      for (int i = 0; i < ne; i++) and_row(cand, p(at + i));
     }
     if (tf & KAD_TERM_HAS_FIELD) {
       if (!(tf & KAD_TERM_FIELD_VALID)) {  // reached only where the expressions matched
-        undecided &= ~cand;
+#pragma unroll
+        for (int k = 0; k < CPL; k++) undecided[k] &= ~cand[k];
         continue;
       }
-      for (int i = 0; i < nf; i++) cand &= row(p[at + ne + i]);
+      for (int i = 0; i < nf; i++) and_row(cand, p(at + ne + i));
     }
-    matched |= cand;
-    undecided &= ~cand;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) matched[k] |= cand[k], undecided[k] &= ~cand[k];
   }
-  return matched;
+#pragma unroll
+  for (int k = 0; k < CPL; k++) out[k] = matched[k];
 }
 
 // bits of the sorted cluster-id list ids[lo, hi) that fall in chunk ch
@@ -696,19 +725,35 @@ __global__ __launch_bounds__(256) void slice_kernel(SnapDev s, uint64_t* out) {
   if (lane == 0) out[((size_t)tbl * 64 + t) * nch + ch] = m;
 }
 
+// SnapDev::taint_tab: lane per (tbl, g, sub, ch); OR over the set bits of sub of slice 8g + b of table tbl
+__global__ __launch_bounds__(256) void taint_table_kernel(SnapDev s, uint64_t* tab) {
+  const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g >= 2u * 8 * 256 * nch) return;
+  const uint32_t ch = g % nch, e = g / nch, sub = e & 255u, grp = (e >> 8) & 7u, tbl = e >> 11;
+  uint64_t m = 0;
+  for (uint32_t r = sub; r; r &= r - 1) m |= s.slices[((size_t)tbl * 64 + grp * 8 + __builtin_ctz(r)) * nch + ch];
+  tab[g] = m;
+}
+
 // TaintToleration.Filter (taint_toleration.go:44-89) and APIResources.Filter (apiresources.go:25-43) of
-// unit w on chunk ch from the slices (TW == 1): clusters with a NoSchedule|NoExecute taint the unit does
-// not tolerate are out — only NoExecute ones on its CurrentClusters (cw) — and clusters without its GVK
+// unit w on chunk ch (TW == 1): clusters with a NoSchedule|NoExecute taint the unit does not tolerate
+// are out — only NoExecute ones on its CurrentClusters (cw) — and clusters without its GVK. The
+// untolerated present taints are looked up 8 ids at a time in SnapDev::taint_tab (independent loads).
 __device__ __forceinline__ uint64_t folded_word(const SnapDev& s, uint32_t fm, uint32_t f, int gvk, uint64_t tol,
                                                 uint64_t cw, uint32_t nch, uint32_t ch) {
   uint64_t m = ~0ull;
   if (fm & (1u << KAD_PL_TAINT_TOLERATION)) {
     const bool cur = f & KAD_W_HAS_CURRENT;
+    const uint64_t u = s.present_taints & ~tol;
     uint64_t bad_ns = 0, bad_ne = 0;
-    for (uint64_t r = s.present_taints & ~tol; r; r &= r - 1) {
-      const int t = (int)__builtin_ctzll(r);
-      bad_ns |= s.slices[(size_t)t * nch + ch];
-      if (cur) bad_ne |= s.slices[((size_t)64 + t) * nch + ch];
+#pragma unroll
+    for (int gi = 0; gi < 8; gi++) {
+      const uint32_t sub = (uint32_t)(u >> (8 * gi)) & 255u;
+      if (sub) {
+        bad_ns |= s.taint_tab[((size_t)gi * 256 + sub) * nch + ch];
+        if (cur) bad_ne |= s.taint_tab[((size_t)(8 + gi) * 256 + sub) * nch + ch];
+      }
     }
     m = cur ? ((cw & ~bad_ne) | (~cw & ~bad_ns)) : ~bad_ns;
   }
@@ -717,29 +762,43 @@ __device__ __forceinline__ uint64_t folded_word(const SnapDev& s, uint32_t fm, u
 }
 
 constexpr int WQ_HEADS_PREP = 8, WQ_STRIDE_PREP = 32;  // = WQ_HEADS, WQ_STRIDE (schedule_wide_kernel)
+constexpr int PREP_CPL = 4;                            // chunks per lane
 __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
+  constexpr int CPL = PREP_CPL;
+  __shared__ int32_t prog_words[256 * CPL];  // words CPL*l .. CPL*l+CPL-1 of its unit's filter program, per lane
   const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
-  const uint32_t per = nch > 0 ? nch : 1u;
+  const uint32_t per = nch > 0 ? (nch + CPL - 1) / CPL : 1u;  // lanes per unit
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
   if (g == 0) {
     *b.defer_n = 0;
     *b.work_n = 0;
   }
   if (g < (uint32_t)WQ_HEADS_PREP) b.wq[g * WQ_STRIDE_PREP] = 0u;  // schedule_wide_kernel's work heads
-  if (g >= (uint32_t)b.W * per) return;
-  const uint32_t w = g / per, ch = g - w * per;
-  // every per-unit load is issued up front by every lane (w < W, the four
-  // lanes of a unit share its cache lines), so the record lanes' chain and the
-  // affinity chain below overlap instead of running one after the other
+  const bool live = g < (uint32_t)b.W * per;
+  const uint32_t w = live ? g / per : 0u, l = g - w * per, ch0 = l * CPL;
+  // the unit's lanes load its program words 0 .. CPL*per-1 with coalesced
+  // loads into LDS: the interpreter's word → row chain then runs on LDS
+  // reads, not on dependent global loads
+  const int32_t fpo = live ? b.fprog_off[w] : 0;
+  const int32_t plen = live ? b.fprog_off[w + 1] - fpo : 0;
+#pragma unroll
+  for (int k = 0; k < CPL; k++) {
+    const int i = (int)ch0 + k;
+    prog_words[threadIdx.x * CPL + k] = i < plen ? b.fprog[fpo + i] : 0;
+  }
+  __syncthreads();
+  if (!live) return;
+  // every per-unit load is issued up front by every lane (the lanes of a
+  // unit share its cache lines), so the record lane's chain and the affinity
+  // chain below overlap instead of running one after the other
   const uint32_t f = b.flags[w];
   const uint32_t fm = p.filter_mask;
   const int32_t gvk = b.gvk[w], tolset = b.tolset[w], sprog = b.sprog_off[w];
   const int64_t rqc = b.req_cpu[w], rqm = b.req_mem[w], maxc = b.maxc[w], desired = b.desired[w];
   const int64_t oo = b.out_off[w];
   const int32_t so0 = b.sreq_off[w], so1 = b.sreq_off[w + 1];
-  const int32_t fpo = b.fprog_off[w];
   const uint64_t tol0 = b.tol_all[(size_t)tolset * b.TW], tolp0 = b.tol_pns[(size_t)tolset * b.TW];
-  if (ch == 0) {
+  if (l == 0) {
     UnitRec r;
     bool full = force_full != 0;
     if ((fm & (1u << KAD_PL_API_RESOURCES)) && gvk >= 64) full = true;
@@ -756,19 +815,34 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
     r.tolp0 = tolp0;
     b.rec[w] = r;
   }
-  if (ch < nch && !(f & KAD_W_STICKY)) {
-    uint64_t m = ~0ull;
-    if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) m = affinity_word(b.req_mask, b.fprog + fpo, nch, ch);
-    if ((fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT))
-      m &= id_list_word(b.place, b.place_off[w], b.place_off[w + 1], ch);
+  if (ch0 >= nch || (f & KAD_W_STICKY)) return;
+  uint64_t m[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; k++) m[k] = ~0ull;
+  if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) {
+    const int32_t* gp = b.fprog + fpo;
+    const int base = ((int)threadIdx.x - (int)l) * CPL;  // the unit's program word 0 in this block (may be < 0)
+    auto word = [&](int i) -> int32_t {
+      const int t = base + i;
+      return (i < (int)(per * CPL) && t >= 0 && t < 256 * CPL) ? prog_words[t] : gp[i];
+    };
+    affinity_words<CPL>(b.req_mask, word, nch, ch0, m);
+  }
+  const bool place = (fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
+  const bool curw = (fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
+#pragma unroll
+  for (int k = 0; k < CPL; k++) {
+    const uint32_t ch = ch0 + k;
+    if (ch >= nch) break;
+    if (place) m[k] &= id_list_word(b.place, b.place_off[w], b.place_off[w + 1], ch);
     uint64_t cw = 0;
-    if ((fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT)) {
+    if (curw) {
       cw = id_list_word(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch);
-      b.cw[g] = cw;
+      b.cw[(size_t)w * nch + ch] = cw;
     }
-    if (s.fold) m &= folded_word(s, fm, f, gvk, tol0, cw, nch, ch);
-    if (ch == nch - 1 && (s.C & 63)) m &= (1ull << (s.C & 63)) - 1;  // clusters past C: never feasible
-    b.sw[g] = m;
+    if (s.fold) m[k] &= folded_word(s, fm, f, gvk, tol0, cw, nch, ch);
+    if (ch == nch - 1 && (s.C & 63)) m[k] &= (1ull << (s.C & 63)) - 1;  // clusters past C: never feasible
+    b.sw[(size_t)w * nch + ch] = m[k];
   }
 }
 
@@ -2440,13 +2514,16 @@ hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st) {
   const long waves = 3L * 64 * nch;
   if (waves == 0) return hipSuccess;
   hipLaunchKernelGGL(slice_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, slices);
+  const long lanes = 2L * 8 * 256 * nch;
+  hipLaunchKernelGGL(taint_table_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, s,
+                     slices + 3L * 64 * nch);
   return hipGetLastError();
 }
 
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
-  const long lanes = (long)b.W * (nch > 0 ? nch : 1);
+  const long lanes = (long)b.W * (nch > 0 ? (nch + PREP_CPL - 1) / PREP_CPL : 1);
   const long grid = lanes > 0 ? (lanes + 255) / 256 : 1;  // one block at W = 0 still resets defer_n
   hipLaunchKernelGGL(prep_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, p, force_full ? 1 : 0);
   return hipGetLastError();
