@@ -1,6 +1,8 @@
 // C ABI of libkad.so (include/kad_sched.h): context, residency, launch, results.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -62,6 +64,9 @@ struct kad_ctx {
   std::vector<uint64_t> h_ns0; // host shadow of NoSchedule|NoExecute taint word 0 [C] (SnapDev::present_taints)
   void* d_slices = nullptr;    // SnapDev::slices [3][64][nch], then SnapDev::taint_tab [2][8][256][nch]
   size_t slices_cap = 0;
+  std::vector<int64_t> h_fit;  // SnapDev::fit_vals / fit_rows (host copy the upload reads from)
+  void* d_fit = nullptr;
+  size_t fit_cap = 0;
   void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
   size_t delta_cap = 0;
   bool batch_defer = false;    // some unit uses a feature the lean kernel defers
@@ -337,7 +342,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -435,6 +440,66 @@ static int check_snapshot_header(kad_ctx* c, const kad_snapshot_header& h, size_
   return 0;
 }
 
+// SnapDev::fit_vals / fit_rows from the host shadow of the resources (clean snapshots, C <= FITFOLD_MAX_C)
+static int build_fit_table(kad_ctx* c) {
+  const int C = c->sd.C;
+  c->sd.fitfold = 0;
+  if (!c->sd.clean || C <= 0 || C > FITFOLD_MAX_C) return 0;
+  const int nch = (C + 63) / 64;
+  std::vector<int64_t> vals[2];
+  std::vector<int> order(C);
+  size_t words = 0;
+  for (int r = 0; r < 2; r++) {
+    vals[r].resize(C);
+    for (int x = 0; x < C; x++) vals[r][x] = c->h_res[(size_t)r * C + x] - c->h_res[(size_t)(2 + r) * C + x];
+    std::vector<int64_t> u = vals[r];
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    c->sd.fit_m[r] = (int)u.size();
+  }
+  int mp = FIT_FENCES;  // vals padded with INT64_MAX to a power of two >= m + 1 (fence search)
+  while (mp < c->sd.fit_m[0] + 1 || mp < c->sd.fit_m[1] + 1) mp *= 2;
+  c->sd.fit_mp = mp;
+  for (int r = 0; r < 2; r++) words += (size_t)mp + ((size_t)c->sd.fit_m[r] + 1) * nch;
+  c->h_fit.assign(words, 0);
+  size_t o = 0;
+  size_t vo[2], ro[2];
+  for (int r = 0; r < 2; r++) {  // vals
+    const int m = c->sd.fit_m[r];
+    std::vector<int64_t> u = vals[r];
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    vo[r] = o;
+    std::copy(u.begin(), u.end(), c->h_fit.begin() + (ptrdiff_t)o);
+    std::fill(c->h_fit.begin() + (ptrdiff_t)(o + m), c->h_fit.begin() + (ptrdiff_t)(o + mp), INT64_MAX);
+    o += (size_t)mp;
+  }
+  for (int r = 0; r < 2; r++) {  // rows, from the largest amount down: row j = row j+1 | clusters at vals[j]
+    const int m = c->sd.fit_m[r];
+    const int64_t* u = c->h_fit.data() + vo[r];
+    ro[r] = o;
+    for (int x = 0; x < C; x++) order[x] = x;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return vals[r][a] > vals[r][b]; });
+    uint64_t* rows = reinterpret_cast<uint64_t*>(c->h_fit.data() + o);
+    int q = 0;
+    for (int j = m - 1; j >= 0; j--) {
+      std::memcpy(rows + (size_t)j * nch, rows + (size_t)(j + 1) * nch, (size_t)nch * 8);
+      for (; q < C && vals[r][order[q]] == u[j]; q++) rows[(size_t)j * nch + (order[q] >> 6)] |= 1ull << (order[q] & 63);
+    }
+    o += ((size_t)m + 1) * nch;
+  }
+  if (int r = grow(c, &c->d_fit, &c->fit_cap, words * 8)) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_fit, c->h_fit.data(), words * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // h_fit may be rebuilt by the next upload / update
+  const int64_t* d = static_cast<const int64_t*>(c->d_fit);
+  for (int r = 0; r < 2; r++) {
+    c->sd.fit_vals[r] = d + vo[r];
+    c->sd.fit_rows[r] = reinterpret_cast<const uint64_t*>(d + ro[r]);
+  }
+  c->sd.fitfold = 1;
+  return 0;
+}
+
 // state derived from the resident snapshot: clean / negative ranges (host shadows) and, with one taint
 // word, the per-id cluster slices prep_kernel folds the taint and API filters from (SnapDev::fold)
 static int refresh_derived(kad_ctx* c) {
@@ -450,7 +515,7 @@ static int refresh_derived(kad_ctx* c) {
   c->sd.slices = static_cast<const uint64_t*>(c->d_slices);
   c->sd.taint_tab = c->sd.slices + 3 * 64 * nc1;
   HIPCHK(c, launch_slices(c->sd, static_cast<uint64_t*>(c->d_slices), c->stream));
-  return 0;
+  return build_fit_table(c);
 }
 
 int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {

@@ -8,6 +8,9 @@
 
 namespace kad {
 
+constexpr int FITFOLD_MAX_C = 4096;
+constexpr int FIT_FENCES = 256;  // prep_kernel's LDS copy of every (fit_mp / 256)-th fit value
+
 struct SnapDev {
   int C, GW, TW, K, S;
   int clean;  // host: every cluster's cpu/mem fit the lean kernel's exact-f64 path (kad_api.hip res_clean)
@@ -20,6 +23,16 @@ struct SnapDev {
   // [2][8][256][nch]: entry (tbl, g, sub, ch) = OR of the chunk-ch slices of taint ids 8g + b, b in sub,
   // table tbl (0: NoSchedule|NoExecute, 1: NoExecute) — a unit's untolerated taints in 8 lookups
   const uint64_t* taint_tab;
+  // clean snapshots with C <= FITFOLD_MAX_C: ClusterResourcesFit's cpu / memory test as a threshold
+  // table per resource r (0 cpu, 1 memory) — fit_vals[r]: the m_r distinct available amounts
+  // (allocatable - used) ascending, then INT64_MAX up to fit_mp; fit_rows[r][j][nch]: clusters whose available
+  // amount is >= fit_vals[r][j] (row m_r empty). prep_kernel ANDs row lower_bound(request) into the
+  // static words, and the schedule kernels skip their own cpu / memory compare (SnapDev::fitfold).
+  int fitfold;
+  int fit_m[2];
+  int fit_mp;  // fit_vals[r] length: a power of two >= FIT_FENCES, > fit_m[r] (INT64_MAX padding)
+  const int64_t* fit_vals[2];
+  const uint64_t* fit_rows[2];
   const int64_t *alloc_cpu, *alloc_mem, *used_cpu, *used_mem, *alloc_s, *used_s, *alloc_cores, *avail_cores;
   const uint64_t *gvk, *nsne, *ne, *pns;
   const int32_t* lval;

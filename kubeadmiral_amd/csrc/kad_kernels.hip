@@ -30,15 +30,18 @@ namespace kad {
 #ifdef KAD_PHASE_PROF
 __device__ unsigned long long g_phase[256 * 32];
 #define KAD_PT(v) const unsigned long long v = __builtin_readcyclecounter()
-#define KAD_PACC uint32_t pacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
+#define KAD_PACC uint32_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
 #define KAD_PFLUSH                                                                       \
   if (lane_id() == 0)                                                                    \
     for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + i_], pacc[i_])
-// lean kernel: its own slots 10..15 (A, B, D, E, straddles, D on straddles)
+// lean / wide kernel: slots 10..15 (A, B, D, E, straddles, D on straddles), 24..29 (replay: setup,
+// partitions, pivots, insertion sorts, #partitions, feasible count of replayed units)
 #define KAD_PFLUSH_LEAN                                                                  \
-  if (lane_id() == 0)                                                                    \
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 10 + i_], pacc[i_])
+  if (lane_id() == 0) {                                                                  \
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 10 + i_], pacc[i_]); \
+    for (int i_ = 6; i_ < 12; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 18 + i_], pacc[i_]); \
+  }
 // plan kernel: slots 16..23 (setup, dynamic weights, first plan, avoid-disruption, output, units)
 #define KAD_PFLUSH_PLAN                                                                  \
   if (lane_id() == 0)                                                                    \
@@ -65,7 +68,7 @@ __host__ __device__ inline RowLayout row_layout(int C) {
   L.idx = L.fx + 4 * Cp;                         // u16[Cp] feasible position → cluster id
   L.perm = L.idx + 2 * Cp;                       // u16[Cp] pdqsort replay permutation
   L.posl = L.perm + 2 * Cp;                      // u16[Cp] replay scratch (partition stoppers)
-  L.posr = L.posl + 2 * Cp;                      // u16[Cp]
+  L.posr = L.posl + 2 * Cp + 128;                // u16[Cp] (posl: Cp + 64 entries, PdqWave)
   L.feas = (L.posr + 2 * Cp + 15) & ~(size_t)15;  // u64[nw] feasibility by cluster
   L.sel = L.feas + 8 * nw;                       // u64[nw] selection by position
   L.place = L.sel + 8 * nw;
@@ -761,6 +764,25 @@ __device__ __forceinline__ uint64_t folded_word(const SnapDev& s, uint32_t fm, u
   return m;
 }
 
+// #(fit_vals[r] < x) for r = 0, 1 (x0, x1): 8 levels over the LDS fences (fence i = value (i+1)*S - 1,
+// S = fit_mp / FIT_FENCES), then log2(S) levels in global memory; both searches interleaved
+__device__ __forceinline__ int2 fit_ranks(const SnapDev& s, const int64_t (*fences)[FIT_FENCES], int64_t x0, int64_t x1) {
+  int f0 = 0, f1 = 0;
+#pragma unroll
+  for (int st = FIT_FENCES / 2; st >= 1; st >>= 1) {
+    f0 = fences[0][f0 + st - 1] < x0 ? f0 + st : f0;
+    f1 = fences[1][f1 + st - 1] < x1 ? f1 + st : f1;
+  }
+  const int S = s.fit_mp / FIT_FENCES;
+  int b0 = f0 * S, b1 = f1 * S;  // the answer lies in [b, b + S - 1]: value b + S - 1 >= x
+  for (int st = S >> 1; st >= 1; st >>= 1) {
+    const int64_t v0 = ldg(s.fit_vals[0], (uint32_t)(b0 + st - 1)), v1 = ldg(s.fit_vals[1], (uint32_t)(b1 + st - 1));
+    b0 = v0 < x0 ? b0 + st : b0;
+    b1 = v1 < x1 ? b1 + st : b1;
+  }
+  return make_int2(b0, b1);
+}
+
 constexpr int WQ_HEADS_PREP = 8, WQ_STRIDE_PREP = 32;  // = WQ_HEADS, WQ_STRIDE (schedule_wide_kernel)
 constexpr int PREP_CPL = 4;                            // chunks per lane
 __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
@@ -785,6 +807,12 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   for (int k = 0; k < CPL; k++) {
     const int i = (int)ch0 + k;
     prog_words[threadIdx.x * CPL + k] = i < plen ? b.fprog[fpo + i] : 0;
+  }
+  __shared__ int64_t fences[2][FIT_FENCES];  // SnapDev::fitfold: every S-th fit value per resource
+  if (s.fitfold) {
+    const int S = s.fit_mp / FIT_FENCES;
+    for (int i = threadIdx.x; i < 2 * FIT_FENCES; i += 256)
+      fences[i / FIT_FENCES][i % FIT_FENCES] = s.fit_vals[i / FIT_FENCES][(i % FIT_FENCES + 1) * S - 1];
   }
   __syncthreads();
   if (!live) return;
@@ -827,6 +855,16 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
       return (i < (int)(per * CPL) && t >= 0 && t < 256 * CPL) ? prog_words[t] : gp[i];
     };
     affinity_words<CPL>(b.req_mask, word, nch, ch0, m);
+  }
+  if (s.fitfold && (fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO)) {
+    // fit.go:73-134 (cpu, memory) by threshold rows: clusters whose available amount >= the request
+    const int2 j = fit_ranks(s, fences, rqc, rqm);
+    const int jc = j.x, jm = j.y;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) {
+      const uint32_t ch = ch0 + k < nch ? ch0 + k : nch - 1;
+      m[k] &= ldg(s.fit_rows[0], (uint32_t)jc * nch + ch) & ldg(s.fit_rows[1], (uint32_t)jm * nch + ch);
+    }
   }
   const bool place = (fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
   const bool curw = (fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
@@ -886,7 +924,7 @@ __host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
   L.idx = L.key + 4 * P;         // u16[P] feasible position → cluster id (NCH > 0: P = Cp)
   L.pid = L.idx + 2 * P;         // u16[P] replay: original position at each position
   L.posl = L.pid + 2 * P;        // u16[P] replay scratch (partition stoppers; then ranks)
-  L.posr = L.posl + 2 * P;       // u16[P]
+  L.posr = L.posl + 2 * P + 128; // u16[P] (posl: P + 64 entries, PdqWave)
   L.bytes = (L.posr + 2 * P + 15) & ~(size_t)15;
   return L;
 }
@@ -968,6 +1006,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   // static filter words carry ClusterAffinity + PlacementFilter, and with SnapDev::fold also TaintToleration
   // + APIResources (prep_kernel)
   const bool fold = largs()->s.fold;
+  const bool fitf = largs()->s.fitfold;  // cpu / memory fit in the static words too
   // the static words are always read: they also clear the last chunk's lanes past C (prep_kernel)
   constexpr bool f_sw = true;
   const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
@@ -1134,7 +1173,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     // 1 (FAST): one taint word, no CurrentClusters; 0: general
     auto filter_chunks = [&](auto mode_t) {
       constexpr int MODE = decltype(mode_t)::value;
-      constexpr bool FAST = MODE >= 1, FOLD = MODE == 2;
+      constexpr bool FAST = MODE >= 1, FOLD = MODE >= 2, FITF = MODE == 3;
       const bool ucur = !FAST && use_cur;
 #pragma unroll
       for (int ch = 0; ch < NC; ++ch) {
@@ -1142,10 +1181,10 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         int64_t acpu, ucpu, amem, umem;
         uint64_t ns0, ne0, pn0, gv0, sw0, cw0;
         if constexpr (NCH > 0) {
-          acpu = clean ? 0 : c_ac[c];
-          ucpu = c_uc[c];  // clean: available cpu as f64
-          amem = clean ? 0 : c_am[c];
-          umem = c_um[c];
+          acpu = (clean || FITF) ? 0 : c_ac[c];
+          ucpu = FITF ? 0 : c_uc[c];  // clean: available cpu as f64
+          amem = (clean || FITF) ? 0 : c_am[c];
+          umem = FITF ? 0 : c_um[c];
           ns0 = FOLD ? 0ull : c_ns[c];
           ne0 = ucur ? c_ne[c] : 0ull;
           pn0 = 0;
@@ -1191,8 +1230,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         }
         // fit.go:73-134: alloc >= req + used (clean: available - req >= 0, exact in f64; with the filter
         // off the compare is against -1, true everywhere)
-        const uint64_t m_fit = clean ? ballot(__builtin_bit_cast(double, ucpu) >= fcpu) & ballot(__builtin_bit_cast(double, umem) >= fmem)
-                                     : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
+        const uint64_t m_fit = FITF    ? ~0ull  // in the static words (SnapDev::fitfold)
+                               : clean ? ballot(__builtin_bit_cast(double, ucpu) >= fcpu) & ballot(__builtin_bit_cast(double, umem) >= fmem)
+                                       : ballot((acpu >= wadd(rqc, ucpu)) & (amem >= wadd(rqm, umem)));
         if constexpr (FOLD) {
           (void)tok;
           m &= sw0 & (clean ? m_fit : (m_fit | o_fit));
@@ -1214,7 +1254,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         }
       }
     };
-    if (fold)
+    if (fold && fitf)
+      filter_chunks(std::integral_constant<int, 3>{});
+    else if (fold)
       filter_chunks(std::integral_constant<int, 2>{});
     else if (!use_cur && TWs == 1)
       filter_chunks(std::integral_constant<int, 1>{});
@@ -1224,7 +1266,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         // every lane stores (no exec branch): infeasible lanes into pid[], rewritten before use
-        idx[((mk[ch] >> lane) & 1) ? n + mbcnt(mk[ch]) : P + lane] = (uint16_t)(ch * WAVE + lane);
+        idx[lane_on(mk[ch]) ? n + mbcnt(mk[ch]) : P + lane] = (uint16_t)(ch * WAVE + lane);
         n += popc64(mk[ch]);
       }
     }
@@ -1591,10 +1633,13 @@ __host__ __device__ inline WideLayout wide_layout() {
   L.idx = L.key + 4 * WIDE_P;     // u16[P] position -> cluster id
   L.pid = L.idx + 2 * WIDE_P;     // u16[P] replay: original position
   L.posl = L.pid + 2 * WIDE_P;    // u16[P] replay scratch, then ranks
-  L.posr = L.posl + 2 * WIDE_P;   // u16[P]
+  L.posr = L.posl + 2 * WIDE_P + 128;  // u16[P] (posl: P + 64 entries, PdqWave)
   L.bytes = L.posr + 2 * WIDE_P;
   return L;
 }
+// the compaction stores every feasible cluster's id at its position, even past P (up to 64*nch):
+// those land in pid / posl of the same wave's region and the unit is deferred
+static_assert(2 * 64 * WIDE_MAX_NCH <= 6 * WIDE_P, "idx overflow past P must stay in the wave's region");
 // block-shared cluster cache: av (f64 x2), tg (u64 x2: NS|NE taints, GVK word),
 // cap (f64 x2), iv (f32 x2), [ne u64], [pn u64]
 __host__ __device__ inline size_t wide_cache_bytes(int C, int cache_ne, int cache_pn) {
@@ -1609,6 +1654,8 @@ struct WideArgs {
   ProfDev p;
   int waves_per_block;
   int cache_ne, cache_pn;
+  int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default): bit 0 skips the
+            // pdqsort replay (ties taken by position; results differ from the reference)
 };
 typedef const __attribute__((address_space(4))) WideArgs* WArgs;
 __device__ __forceinline__ WArgs wargs() {
@@ -1724,6 +1771,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
   }
   const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
   const bool fold = wargs()->s.fold;  // taint + API filters in the static words (prep_kernel)
+  const bool fitf = wargs()->s.fitfold;  // and the cpu / memory fit test
   // the static words are always read: they also clear the last chunk's lanes past C (prep_kernel)
   const bool f_fit = fm & BIT(KAD_PL_CLUSTER_RESOURCES_FIT);
   const bool s_res =
@@ -1822,7 +1870,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       // CurrentClusters; 0: general
       auto filter_chunks = [&](auto mode_t) {
         constexpr int MODE = decltype(mode_t)::value;
-        constexpr bool FAST = MODE >= 1, FOLD = MODE == 2;
+        constexpr bool FAST = MODE >= 1, FOLD = MODE >= 2, FITF = MODE == 3;
         // FOLD: fully unrolled (constant readlane lanes for the static words); else one 4-chunk group per trip
 #pragma unroll
         for (int g = 0; g < (FOLD ? NCH : nch); g += 4) {
@@ -1834,7 +1882,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
             const int c = ch * WAVE + lane;
             uint64_t m = ~0ull;  // lanes past C and chunks past nch: cleared in the static words
             const int cc = c < Cp ? c : 0;
-            const double2 av = c_av[cc];
+            const double2 av = FITF ? make_double2(0.0, 0.0) : c_av[cc];
             const ulonglong2 tg = FOLD ? make_ulonglong2(0ull, 0ull) : c_tg[cc];
             const uint64_t sw0 = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)cur, 17 + 2 * ch)) << 32) |
                                  (uint32_t)__builtin_amdgcn_readlane((int)cur, 16 + 2 * ch);
@@ -1851,8 +1899,8 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
                 tok &= (xt & ~ldc(a->b.tol_all + (size_t)tsc * TWs + tw)) == 0;
               }
             }
-            // fit.go:73-134 on exact f64: available - request >= 0
-            const uint64_t m_fit = ballot(av.x >= fcpu) & ballot(av.y >= fmem);
+            // fit.go:73-134 on exact f64: available - request >= 0 (FITF: in the static words)
+            const uint64_t m_fit = FITF ? ~0ull : ballot(av.x >= fcpu) & ballot(av.y >= fmem);
             if constexpr (FOLD) {
               (void)tok;
               m &= sw0 & m_fit;
@@ -1865,15 +1913,17 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int pos = n + mbcnt(mk[j]);
-            idx[(((mk[j] >> lane) & 1) && pos < P) ? pos : P + lane] = (uint16_t)((g + j) * WAVE + lane);
+            // positions past P (the unit is then deferred) stay inside the wave's region (pid, posl)
+            idx[lane_on(mk[j]) ? n + mbcnt(mk[j]) : P + lane] = (uint16_t)((g + j) * WAVE + lane);
             n += popc64(mk[j]);
           }
         }
       };
-      if (fold)
-        filter_chunks(std::integral_constant<int, 2>{});
-      else if (!use_cur && TWs == 1)
+      // (the wide kernel runs on clean snapshots of C <= 1024: fold implies fitf; the general mode is
+      // correct for any snapshot, re-testing what the static words hold)
+      if (fold && fitf)
+        filter_chunks(std::integral_constant<int, 3>{});
+      else if (!fold && !use_cur && TWs == 1)
         filter_chunks(std::integral_constant<int, 1>{});
       else
         filter_chunks(std::integral_constant<int, 0>{});
@@ -2032,12 +2082,13 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           mode = 1;
         } else {
           rflags = KAD_RF_TIE_STRADDLE;
-          if (n <= 12) {  // pdqsort_func: a single (stable) insertionSort
+          if (n <= 12 || (ad->exp & 1)) {  // pdqsort_func: a single (stable) insertionSort
             mode = 2;
           } else {
             // restricted pdqsort replay, wave-parallel, on u32 keys total - min (order-preserving)
             const int xs_b = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
             const int xs_c = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+            KAD_PT(r0);
 #pragma unroll
             for (int q = 0; q < Q; ++q)
               if (q < nq && q * 64 + lane < n) {
@@ -2046,9 +2097,20 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
               }
             wave_sync();
             PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
+            KAD_PT(r1);
             pw.select(n, k);
+            KAD_PT(r2);
             for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
             wave_sync();
+            KAD_PT(r3);
+            KAD_PADD(6, (r1 - r0) + (r3 - r2));
+#ifdef KAD_PHASE_PROF
+            KAD_PADD(7, pw.pr[0]);
+            KAD_PADD(8, pw.pr[1]);
+            KAD_PADD(9, pw.pr[2]);
+            KAD_PADD(10, pw.pr[3]);
+            KAD_PADD(11, n);
+#endif
             mode = 3;
           }
         }
@@ -2072,21 +2134,24 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         if ((dup || replicas) && mode >= 0) {
           int32_t* oc = ae->o.cluster + ooff;
           int64_t* orp = ae->o.replicas + ooff;
-          int eq_before = 0;  // mode 2: ties at T in earlier positions (q = 0 only: n <= 12)
+          int eq_before = 0;  // mode 2: ties at T in earlier positions
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
             if (q >= nq) continue;
             const int p = q * 64 + lane;
             const bool v = p < n;
             bool s;
-            if (mode == 0)
+            if (mode == 0) {
               s = v;
-            else if (mode == 1)
+            } else if (mode == 1) {
               s = v && t[q] >= T;
-            else if (mode == 2)
-              s = v && (t[q] > T || (t[q] == T && mbcnt(ballot(v && t[q] == T)) + eq_before < need));
-            else
+            } else if (mode == 2) {
+              const uint64_t eqm = ballot(v && t[q] == T);
+              s = v && (t[q] > T || (t[q] == T && mbcnt(eqm) + eq_before < need));
+              eq_before += popc64(eqm);
+            } else {
               s = v && inv[p] < k;
+            }
             const uint64_t sel = ballot(s);
             if (s) {
               const uint32_t at = (uint32_t)(base + mbcnt(sel));
@@ -2599,7 +2664,8 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     long grid = n_cus();
     const long need = ((long)b.W + wpb - 1) / wpb;
     if (grid > need) grid = need;
-    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn};
+    static const int exp = getenv("KAD_WIDE_EXPERIMENT") ? atoi(getenv("KAD_WIDE_EXPERIMENT")) : 0;
+    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, exp};
     hipLaunchKernelGGL(schedule_wide_kernel<WIDE_MAX_NCH>, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
     if (hipError_t e = hipGetLastError()) return e;
     if (after_main)

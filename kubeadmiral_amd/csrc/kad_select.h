@@ -283,7 +283,17 @@ struct KeyLdsStoreT {
 //     rotation whose stop position is found by ballot.
 // heapSort (only after log2(n) unbalanced partitions) falls back to lane 0.
 // key/id: the n positions' keys (swapped in place) and original positions;
-// posL/posR: u16 scratch of n entries each.
+// posL: u16 scratch of n + 64 entries (lanes past the range write into the
+// tail, so the stopper scatter needs no exec mask); posR: n entries.
+#ifdef KAD_PHASE_PROF
+// replay sub-phase counters (profiling build): cycles in partitions, pivot choice + breakPatterns,
+// insertion sorts (partial and final), and the number of partitions
+#define PQ_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define PQ_ADD(i, x) pr[i] += (uint32_t)(x)
+#else
+#define PQ_T(v)
+#define PQ_ADD(i, x)
+#endif
 template <class KeyT, bool GS = false>
 struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
   KeyT* key;
@@ -291,6 +301,9 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
   uint16_t* posL;
   uint16_t* posR;
   int xs_b, xs_c;
+#ifdef KAD_PHASE_PROF
+  mutable uint32_t pr[4] = {0, 0, 0, 0};
+#endif
 
   __device__ __forceinline__ KeyT K(int p) const {
     const KeyT v = key[p];
@@ -315,21 +328,30 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
     }
     wsync<GS>();
   }
+  __device__ __forceinline__ KeyT rl(KeyT v, int l) const {
+    if constexpr (sizeof(KeyT) == 8) {
+      const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+      const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+      return (KeyT)(((uint64_t)hi << 32) | lo);
+    } else {
+      return (KeyT)__builtin_amdgcn_readlane((int)v, l);
+    }
+  }
+  // m = b - a <= 12: lane x takes rank #greater + #equal before (stable); the
+  // keys come from the lanes by readlane, fully unrolled (no loop, no LDS reads)
   __device__ void insertion_sort(int a, int b) const {
     const int m = b - a, lane = lane_id();
-    KeyT kp = 0;
-    uint16_t ip = 0;
-    if (lane < m) {
-      kp = key[a + lane];
-      ip = id[a + lane];
-    }
+    const bool in = lane < m;
+    const KeyT kp = key[in ? a + lane : a];
+    const uint16_t ip = id[in ? a + lane : a];
     int r = 0;
-    for (int q = 0; q < m; ++q) {
-      const KeyT kq = key[a + q];
-      r += (int)(kq > kp) | (int)((kq == kp) & (q < lane));
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      const KeyT kq = rl(kp, q);
+      r += (q < m) & ((int)(kq > kp) | (int)((kq == kp) & (q < lane)));
     }
     wsync<GS>();
-    if (lane < m) {
+    if (in) {
       key[a + r] = kp;
       id[a + r] = ip;
     }
@@ -365,48 +387,49 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
     order2(a, b, swaps);
     return b;
   }
-  // choosePivot with the candidate keys gathered by one LDS read across lanes
-  // (lane x reads position x of the candidate list), medians on scalars.
-  __device__ int choose_pivot(int a, int b, int& hint) const {
+  // choosePivot: lanes 0-2 each take one candidate triple (i-1, i, i+1 / j.. / k.. for l >= 50) with
+  // three LDS reads and order it in VALU (Go's medianAdjacent: order2(a,b), order2(b,c), order2(a,b),
+  // counting swaps); the median of the three medians on scalars. Returns the pivot position, *pkey its key.
+  __device__ int choose_pivot(int a, int b, int& hint, KeyT& pkey) const {
     const int lane = lane_id();
     const int l = b - a;
     int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
     int swaps = 0;
     if (l >= 8) {
-      // candidates: l >= 50: i-1,i,i+1, j-1,j,j+1, k-1,k,k+1 ; else i, j, k
       const bool adj = l >= 50;
-      const int g = adj ? lane / 3 : lane, d = adj ? lane % 3 - 1 : 0;
+      const int g = lane < 3 ? lane : 0;
       const int base = g == 0 ? i : (g == 1 ? j : k);
-      const KeyT v = key[lane < (adj ? 9 : 3) ? base + d : a];
-      auto kv = [&](int x) -> KeyT {
-        if constexpr (sizeof(KeyT) == 8) {
-          const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, x);
-          const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), x);
-          return (KeyT)(((uint64_t)hi << 32) | lo);
-        } else {
-          return (KeyT)__builtin_amdgcn_readlane((int)v, x);
-        }
-      };
-      // (position, key) triples; order2/median exactly as Go's (less = key greater)
-      auto med = [&](int pa, KeyT ka, int pb, KeyT kb, int pc, KeyT kc, KeyT& km) -> int {
-        if (kb > ka) { int tp = pa; pa = pb; pb = tp; KeyT tk = ka; ka = kb; kb = tk; swaps++; }
-        if (kc > kb) { int tp = pb; pb = pc; pc = tp; KeyT tk = kb; kb = kc; kc = tk; swaps++; }
-        if (kb > ka) { int tp = pa; pa = pb; pb = tp; KeyT tk = ka; ka = kb; kb = tk; swaps++; }
-        km = kb;
-        return pb;
-      };
-      KeyT ki, kj, kk;
+      int pa = adj ? base - 1 : base, pb = base, pc = adj ? base + 1 : base;
+      KeyT ka = key[pa], kb = key[pb], kc = key[pc];
+      int sw = 0;
       if (adj) {
-        i = med(i - 1, kv(0), i, kv(1), i + 1, kv(2), ki);
-        j = med(j - 1, kv(3), j, kv(4), j + 1, kv(5), kj);
-        k = med(k - 1, kv(6), k, kv(7), k + 1, kv(8), kk);
-      } else {
-        ki = kv(0);
-        kj = kv(1);
-        kk = kv(2);
+        auto o2 = [&](int& p0, KeyT& k0, int& p1, KeyT& k1) {  // order2: less(p1, p0) = k1 > k0
+          const bool x = k1 > k0;
+          const int tp = x ? p1 : p0, tq = x ? p0 : p1;
+          const KeyT tk = x ? k1 : k0, tl = x ? k0 : k1;
+          p0 = tp;
+          p1 = tq;
+          k0 = tk;
+          k1 = tl;
+          sw += x;
+        };
+        o2(pa, ka, pb, kb);
+        o2(pb, kb, pc, kc);
+        o2(pa, ka, pb, kb);
       }
-      KeyT km;
-      j = med(i, ki, j, kj, k, kk, km);
+      // lane g: the median (pb, kb) of its triple and its swap count
+      i = __builtin_amdgcn_readlane(pb, 0);
+      j = __builtin_amdgcn_readlane(pb, 1);
+      k = __builtin_amdgcn_readlane(pb, 2);
+      KeyT ki = rl(kb, 0), kj = rl(kb, 1), kk = rl(kb, 2);
+      if (adj) swaps = __builtin_amdgcn_readlane(sw, 0) + __builtin_amdgcn_readlane(sw, 1) + __builtin_amdgcn_readlane(sw, 2);
+      // median(i, j, k) with Go's order2 sequence
+      if (kj > ki) { int tp = i; i = j; j = tp; KeyT tk = ki; ki = kj; kj = tk; swaps++; }
+      if (kk > kj) { int tp = j; j = k; k = tp; KeyT tk = kj; kj = kk; kk = tk; swaps++; }
+      if (kj > ki) { int tp = i; i = j; j = tp; KeyT tk = ki; ki = kj; kj = tk; swaps++; }
+      pkey = kj;
+    } else {
+      pkey = K(j);
     }
     hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
     return j;
@@ -530,26 +553,29 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
     const int lane = lane_id();
     int cL = 0, cR = 0;
     for (int c0 = lo; c0 < hi; c0 += WAVE) {
+      // exec-free: lanes past hi read position hi-1 and write their (unused) position into posL's
+      // tail, at cL + lane - #R >= the final #L (posL has 64 spare entries)
       const int p = c0 + lane;
       const bool in = p < hi;
-      const KeyT kk = in ? key[p] : (KeyT)0;
-      const bool isR = in && (strict ? kk > P : kk >= P), isL = in && !isR;
-      const uint64_t mR = ballot(isR), mL = ballot(isL);
-      if (isL) posL[cL + mbcnt(mL)] = (uint16_t)p;
-      if (isR) posR[cR + mbcnt(mR)] = (uint16_t)p;
-      cL += popc64(mL);
-      cR += popc64(mR);
+      const KeyT kk = key[in ? p : hi - 1];
+      const bool isR = in && (strict ? kk > P : kk >= P);
+      const uint64_t mR = ballot(isR);
+      const int rR = mbcnt(mR);
+      uint16_t* dst = isR ? posR + (cR + rR) : posL + (cL + lane - rR);
+      *dst = (uint16_t)p;
+      const int nin = hi - c0 < WAVE ? hi - c0 : WAVE;
+      const int nr = popc64(mR);
+      cR += nr;
+      cL += nin - nr;
     }
     wsync<GS>();
     const int np = cL < cR ? cL : cR;
     int t_n = 0;
     for (int t0 = 0; t0 < np; t0 += WAVE) {
-      const int t = t0 + lane;
-      int l = 0, r = 0;
-      if (t < np) {
-        l = posL[t];
-        r = posR[cR - 1 - t];
-      }
+      const int t = t0 + lane;  // t < np + 64 <= n + 64: inside posL; posR index clamped
+      const int l = posL[t];
+      const int ri = cR - 1 - t;
+      const int r = posR[ri > 0 ? ri : 0];
       const bool sw = t < np && l < r;
       const uint64_t m = ballot(sw);
       t_n += popc64(m);
@@ -567,18 +593,17 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
     *T = t_n;
     return cR;
   }
-  __device__ int partition(int a, int b, int pivot, bool& already) const {
+  // P: the pivot's key (choose_pivot)
+  __device__ int partition(int a, int b, int pivot, KeyT P, bool& already) const {
     swap1(a, pivot);
-    const KeyT P = K(a);
     int T;
     const int j = a + pair_partition(a + 1, b, P, true, &T);
     swap1(j, a);
     already = T == 0;
     return j;
   }
-  __device__ int partition_equal(int a, int b, int pivot) const {
+  __device__ int partition_equal(int a, int b, int pivot, KeyT P) const {
     swap1(a, pivot);
-    const KeyT P = K(a);
     int T;
     return a + 1 + pair_partition(a + 1, b, P, false, &T);
   }
@@ -589,7 +614,10 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
     while (a < k && k < b) {
       const int length = b - a;
       if (length <= 12) {
+        PQ_T(i0);
         insertion_sort(a, b);
+        PQ_T(i1);
+        PQ_ADD(2, i1 - i0);
         return;
       }
       if (limit == 0) {
@@ -601,26 +629,40 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
         wsync<GS>();
         return;
       }
+      PQ_T(c0);
       if (!wasBalanced) {
         break_patterns(a, b);
         limit--;
       }
       int hint;
-      int pivot = choose_pivot(a, b, hint);
+      KeyT pk;
+      int pivot = choose_pivot(a, b, hint, pk);
       if (hint == 2) {
         reverse_range(a, b);
         pivot = (b - 1) - (pivot - a);
         hint = 1;
       }
+      PQ_T(c1);
+      PQ_ADD(1, c1 - c0);
       if (wasBalanced && wasPartitioned && hint == 1) {
-        if (partial_insertion_sort(a, b)) return;
+        const bool done = partial_insertion_sort(a, b);
+        PQ_T(c2);
+        PQ_ADD(2, c2 - c1);
+        if (done) return;
+        pk = K(pivot);  // the shifts may have moved another element to the pivot's position
       }
-      if (a > 0 && !less(a - 1, pivot)) {
-        a = partition_equal(a, b, pivot);
+      PQ_T(c3);
+      PQ_ADD(3, 1);
+      if (a > 0 && !(K(a - 1) > pk)) {  // !less(a-1, pivot)
+        a = partition_equal(a, b, pivot, pk);
+        PQ_T(c4);
+        PQ_ADD(0, c4 - c3);
         continue;
       }
       bool already;
-      const int mid = partition(a, b, pivot, already);
+      const int mid = partition(a, b, pivot, pk, already);
+      PQ_T(c5);
+      PQ_ADD(0, c5 - c3);
       wasPartitioned = already;
       const int leftLen = mid - a, rightLen = b - mid, thr = length / 8;
       if (leftLen < rightLen) {

@@ -65,6 +65,9 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int popc64(uint64_t x) { return __popcll(x); }
 
 // number of set bits of m in lanes below this lane
+// this lane's bit of a wave-uniform mask: the mask's SGPR pair is the lane predicate (v_cndmask
+// reads it directly, no shift / compare)
+__device__ __forceinline__ bool lane_on(uint64_t uniform_mask) { return __builtin_amdgcn_inverse_ballot_w64(uniform_mask); }
 __device__ __forceinline__ int mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }

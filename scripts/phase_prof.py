@@ -27,7 +27,9 @@ PROF_LIB = os.path.join(kbuild.HERE, "libkad_prof.so")
 NAMES = ["A_filter", "B_score", "C_normalize", "D_select", "E_output", "n_straddle", "n_select", "sum_feasible",
          "D_select_straddle", "-", "lean_A_filter", "lean_B_score", "lean_D_select", "lean_E_output",
          "lean_n_straddle", "lean_D_select_straddle", "plan_P0_setup", "plan_P1_weights", "plan_P2_plan",
-         "plan_P3_output", "-", "plan_rows"]
+         "plan_P3_output", "-", "plan_rows", "-", "-",
+         "replay_setup", "replay_partition", "replay_pivot", "replay_insertion", "replay_n_partitions",
+         "replay_sum_n"]
 
 
 def main():
@@ -69,6 +71,9 @@ def main():
             continue
         if nm.startswith("plan_P"):
             out[nm + "_cycles_per_row"] = round(v / max(1.0, float(cnt[21])), 1)
+            continue
+        if nm.startswith("replay_"):  # per straddling unit (wide kernel)
+            out[nm + "_per_straddle"] = round(v / max(1.0, float(cnt[14])), 1)
             continue
         if nm.startswith(("A_", "B_", "C_", "D_", "E_", "lean_A", "lean_B", "lean_D", "lean_E")):
             out[nm + "_cycles_per_unit"] = round(v / W, 1)

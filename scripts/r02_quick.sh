@@ -23,4 +23,4 @@ print("C3", d["value"], d["ms_per_step"], d["config"]["stage_ms"])
 print("C2", d["extra"]["c2"]["value"], d["extra"]["c2"]["ms_per_step"], d["extra"]["c2"]["config"]["stage_ms"])
 PY
 run phase 300 python scripts/phase_prof.py --config c3 --units 100000 --out gpurun_out/${tag}_phase_c3.json
-grep -h "lean_[ABDE]\|straddle_cy" gpurun_out/${tag}_phase_c3.json
+grep -h "lean_[ABDE]\|straddle_cy\|replay_" gpurun_out/${tag}_phase_c3.json
