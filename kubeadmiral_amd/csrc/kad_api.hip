@@ -50,7 +50,7 @@ struct kad_ctx {
   size_t cw_cap = 0;
   void* d_defer = nullptr;  // i32[W + 2]: defer_n, work_n, then the defer list
   size_t defer_cap = 0;
-  void* d_wq = nullptr;     // u32[8 * 32]: schedule_wide_kernel work heads
+  void* d_wq = nullptr;     // u32[WQ_HEADS * WQ_STRIDE]: schedule kernels' work heads
   size_t wq_cap = 0;
   // scratch (per-wave slabs for rows that do not fit LDS)
   void* d_scratch = nullptr;
@@ -716,7 +716,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_defer, &c->defer_cap, ((size_t)W + 2) * 4)) return r;
-  if (int r = grow(c, &c->d_wq, &c->wq_cap, 8 * 32 * 4)) return r;
+  if (int r = grow(c, &c->d_wq, &c->wq_cap, (size_t)WQ_HEADS * WQ_STRIDE * 4)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->batch_hdr = h;
   const char* base = static_cast<const char*>(c->d_batch);

@@ -9,6 +9,8 @@
 namespace kad {
 
 constexpr int FITFOLD_MAX_C = 4096;
+// unit work queue of the schedule kernels: WQ_HEADS counters, one 128-B line apart (BatchDev::wq)
+constexpr int WQ_HEADS = 64, WQ_STRIDE = 32;
 constexpr int FIT_FENCES = 256;  // prep_kernel's LDS copy of every (fit_mp / 256)-th fit value
 
 struct SnapDev {
@@ -69,7 +71,7 @@ struct BatchDev {
   int32_t* defer;           // [W] units the lean kernel hands to schedule_kernel
   int32_t* defer_n;         // [1] length of defer
   int32_t* work_n;          // [1] lean kernel work queue: next batch of LEAN_BATCH units
-  uint32_t* wq;             // [8 * 32] schedule_wide_kernel work heads (reset by prep_kernel)
+  uint32_t* wq;             // [WQ_HEADS * WQ_STRIDE] schedule kernels' work heads (reset by prep_kernel)
 };
 
 // Per-unit record, rebuilt by prep_kernel at every kad_schedule: the fixed-size

@@ -783,7 +783,6 @@ __device__ __forceinline__ int2 fit_ranks(const SnapDev& s, const int64_t (*fenc
   return make_int2(b0, b1);
 }
 
-constexpr int WQ_HEADS_PREP = 8, WQ_STRIDE_PREP = 32;  // = WQ_HEADS, WQ_STRIDE (schedule_wide_kernel)
 constexpr int PREP_CPL = 4;                            // chunks per lane
 __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
   constexpr int CPL = PREP_CPL;
@@ -795,7 +794,7 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
     *b.defer_n = 0;
     *b.work_n = 0;
   }
-  if (g < (uint32_t)WQ_HEADS_PREP) b.wq[g * WQ_STRIDE_PREP] = 0u;  // schedule_wide_kernel's work heads
+  if (g < (uint32_t)WQ_HEADS) b.wq[g * WQ_STRIDE] = 0u;  // the schedule kernels' work heads
   const bool live = g < (uint32_t)b.W * per;
   const uint32_t w = live ? g / per : 0u, l = g - w * per, ch0 = l * CPL;
   // the unit's lanes load its program words 0 .. CPL*per-1 with coalesced
@@ -884,6 +883,69 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   }
 }
 
+// ====================================================== unit work queue
+constexpr int WQ_BATCH = 4;  // units per dequeue
+static_assert(WQ_HEADS == 64, "drained-head set is one u64; heads map to XCDs by h & 7");
+// Work queue: WQ_HEADS = 64 heads; head h hands out the batches of the h-th contiguous 64th of the
+// units. 64 counters (not 8) spread the returning atomics over as many lines: the device-scope
+// atomics of 8 XCDs on a few addresses serialise. A wave of block b starts at head b & 63 (blocks go
+// round-robin over the 8 XCDs, so head h is started by XCD h & 7) and, when it is drained, moves to
+// the next head of its own XCD (h + 8, h + 16, ...) that still has batches, then to any other. A ticket is one
+// returning atomicAdd (lane 0), resolved into a batch one batch later, so its latency hides behind a
+// batch of work. Every wave's first batch is static (no atomic): wave wv of block b takes batch
+// (b >> 6) * wpb + wv of head b & 63, and that head's atomics count on from its static_batches.
+// Every wave ends once all heads are drained.
+struct WorkTicket {
+  int x;             // head of the pending ticket
+  int i;             // its atomicAdd result (lane 0); batch index = i + static_batches(x)
+  int wpb, nblocks;  // waves per block, grid size: the static first round
+};
+// the static first-round batches of head x: one per wave of every block b < nblocks with b & 63 == x
+__device__ __forceinline__ int static_batches(const WorkTicket& t, int x) { return t.wpb * ((t.nblocks - x + 63) >> 6); }
+__device__ __forceinline__ WorkTicket wq_start(int wpb) {
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  WorkTicket t{(int)(blockIdx.x & (WQ_HEADS - 1)), 0, wpb, (int)gridDim.x};
+  t.i = (int)(blockIdx.x >> 6) * wpb + wv - static_batches(t, t.x);
+  return t;
+}
+__device__ __forceinline__ void wq_issue(uint32_t* heads, WorkTicket& t) {
+  if (lane_id() == 0) t.i = (int)atomicAdd(heads + t.x * WQ_STRIDE, 1u);
+}
+__device__ __forceinline__ int wq_head_batches(int W, int x) {
+  const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
+  return (s1 - s0 + WQ_BATCH - 1) / WQ_BATCH;
+}
+// the batch [first, first + count) of a ticket; count 0 = queue drained. A drained head costs one
+// wave-wide look at all 64 counters (lane l loads head l, device-coherent) and one atomic on a head
+// that still has batches — not a walk over the heads with one atomic round trip each.
+__device__ __forceinline__ int2 wq_resolve(uint32_t* heads, int W, WorkTicket& t) {
+  const int lane = lane_id();
+  for (;;) {
+    const int x = t.x;
+    const int bi = __builtin_amdgcn_readfirstlane(t.i) + static_batches(t, x);
+    if (bi < wq_head_batches(W, x)) {
+      const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
+      const int first = s0 + bi * WQ_BATCH;
+      return make_int2(first, (s1 - first) < WQ_BATCH ? (s1 - first) : WQ_BATCH);
+    }
+    const uint32_t taken = __hip_atomic_load(heads + lane * WQ_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t open = ballot((int)taken + static_batches(t, lane) < wq_head_batches(W, lane));
+    if (!open) return make_int2(0, 0);
+    // same XCD first (heads x & 7 + 8j), in rotation order after x; then the lowest open head
+    const uint64_t same = open & (0x0101010101010101ull << (x & 7));
+    int nx;
+    if (same) {
+      const int sh = (x + 1) & 63;
+      const uint64_t rot = sh ? (same >> sh) | (same << (64 - sh)) : same;
+      nx = (x + 1 + __builtin_ctzll(rot)) & 63;
+    } else {
+      nx = __builtin_ctzll(open);
+    }
+    t.x = nx;
+    if (lane == 0) t.i = (int)atomicAdd(heads + nx * WQ_STRIDE, 1u);
+  }
+}
+
 // ================================================= lean schedule kernel
 // schedule_lean_kernel<NCH, CL> — the common case, used whenever C fits the
 // per-wave LDS budget (fast_path). Each wave owns a run of consecutive units.
@@ -909,6 +971,7 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
 // feasible clusters, go to the defer list and schedule_kernel afterwards.
 constexpr int LEAN_QMAX_DYN = 4;
 constexpr int LEAN_BATCH = 4;  // units per work-queue batch (one VGPR of UnitRecs)
+static_assert(LEAN_BATCH == WQ_BATCH, "the lean kernel dequeues WQ_BATCH units per ticket");
 __host__ __device__ constexpr int lean_qmax(int nch_t) { return nch_t > 0 ? nch_t : LEAN_QMAX_DYN; }
 // cached attributes: alloc/used cpu & mem, NS|NE taints, GVK word 0 (always),
 // NE taints (taint filter and some unit has CurrentClusters), PNS taints (TaintToleration score)
@@ -922,9 +985,10 @@ __host__ __device__ inline LeanLayout lean_layout(int C, int qmax) {
   LeanLayout L;
   L.key = 0;                     // u32[P] replay keys (total - row minimum)
   L.idx = L.key + 4 * P;         // u16[P] feasible position → cluster id (NCH > 0: P = Cp)
-  L.pid = L.idx + 2 * P;         // u16[P] replay: original position at each position
-  L.posl = L.pid + 2 * P;        // u16[P] replay scratch (partition stoppers; then ranks)
-  L.posr = L.posl + 2 * P + 128; // u16[P] (posl: P + 64 entries, PdqWave)
+  L.posl = L.idx;                // u16[P + 64] replay scratch (partition stoppers; then ranks): idx is
+                                 // dead once the scores have read the cluster ids into registers
+  L.pid = L.idx + 2 * P + 128;   // u16[P] replay: original position at each position
+  L.posr = L.pid + 2 * P;        // u16[P]
   L.bytes = (L.posr + 2 * P + 15) & ~(size_t)15;
   return L;
 }
@@ -1070,41 +1134,42 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   // lanes 2*(u*nch+ch)+{0,1} of svv) and read per unit with v_readlane: no
   // scalar or vector memory round trip per unit (an SMEM load would be
   // waited by the next LDS wait; a vector load by the last unit's stores).
-  // Each wave owns a contiguous share of the units; the grid is the resident
-  // wave count (launch_schedule), so every wave runs from start to finish
-  // concurrently and shares differ by at most one unit. Records are loaded
-  // in batches of LEAN_BATCH units.
+  // Units are dequeued in batches of LEAN_BATCH from the work heads (WorkTicket: one returning atomicAdd
+  // per batch, resolved one batch later); the grid is the resident wave count (launch_schedule) and
+  // every wave runs until all heads are drained, so no wave idles on a static share while others work.
   const UnitRec* recs = largs()->b.rec;
   const uint64_t* sws = largs()->b.sw;
-  int w, wend;
-  {
-    LArgs a = largs();
-    const long G = (long)gridDim.x * a->waves_per_block;
-    const long gw = (long)blockIdx.x * a->waves_per_block + wv;
-    w = (int)(W * gw / G) - 1;
-    wend = (int)(W * (gw + 1) / G);
-  }
+  uint32_t* heads = largs()->b.wq;
+  WorkTicket tk = wq_start((int)(blockDim.x >> 6));
   // the next batch's records are loaded one batch ahead (nrvA/nsvv): the
   // wait at a batch start then only covers the previous unit's stores
   uint32_t rvA = 0, svv = ~0u, nrvA = 0, nsvv = ~0u;
-  auto fetch = [&](int wb) {
-    const int nb = (wb + LEAN_BATCH < wend ? wb + LEAN_BATCH : wend) - wb;
+  auto fetch = [&](int wb, int nb) {
     nrvA = lane < nb * 16 ? ldg((const uint32_t*)(recs + wb), (uint32_t)lane) : 0u;
     if (NCH > 0 && f_sw) nsvv = lane < nb * 2 * nch ? ldg((const uint32_t*)(sws + (size_t)wb * nch), (uint32_t)lane) : ~0u;
   };
-  fetch(w + 1);
-  int w1 = w + 1, u = 0;
+  int2 cb = wq_resolve(heads, W, tk);  // the static first batch; then the ticket of the one after
+  if (cb.y > 0) {
+    wq_issue(heads, tk);
+    fetch(cb.x, cb.y);
+  }
+  int w = -1, bend = 0, u = 0;
   KAD_PACC;
   for (;;) {
     ++w;
     ++u;
-    if (w >= wend) break;
-    if (w >= w1) {  // next batch
-      w1 = w + LEAN_BATCH < wend ? w + LEAN_BATCH : wend;
+    if (w >= bend) {  // next batch
+      if (cb.y <= 0) break;
+      w = cb.x;
+      bend = cb.x + cb.y;
+      u = 0;
       rvA = nrvA;
       svv = nsvv;
-      fetch(w1);
-      u = 0;
+      cb = wq_resolve(heads, W, tk);
+      if (cb.y > 0) {
+        wq_issue(heads, tk);
+        fetch(cb.x, cb.y);
+      }
     }
     KAD_PT(t0);
     auto fld = [&](int d) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)rvA, (u << 4) + d); };
@@ -1619,9 +1684,6 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 constexpr int WIDE_Q = 8;
 constexpr int WIDE_P = WIDE_Q * 64;
 constexpr int WIDE_MAX_NCH = 16;
-constexpr int WQ_BATCH = 4;          // units per dequeue
-constexpr int WQ_HEADS = WQ_HEADS_PREP;    // work heads, one 128-B line each
-constexpr int WQ_STRIDE = WQ_STRIDE_PREP;  // u32 words between heads
 constexpr int WIDE_THREADS = 1024;
 
 struct WideLayout {
@@ -1631,14 +1693,15 @@ __host__ __device__ inline WideLayout wide_layout() {
   WideLayout L;
   L.key = 0;                      // u32[P] replay keys / histogram
   L.idx = L.key + 4 * WIDE_P;     // u16[P] position -> cluster id
-  L.pid = L.idx + 2 * WIDE_P;     // u16[P] replay: original position
-  L.posl = L.pid + 2 * WIDE_P;    // u16[P] replay scratch, then ranks
-  L.posr = L.posl + 2 * WIDE_P + 128;  // u16[P] (posl: P + 64 entries, PdqWave)
+  L.posl = L.idx;                 // u16[P + 64] replay scratch, then ranks (idx is dead by then: the
+                                  // cluster ids are in registers)
+  L.pid = L.idx + 2 * WIDE_P + 128;  // u16[P] replay: original position
+  L.posr = L.pid + 2 * WIDE_P;    // u16[P]
   L.bytes = L.posr + 2 * WIDE_P;
   return L;
 }
 // the compaction stores every feasible cluster's id at its position, even past P (up to 64*nch):
-// those land in pid / posl of the same wave's region and the unit is deferred
+// those land in pid / posr of the same wave's region and the unit is deferred
 static_assert(2 * 64 * WIDE_MAX_NCH <= 6 * WIDE_P, "idx overflow past P must stay in the wave's region");
 // block-shared cluster cache: av (f64 x2), tg (u64 x2: NS|NE taints, GVK word),
 // cap (f64 x2), iv (f32 x2), [ne u64], [pn u64]
@@ -1660,52 +1723,6 @@ struct WideArgs {
 typedef const __attribute__((address_space(4))) WideArgs* WArgs;
 __device__ __forceinline__ WArgs wargs() {
   return (WArgs)opq((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
-}
-
-// Work queue: WQ_HEADS heads, head x hands out the batches of the x-th
-// contiguous eighth of the units. A ticket is one returning atomicAdd on a
-// head (issued by lane 0); it is resolved into a batch one batch later, so
-// the atomic's latency hides behind a unit's work. A drained head sends the
-// wave to the next head that is not drained (synchronous retries: only at the
-// end of the queue). Every wave ends once all heads are drained.
-struct WorkTicket {
-  int x;        // head of the pending ticket
-  uint32_t i;   // its atomicAdd result (lane 0)
-  uint32_t drained;
-};
-__device__ __forceinline__ void wq_issue(uint32_t* heads, WorkTicket& t) {
-  if (lane_id() == 0) t.i = atomicAdd(heads + t.x * WQ_STRIDE, 1u);
-}
-// the batch [first, first + count) of a ticket; count 0 = queue drained
-__device__ __forceinline__ int2 wq_resolve(uint32_t* heads, int W, WorkTicket& t) {
-  int first = 0, count = 0;
-  if (lane_id() == 0) {
-    for (int tries = 0; tries < WQ_HEADS; ++tries) {
-      const int x = t.x;
-      const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
-      const int nb = (s1 - s0 + WQ_BATCH - 1) / WQ_BATCH;
-      if ((int)t.i < nb) {
-        first = s0 + (int)t.i * WQ_BATCH;
-        count = (s1 - first) < WQ_BATCH ? (s1 - first) : WQ_BATCH;
-        break;
-      }
-      t.drained |= 1u << x;
-      int nx = -1;
-      for (int u = 1; u < WQ_HEADS; ++u) {
-        const int y = (x + u) & (WQ_HEADS - 1);
-        if (!((t.drained >> y) & 1)) {
-          nx = y;
-          break;
-        }
-      }
-      if (nx < 0) break;
-      t.x = nx;
-      t.i = atomicAdd(heads + nx * WQ_STRIDE, 1u);
-    }
-  }
-  first = __builtin_amdgcn_readfirstlane(__shfl(first, 0));
-  count = __builtin_amdgcn_readfirstlane(__shfl(count, 0));
-  return make_int2(first, count);
 }
 
 __device__ __forceinline__ void wide_status(int w, int32_t st) {
@@ -1803,7 +1820,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     recs = a->b.rec;
     sws = a->b.sw;
   }
-  WorkTicket tk{(int)(blockIdx.x & (WQ_HEADS - 1)), 0u, 0u};
+  WorkTicket tk = wq_start(nwaves);
   // one VGPR per unit: lanes 0-15 its UnitRec dwords, lanes 16..16+2*nch its static filter words
   auto fetch = [&](int w) -> uint32_t {
     if (w < 0) return 0u;
@@ -1811,9 +1828,8 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     if (lane < 16 + 2 * nch) return ldg((const uint32_t*)(sws + (size_t)w * nch), (uint32_t)(lane - 16));
     return 0u;  // chunks past nch: nothing feasible
   };
-  wq_issue(heads, tk);
-  int2 cb = wq_resolve(heads, W, tk);
-  if (cb.y > 0) wq_issue(heads, tk);  // the next batch's ticket, resolved when this batch ends
+  int2 cb = wq_resolve(heads, W, tk);  // the static first batch
+  if (cb.y > 0) wq_issue(heads, tk);   // the next batch's ticket, resolved when this batch ends
   int w = cb.y > 0 ? cb.x : -1;
   uint32_t cur = fetch(w);
   int bend = cb.x + cb.y;
