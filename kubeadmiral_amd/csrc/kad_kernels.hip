@@ -78,6 +78,21 @@ __host__ __device__ inline RowLayout row_layout(int C) {
   return L;
 }
 size_t select_wave_bytes(int C) { return row_layout(C).bytes; }
+// GSCR rows (state in a global slab): the small per-wave arrays that take atomics — selection, placement
+// and current-cluster bitmaps, the radix histogram — stay in LDS (dynamic LDS of the 1-wave blocks)
+struct SmallLayout {
+  size_t sel, place, cur, hist, bytes;
+};
+__host__ __device__ inline SmallLayout small_layout(int C) {
+  const size_t nw = (size_t)((C + 63) / 64);
+  SmallLayout L;
+  L.sel = 0;
+  L.place = 8 * nw;
+  L.cur = 16 * nw;
+  L.hist = 24 * nw;
+  L.bytes = L.hist + 4 * 256;
+  return L;
+}
 
 // ---------------------------------------------------------- predicate programs
 // labels.Requirement.Matches / fields one-term selectors (apimachinery v0.26.6)
@@ -377,10 +392,11 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
   uint32_t* fx = (uint32_t*)(region + L.fx);
   uint16_t* idx = (uint16_t*)(region + L.idx);
   uint16_t* perm = (uint16_t*)(region + L.perm);
-  uint64_t* selb = (uint64_t*)(region + L.sel);
-  uint64_t* plb = (uint64_t*)(region + L.place);
-  uint64_t* curb = (uint64_t*)(region + L.cur);
-  uint32_t* hist = (uint32_t*)(region + L.hist);
+  const SmallLayout SL = small_layout(C);
+  uint64_t* selb = (uint64_t*)(GSCR ? smem + SL.sel : region + L.sel);
+  uint64_t* plb = (uint64_t*)(GSCR ? smem + SL.place : region + L.place);
+  uint64_t* curb = (uint64_t*)(GSCR ? smem + SL.cur : region + L.cur);
+  uint32_t* hist = (uint32_t*)(GSCR ? smem + SL.hist : region + L.hist);
   uint16_t* posl = (uint16_t*)(region + L.posl);
   uint16_t* posr = (uint16_t*)(region + L.posr);
   const int nch = (C + 63) >> 6;
@@ -1486,10 +1502,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       for (int q = 0; q < Q; ++q) {
         const int r = n - q * 64;
         vm[q] = q < nq ? (r >= 64 ? ~0ull : ((1ull << r) - 1)) : 0ull;
-        if ((vm[q] >> lane) & 1) {
-          mn = t[q] < mn ? t[q] : mn;
-          mx = t[q] > mx ? t[q] : mx;
-        }
+        const bool vq = lane_on(vm[q]);
+        mn = (vq && t[q] < mn) ? t[q] : mn;
+        mx = (vq && t[q] > mx) ? t[q] : mx;
       }
       // k-th largest total T: the largest T with #(total >= T) >= k, by
       // bisection over [min, max] — in 32 bits when every total fits (the
@@ -1513,7 +1528,10 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           wave_sync();
 #pragma unroll
           for (int q = 0; q < Q; ++q)
-            if ((vm[q] >> lane) & 1) atomicAdd(hist + (127 - (t32[q] - mn32)), 1u);
+            if (q < nq) {  // exec-free: lanes past n add 0 to bin 127
+              const bool vq = lane_on(vm[q]);
+              atomicAdd(hist + (vq ? 127 - (t32[q] - mn32) : 127), vq ? 1u : 0u);
+            }
           wave_sync();
           const uint2 hh = *(const uint2*)(hist + 2 * lane);  // bins 127-2l, 126-2l
           const int pre = wave_incl_sum_i32((int)(hh.x + hh.y));  // #(total >= mn + 126 - 2l)
@@ -2047,9 +2065,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         int mn = INT32_MAX, mx = INT32_MIN;
 #pragma unroll
         for (int q = 0; q < Q; ++q)
-          if (q < nq && q * 64 + lane < n) {
-            mn = t[q] < mn ? t[q] : mn;
-            mx = t[q] > mx ? t[q] : mx;
+          if (q < nq) {
+            const bool vq = q * 64 + lane < n;
+            mn = (vq && t[q] < mn) ? t[q] : mn;
+            mx = (vq && t[q] > mx) ? t[q] : mx;
           }
         int mn32, mx32;
         wave_minmax_u_i32(mn, mx, mn32, mx32);
@@ -2061,7 +2080,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           wave_sync();
 #pragma unroll
           for (int q = 0; q < Q; ++q)
-            if (q < nq && q * 64 + lane < n) atomicAdd(hist + (127 - (t[q] - mn32)), 1u);
+            if (q < nq) {  // exec-free: lanes past n add 0 to bin 127
+              const bool vq = q * 64 + lane < n;
+              atomicAdd(hist + (vq ? 127 - (t[q] - mn32) : 127), vq ? 1u : 0u);
+            }
           wave_sync();
           const uint2 hh = *(const uint2*)(hist + 2 * lane);  // bins 127-2l, 126-2l
           const int pre = wave_incl_sum_i32((int)(hh.x + hh.y));
@@ -2272,17 +2294,23 @@ __device__ __forceinline__ int find_sorted(const int32_t* a, int lo, int hi, int
   return -1;
 }
 
-template <bool GSCR>
-__global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev o, const int32_t* rows, int n_rows,
-                                                  int kmax, char* gscratch, int wave_bytes, int r_stride, int tbl_cp) {
+// LANES: rows of K <= 64 only, the planner in registers (8 waves / SIMD: <= 64 VGPRs); else rows of
+// K > 64 only, with the LDS / global-scratch workspace (GSCR). launch_plan runs the first and, when
+// some row may exceed 64 clusters, the second; each skips the other's rows.
+template <bool GSCR, bool LANES>
+__global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, BatchDev b, OutDev o, const int32_t* rows,
+                                                                 int n_rows, int kmax, char* gscratch, int wave_bytes,
+                                                                 int r_stride, int tbl_cp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   const int gw = blockIdx.x;
+  // LDS: the row workspace of rows with K > 64 (kmax > 64 only), then the lookup tables
   char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem;
+  const size_t ws_bytes = (GSCR || LANES || kmax <= WAVE) ? 0 : plan_layout(kmax).bytes;
   // cluster id → (preference / current-cluster index + 1) lookup tables in LDS
   // (tbl_cp > 0), set and cleared per unit: replaces two binary searches in
   // global memory per selected cluster
-  uint16_t* tbl_p = (uint16_t*)(smem + plan_layout(kmax).bytes);
+  uint16_t* tbl_p = (uint16_t*)(smem + ws_bytes);
   uint16_t* tbl_c = tbl_p + tbl_cp;
   const bool use_tbl = !GSCR && tbl_cp > 0;
   if (use_tbl) {
@@ -2290,9 +2318,11 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
     wsync<GSCR>();
   }
   KAD_PACC;
+  int wn = gw < n_rows ? rows[gw] : 0;  // the next row's unit, loaded one row ahead
   for (int r = gw; r < n_rows; r += r_stride) {
     KAD_PT(t0);
-    const int w = rows[r];
+    const int w = wn;
+    if (r + r_stride < n_rows) wn = rows[r + r_stride];
     // every per-unit scalar is loaded before the status test so the loads
     // issue together (one memory round trip instead of three dependent ones;
     // w < W, so each index is in bounds whatever the status)
@@ -2304,8 +2334,8 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
     const int c0 = b.cur_off[w], c1 = b.cur_off[w + 1];
     const int ko0 = b.key_off[w], ko1 = b.key_off[w + 1];
     const int64_t desired = b.desired[w];
-    if (st != KAD_ST_OK || K <= 0) continue;
-    PlanWs ws = plan_ws(region, K);
+    const uint32_t rflags0 = o.flags[w];
+    if (st != KAD_ST_OK || K <= 0 || (K <= WAVE) != LANES) continue;
     const uint8_t* key = b.key + ko0;
     const int klen = ko1 - ko0;
     const int64_t total = (f & KAD_W_HAS_DESIRED) ? desired : 0;
@@ -2318,10 +2348,9 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
     // su.Key() bytes in lanes (uniform): the FNV-1 continuation of every element
     // reads them with v_readlane instead of one dependent load per byte
     const uint32_t kb0 = lane < klen ? (uint32_t)key[lane] : 0u;
-    for (int i0 = 0; i0 < K; i0 += WAVE) {
-      const int i = i0 + lane;
-      const bool v = i < K;
-      const int c = v ? o.cluster[off + i] : 0;
+    // element i: cluster id, hash, preference columns, current replicas
+    auto gather = [&](int i, int& c, PlanLane& e) {
+      c = o.cluster[off + i];
       uint32_t h = s.name_fnv[c];
       for (int k0 = 0; k0 < klen; k0 += WAVE) {
         const uint32_t kb = k0 == 0 ? kb0 : (k0 + lane < klen ? (uint32_t)key[k0 + lane] : 0u);
@@ -2331,41 +2360,124 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
           h ^= (uint32_t)__builtin_amdgcn_readlane((int)kb, q);
         }
       }
-      if (v) {
-        ws.cid[i] = c;
-        ws.hash[i] = h;
-        int pi, ci;
-        if (use_tbl) {
-          const int tp = tbl_p[c], tc = tbl_c[c];
-          pi = tp ? p0 + tp - 1 : -1;
-          ci = tc ? c0 + tc - 1 : -1;
+      e.hash = h;
+      int pi, ci;
+      if (use_tbl) {
+        const int tp = tbl_p[c], tc = tbl_c[c];
+        pi = tp ? p0 + tp - 1 : -1;
+        ci = tc ? c0 + tc - 1 : -1;
+      } else {
+        pi = find_sorted(b.pref_id, p0, p1, c);
+        ci = find_sorted(b.cur_id, c0, c1, c);
+      }
+      e.fl = 0;
+      e.w = e.mn = e.mx = e.cap = 0;
+      if (pi >= 0) {
+        // all five columns in one round trip (pi is in bounds), flags select after
+        const uint32_t pf = b.pref_fl[pi];
+        const int64_t pw = b.pref_w[pi], pmx = b.pref_max[pi], pcp = b.pref_cap[pi];
+        e.mn = b.pref_min[pi];
+        if (pf & KAD_PREF_HAS_WEIGHT) e.w = pw;
+        if (pf & KAD_PREF_HAS_MAX) {
+          e.fl |= EF_HAS_MAX;
+          e.mx = pmx;
+        }
+        if (pf & KAD_PREF_HAS_CAP) {
+          e.fl |= EF_HAS_CAP;
+          e.cap = pcp;
+        }
+      }
+      e.cur = ci >= 0 ? b.cur_rep[ci] : 0;
+    };
+    const bool avoid = f & KAD_W_AVOID_DISRUPTION;
+    const bool keep = f & KAD_W_KEEP_UNSCHED;
+    uint32_t rflags = rflags0;
+    if constexpr (LANES) {
+      // ---------------- one element per lane, the planner in registers (kad_plan.h plan_row_lanes)
+      const bool v = lane < K;
+      // every lane runs the gather (its FNV loop reads the key bytes of all lanes with v_readlane, so the
+      // lanes that hold them must be live); lanes past K take element 0 and are masked off
+      int c = 0;
+      PlanLane e;
+      gather(v ? lane : 0, c, e);
+      if (!v) {
+        e = PlanLane{0, 0, 0, 0, 0, 0u, 0u};
+        c = 0;
+      }
+      if (use_tbl) {
+        wsync<GSCR>();
+        for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = 0;
+        for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = 0;
+        wsync<GSCR>();
+      }
+      KAD_PT(t1);
+      KAD_PADD(0, t1 - t0);
+      KAD_PADD(5, 1);
+      if (f & KAD_W_DYNAMIC_WEIGHTS) {
+        // CalcWeightLimit (rsp.go:183-213) + AvailableToPercentage (rsp.go:215-272)
+        const int64_t ac = v ? s.alloc_cores[c] : 0, av = v ? s.avail_cores[c] : 0;
+        const double sum = wave_sum_f64(v ? (double)ac : 0.0);
+        const double suma = wave_sum_f64((v && av > 0) ? (double)av : 0.0);
+        if (suma == 0) {
+          e.w = v ? go_f2i(round(1000.0 / (double)K)) : 0;
         } else {
-          pi = find_sorted(b.pref_id, p0, p1, c);
-          ci = find_sorted(b.cur_id, c0, c1, c);
-        }
-        uint32_t fl = 0;
-        int64_t wt = 0, mn = 0, mx = 0, cp = 0;
-        if (pi >= 0) {
-          // all five columns in one round trip (pi is in bounds), flags select after
-          const uint32_t pf = b.pref_fl[pi];
-          const int64_t pw = b.pref_w[pi], pmx = b.pref_max[pi], pcp = b.pref_cap[pi];
-          mn = b.pref_min[pi];
-          if (pf & KAD_PREF_HAS_WEIGHT) wt = pw;
-          if (pf & KAD_PREF_HAS_MAX) {
-            fl |= EF_HAS_MAX;
-            mx = pmx;
-          }
-          if (pf & KAD_PREF_HAS_CAP) {
-            fl |= EF_HAS_CAP;
-            cp = pcp;
+          const int64_t lim = sum == 0 ? go_f2i(round(1000.0 / (double)K))
+                                       : go_f2i(round((double)ac / sum * 1000.0 * 1.4));
+          const double avd = av < 0 ? 0.0 : (double)av;
+          int64_t wt = go_f2i(round(avd / suma * 1000.0));
+          if (wt > lim) wt = lim;
+          const int64_t sumtmp = wave_sum_i64(v ? wt : 0);
+          wt = go_f2i(round((double)wt / (double)sumtmp * 1000.0));
+          const int64_t other = wave_sum_i64(v ? wt : 0);
+          const int64_t maxw = wave_max_i64(v ? wt : 0);
+          e.w = v ? wt : 0;
+          if (maxw > 0) {  // remainder → first strict maximum (lowest cluster id among ties)
+            const uint64_t tm = ballot(v && wt == maxw);
+            const int first = (int)__builtin_ctzll(tm);
+            if (popc64(tm) > 1) rflags |= KAD_RF_REMAINDER_TIE;
+            if (lane == first) e.w = wadd(e.w, wsub(1000, other));
           }
         }
-        ws.w[i] = wt;
-        ws.mn[i] = mn;
-        ws.mx[i] = mx;
-        ws.cap[i] = cp;
-        ws.fl[i] = fl;
-        ws.cur[i] = ci >= 0 ? b.cur_rep[ci] : 0;
+      }
+      KAD_PT(t2);
+      KAD_PADD(1, t2 - t1);
+      PlanOut po;
+      rflags |= plan_row_lanes(e, K, total, avoid, keep, po);
+      KAD_PT(t3);
+      KAD_PADD(2, t3 - t2);
+      // result = plan + overflow, zeros dropped (rsp.go:162-179), ascending cluster id
+      const int64_t rr = v ? wadd(po.plan, (po.ofl & EF_HAS_OVER) ? po.over : 0) : 0;
+      const bool nz = v && rr != 0;
+      const uint64_t m = ballot(nz);
+      if (nz) {
+        const int64_t at = off + mbcnt(m);
+        o.cluster[at] = c;
+        o.replicas[at] = rr;
+      }
+      if (lane == 0) {
+        o.count[w] = popc64(m);
+        o.flags[w] = rflags;
+      }
+      KAD_PT(t4);
+      KAD_PADD(3, t4 - t3);
+      continue;
+    } else {
+    // ---------------- K > 64: the row state in the LDS / global-scratch workspace (kad_plan.h plan_row)
+    PlanWs ws = plan_ws(region, K);
+    for (int i0 = 0; i0 < K; i0 += WAVE) {
+      const int i = i0 + lane;
+      int c;
+      PlanLane e;
+      gather(i < K ? i : 0, c, e);  // every lane (see the K <= 64 path)
+      if (i < K) {
+        ws.cid[i] = c;
+        ws.hash[i] = e.hash;
+        ws.w[i] = e.w;
+        ws.mn[i] = e.mn;
+        ws.mx[i] = e.mx;
+        ws.cap[i] = e.cap;
+        ws.fl[i] = e.fl;
+        ws.cur[i] = e.cur;
       }
     }
     wsync<GSCR>();
@@ -2377,7 +2489,6 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
     KAD_PT(t1);
     KAD_PADD(0, t1 - t0);
     KAD_PADD(5, 1);
-    uint32_t rflags = o.flags[w];
     if (f & KAD_W_DYNAMIC_WEIGHTS) {
       // CalcWeightLimit (rsp.go:183-213) + AvailableToPercentage (rsp.go:215-272)
       double sum = 0.0, suma = 0.0;
@@ -2435,8 +2546,6 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
       }
       wsync<GSCR>();
     }
-    const bool avoid = f & KAD_W_AVOID_DISRUPTION;
-    const bool keep = f & KAD_W_KEEP_UNSCHED;
     KAD_PT(t2);
     KAD_PADD(1, t2 - t1);
     rflags |= plan_row<GSCR>(ws, K, total, avoid, keep);
@@ -2464,6 +2573,7 @@ __global__ __launch_bounds__(64) void plan_kernel(SnapDev s, BatchDev b, OutDev 
     wsync<GSCR>();
     KAD_PT(t4);
     KAD_PADD(3, t4 - t3);
+    }
   }
   KAD_PFLUSH_PLAN;
 }
@@ -2524,13 +2634,34 @@ __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32
 }
 
 template <bool GSCR>
-__global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscratch, int wave_bytes, int r_stride) {
+__global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscratch, int wave_bytes, int r_stride,
+                                                       int force_ws) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   char* region = GSCR ? gscratch + (size_t)blockIdx.x * wave_bytes : smem;
   for (int r = blockIdx.x; r < R.n_rows; r += r_stride) {
     const int a = R.row_off[r], K = R.row_off[r + 1] - a;
     if (K <= 0) continue;
+    if (K <= WAVE && !force_ws) {  // the register planner (plan_kernel's path for K <= 64)
+      const bool v = lane < K;
+      PlanLane e{0, 0, 0, 0, 0, 0u, 0u};
+      if (v) {
+        e.hash = R.hash[a + lane];
+        e.w = R.weight[a + lane];
+        e.mn = R.min_r[a + lane];
+        e.mx = R.max_r[a + lane];
+        e.cap = R.cap[a + lane];
+        e.cur = R.current[a + lane];
+        e.fl = R.elem_flags[a + lane] & (EF_HAS_MAX | EF_HAS_CAP);
+      }
+      PlanOut po;
+      plan_row_lanes(e, K, R.total[r], R.row_flags[r] & 1, (R.row_flags[r] >> 1) & 1, po);
+      if (v) {
+        R.out_plan[a + lane] = po.plan;
+        R.out_overflow[a + lane] = (po.ofl & EF_HAS_OVER) ? po.over : -1;
+      }
+      continue;
+    }
     PlanWs ws = plan_ws(region, K);
     for (int i = lane; i < K; i += WAVE) {
       ws.cid[i] = i;
@@ -2650,7 +2781,7 @@ static hipError_t launch_defer_pass(const SnapDev& s, const BatchDev& b, const O
     if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
     if (slots > (size_t)b.W) slots = b.W;
     const SchedArgs A2{s, b, o, p, (char*)gscr, (int)wb, 1, (int)slots, b.defer, b.defer_n};
-    hipLaunchKernelGGL(schedule_kernel<true>, dim3((int)slots), dim3(64), 0, st, A2);
+    hipLaunchKernelGGL(schedule_kernel<true>, dim3((int)slots), dim3(64), small_layout(s.C).bytes, st, A2);
   }
   return hipGetLastError();
 }
@@ -2749,7 +2880,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (slots > (size_t)b.W) slots = b.W;
     const int grid = (int)slots;
     const SchedArgs A{s, b, o, p, (char*)gscr, (int)wb, 1, grid, nullptr, nullptr};
-    hipLaunchKernelGGL(schedule_kernel<true>, dim3(grid), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(schedule_kernel<true>, dim3(grid), dim3(64), small_layout(s.C).bytes, st, A);
   }
   return hipGetLastError();
 }
@@ -2759,21 +2890,40 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   (void)p;
   if (n_rows == 0 || kmax <= 0) return hipSuccess;
-  const size_t wb = plan_layout(kmax).bytes;
   const int cp = (s.C + 63) & ~63;
+  // persistent grid: the resident block count, rows round-robin (r += grid)
+  auto persistent = [&](const void* fn, size_t lds) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess || per_cu < 1) per_cu = 8;
+    long grid = (long)n_cus() * per_cu;
+    return (int)(grid > n_rows ? n_rows : grid);
+  };
+  // rows of K <= 64: the register planner, lookup tables only in LDS (4 B per cluster)
+  {
+    const int tbl_cp = cp <= 1024 ? cp : 0;
+    const size_t lds = (size_t)tbl_cp * 4;
+    const int grid = persistent((const void*)plan_kernel<false, true>, lds);
+    hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows, kmax,
+                       (char*)nullptr, 0, grid, tbl_cp);
+    if (hipError_t e = hipGetLastError()) return e;
+  }
+  if (kmax <= WAVE) return hipSuccess;
+  // rows of K > 64: the workspace planner
+  const size_t wb = plan_layout(kmax).bytes;
   // per-wave lookup tables (4 B per cluster) when they fit beside the row state
   const int tbl_cp = (cp <= 1024 && wb + (size_t)cp * 4 <= (size_t)LDS_BUDGET) ? cp : 0;
   const size_t wbt = wb + (size_t)tbl_cp * 4;
   if (wbt <= (size_t)LDS_BUDGET) {
-    hipLaunchKernelGGL(plan_kernel<false>, dim3(n_rows), dim3(64), wbt, st, s, b, o, rows, n_rows, kmax,
-                       (char*)nullptr, (int)wb, n_rows, tbl_cp);
+    const int grid = persistent((const void*)plan_kernel<false, false>, wbt);
+    hipLaunchKernelGGL((plan_kernel<false, false>), dim3((unsigned)grid), dim3(64), wbt, st, s, b, o, rows, n_rows,
+                       kmax, (char*)nullptr, (int)wb, grid, tbl_cp);
   } else {
     size_t slots = scr_bytes / wb;
     if (slots < 1) return hipErrorInvalidValue;
     if (slots > (size_t)MAX_RESIDENT_WAVES) slots = MAX_RESIDENT_WAVES;
     if (slots > (size_t)n_rows) slots = n_rows;
-    hipLaunchKernelGGL(plan_kernel<true>, dim3(slots), dim3(64), 0, st, s, b, o, rows, n_rows, kmax, (char*)gscr,
-                       (int)wb, (int)slots, 0);
+    hipLaunchKernelGGL((plan_kernel<true, false>), dim3(slots), dim3(64), 0, st, s, b, o, rows, n_rows, kmax,
+                       (char*)gscr, (int)wb, (int)slots, 0);
   }
   return hipGetLastError();
 }
@@ -2801,14 +2951,17 @@ hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, void* gscr, size_t s
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (r.n_rows == 0 || kmax <= 0) return hipSuccess;
   const size_t wb = plan_layout(kmax).bytes;
+  // KAD_PLAN_FORCE_WS=1 (tests): rows of K <= 64 through the LDS-workspace planner too
+  const int force_ws = getenv("KAD_PLAN_FORCE_WS") ? atoi(getenv("KAD_PLAN_FORCE_WS")) : 0;
   if (wb <= (size_t)LDS_BUDGET) {
     hipLaunchKernelGGL(plan_rows_kernel<false>, dim3(r.n_rows), dim3(64), wb, st, r, (char*)nullptr, (int)wb,
-                       r.n_rows);
+                       r.n_rows, force_ws);
   } else {
     size_t slots = scr_bytes / wb;
     if (slots < 1) return hipErrorInvalidValue;
     if (slots > (size_t)r.n_rows) slots = r.n_rows;
-    hipLaunchKernelGGL(plan_rows_kernel<true>, dim3(slots), dim3(64), 0, st, r, (char*)gscr, (int)wb, (int)slots);
+    hipLaunchKernelGGL(plan_rows_kernel<true>, dim3(slots), dim3(64), 0, st, r, (char*)gscr, (int)wb, (int)slots,
+                       force_ws);
   }
   return hipGetLastError();
 }

@@ -392,4 +392,216 @@ __device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid,
   return rflags;
 }
 
+// ------------------------------------------------ rows of K <= 64 elements
+// The same planner with one element per lane and every per-element array in
+// registers: no LDS workspace, no wave syncs. Element i (ascending cluster id)
+// lives in lane i; the sorted passes permute the operands into sorted lanes
+// (ds_permute by rank), scan there with inactive lanes as the identity clamp
+// (0, -inf) — which is what compacting the active list does — and send the
+// results back (ds_bpermute by rank).
+struct PlanLane {
+  int64_t w, mn, mx, cap, cur;  // weight, MinReplicas, MaxReplicas (EF_HAS_MAX), capacity (EF_HAS_CAP), current
+  uint32_t fl, hash;            // EF_HAS_MAX | EF_HAS_CAP; FNV-1 of name ‖ key
+};
+struct PlanOut {
+  int64_t plan, over;  // final plan, overflow (EF_HAS_OVER in ofl)
+  uint32_t ofl;
+};
+
+__device__ __forceinline__ int lane_perm32(int dst, int v) { return __builtin_amdgcn_ds_permute(dst << 2, v); }
+__device__ __forceinline__ int lane_bperm32(int src, int v) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ int64_t lane_perm64(int dst, int64_t v) {
+  const uint32_t lo = (uint32_t)lane_perm32(dst, (int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)lane_perm32(dst, (int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t lane_bperm64(int src, int64_t v) {
+  const uint32_t lo = (uint32_t)lane_bperm32(src, (int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)lane_bperm32(src, (int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l));
+}
+
+// rank of each listed lane (in = true) by (weight desc, hash asc, element asc) among the listed
+// lanes (sort_by_weight_hash); unlisted lanes get m + their order among the unlisted, so the ranks are a
+// permutation of 0..63. *tie: two listed elements equal on (weight, hash).
+__device__ __forceinline__ int lane_sort_rank(bool in, int64_t we, uint32_t he, bool* tie) {
+  const int lane = lane_id();
+  const uint64_t lm = ballot(in);
+  const int m = popc64(lm);
+  int rank = 0;
+  bool t = false;
+  if (!ballot(in && (we < 0 || we > 0x7FFFFFFF))) {
+    // every listed weight in [0, 2^31): (weight desc, hash asc) as one ascending u64 key
+    const uint64_t ke = ((uint64_t)(uint32_t)(0x7FFFFFFF - (int)(in ? we : 0)) << 32) | he;
+    for (uint64_t r = lm; r; r &= r - 1) {
+      const int j = __builtin_ctzll(r);
+      const uint64_t kf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ke >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ke, j);
+      rank += kf < ke || (kf == ke && j < lane);
+      t |= (j != lane && kf == ke);
+    }
+  } else {
+    for (uint64_t r = lm; r; r &= r - 1) {
+      const int j = __builtin_ctzll(r);
+      const int64_t wf = readlane64(we, j);
+      const uint32_t hf = (uint32_t)__builtin_amdgcn_readlane((int)he, j);
+      rank += wf > we || (wf == we && (hf < he || (hf == he && j < lane)));
+      t |= (j != lane && wf == we && hf == he);
+    }
+  }
+  *tie = ballot(in && t) != 0;
+  return in ? rank : m + mbcnt(~lm);
+}
+
+// getDesiredPlan (planner.go:211-304) on sorted lanes: lane s < m holds the s-th element of the
+// sorted list (wt, mxv = I64_MAX for none, mn when use_min, cap when hc). Returns R; plan / over /
+// ofl per sorted lane.
+__device__ __forceinline__ int64_t desired_plan_lanes(int m, int64_t wt, int64_t mxv, int64_t Mn, bool hc, int64_t cap,
+                                                      int64_t total, bool keep, int64_t& plan, int64_t& over,
+                                                      uint32_t& ofl) {
+  const int lane = lane_id();
+  const bool v = lane < m;
+  // ---- minimum pass
+  int64_t R = total;
+  {
+    const int64_t U = hc ? cap : I64_MAX;
+    Clamp f;
+    if (!v)
+      f = {0, NEG_INF};
+    else if (Mn >= 0)
+      f = {Mn < U ? Mn : U, 0};
+    else
+      f = {Mn, NEG_INF};
+    const Clamp inc = wave_scan_clamp_n(f, clamp_narrow(f, R));
+    const int64_t Ri = clamp_apply(wave_shr1_clamp(inc), R);
+    int64_t mt = Mn < Ri ? Mn : Ri;
+    ofl = v ? EF_HAS_PLAN : 0u;
+    over = 0;
+    if (v && hc && cap < mt) {
+      over = mt - cap;
+      ofl |= EF_HAS_OVER;
+      mt = cap;
+    }
+    plan = v ? mt : 0;
+    R = clamp_apply(readlane_clamp(inc, WAVE - 1), R);
+  }
+  // ---- weighted rounds over the active lanes (the reference's compacted list)
+  bool active = v;
+  bool modified = true;
+  int rounds = 0;  // see desired_plan: guards only adversarial negative weights
+  while (modified && R > 0 && rounds++ < 4 * m + 64) {
+    const int64_t wsum = wave_sum_i64(active ? wt : 0);
+    if (wsum <= 0) break;
+    const int64_t D = R;
+    const int64_t start = plan;
+    const int64_t ee = active ? ceil_extra(D, wt, wsum) : 0;
+    const bool hm = active && mxv != I64_MAX;
+    const bool hcap = active && hc;
+    int64_t U = I64_MAX;
+    if (hm) U = mxv;
+    if (hcap && cap < U) U = cap;
+    const int64_t V = U == I64_MAX ? I64_MAX : wsub(U, start);
+    const int64_t mm = ee < V ? ee : V;
+    const Clamp f = !active ? Clamp{0, NEG_INF} : (mm >= 0 ? Clamp{mm, 0} : Clamp{mm, NEG_INF});
+    const Clamp inc = wave_scan_clamp_n(f, clamp_narrow(f, R));
+    const int64_t Ri = clamp_apply(wave_shr1_clamp(inc), R);
+    bool full = false, mod = false;
+    if (active) {
+      const int64_t extra = ee < Ri ? ee : Ri;
+      int64_t t = wadd(start, extra);
+      if (hm && t > mxv) {
+        t = mxv;
+        full = true;
+      }
+      if (hcap && t > cap) {
+        over = wadd((ofl & EF_HAS_OVER) ? over : 0, wsub(t, cap));
+        ofl |= EF_HAS_OVER;
+        t = cap;
+        full = true;
+      }
+      plan = t;
+      mod = t > start;
+    }
+    active = active && !full;
+    R = clamp_apply(readlane_clamp(inc, WAVE - 1), R);
+    modified = ballot(mod) != 0;
+  }
+  if (!keep && v && (ofl & EF_HAS_OVER)) {
+    const int64_t x = over < R ? over : R;
+    if (x > 0) {
+      over = x;
+    } else {
+      over = 0;
+      ofl &= ~EF_HAS_OVER;
+    }
+  }
+  return R;
+}
+
+// planner.Plan (planner.go:83-177) for K <= 64 elements, element i in lane i. Returns KAD_RF_HASH_TIE
+// when a sort met a (weight, hash) tie.
+__device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int64_t total, bool avoid, bool keep,
+                                                   PlanOut& out) {
+  const int lane = lane_id();
+  const bool v = lane < K;
+  uint32_t rflags = 0;
+  const bool hmax = v && (e.fl & EF_HAS_MAX), hcap = v && (e.fl & EF_HAS_CAP);
+  const int64_t mx2 = hmax ? e.mx : I64_MAX;
+  bool tie;
+  const int rank = lane_sort_rank(v, e.w, e.hash, &tie);
+  if (tie) rflags |= KAD_RF_HASH_TIE;
+  if (!avoid) keep = true;
+  // element lanes → sorted lanes
+  const int64_t s_w = lane_perm64(rank, e.w), s_mx = lane_perm64(rank, mx2), s_mn = lane_perm64(rank, e.mn);
+  const int64_t s_cap = lane_perm64(rank, e.cap);
+  const bool s_hc = lane_perm32(rank, hcap ? 1 : 0) != 0;
+  int64_t p_s, o_s;
+  uint32_t f_s;
+  desired_plan_lanes(K, s_w, s_mx, s_mn, s_hc, s_cap, total, keep, p_s, o_s, f_s);
+  // sorted lanes → element lanes
+  int64_t plan = lane_bperm64(rank, p_s);
+  out.over = lane_bperm64(rank, o_s);
+  out.ofl = (uint32_t)lane_bperm32(rank, (int)f_s);
+  if (avoid) {
+    // currentPlan, capped by capacity (planner.go:134-146)
+    int64_t adj = v ? e.cur : 0;
+    if (hcap && e.cap < adj) adj = e.cap;
+    const int64_t cur_total = wave_sum_i64(adj), des_total = wave_sum_i64(v ? plan : 0);
+    if (cur_total != des_total) {
+      const bool up = cur_total < des_total;
+      const int64_t count = up ? des_total - cur_total : cur_total - des_total;
+      // preferences of the clusters to scale (planner.go:306-366)
+      const bool sel = v && (up ? plan > adj : plan < adj);
+      const int64_t w2 = up ? plan - adj : adj - plan;
+      const int64_t m2 = up ? (hmax ? e.mx - adj : I64_MAX) : adj;
+      const int m = popc64(ballot(sel));
+      int64_t plan2 = 0;
+      uint32_t ofl2 = 0;
+      if (m > 0) {
+        bool tie2;
+        const int r2 = lane_sort_rank(sel, w2, e.hash, &tie2);
+        if (tie2) rflags |= KAD_RF_HASH_TIE;
+        int64_t p2s, o2s;
+        uint32_t f2s;
+        // scale plan: no capacity, no minimums, keepUnschedulable = false (its overflow is discarded)
+        desired_plan_lanes(m, lane_perm64(r2, w2), lane_perm64(r2, m2), 0, false, 0, count, false, p2s, o2s, f2s);
+        plan2 = lane_bperm64(r2, p2s);
+        // every lane takes part in the bpermute (a disabled source lane reads as 0), then the select
+        const uint32_t f2 = (uint32_t)lane_bperm32(r2, (int)f2s);
+        ofl2 = sel ? f2 : 0u;
+      }
+      plan = adj;
+      if (ofl2 & EF_HAS_PLAN) plan = up ? wadd(adj, plan2) : wsub(adj, plan2);
+    } else {
+      plan = adj;
+    }
+  }
+  out.plan = plan;
+  return rflags;
+}
+
 }  // namespace kad

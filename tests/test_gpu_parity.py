@@ -106,10 +106,15 @@ def _gpu_plan(ctx, rsp, replicas, clusters, existing, est, avoid, keep):
             {n: v for (n, _), v in zip(prefs, over) if v is not None})
 
 
+@pytest.mark.parametrize("path", ["lanes", "ws"])
 @pytest.mark.parametrize("c", PLANNER, ids=[f"{case_id(c)}-a{int(c['avoidDisruption'])}k{int(c['keepUnschedulableReplicas'])}"
                                             for c in PLANNER])
-def test_golden_planner_on_gpu(ctx, c):
+def test_golden_planner_on_gpu(ctx, c, path, monkeypatch):
+    """planner_test.go's cases through kad_plan_rows: the register planner (rows of K <= 64, plan_row_lanes)
+    and the LDS-workspace planner (KAD_PLAN_FORCE_WS=1, the path of rows with K > 64)."""
     from test_oracle_golden import run_planner_case
+    if path == "ws":
+        monkeypatch.setenv("KAD_PLAN_FORCE_WS", "1")
     converged, plan, over = run_planner_case(
         c, lambda rsp, r, cl, ex, est, key, av, kp: _gpu_plan(ctx, rsp, r, cl, ex, est, av, kp))
     assert converged
@@ -117,6 +122,30 @@ def test_golden_planner_on_gpu(ctx, c):
         assert plan == c["want_plan"]
     if over or c["want_overflow"]:
         assert over == c["want_overflow"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_plan_rows_lanes_equal_workspace(ctx, seed, monkeypatch):
+    """Random rows (K 1..64, weights/minimums/maximums/capacities/current replicas incl. zero, tie-heavy
+    hashes, avoid/keep both ways): the register planner and the LDS-workspace planner agree exactly."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for _ in range(300):
+        K = int(rng.integers(1, 65))
+        hs = rng.integers(0, 4 if rng.random() < 0.3 else 1 << 32, K)
+        elems = []
+        for i in range(K):
+            elems.append({"hash": int(hs[i]), "weight": int(rng.integers(0, 5 if rng.random() < 0.4 else 1000)),
+                          "min": int(rng.integers(0, 6)) if rng.random() < 0.3 else 0,
+                          "max": int(rng.integers(0, 200)) if rng.random() < 0.3 else None,
+                          "cap": int(rng.integers(0, 300)) if rng.random() < 0.25 else None,
+                          "current": int(rng.integers(0, 400)) if rng.random() < 0.5 else 0})
+        rows.append({"elems": elems, "total": int(rng.integers(0, 20_000)), "avoid": bool(rng.random() < 0.5),
+                     "keep": bool(rng.random() < 0.5)})
+    lanes = ctx.plan_rows(rows)
+    monkeypatch.setenv("KAD_PLAN_FORCE_WS", "1")
+    ws = ctx.plan_rows(rows)
+    assert lanes == ws
 
 
 @pytest.mark.parametrize("c", RSP, ids=[case_id(c) for c in RSP])
