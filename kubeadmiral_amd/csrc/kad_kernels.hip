@@ -2307,13 +2307,15 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
   // LDS: the row workspace of rows with K > 64 (kmax > 64 only), then the lookup tables
   char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem;
   const size_t ws_bytes = (GSCR || LANES || kmax <= WAVE) ? 0 : plan_layout(kmax).bytes;
-  // cluster id → (preference / current-cluster index + 1) lookup tables in LDS
-  // (tbl_cp > 0), set and cleared per unit: replaces two binary searches in
-  // global memory per selected cluster
-  uint16_t* tbl_p = (uint16_t*)(smem + ws_bytes);
-  uint16_t* tbl_c = tbl_p + tbl_cp;
+  // cluster id → (row tag << 16 | preference / current-cluster index + 1) lookup tables in LDS
+  // (tbl_cp > 0), written per row and never cleared: an entry counts only with the row's tag (the wave's
+  // row counter; the tables are zeroed when it wraps). Replaces two binary searches in global memory per
+  // selected cluster.
+  uint32_t* tbl_p = (uint32_t*)(smem + ws_bytes);
+  uint32_t* tbl_c = tbl_p + tbl_cp;
   const bool use_tbl = !GSCR && tbl_cp > 0;
-  if (use_tbl) {
+  uint32_t tag = 0;
+  if (use_tbl) {  // LDS starts undefined: no entry may carry a tag before its row writes it
     for (int i = lane; i < 2 * tbl_cp; i += WAVE) tbl_p[i] = 0;
     wsync<GSCR>();
   }
@@ -2339,19 +2341,44 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
     const uint8_t* key = b.key + ko0;
     const int klen = ko1 - ko0;
     const int64_t total = (f & KAD_W_HAS_DESIRED) ? desired : 0;
-    // preferences (rsp.go:99-126)
-    if (use_tbl) {
-      for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = (uint16_t)(j - p0 + 1);
-      for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = (uint16_t)(j - c0 + 1);
-      wsync<GSCR>();
-    }
     // su.Key() bytes in lanes (uniform): the FNV-1 continuation of every element
     // reads them with v_readlane instead of one dependent load per byte
     const uint32_t kb0 = lane < klen ? (uint32_t)key[lane] : 0u;
+    // rows of K <= 64: element `lane`'s cluster id and name hash are loaded before the lookup tables are
+    // filled, so those loads and the tables' index loads share one memory round trip
+    int c_l = 0;
+    uint32_t h_l = 0;
+    int64_t ac_l = 0, av_l = 0;  // cores for dynamic weights (rsp.go:183-272)
+    if constexpr (LANES) {
+      c_l = o.cluster[off + (lane < K ? lane : 0)];
+      h_l = s.name_fnv[c_l];
+      if (f & KAD_W_DYNAMIC_WEIGHTS) {
+        ac_l = s.alloc_cores[c_l];
+        av_l = s.avail_cores[c_l];
+      }
+    }
+    // preferences (rsp.go:99-126)
+    if (use_tbl) {
+      tag = (tag + 1) & 0xFFFFu;
+      if (tag == 0) {  // wrapped: no stale entry may carry a live tag
+        for (int i = lane; i < 2 * tbl_cp; i += WAVE) tbl_p[i] = 0;
+        wsync<GSCR>();
+        tag = 1;
+      }
+      for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = (tag << 16) | (uint32_t)(j - p0 + 1);
+      for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = (tag << 16) | (uint32_t)(j - c0 + 1);
+      wsync<GSCR>();
+    }
     // element i: cluster id, hash, preference columns, current replicas
     auto gather = [&](int i, int& c, PlanLane& e) {
-      c = o.cluster[off + i];
-      uint32_t h = s.name_fnv[c];
+      uint32_t h;
+      if constexpr (LANES) {
+        c = c_l;  // i == lane (or 0 past K)
+        h = h_l;
+      } else {
+        c = o.cluster[off + i];
+        h = s.name_fnv[c];
+      }
       for (int k0 = 0; k0 < klen; k0 += WAVE) {
         const uint32_t kb = k0 == 0 ? kb0 : (k0 + lane < klen ? (uint32_t)key[k0 + lane] : 0u);
         const int m = klen - k0 < WAVE ? klen - k0 : WAVE;
@@ -2363,9 +2390,9 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
       e.hash = h;
       int pi, ci;
       if (use_tbl) {
-        const int tp = tbl_p[c], tc = tbl_c[c];
-        pi = tp ? p0 + tp - 1 : -1;
-        ci = tc ? c0 + tc - 1 : -1;
+        const uint32_t tp = tbl_p[c], tc = tbl_c[c];
+        pi = (tp >> 16) == tag ? p0 + (int)(tp & 0xFFFFu) - 1 : -1;
+        ci = (tc >> 16) == tag ? c0 + (int)(tc & 0xFFFFu) - 1 : -1;
       } else {
         pi = find_sorted(b.pref_id, p0, p1, c);
         ci = find_sorted(b.cur_id, c0, c1, c);
@@ -2404,18 +2431,13 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
         e = PlanLane{0, 0, 0, 0, 0, 0u, 0u};
         c = 0;
       }
-      if (use_tbl) {
-        wsync<GSCR>();
-        for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = 0;
-        for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = 0;
-        wsync<GSCR>();
-      }
+      wsync<GSCR>();  // the next row's table writes follow this row's reads
       KAD_PT(t1);
       KAD_PADD(0, t1 - t0);
       KAD_PADD(5, 1);
       if (f & KAD_W_DYNAMIC_WEIGHTS) {
         // CalcWeightLimit (rsp.go:183-213) + AvailableToPercentage (rsp.go:215-272)
-        const int64_t ac = v ? s.alloc_cores[c] : 0, av = v ? s.avail_cores[c] : 0;
+        const int64_t ac = v ? ac_l : 0, av = v ? av_l : 0;
         const double sum = wave_sum_f64(v ? (double)ac : 0.0);
         const double suma = wave_sum_f64((v && av > 0) ? (double)av : 0.0);
         if (suma == 0) {
@@ -2481,11 +2503,6 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
       }
     }
     wsync<GSCR>();
-    if (use_tbl) {
-      for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = 0;
-      for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = 0;
-      wsync<GSCR>();
-    }
     KAD_PT(t1);
     KAD_PADD(0, t1 - t0);
     KAD_PADD(5, 1);
@@ -2898,10 +2915,10 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
     long grid = (long)n_cus() * per_cu;
     return (int)(grid > n_rows ? n_rows : grid);
   };
-  // rows of K <= 64: the register planner, lookup tables only in LDS (4 B per cluster)
+  // rows of K <= 64: the register planner, lookup tables only in LDS (8 B per cluster)
   {
     const int tbl_cp = cp <= 1024 ? cp : 0;
-    const size_t lds = (size_t)tbl_cp * 4;
+    const size_t lds = (size_t)tbl_cp * 8;
     const int grid = persistent((const void*)plan_kernel<false, true>, lds);
     hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows, kmax,
                        (char*)nullptr, 0, grid, tbl_cp);
@@ -2910,9 +2927,9 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
   if (kmax <= WAVE) return hipSuccess;
   // rows of K > 64: the workspace planner
   const size_t wb = plan_layout(kmax).bytes;
-  // per-wave lookup tables (4 B per cluster) when they fit beside the row state
-  const int tbl_cp = (cp <= 1024 && wb + (size_t)cp * 4 <= (size_t)LDS_BUDGET) ? cp : 0;
-  const size_t wbt = wb + (size_t)tbl_cp * 4;
+  // per-wave lookup tables (8 B per cluster) when they fit beside the row state
+  const int tbl_cp = (cp <= 1024 && wb + (size_t)cp * 8 <= (size_t)LDS_BUDGET) ? cp : 0;
+  const size_t wbt = wb + (size_t)tbl_cp * 8;
   if (wbt <= (size_t)LDS_BUDGET) {
     const int grid = persistent((const void*)plan_kernel<false, false>, wbt);
     hipLaunchKernelGGL((plan_kernel<false, false>), dim3((unsigned)grid), dim3(64), wbt, st, s, b, o, rows, n_rows,

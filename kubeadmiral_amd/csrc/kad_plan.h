@@ -56,6 +56,7 @@ __device__ __forceinline__ Clamp wave_scan_clamp(Clamp v) {
 // no value wraps in either width and the results are identical): half the DPP
 // moves and 32-bit compose. -inf is INT32_MIN in the narrow form.
 constexpr int NEG32 = INT32_MIN;
+constexpr int NEG30 = -(1 << 30);  // -inf of desired_plan_lanes32 (see there)
 __device__ __forceinline__ bool clamp_narrow(Clamp f, int64_t R) {
   return R >= 0 && R < (1ll << 24) && !ballot(f.s <= -(1ll << 24) || f.s >= (1ll << 24));
 }
@@ -105,6 +106,23 @@ __device__ __forceinline__ int64_t ceil_extra(int64_t D, int64_t w, int64_t wsum
     const double nd = (double)num, sd = (double)wsum;
     int64_t q = (int64_t)(nd / sd);
     double r = nd - (double)q * sd;  // exact: q * sd <= nd + sd < 2^53
+    q += (r >= sd) - (r < 0.0);
+    r = nd - (double)q * sd;
+    q += (r >= sd) - (r < 0.0);
+    return q;
+  }
+  return go_div(num, wsum);
+}
+
+// ceil_extra with 1/weightSum precomputed (inv = 1.0 / wsum, wave-uniform): the f64 quotient estimate is
+// within one of the truncated quotient, and the two exact corrections make it the integer quotient
+__device__ __forceinline__ int64_t ceil_extra_inv(int64_t D, int64_t w, int64_t wsum, double inv) {
+  const int64_t num = wsub(wadd(wmul(D, w), wsum), 1);
+  const bool small = D >= 0 && D < (1ll << 26) && w >= 0 && w < (1ll << 26) && wsum > 0 && wsum < (1ll << 52);
+  if (small && num >= 0 && num < (1ll << 52)) {
+    const double nd = (double)num, sd = (double)wsum;
+    int64_t q = (int64_t)(nd * inv);
+    double r = nd - (double)q * sd;  // exact: q * sd <= nd + 2 sd < 2^53
     q += (r >= sd) - (r < 0.0);
     r = nd - (double)q * sd;
     q += (r >= sd) - (r < 0.0);
@@ -434,16 +452,23 @@ __device__ __forceinline__ int lane_sort_rank(bool in, int64_t we, uint32_t he, 
   const int m = popc64(lm);
   int rank = 0;
   bool t = false;
-  if (!ballot(in && (we < 0 || we > 0x7FFFFFFF))) {
-    // every listed weight in [0, 2^31): (weight desc, hash asc) as one ascending u64 key
-    const uint64_t ke = ((uint64_t)(uint32_t)(0x7FFFFFFF - (int)(in ? we : 0)) << 32) | he;
+  if (!ballot(in && (we < 0 || we >= (1 << 25)))) {
+    // every listed weight in [0, 2^25): (weight desc, hash asc, lane asc) as one unique ascending u64 key
+    // — one compare per listed element; a (weight, hash) tie = equal keys but for the lane bits
+    const uint64_t ke = ((uint64_t)(uint32_t)((1 << 25) - 1 - (int)(in ? we : 0)) << 38) | ((uint64_t)he << 6) | (uint64_t)lane;
+    const uint32_t khi = (uint32_t)(ke >> 32), klo = (uint32_t)ke;
     for (uint64_t r = lm; r; r &= r - 1) {
       const int j = __builtin_ctzll(r);
-      const uint64_t kf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ke >> 32), j) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ke, j);
-      rank += kf < ke || (kf == ke && j < lane);
-      t |= (j != lane && kf == ke);
+      const uint64_t kf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)khi, j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)klo, j);
+      rank += kf < ke;
     }
+    // ties: neighbours in sorted order with equal (weight, hash)
+    const int rk = in ? rank : m + mbcnt(~lm);
+    const int64_t sk = lane_perm64(rk, (int64_t)(ke >> 6));
+    const int64_t pk = dpp64<0x138, 0xf>(-1, sk);  // wave_shr:1: the previous sorted lane's key
+    *tie = ballot(lane > 0 && lane < m && sk == pk) != 0;
+    return rk;
   } else {
     for (uint64_t r = lm; r; r &= r - 1) {
       const int j = __builtin_ctzll(r);
@@ -498,7 +523,8 @@ __device__ __forceinline__ int64_t desired_plan_lanes(int m, int64_t wt, int64_t
     if (wsum <= 0) break;
     const int64_t D = R;
     const int64_t start = plan;
-    const int64_t ee = active ? ceil_extra(D, wt, wsum) : 0;
+    const double inv = 1.0 / (double)wsum;  // wave-uniform
+    const int64_t ee = active ? ceil_extra_inv(D, wt, wsum, inv) : 0;
     const bool hm = active && mxv != I64_MAX;
     const bool hcap = active && hc;
     int64_t U = I64_MAX;
@@ -542,6 +568,137 @@ __device__ __forceinline__ int64_t desired_plan_lanes(int m, int64_t wt, int64_t
   return R;
 }
 
+// The same getDesiredPlan in int32 for narrow rows (desired_narrow: total < 2^24; every listed weight in
+// [0, 2^20); minimums in [0, 2^18); maximums and capacities in [0, 2^24); minimum <= maximum). Then no
+// element starts a round above its bound (V >= 0), remainingReplicas only falls (R <= total), every
+// clamp step is >= 0 and the steps of one scan sum below 2^25 (minimums: 64 · 2^18; rounds: Σ ceil ≤
+// R + 64), so every value fits int32 and the results equal the int64 path's. -inf is NEG30 = -2^30:
+// a genuine floor is >= -2^25, and -2^30 minus any scan's steps stays above INT32_MIN, so the clamp
+// composition needs no -inf test (max(t_a − s_b, t_b) keeps both orders). weightSum < 2^26 and
+// D·w + weightSum < 2^53 make the f64 quotient of ceil_extra exact after the two corrections.
+__device__ __forceinline__ bool desired_narrow(bool v, int64_t total, int64_t wt, int64_t mxv, int64_t Mn, bool hc,
+                                               int64_t cap) {
+  return total >= 0 && total < (1 << 24) &&
+         !ballot(v && (wt < 0 || wt >= (1 << 20) || Mn < 0 || Mn >= (1 << 18) ||
+                       (mxv != I64_MAX && (mxv < 0 || mxv >= (1 << 24) || Mn > mxv)) ||
+                       (hc && (cap < 0 || cap >= (1 << 24)))));
+}
+__device__ __forceinline__ int64_t desired_plan_lanes32(int m, int wt, int mxv, int Mn, bool hc, int cap, int total,
+                                                        bool keep, int64_t& plan64, int64_t& over64, uint32_t& ofl) {
+  constexpr int NONE = INT32_MAX;  // no maximum / capacity
+  const int lane = lane_id();
+  const bool v = lane < m;
+  auto scan = [](int s, int t) {  // inclusive clamp scan; lanes without a source combine with (0, NEG30)
+#define KAD_C32(CTRL, RM)                                                                  \
+  {                                                                                        \
+    const int pt = __builtin_amdgcn_update_dpp(NEG30, t, CTRL, RM, 0xf, false);           \
+    const int at = pt - s;                                                                 \
+    t = at > t ? at : t;                                                                   \
+    s += __builtin_amdgcn_update_dpp(0, s, CTRL, RM, 0xf, true);                           \
+  }
+    KAD_C32(0x111, 0xf)
+    KAD_C32(0x112, 0xf)
+    KAD_C32(0x114, 0xf)
+    KAD_C32(0x118, 0xf)
+    KAD_C32(0x142, 0xa)
+    KAD_C32(0x143, 0xc)
+#undef KAD_C32
+    return make_int2(s, t);
+  };
+  auto apply = [](int s, int t, int R) { const int x = R - s; return x > t ? x : t; };
+  // ---- minimum pass
+  int R = total;
+  int plan, over = 0;
+  {
+    const int U = hc ? cap : NONE;
+    const int fs = v ? (Mn < U ? Mn : U) : 0, ft = v ? 0 : NEG30;
+    const int2 inc = scan(fs, ft);
+    const int es = dpp32<0x138, 0xf>(0, inc.x), et = dpp32<0x138, 0xf>(NEG30, inc.y);  // exclusive
+    const int Ri = apply(es, et, R);
+    int mt = Mn < Ri ? Mn : Ri;
+    ofl = v ? EF_HAS_PLAN : 0u;
+    if (v && hc && cap < mt) {
+      over = mt - cap;
+      ofl |= EF_HAS_OVER;
+      mt = cap;
+    }
+    plan = v ? mt : 0;
+    R = apply(__builtin_amdgcn_readlane(inc.x, WAVE - 1), __builtin_amdgcn_readlane(inc.y, WAVE - 1), R);
+  }
+  bool active = v;
+  bool modified = true;
+  int rounds = 0;
+  while (modified && R > 0 && rounds++ < 4 * m + 64) {
+    const int wsum = wave_sum_i32(active ? wt : 0);
+    if (wsum <= 0) break;
+    const int D = R;
+    const int start = plan;
+    const double sd = (double)wsum, inv = 1.0 / sd;  // wave-uniform
+    int ee = 0;
+    if (active) {  // ceil((D·w + wsum − 1) / wsum), exact
+      const double nd = (double)D * (double)wt + (double)(wsum - 1);
+      int q = (int)(nd * inv);
+      double r = nd - (double)q * sd;
+      q += (r >= sd) - (r < 0.0);
+      r = nd - (double)q * sd;
+      q += (r >= sd) - (r < 0.0);
+      ee = q;
+    }
+    const bool hm = active && mxv != NONE;
+    const bool hcap = active && hc;
+    int U = NONE;
+    if (hm) U = mxv;
+    if (hcap && cap < U) U = cap;
+    const int V = U == NONE ? NONE : U - start;
+    const int mm = ee < V ? ee : V;
+    const int fs = active ? mm : 0, ft = (active && mm >= 0) ? 0 : NEG30;
+    const int2 inc = scan(fs, ft);
+    const int es = dpp32<0x138, 0xf>(0, inc.x), et = dpp32<0x138, 0xf>(NEG30, inc.y);
+    const int Ri = apply(es, et, R);
+    bool full = false, mod = false;
+    if (active) {
+      const int extra = ee < Ri ? ee : Ri;
+      int t = start + extra;
+      if (hm && t > mxv) {
+        t = mxv;
+        full = true;
+      }
+      if (hcap && t > cap) {
+        over = ((ofl & EF_HAS_OVER) ? over : 0) + (t - cap);
+        ofl |= EF_HAS_OVER;
+        t = cap;
+        full = true;
+      }
+      plan = t;
+      mod = t > start;
+    }
+    active = active && !full;
+    R = apply(__builtin_amdgcn_readlane(inc.x, WAVE - 1), __builtin_amdgcn_readlane(inc.y, WAVE - 1), R);
+    modified = ballot(mod) != 0;
+  }
+  if (!keep && v && (ofl & EF_HAS_OVER)) {
+    const int x = over < R ? over : R;
+    if (x > 0) {
+      over = x;
+    } else {
+      over = 0;
+      ofl &= ~EF_HAS_OVER;
+    }
+  }
+  plan64 = plan;
+  over64 = over;
+  return R;
+}
+// getDesiredPlan on sorted lanes, narrow rows in int32
+__device__ __forceinline__ int64_t desired_plan_any(int m, int64_t wt, int64_t mxv, int64_t Mn, bool hc, int64_t cap,
+                                                    int64_t total, bool keep, int64_t& plan, int64_t& over,
+                                                    uint32_t& ofl) {
+  if (desired_narrow(lane_id() < m, total, wt, mxv, Mn, hc, cap))
+    return desired_plan_lanes32(m, (int)wt, mxv == I64_MAX ? INT32_MAX : (int)mxv, (int)Mn, hc, (int)cap, (int)total,
+                                keep, plan, over, ofl);
+  return desired_plan_lanes(m, wt, mxv, Mn, hc, cap, total, keep, plan, over, ofl);
+}
+
 // planner.Plan (planner.go:83-177) for K <= 64 elements, element i in lane i. Returns KAD_RF_HASH_TIE
 // when a sort met a (weight, hash) tie.
 __device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int64_t total, bool avoid, bool keep,
@@ -561,7 +718,7 @@ __device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int
   const bool s_hc = lane_perm32(rank, hcap ? 1 : 0) != 0;
   int64_t p_s, o_s;
   uint32_t f_s;
-  desired_plan_lanes(K, s_w, s_mx, s_mn, s_hc, s_cap, total, keep, p_s, o_s, f_s);
+  desired_plan_any(K, s_w, s_mx, s_mn, s_hc, s_cap, total, keep, p_s, o_s, f_s);
   // sorted lanes → element lanes
   int64_t plan = lane_bperm64(rank, p_s);
   out.over = lane_bperm64(rank, o_s);
@@ -588,7 +745,7 @@ __device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int
         int64_t p2s, o2s;
         uint32_t f2s;
         // scale plan: no capacity, no minimums, keepUnschedulable = false (its overflow is discarded)
-        desired_plan_lanes(m, lane_perm64(r2, w2), lane_perm64(r2, m2), 0, false, 0, count, false, p2s, o2s, f2s);
+        desired_plan_any(m, lane_perm64(r2, w2), lane_perm64(r2, m2), 0, false, 0, count, false, p2s, o2s, f2s);
         plan2 = lane_bperm64(r2, p2s);
         // every lane takes part in the bpermute (a disabled source lane reads as 0), then the select
         const uint32_t f2 = (uint32_t)lane_bperm32(r2, (int)f2s);
