@@ -2313,6 +2313,7 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
   // selected cluster.
   uint32_t* tbl_p = (uint32_t*)(smem + ws_bytes);
   uint32_t* tbl_c = tbl_p + tbl_cp;
+  uint64_t* kbuf = LANES ? (uint64_t*)(smem + ws_bytes + (size_t)tbl_cp * 8) : nullptr;  // sort keys (64)
   const bool use_tbl = !GSCR && tbl_cp > 0;
   uint32_t tag = 0;
   if (use_tbl) {  // LDS starts undefined: no entry may carry a tag before its row writes it
@@ -2464,7 +2465,7 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
       KAD_PT(t2);
       KAD_PADD(1, t2 - t1);
       PlanOut po;
-      rflags |= plan_row_lanes(e, K, total, avoid, keep, po);
+      rflags |= plan_row_lanes(e, K, total, avoid, keep, po, kbuf);
       KAD_PT(t3);
       KAD_PADD(2, t3 - t2);
       // result = plan + overflow, zeros dropped (rsp.go:162-179), ascending cluster id
@@ -2918,7 +2919,7 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
   // rows of K <= 64: the register planner, lookup tables only in LDS (8 B per cluster)
   {
     const int tbl_cp = cp <= 1024 ? cp : 0;
-    const size_t lds = (size_t)tbl_cp * 8;
+    const size_t lds = (size_t)tbl_cp * 8 + 64 * 8;  // tables + sort keys
     const int grid = persistent((const void*)plan_kernel<false, true>, lds);
     hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows, kmax,
                        (char*)nullptr, 0, grid, tbl_cp);

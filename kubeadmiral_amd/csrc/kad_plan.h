@@ -446,7 +446,9 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
 // rank of each listed lane (in = true) by (weight desc, hash asc, element asc) among the listed
 // lanes (sort_by_weight_hash); unlisted lanes get m + their order among the unlisted, so the ranks are a
 // permutation of 0..63. *tie: two listed elements equal on (weight, hash).
-__device__ __forceinline__ int lane_sort_rank(bool in, int64_t we, uint32_t he, bool* tie) {
+// kbuf (optional): 64 u64 of the wave's LDS; the listed keys are compacted there and read back as
+// broadcasts (LDS reads instead of two v_readlane per compare)
+__device__ __forceinline__ int lane_sort_rank(bool in, int64_t we, uint32_t he, bool* tie, uint64_t* kbuf = nullptr) {
   const int lane = lane_id();
   const uint64_t lm = ballot(in);
   const int m = popc64(lm);
@@ -456,12 +458,20 @@ __device__ __forceinline__ int lane_sort_rank(bool in, int64_t we, uint32_t he, 
     // every listed weight in [0, 2^25): (weight desc, hash asc, lane asc) as one unique ascending u64 key
     // — one compare per listed element; a (weight, hash) tie = equal keys but for the lane bits
     const uint64_t ke = ((uint64_t)(uint32_t)((1 << 25) - 1 - (int)(in ? we : 0)) << 38) | ((uint64_t)he << 6) | (uint64_t)lane;
-    const uint32_t khi = (uint32_t)(ke >> 32), klo = (uint32_t)ke;
-    for (uint64_t r = lm; r; r &= r - 1) {
-      const int j = __builtin_ctzll(r);
-      const uint64_t kf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)khi, j) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)klo, j);
-      rank += kf < ke;
+    if (kbuf) {
+      if (in) kbuf[mbcnt(lm)] = ke;
+      wave_sync();
+#pragma unroll 4
+      for (int i = 0; i < m; ++i) rank += kbuf[i] < ke;
+      wave_sync();  // the buffer is reused by the next sort
+    } else {
+      const uint32_t khi = (uint32_t)(ke >> 32), klo = (uint32_t)ke;
+      for (uint64_t r = lm; r; r &= r - 1) {
+        const int j = __builtin_ctzll(r);
+        const uint64_t kf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)khi, j) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)klo, j);
+        rank += kf < ke;
+      }
     }
     // ties: neighbours in sorted order with equal (weight, hash)
     const int rk = in ? rank : m + mbcnt(~lm);
@@ -702,14 +712,14 @@ __device__ __forceinline__ int64_t desired_plan_any(int m, int64_t wt, int64_t m
 // planner.Plan (planner.go:83-177) for K <= 64 elements, element i in lane i. Returns KAD_RF_HASH_TIE
 // when a sort met a (weight, hash) tie.
 __device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int64_t total, bool avoid, bool keep,
-                                                   PlanOut& out) {
+                                                   PlanOut& out, uint64_t* kbuf = nullptr) {
   const int lane = lane_id();
   const bool v = lane < K;
   uint32_t rflags = 0;
   const bool hmax = v && (e.fl & EF_HAS_MAX), hcap = v && (e.fl & EF_HAS_CAP);
   const int64_t mx2 = hmax ? e.mx : I64_MAX;
   bool tie;
-  const int rank = lane_sort_rank(v, e.w, e.hash, &tie);
+  const int rank = lane_sort_rank(v, e.w, e.hash, &tie, kbuf);
   if (tie) rflags |= KAD_RF_HASH_TIE;
   if (!avoid) keep = true;
   // element lanes → sorted lanes
@@ -740,7 +750,7 @@ __device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int
       uint32_t ofl2 = 0;
       if (m > 0) {
         bool tie2;
-        const int r2 = lane_sort_rank(sel, w2, e.hash, &tie2);
+        const int r2 = lane_sort_rank(sel, w2, e.hash, &tie2, kbuf);
         if (tie2) rflags |= KAD_RF_HASH_TIE;
         int64_t p2s, o2s;
         uint32_t f2s;
