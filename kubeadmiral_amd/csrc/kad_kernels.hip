@@ -713,9 +713,14 @@ __device__ __forceinline__ void affinity_words(const uint64_t* rows, Prog p, uin
   for (int k = 0; k < CPL; k++) out[k] = matched[k];
 }
 
-// bits of the sorted cluster-id list ids[lo, hi) that fall in chunk ch
-__device__ uint64_t id_list_word(const int32_t* ids, int lo, int hi, uint32_t ch) {
-  const int base = (int)ch * WAVE;
+
+// the words of chunks ch0 .. ch0+CPL-1 of the sorted cluster-id list ids[lo, hi): one lower bound of the
+// first chunk's base, then the ids inside the CPL chunks four at a time (independent loads)
+template <int CPL>
+__device__ __forceinline__ void id_list_words(const int32_t* ids, int lo, int hi, uint32_t ch0, uint64_t (&out)[CPL]) {
+#pragma unroll
+  for (int k = 0; k < CPL; k++) out[k] = 0;
+  const int base = (int)ch0 * WAVE, end = base + CPL * WAVE;
   int a = lo, b = hi;
   while (a < b) {  // lower bound of base
     const int mid = (a + b) >> 1;
@@ -724,9 +729,23 @@ __device__ uint64_t id_list_word(const int32_t* ids, int lo, int hi, uint32_t ch
     else
       b = mid;
   }
-  uint64_t m = 0;
-  for (int j = a; j < hi && ids[j] < base + WAVE; ++j) m |= 1ull << (ids[j] - base);
-  return m;
+  for (int j = a; j < hi; j += 4) {
+    int v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = j + u < hi ? ids[j + u] : INT32_MAX;
+    bool past = false;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int d = v[u] - base;
+      if (d >= 0 && d < CPL * WAVE) {
+#pragma unroll
+        for (int k = 0; k < CPL; k++)
+          if ((d >> 6) == k) out[k] |= 1ull << (d & 63);
+      }
+      past |= v[u] >= end;
+    }
+    if (past) break;
+  }
 }
 
 // cluster bitmask of id t in table tbl (0: NoSchedule|NoExecute taints, 1: NoExecute taints, 2: GVKs),
@@ -883,14 +902,20 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   }
   const bool place = (fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
   const bool curw = (fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
+  uint64_t pw[CPL], cwv[CPL];
+  if (place) {
+    id_list_words<CPL>(b.place, b.place_off[w], b.place_off[w + 1], ch0, pw);
+#pragma unroll
+    for (int k = 0; k < CPL; k++) m[k] &= pw[k];
+  }
+  if (curw) id_list_words<CPL>(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch0, cwv);
 #pragma unroll
   for (int k = 0; k < CPL; k++) {
     const uint32_t ch = ch0 + k;
     if (ch >= nch) break;
-    if (place) m[k] &= id_list_word(b.place, b.place_off[w], b.place_off[w + 1], ch);
     uint64_t cw = 0;
     if (curw) {
-      cw = id_list_word(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch);
+      cw = cwv[k];
       b.cw[(size_t)w * nch + ch] = cw;
     }
     if (s.fold) m[k] &= folded_word(s, fm, f, gvk, tol0, cw, nch, ch);

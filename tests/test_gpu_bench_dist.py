@@ -1,0 +1,26 @@
+"""bench.py's multi-GPU path on the one-GPU box: `--gpus 2` starts two ranks itself (torch.distributed.run),
+`--share-gpu` puts both on device 0 and `--backend gloo` stands in for RCCL (two ranks on one GPU cannot use
+RCCL). Checks the line the driver parses: world size, whole-job value, the timed placement all-gather."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_share_one_gpu():
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--backend", "gloo",
+           "--config", "c2", "--units", "20000", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-extra"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["rccl_world_size"] == 2
+    assert line["config"]["units_total"] == 20000 and line["config"]["units_per_gpu"] == 10000
+    assert line["value"] > 0 and line["scaling"] == "strong"
+    assert line["allgather"] is not None and line["allgather"]["ms"] > 0
