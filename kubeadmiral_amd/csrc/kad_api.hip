@@ -48,7 +48,7 @@ struct kad_ctx {
   size_t sw_cap = 0;
   void* d_cw = nullptr;   // u64[W][nch] current-cluster words (prep_kernel)
   size_t cw_cap = 0;
-  void* d_defer = nullptr;  // i32[W + 2]: defer_n, work_n, then the defer list
+  void* d_defer = nullptr;  // i32[2W + 4]: defer_n, work_n, rows_n, rows_head, the defer list, the row list
   size_t defer_cap = 0;
   void* d_wq = nullptr;     // u32[WQ_HEADS * WQ_STRIDE]: schedule kernels' work heads
   size_t wq_cap = 0;
@@ -61,8 +61,8 @@ struct kad_ctx {
   bool timing = false, timed = false;
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
   std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
-  std::vector<uint64_t> h_ns0; // host shadow of NoSchedule|NoExecute taint word 0 [C] (SnapDev::present_taints)
-  void* d_slices = nullptr;    // SnapDev::slices [3][64][nch], then SnapDev::taint_tab [2][8][256][nch]
+  std::vector<uint64_t> h_ns;  // host shadow of the NoSchedule|NoExecute taint words [TW][C] (SnapDev::present_taints)
+  void* d_slices = nullptr;    // SnapDev::slices [128*TW + 64][nch], then SnapDev::taint_tab [2][8*TW][256][nch]
   size_t slices_cap = 0;
   std::vector<int64_t> h_fit;  // SnapDev::fit_vals / fit_rows (host copy the upload reads from)
   void* d_fit = nullptr;
@@ -505,15 +505,21 @@ static int build_fit_table(kad_ctx* c) {
 static int refresh_derived(kad_ctx* c) {
   c->snap_negative = res_negative(c->h_res);
   c->sd.clean = res_clean(c->h_res);
-  uint64_t present = 0;
-  for (uint64_t x : c->h_ns0) present |= x;
-  c->sd.present_taints = present;
-  c->sd.fold = c->sd.TW == 1;
-  const size_t nch = (size_t)((c->sd.C + 63) / 64);
+  const int C = c->sd.C, TW = c->sd.TW;
+  c->sd.fold = TW >= 1 && TW <= TFOLD_MAX_TW;
+  for (int t = 0; t < TFOLD_MAX_TW; t++) {
+    uint64_t present = 0;
+    if (t < TW)
+      for (int x = 0; x < C; x++) present |= c->h_ns[(size_t)t * C + x];
+    c->sd.present_taints[t] = present;
+  }
+  if (!c->sd.fold) return build_fit_table(c);
+  const size_t nch = (size_t)((C + 63) / 64);
   const size_t nc1 = nch ? nch : 1;
-  if (int r = grow(c, &c->d_slices, &c->slices_cap, (3 * 64 + 2 * 8 * 256) * nc1 * 8)) return r;
+  const size_t n_slices = ((size_t)128 * TW + 64) * nc1, n_tab = (size_t)2 * 8 * TW * 256 * nc1;
+  if (int r = grow(c, &c->d_slices, &c->slices_cap, (n_slices + n_tab) * 8)) return r;
   c->sd.slices = static_cast<const uint64_t*>(c->d_slices);
-  c->sd.taint_tab = c->sd.slices + 3 * 64 * nc1;
+  c->sd.taint_tab = c->sd.slices + n_slices;
   HIPCHK(c, launch_slices(c->sd, static_cast<uint64_t*>(c->d_slices), c->stream));
   return build_fit_table(c);
 }
@@ -535,7 +541,8 @@ int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
     for (int q = 0; q < 4; q++)
       if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
   }
-  c->h_ns0.assign(at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE), at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + h.n_clusters);
+  c->h_ns.assign(at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE),
+                at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + (size_t)h.n_taint_words * h.n_clusters);
   if (int r = refresh_derived(c)) return r;
   c->have_snapshot = true;
   c->have_batch = false;
@@ -555,13 +562,13 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
   c->snap_hdr = h;
   if (int r = bind_snapshot(c, h)) return r;
   c->h_res.assign((size_t)4 * h.n_clusters, 0);
-  c->h_ns0.assign((size_t)h.n_clusters, 0);
+  c->h_ns.assign((size_t)h.n_taint_words * h.n_clusters, 0);
   if (h.n_clusters) {
     for (int q = 0; q < 4; q++)
       HIPCHK(c, hipMemcpy(c->h_res.data() + (size_t)q * h.n_clusters, static_cast<const char*>(dev_blob) + h.off[kResArrays[q]],
                           (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemcpy(c->h_ns0.data(), static_cast<const char*>(dev_blob) + h.off[KAD_S_TAINT_NSNE],
-                        (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(c->h_ns.data(), static_cast<const char*>(dev_blob) + h.off[KAD_S_TAINT_NSNE],
+                        (size_t)h.n_taint_words * h.n_clusters * 8, hipMemcpyDeviceToHost));
   }
   if (int r = refresh_derived(c)) return r;
   c->have_snapshot = true;
@@ -620,8 +627,9 @@ int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
       const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
       for (int j = 0; j < n; j++) c->h_res[(size_t)q * C + idx[j]] = v[j];
     }
-    const uint64_t* ns = at<uint64_t>(delta, h.off, KAD_S_TAINT_NSNE);  // row 0 of [TW][n_changed]
-    for (int j = 0; j < n; j++) c->h_ns0[idx[j]] = ns[j];
+    const uint64_t* ns = at<uint64_t>(delta, h.off, KAD_S_TAINT_NSNE);  // [TW][n_changed]
+    for (int t = 0; t < sh.n_taint_words; t++)
+      for (int j = 0; j < n; j++) c->h_ns[(size_t)t * C + idx[j]] = ns[(size_t)t * n + j];
   }
   if (int r = refresh_derived(c)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -715,7 +723,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   if (int r = grow(c, &c->d_rec, &c->rec_cap, (size_t)W * sizeof(UnitRec))) return r;
   if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
-  if (int r = grow(c, &c->d_defer, &c->defer_cap, ((size_t)W + 2) * 4)) return r;
+  if (int r = grow(c, &c->d_defer, &c->defer_cap, (2 * (size_t)W + 4) * 4)) return r;
   if (int r = grow(c, &c->d_wq, &c->wq_cap, (size_t)WQ_HEADS * WQ_STRIDE * 4)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->batch_hdr = h;
@@ -765,7 +773,10 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   b.cw = static_cast<uint64_t*>(c->d_cw);
   b.defer_n = static_cast<int32_t*>(c->d_defer);
   b.work_n = b.defer_n + 1;
-  b.defer = b.defer_n + 2;
+  b.rows_n = b.defer_n + 2;
+  b.rows_head = b.defer_n + 3;
+  b.defer = b.defer_n + 4;
+  b.rows = b.defer + W;
   b.wq = static_cast<uint32_t*>(c->d_wq);
   c->have_batch = true;
   c->ran = false;
@@ -820,6 +831,9 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total || wide_path(c->sd);
+  // long feasible lists go to schedule_row_kernel when every filter is in the static words
+  static const bool no_rows = getenv("KAD_NO_ROWS") && atoi(getenv("KAD_NO_ROWS"));
+  c->bd.use_rows = !no_rows && c->sd.clean && c->sd.fold && c->sd.fitfold && row_kernel_fits(c->sd.C);
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[4], c->stream));

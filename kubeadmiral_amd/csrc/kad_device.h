@@ -8,7 +8,9 @@
 
 namespace kad {
 
-constexpr int FITFOLD_MAX_C = 4096;
+constexpr int FITFOLD_MAX_C = 16384;
+// taint words (64 ids each) prep_kernel folds into the static filter words (SnapDev::fold): up to 256 ids
+constexpr int TFOLD_MAX_TW = 4;
 // unit work queue of the schedule kernels: WQ_HEADS counters, one 128-B line apart (BatchDev::wq)
 constexpr int WQ_HEADS = 64, WQ_STRIDE = 32;
 constexpr int FIT_FENCES = 256;  // prep_kernel's LDS copy of every (fit_mp / 256)-th fit value
@@ -16,14 +18,15 @@ constexpr int FIT_FENCES = 256;  // prep_kernel's LDS copy of every (fit_mp / 25
 struct SnapDev {
   int C, GW, TW, K, S;
   int clean;  // host: every cluster's cpu/mem fit the lean kernel's exact-f64 path (kad_api.hip res_clean)
-  // TW == 1: prep_kernel folds TaintToleration's and APIResources' filters into each unit's static
-  // filter words from per-id cluster bitmask slices ([3][64][nch]: NoSchedule|NoExecute taint id t,
-  // NoExecute taint id t, GVK id g), so the schedule kernels only test resource fit per lane
+  // TW <= TFOLD_MAX_TW: prep_kernel folds TaintToleration's and APIResources' filters into each unit's
+  // static filter words from per-id cluster bitmask slices ([128*TW + 64][nch]: rows t < 64*TW the
+  // NoSchedule|NoExecute taint id t, rows 64*TW + t the NoExecute taint id t, rows 128*TW + g GVK id g),
+  // so the schedule kernels only test resource fit per lane (or nothing, with SnapDev::fitfold)
   int fold;
-  uint64_t present_taints;    // OR of every cluster's NoSchedule|NoExecute word 0 (host shadow)
+  uint64_t present_taints[TFOLD_MAX_TW];  // per taint word: OR of every cluster's NoSchedule|NoExecute word
   const uint64_t* slices;
-  // [2][8][256][nch]: entry (tbl, g, sub, ch) = OR of the chunk-ch slices of taint ids 8g + b, b in sub,
-  // table tbl (0: NoSchedule|NoExecute, 1: NoExecute) — a unit's untolerated taints in 8 lookups
+  // [2][8*TW][256][nch]: entry (tbl, g, sub, ch) = OR of the chunk-ch slices of taint ids 8g + b, b in sub,
+  // table tbl (0: NoSchedule|NoExecute, 1: NoExecute) — a unit's untolerated taints in <= 8*TW lookups
   const uint64_t* taint_tab;
   // clean snapshots with C <= FITFOLD_MAX_C: ClusterResourcesFit's cpu / memory test as a threshold
   // table per resource r (0 cpu, 1 memory) — fit_vals[r]: the m_r distinct available amounts
@@ -71,6 +74,10 @@ struct BatchDev {
   int32_t* defer;           // [W] units the lean kernel hands to schedule_kernel
   int32_t* defer_n;         // [1] length of defer
   int32_t* work_n;          // [1] lean kernel work queue: next batch of LEAN_BATCH units
+  int use_rows;             // host: schedule_row_kernel runs (clean, folded, fit-folded snapshot, C <= ROW_MAX_C)
+  int32_t* rows;            // [W] units whose feasible list outgrows the lean / wide kernels' registers
+  int32_t* rows_n;          // [1] length of rows (reset by prep_kernel)
+  int32_t* rows_head;       // [1] schedule_row_kernel's dequeue counter (reset by prep_kernel)
   uint32_t* wq;             // [WQ_HEADS * WQ_STRIDE] schedule kernels' work heads (reset by prep_kernel)
 };
 
@@ -138,6 +145,8 @@ hipError_t launch_trigger_objects(const TriggerDev& t, hipStream_t st);
 
 // bytes of per-wave scratch for the filter/score/select kernel at C clusters
 size_t select_wave_bytes(int C);
+// true if schedule_row_kernel can take the long feasible lists of this snapshot (C <= ROW_MAX_C)
+bool row_kernel_fits(int C);
 size_t plan_wave_bytes(int K);
 
 // phase counters of a -DKAD_PHASE_PROF build (returns 0 in product builds)

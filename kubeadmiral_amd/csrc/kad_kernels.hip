@@ -748,55 +748,92 @@ __device__ __forceinline__ void id_list_words(const int32_t* ids, int lo, int hi
   }
 }
 
-// cluster bitmask of id t in table tbl (0: NoSchedule|NoExecute taints, 1: NoExecute taints, 2: GVKs),
-// chunk ch: one wave per (tbl, t, ch), lane = cluster
+// SnapDev::slices row r (r < 64*TW: NoSchedule|NoExecute taint id r; r < 128*TW: NoExecute taint id
+// r - 64*TW; else GVK id r - 128*TW of word 0), chunk ch: one wave per (row, ch), lane = cluster
 __global__ __launch_bounds__(256) void slice_kernel(SnapDev s, uint64_t* out) {
   const int lane = lane_id();
   const int nch = (s.C + 63) >> 6;
+  const int TW = s.TW;
   const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gw >= 3L * 64 * nch) return;
-  const int ch = (int)(gw % nch), t = (int)((gw / nch) % 64), tbl = (int)(gw / (64L * nch));
+  if (gw >= (128L * TW + 64) * nch) return;
+  const int ch = (int)(gw % nch), r = (int)(gw / nch);
   const int c = ch * WAVE + lane;
   const uint32_t cl = c < s.C ? (uint32_t)c : 0u;
-  const uint64_t word = tbl == 0 ? ldg(s.nsne, cl) : (tbl == 1 ? ldg(s.ne, cl) : ldg(s.gvk, cl));
-  const uint64_t m = ballot(c < s.C && ((word >> t) & 1));
-  if (lane == 0) out[((size_t)tbl * 64 + t) * nch + ch] = m;
+  uint64_t word;
+  int bit;
+  if (r < 128 * TW) {
+    const int t = r % (64 * TW);
+    const uint32_t at = (uint32_t)(t >> 6) * (uint32_t)s.C + cl;
+    word = r < 64 * TW ? ldg(s.nsne, at) : ldg(s.ne, at);
+    bit = t & 63;
+  } else {
+    word = ldg(s.gvk, cl);
+    bit = r - 128 * TW;
+  }
+  const uint64_t m = ballot(c < s.C && ((word >> bit) & 1));
+  if (lane == 0) out[(size_t)r * nch + ch] = m;
 }
 
 // SnapDev::taint_tab: lane per (tbl, g, sub, ch); OR over the set bits of sub of slice 8g + b of table tbl
 __global__ __launch_bounds__(256) void taint_table_kernel(SnapDev s, uint64_t* tab) {
   const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
+  const uint32_t ng = 8u * (uint32_t)s.TW;  // 8-id groups per table
   const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  if (g >= 2u * 8 * 256 * nch) return;
-  const uint32_t ch = g % nch, e = g / nch, sub = e & 255u, grp = (e >> 8) & 7u, tbl = e >> 11;
+  if (g >= 2u * ng * 256 * nch) return;
+  const uint32_t ch = g % nch, e = g / nch, sub = e & 255u, grp = (e >> 8) % ng, tbl = (e >> 8) / ng;
   uint64_t m = 0;
-  for (uint32_t r = sub; r; r &= r - 1) m |= s.slices[((size_t)tbl * 64 + grp * 8 + __builtin_ctz(r)) * nch + ch];
+  for (uint32_t r = sub; r; r &= r - 1) m |= s.slices[((size_t)tbl * 8 * ng + grp * 8 + __builtin_ctz(r)) * nch + ch];
   tab[g] = m;
 }
 
 // TaintToleration.Filter (taint_toleration.go:44-89) and APIResources.Filter (apiresources.go:25-43) of
-// unit w on chunk ch (TW == 1): clusters with a NoSchedule|NoExecute taint the unit does not tolerate
-// are out — only NoExecute ones on its CurrentClusters (cw) — and clusters without its GVK. The
-// untolerated present taints are looked up 8 ids at a time in SnapDev::taint_tab (independent loads).
-__device__ __forceinline__ uint64_t folded_word(const SnapDev& s, uint32_t fm, uint32_t f, int gvk, uint64_t tol,
-                                                uint64_t cw, uint32_t nch, uint32_t ch) {
-  uint64_t m = ~0ull;
+// unit w on chunks cc[0..CPL) (TW <= TFOLD_MAX_TW): clusters with a NoSchedule|NoExecute taint the unit
+// does not tolerate are out — only NoExecute ones on its CurrentClusters (cw) — and clusters without its
+// GVK. The untolerated present taints are looked up 8 ids at a time in SnapDev::taint_tab, each lookup
+// serving the lane's CPL chunks (independent loads).
+template <int CPL>
+__device__ __forceinline__ void folded_words(const SnapDev& s, uint32_t fm, uint32_t f, int gvk, const uint64_t* tol,
+                                             const uint64_t (&cw)[CPL], uint32_t nch, const uint32_t (&cc)[CPL],
+                                             uint64_t (&out)[CPL]) {
+#pragma unroll
+  for (int k = 0; k < CPL; k++) out[k] = ~0ull;
   if (fm & (1u << KAD_PL_TAINT_TOLERATION)) {
     const bool cur = f & KAD_W_HAS_CURRENT;
-    const uint64_t u = s.present_taints & ~tol;
-    uint64_t bad_ns = 0, bad_ne = 0;
+    const int TW = s.TW;
+    const size_t ng = (size_t)8 * TW;
+    uint64_t bad_ns[CPL], bad_ne[CPL];
 #pragma unroll
-    for (int gi = 0; gi < 8; gi++) {
-      const uint32_t sub = (uint32_t)(u >> (8 * gi)) & 255u;
-      if (sub) {
-        bad_ns |= s.taint_tab[((size_t)gi * 256 + sub) * nch + ch];
-        if (cur) bad_ne |= s.taint_tab[((size_t)(8 + gi) * 256 + sub) * nch + ch];
+    for (int k = 0; k < CPL; k++) bad_ns[k] = bad_ne[k] = 0;
+    for (int tw = 0; tw < TW; tw++) {
+      const uint64_t u = s.present_taints[tw] & ~tol[tw];
+#pragma unroll
+      for (int gi = 0; gi < 8; gi++) {
+        const uint32_t sub = (uint32_t)(u >> (8 * gi)) & 255u;
+        if (sub) {
+          const uint64_t* rn = s.taint_tab + ((size_t)(8 * tw + gi) * 256 + sub) * nch;
+          uint64_t x[CPL];
+#pragma unroll
+          for (int k = 0; k < CPL; k++) x[k] = rn[cc[k]];
+#pragma unroll
+          for (int k = 0; k < CPL; k++) bad_ns[k] |= x[k];
+          if (cur) {
+            const uint64_t* re = s.taint_tab + ((ng + 8 * tw + gi) * 256 + sub) * nch;
+#pragma unroll
+            for (int k = 0; k < CPL; k++) x[k] = re[cc[k]];
+#pragma unroll
+            for (int k = 0; k < CPL; k++) bad_ne[k] |= x[k];
+          }
+        }
       }
     }
-    m = cur ? ((cw & ~bad_ne) | (~cw & ~bad_ns)) : ~bad_ns;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) out[k] = cur ? ((cw[k] & ~bad_ne[k]) | (~cw[k] & ~bad_ns[k])) : ~bad_ns[k];
   }
-  if (fm & (1u << KAD_PL_API_RESOURCES)) m &= (gvk >= 0 && gvk < 64) ? s.slices[((size_t)128 + gvk) * nch + ch] : 0ull;
-  return m;
+  if (fm & (1u << KAD_PL_API_RESOURCES)) {
+    const uint64_t* rg = s.slices + ((size_t)128 * s.TW + (gvk >= 0 && gvk < 64 ? gvk : 0)) * nch;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) out[k] &= (gvk >= 0 && gvk < 64) ? rg[cc[k]] : 0ull;
+  }
 }
 
 // #(fit_vals[r] < x) for r = 0, 1 (x0, x1): 8 levels over the LDS fences (fence i = value (i+1)*S - 1,
@@ -828,6 +865,8 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   if (g == 0) {
     *b.defer_n = 0;
     *b.work_n = 0;
+    *b.rows_n = 0;
+    *b.rows_head = 0;
   }
   if (g < (uint32_t)WQ_HEADS) b.wq[g * WQ_STRIDE] = 0u;  // the schedule kernels' work heads
   const bool live = g < (uint32_t)b.W * per;
@@ -908,17 +947,26 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
 #pragma unroll
     for (int k = 0; k < CPL; k++) m[k] &= pw[k];
   }
+#pragma unroll
+  for (int k = 0; k < CPL; k++) cwv[k] = 0;
   if (curw) id_list_words<CPL>(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch0, cwv);
+  if (s.fold) {
+    uint32_t cc[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; k++) cc[k] = ch0 + k < nch ? ch0 + k : nch - 1;
+    uint64_t tw[TFOLD_MAX_TW];
+    tw[0] = tol0;
+    for (int t = 1; t < s.TW && t < TFOLD_MAX_TW; t++) tw[t] = b.tol_all[(size_t)tolset * b.TW + t];
+    uint64_t fw[CPL];
+    folded_words<CPL>(s, fm, f, gvk, tw, cwv, nch, cc, fw);
+#pragma unroll
+    for (int k = 0; k < CPL; k++) m[k] &= fw[k];
+  }
 #pragma unroll
   for (int k = 0; k < CPL; k++) {
     const uint32_t ch = ch0 + k;
     if (ch >= nch) break;
-    uint64_t cw = 0;
-    if (curw) {
-      cw = cwv[k];
-      b.cw[(size_t)w * nch + ch] = cw;
-    }
-    if (s.fold) m[k] &= folded_word(s, fm, f, gvk, tol0, cw, nch, ch);
+    if (curw) b.cw[(size_t)w * nch + ch] = cwv[k];
     if (ch == nch - 1 && (s.C & 63)) m[k] &= (1ull << (s.C & 63)) - 1;  // clusters past C: never feasible
     b.sw[(size_t)w * nch + ch] = m[k];
   }
@@ -1064,6 +1112,21 @@ __device__ __forceinline__ void lean_defer(int w) {
     LArgs a = largs();
     const int slot = atomicAdd(a->b.defer_n, 1);
     a->b.defer[slot] = w;
+  }
+}
+
+// feasible lists longer than the kernel's register positions: the row kernel's list when it runs
+// (BatchDev::use_rows: every filter is in the static words), else the full kernel's defer list
+__device__ __forceinline__ void lean_row_or_defer(int w) {
+  if (lane_id() == 0) {
+    LArgs a = largs();
+    if (a->b.use_rows) {
+      const int slot = atomicAdd(a->b.rows_n, 1);
+      a->b.rows[slot] = w;
+    } else {
+      const int slot = atomicAdd(a->b.defer_n, 1);
+      a->b.defer[slot] = w;
+    }
   }
 }
 
@@ -1262,17 +1325,24 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     // chunk ch is filtered (software pipeline; one exposed round trip per unit)
     int64_t p_ac = 0, p_uc = 0, p_am = 0, p_um = 0;
     uint64_t p_ns = 0, p_ne = 0, p_gv = 0;
-    if constexpr (NCH == 0) {
-      LArgs a = largs();
-      const uint32_t cl = lane < C ? (uint32_t)lane : 0u;
-      p_ac = ldg(a->s.alloc_cpu, cl);
-      p_uc = ldg(a->s.used_cpu, cl);
-      p_am = ldg(a->s.alloc_mem, cl);
-      p_um = ldg(a->s.used_mem, cl);
-      p_ns = ldg(a->s.nsne, cl);
-      p_ne = ldg(a->s.ne, cl);
-      p_gv = ldg(a->s.gvk, cl);
-    }
+    // NCH == 0: the attributes of chunk cn (lanes = its clusters) that the mode's filters read: none
+    // when every filter is in the static words (FITF), the resources only with FOLD
+    auto load_attrs = [&](auto mode_t, int cn) {
+      constexpr int MODE = decltype(mode_t)::value;
+      if constexpr (MODE != 3) {
+        LArgs a = largs();
+        const uint32_t cl = cn < C ? (uint32_t)cn : 0u;
+        p_ac = ldg(a->s.alloc_cpu, cl);
+        p_uc = ldg(a->s.used_cpu, cl);
+        p_am = ldg(a->s.alloc_mem, cl);
+        p_um = ldg(a->s.used_mem, cl);
+        if constexpr (MODE < 2) {
+          p_ns = ldg(a->s.nsne, cl);
+          p_ne = ldg(a->s.ne, cl);
+          p_gv = ldg(a->s.gvk, cl);
+        }
+      }
+    };
     // the chunk loop twice: FAST (no CurrentClusters, one taint word) has no
     // uniform branch inside, so the cache reads of every chunk issue together
     // MODE 2 (FOLD): taint and API filters already in the static words (prep_kernel, SnapDev::fold);
@@ -1281,6 +1351,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       constexpr int MODE = decltype(mode_t)::value;
       constexpr bool FAST = MODE >= 1, FOLD = MODE >= 2, FITF = MODE == 3;
       const bool ucur = !FAST && use_cur;
+      if constexpr (NCH == 0) load_attrs(mode_t, lane);
 #pragma unroll
       for (int ch = 0; ch < NC; ++ch) {
         const int c = ch * WAVE + lane;
@@ -1306,18 +1377,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           ne0 = p_ne;
           gv0 = p_gv;
           pn0 = 0;
-          if (ch + 1 < NC) {
-            LArgs a = largs();
-            const int cn = c + WAVE;
-            const uint32_t cl = cn < C ? (uint32_t)cn : 0u;
-            p_ac = ldg(a->s.alloc_cpu, cl);
-            p_uc = ldg(a->s.used_cpu, cl);
-            p_am = ldg(a->s.alloc_mem, cl);
-            p_um = ldg(a->s.used_mem, cl);
-            p_ns = ldg(a->s.nsne, cl);
-            p_ne = ldg(a->s.ne, cl);
-            p_gv = ldg(a->s.gvk, cl);
-          }
+          if (ch + 1 < NC) load_attrs(mode_t, c + WAVE);
           if (ch > 0 && (ch & 63) == 0) load_words(ch);
           sw0 = readlane64(dsw, ch & 63);
           cw0 = readlane64(dcw, ch & 63);
@@ -1357,6 +1417,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
             if (pos < P) idx[pos] = (uint16_t)c;  // more than P feasible: the unit is deferred
           }
           n += popc64(m);
+          if (n > P) break;  // deferred whatever the remaining chunks hold
         }
       }
     };
@@ -1382,8 +1443,8 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       lean_status(w, KAD_ST_NO_FEASIBLE);
       continue;
     }
-    if (NCH == 0 && n > P) {
-      lean_defer(w);
+    if (NCH == 0 && n > P) {  // more feasible clusters than registers: the row kernel (or the full kernel)
+      lean_row_or_defer(w);
       continue;
     }
     if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && (fc & KAD_W_SCORE_ERROR)) {  // framework.go:149-159
@@ -1784,6 +1845,19 @@ __device__ __forceinline__ void wide_defer(int w) {
   }
 }
 
+__device__ __forceinline__ void wide_row_or_defer(int w) {
+  if (lane_id() == 0) {
+    WArgs a = wargs();
+    if (a->b.use_rows) {
+      const int slot = atomicAdd(a->b.rows_n, 1);
+      a->b.rows[slot] = w;
+    } else {
+      const int slot = atomicAdd(a->b.defer_n, 1);
+      a->b.defer[slot] = w;
+    }
+  }
+}
+
 template <int NCH>
 __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs args) {
   (void)args;  // read through wargs()
@@ -1993,7 +2067,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         break;
       }
       if (n > P) {
-        wide_defer(w);
+        wide_row_or_defer(w);
         break;
       }
       if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && (fc & KAD_W_SCORE_ERROR)) {  // framework.go:149-159
@@ -2239,6 +2313,365 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     w = wn;
   }
   KAD_PFLUSH_LEAN;
+}
+
+
+// ================================================== row schedule kernel
+// schedule_row_kernel — the units whose feasible list is longer than the lean / wide kernels' register
+// positions (C5: 16 % of the units, a few thousand feasible clusters of 10 000), on snapshots where
+// every filter is in the static words (BatchDev::use_rows: clean, SnapDev::fold and ::fitfold,
+// C <= ROW_MAX_C). One 1024-thread workgroup per unit, persistent (units dequeued from BatchDev::rows):
+//   * compaction: the unit's static words → per-chunk popcounts → block prefix → cluster ids in LDS
+//     (findClustersThatFitWorkload order, generic_scheduler.go:152-169);
+//   * scores spread over the 16 waves (RunScorePlugins, framework.go:139-181), the clean-snapshot
+//     arithmetic of the wide kernel (exact f64 quotients, 32-bit totals), block maxima for
+//     DefaultNormalizeScore (framework/util.go:455-483);
+//   * MaxCluster (max_cluster.go:42-66): the k-th largest total by a block-wide 8-bit radix histogram;
+//     the cut takes every tie, or wave 0 replays Go's pdqsort restricted to k (PdqWave) on the LDS keys;
+//   * output in ascending cluster id by per-chunk ballots and a block prefix.
+// Units outside the clean-f64 range (requests >= 2^46, wide affinity weights) go on to the defer list.
+constexpr int ROW_THREADS = 1024;
+constexpr int ROW_WAVES = ROW_THREADS / 64;
+constexpr int ROW_MAX_C = 12288;
+struct RowKLayout {
+  size_t key, idx, pid, posl, posr, sw, cnt, hist, red, bytes;
+};
+__host__ __device__ inline RowKLayout rowk_layout(int C) {
+  const size_t Cp = (size_t)((C + 63) & ~63), nch = Cp / 64;
+  RowKLayout L;
+  L.key = 0;                              // u32[Cp]: fixed | TT raw << 16, then totals (sign-flipped), replay keys
+  L.idx = L.key + 4 * Cp;                 // u16[Cp]: position → cluster id
+  L.pid = L.idx + 2 * Cp;                 // u16[Cp]: replay: original position
+  L.posl = L.pid + 2 * Cp;                // u16[Cp + 64] replay scratch, then ranks; with posr: i32 affinity raw
+  L.posr = L.posl + 2 * Cp + 128;         // u16[Cp]
+  L.sw = (L.posr + 2 * Cp + 15) & ~(size_t)15;  // u64[nch]: the unit's static words
+  L.cnt = L.sw + 8 * nch;                 // i32[nch + 1]: chunk counts → exclusive prefix (+ total)
+  L.hist = (L.cnt + 4 * (nch + 1) + 15) & ~(size_t)15;  // u32[256]
+  L.red = L.hist + 4 * 256;               // i32[4][ROW_WAVES] per-wave partials, i32[8] broadcasts
+  L.bytes = L.red + 4 * (4 * ROW_WAVES + 8);
+  return L;
+}
+size_t row_kernel_lds(int C) { return rowk_layout(C).bytes; }
+bool row_kernel_fits(int C) { return C > 0 && C <= ROW_MAX_C; }
+
+struct RowArgs {
+  SnapDev s;
+  BatchDev b;
+  OutDev o;
+  ProfDev p;
+};
+typedef const __attribute__((address_space(4))) RowArgs* RArgs;
+__device__ __forceinline__ RArgs rargs() {
+  return (RArgs)opq((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
+}
+
+// block-wide reductions of one i32 per thread: wave partials in red[ROW_WAVES], every thread reads all
+__device__ __forceinline__ int row_block_max(int v, int* red) {
+  const int r = wave_max_u_i32(v);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = r;
+  __syncthreads();
+  int m = red[0];
+#pragma unroll
+  for (int i = 1; i < ROW_WAVES; ++i) m = red[i] > m ? red[i] : m;
+  __syncthreads();
+  return m;
+}
+__device__ __forceinline__ int row_block_min(int v, int* red) { return -row_block_max(-v, red); }
+__device__ __forceinline__ int row_block_sum(int v, int* red) {
+  const int r = wave_sum_u_i32(v);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = r;
+  __syncthreads();
+  int m = 0;
+#pragma unroll
+  for (int i = 0; i < ROW_WAVES; ++i) m += red[i];
+  __syncthreads();
+  return m;
+}
+// exclusive prefix of cnt[0..m) in place by wave 0, total in cnt[m]; callers sync before and after
+__device__ __forceinline__ void row_exclusive_scan(int* cnt, int m) {
+  if ((threadIdx.x >> 6) != 0) return;
+  const int lane = lane_id();
+  int carry = 0;
+  for (int c0 = 0; c0 < m; c0 += WAVE) {
+    const int i = c0 + lane;
+    const int v = i < m ? cnt[i] : 0;
+    const int inc = wave_incl_sum_i32(v);
+    if (i < m) cnt[i] = carry + inc - v;
+    carry += __builtin_amdgcn_readlane(inc, 63);
+  }
+  if (lane == 0) cnt[m] = carry;
+}
+
+__global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs args) {
+  (void)args;  // read through rargs()
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int C, TW;
+  uint32_t fm, sm;
+  {
+    RArgs a = rargs();
+    C = a->s.C;
+    TW = a->s.TW;
+    fm = a->p.filter_mask;
+    sm = a->p.score_mask;
+  }
+  (void)fm;
+  const int nch = (C + 63) >> 6;
+  const RowKLayout L = rowk_layout(C);
+  uint32_t* key = (uint32_t*)(smem + L.key);
+  uint16_t* idx = (uint16_t*)(smem + L.idx);
+  uint16_t* pid = (uint16_t*)(smem + L.pid);
+  uint16_t* posl = (uint16_t*)(smem + L.posl);
+  uint16_t* posr = (uint16_t*)(smem + L.posr);
+  int32_t* aff = (int32_t*)(smem + L.posl);  // i32[Cp] over posl | posr while scoring
+  uint16_t* inv = posl;                      // ranks after the replay
+  uint64_t* swl = (uint64_t*)(smem + L.sw);
+  int32_t* cnt = (int32_t*)(smem + L.cnt);
+  uint32_t* hist = (uint32_t*)(smem + L.hist);
+  int32_t* red = (int32_t*)(smem + L.red);
+  int32_t* bc = red + 4 * ROW_WAVES;  // broadcasts
+  const bool s_res =
+      sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
+  const bool s_tt = sm & BIT(KAD_PL_TAINT_TOLERATION);
+
+  for (;;) {
+    __syncthreads();  // the previous unit's LDS reads are done
+    if (tid == 0) {
+      RArgs a = rargs();
+      const int i = atomicAdd(a->b.rows_head, 1);
+      bc[0] = i < __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? a->b.rows[i] : -1;
+    }
+    __syncthreads();
+    const int w = __builtin_amdgcn_readfirstlane(bc[0]);
+    if (w < 0) break;
+    RArgs a = rargs();
+    const UnitRec* rec = a->b.rec + w;
+    const uint32_t fc = ldc(&rec->flags);
+    const int64_t rqc = ldc(&rec->req_cpu), rqm = ldc(&rec->req_mem);
+    if ((uint64_t)rqc >= (1ull << 46) || (uint64_t)rqm >= (1ull << 46) || (fc & KAD_W_WIDE_SCORES)) {
+      if (tid == 0) {  // outside the exact clean-f64 range: the full kernel
+        const int slot = atomicAdd(a->b.defer_n, 1);
+        a->b.defer[slot] = w;
+      }
+      continue;
+    }
+    const int tsc = ldc(&rec->tolset), spo = ldc(&rec->sprog_off);
+    const int64_t mc = ldc(&rec->maxc), ooff = ldc(&rec->out_off);
+    auto status = [&](int32_t st) {
+      if (tid == 0) {
+        RArgs ao = rargs();
+        ao->o.status[w] = st;
+        ao->o.count[w] = 0;
+        ao->o.flags[w] = 0;
+      }
+    };
+
+    // ---------------- compaction of the static words (every filter folded by prep_kernel)
+    for (int ch = tid; ch < nch; ch += ROW_THREADS) {
+      const uint64_t m = ldg(a->b.sw, (uint32_t)(w * nch + ch));
+      swl[ch] = m;
+      cnt[ch] = popc64(m);
+    }
+    __syncthreads();
+    row_exclusive_scan(cnt, nch);
+    __syncthreads();
+    const int n = __builtin_amdgcn_readfirstlane(cnt[nch]);
+    for (int ch = wv; ch < nch; ch += ROW_WAVES) {
+      const uint64_t m = swl[ch];
+      if (lane_on(m)) idx[cnt[ch] + mbcnt(m)] = (uint16_t)(ch * WAVE + lane);
+    }
+    if (n == 0) {  // generic_scheduler.go:112-114
+      status(KAD_ST_NO_FEASIBLE);
+      continue;
+    }
+    if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && (fc & KAD_W_SCORE_ERROR)) {  // framework.go:149-159
+      status(KAD_ST_ERR_SCORE);
+      continue;
+    }
+    int k = n;
+    if (a->p.select_plugin == KAD_PL_MAX_CLUSTER) {
+      const bool hm = fc & KAD_W_HAS_MAX_CLUSTERS;
+      if (hm && mc < 0) {
+        status(KAD_ST_ERR_SELECT);
+        continue;
+      }
+      if (hm && mc < k) k = (int)mc;
+    }
+    __syncthreads();
+
+    // ---------------- raw scores (RunScorePlugins, framework.go:139-181)
+    const int32_t* sp = a->b.sprog + spo;
+    const bool s_aff = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && ldc(sp) > 0;  // no preferred terms: 0 everywhere
+    const double rqcd = (double)rqc, rqmd = (double)rqm;
+    int ttmax = 0, amax = 0;
+    for (int j = tid; j < n; j += ROW_THREADS) {
+      RArgs as = rargs();
+      const uint32_t c = idx[j];
+      int x = 0;
+      if (s_res) {  // the wide kernel's clean path: x = available - request, exact in f64
+        const int64_t ac = ldg(as->s.alloc_cpu, c), uc = ldg(as->s.used_cpu, c);
+        const int64_t am = ldg(as->s.alloc_mem, c), um = ldg(as->s.used_mem, c);
+        const double capc = (double)ac, capm = (double)am;
+        const double xc = (double)(ac - uc) - rqcd, xm = (double)(am - um) - rqmd;
+        const float ivc = (float)(100.0 / capc), ivm = (float)(100.0 / capm);
+        const double xcp = fmax(xc, 0.0), xmp = fmax(xm, 0.0);
+        const int okc = -(int)(xc >= 0.0), okm = -(int)(xm >= 0.0);
+        if (sm & BIT(KAD_PL_LEAST_ALLOCATED)) x += (quot100(xcp, capc, ivc) + quot100(xmp, capm, ivm)) >> 1;
+        if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+          x += ((quot100(capc - xcp, capc, ivc) & okc) + (quot100(capm - xmp, capm, ivm) & okm)) >> 1;
+        if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x += (int)balanced_d((capc - xc) / capc, (capm - xm) / capm);
+      }
+      int tc = 0;
+      if (s_tt)  // taint_toleration.go:91-118: PreferNoSchedule taints not tolerated
+        for (int tw = 0; tw < TW; ++tw)
+          tc += popc64(ldg(as->s.pns, (uint32_t)(tw * C) + c) & ~ldc(as->b.tol_pns + (size_t)tsc * TW + tw));
+      key[j] = (uint32_t)x | ((uint32_t)tc << 16);
+      ttmax = tc > ttmax ? tc : ttmax;
+      if (s_aff) {  // cluster_affinity.go:96-135; |raw| <= 2^20 (wider units were deferred above)
+        const int af = (int)affinity_score(as->b.req_mask, sp, nch, (int)c);
+        aff[j] = af;
+        amax = af > amax ? af : amax;
+      }
+    }
+    if (s_tt) ttmax = row_block_max(ttmax, red);
+    if (s_aff) amax = row_block_max(amax, red);
+
+    // ---------------- DefaultNormalizeScore + totals, stored order-preserving as u32 (total ^ 2^31)
+    int mn = INT32_MAX, mx = INT32_MIN;
+    for (int j = tid; j < n; j += ROW_THREADS) {
+      const uint32_t x = key[j];
+      int t = (int)(x & 0xFFFFu);
+      if (s_tt) t += ttmax == 0 ? 100 : 100 - (int)small_quot(100 * (int)(x >> 16), ttmax);
+      if (s_aff) {
+        const int af = aff[j];
+        const int num = 100 * af;
+        t += amax == 0 ? af : (num >= 0 && num < (1 << 24) ? (int)small_quot(num, amax) : num / amax);
+      }
+      key[j] = (uint32_t)t ^ 0x80000000u;
+      mn = t < mn ? t : mn;
+      mx = t > mx ? t : mx;
+    }
+    mn = row_block_min(mn, red);
+    mx = row_block_max(mx, red);
+
+    // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
+    // mode: -1 nothing, 0 all, 1 total >= T, 3 replay ranks < k
+    int mode = k >= n ? 0 : (k <= 0 ? -1 : 1);
+    uint32_t rflags = 0;
+    uint32_t Tk = 0;  // the k-th largest total, sign-flipped
+    if (mode == 1) {
+      const uint32_t base = (uint32_t)mn ^ 0x80000000u;
+      const uint32_t span = (uint32_t)mx - (uint32_t)mn;
+      uint32_t prefix = 0, pmask = 0;
+      int kk = k;
+      if (span != 0) {
+        const int bits = 32 - __builtin_clz(span);
+        for (int shift = ((bits + 7) / 8 - 1) * 8; shift >= 0; shift -= 8) {
+          if (tid < 256) hist[tid] = 0;
+          __syncthreads();
+          for (int j = tid; j < n; j += ROW_THREADS) {
+            const uint32_t d = key[j] - base;
+            if ((d & pmask) == prefix) atomicAdd(&hist[(d >> shift) & 255u], 1u);
+          }
+          __syncthreads();
+          if (wv == 0) {  // lane l owns digits 255-4l .. 252-4l (descending)
+            int h[4], s4 = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              h[q] = (int)hist[255 - 4 * lane - q];
+              s4 += h[q];
+            }
+            const int incl = wave_incl_sum_i32(s4);
+            const int excl = incl - s4;
+            if (excl < kk && kk <= incl) {
+              int cum = excl;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                if (cum + h[q] >= kk) {
+                  bc[1] = 255 - 4 * lane - q;
+                  bc[2] = cum;
+                  break;
+                }
+                cum += h[q];
+              }
+            }
+          }
+          __syncthreads();
+          const int digit = __builtin_amdgcn_readfirstlane(bc[1]), above = __builtin_amdgcn_readfirstlane(bc[2]);
+          kk -= above;
+          prefix |= (uint32_t)digit << shift;
+          pmask |= 255u << shift;
+        }
+      }
+      Tk = base + prefix;
+      int g = 0, e = 0;
+      for (int j = tid; j < n; j += ROW_THREADS) {
+        const uint32_t t = key[j];
+        g += t > Tk;
+        e += t == Tk;
+      }
+      g = row_block_sum(g, red);
+      e = row_block_sum(e, red);
+      if (k - g != e) {  // ties straddle the cut: Go's pdqsort decides which tied clusters stay (n > 256)
+        rflags = KAD_RF_TIE_STRADDLE;
+        mode = 3;
+        for (int j = tid; j < n; j += ROW_THREADS) pid[j] = (uint16_t)j;
+        __syncthreads();
+        if (wv == 0) {
+          const int xs_b = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
+          const int xs_c = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+          PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
+          pw.select(n, k);
+        }
+        __syncthreads();
+        for (int r = tid; r < n; r += ROW_THREADS) inv[pid[r]] = (uint16_t)r;
+        __syncthreads();
+      }
+    }
+
+    // ---------------- output, ascending cluster id (= ascending position)
+    const bool dup = fc & KAD_W_DUPLICATE;
+    const bool replicas =
+        !dup && a->p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (fc & REC_DESIRED_POS) && k > 0;
+    int total = 0;
+    if ((dup || replicas) && mode >= 0) {
+      const int nq = (n + 63) >> 6;
+      auto selected = [&](int p) -> bool {
+        if (p >= n) return false;
+        if (mode == 0) return true;
+        if (mode == 1) return key[p] >= Tk;
+        return inv[p] < k;
+      };
+      for (int q = wv; q < nq; q += ROW_WAVES) {
+        const uint64_t m = ballot(selected(q * WAVE + lane));
+        if (lane == 0) cnt[q] = popc64(m);
+      }
+      __syncthreads();
+      row_exclusive_scan(cnt, nq);
+      __syncthreads();
+      total = __builtin_amdgcn_readfirstlane(cnt[nq]);
+      RArgs ao = rargs();
+      int32_t* oc = ao->o.cluster + ooff;
+      int64_t* orp = ao->o.replicas + ooff;
+      for (int q = wv; q < nq; q += ROW_WAVES) {
+        const int p = q * WAVE + lane;
+        const bool s = selected(p);
+        const uint64_t m = ballot(s);
+        if (s) {
+          const uint32_t at = (uint32_t)(cnt[q] + mbcnt(m));
+          stg(oc, at, (int32_t)idx[p]);
+          stg(orp, at, (int64_t)(dup ? -1 : 0));
+        }
+      }
+    }
+    if (tid == 0) {
+      RArgs ao = rargs();
+      ao->o.status[w] = KAD_ST_OK;
+      ao->o.count[w] = total;  // Divide without replicas plugin: empty map
+      ao->o.flags[w] = rflags;
+    }
+  }
 }
 
 // ============================================================ plan kernel
@@ -2766,12 +3199,12 @@ hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st)
 hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
-  const long waves = 3L * 64 * nch;
+  const long waves = (128L * s.TW + 64) * nch;
   if (waves == 0) return hipSuccess;
   hipLaunchKernelGGL(slice_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, slices);
-  const long lanes = 2L * 8 * 256 * nch;
+  const long lanes = 2L * 8 * s.TW * 256 * nch;
   hipLaunchKernelGGL(taint_table_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, s,
-                     slices + 3L * 64 * nch);
+                     slices + (128L * s.TW + 64) * nch);
   return hipGetLastError();
 }
 
@@ -2829,6 +3262,29 @@ static hipError_t launch_defer_pass(const SnapDev& s, const BatchDev& b, const O
   return hipGetLastError();
 }
 
+// schedule_row_kernel over BatchDev::rows (its length is only known on the device: the persistent
+// workgroups dequeue until the list is drained)
+static hipError_t launch_rows(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, hipStream_t st) {
+  if (!b.use_rows) return hipSuccess;
+  const size_t lds = row_kernel_lds(s.C);
+  static bool attr = false;
+  if (!attr) {
+    if (hipError_t e = hipFuncSetAttribute((const void*)schedule_row_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024))
+      return e;
+    attr = true;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_row_kernel, ROW_THREADS, lds) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  long grid = (long)n_cus() * per_cu;
+  if (grid > b.W) grid = b.W;
+  const RowArgs A{s, b, o, p};
+  hipLaunchKernelGGL(schedule_row_kernel, dim3((unsigned)grid), dim3(ROW_THREADS), lds, st, A);
+  return hipGetLastError();
+}
+
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
                            size_t scr_bytes, hipStream_t st, hipEvent_t after_main) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
@@ -2860,6 +3316,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (hipError_t e = hipGetLastError()) return e;
     if (after_main)
       if (hipError_t e = hipEventRecord(after_main, st)) return e;
+    if (hipError_t e = launch_rows(s, b, o, p, st)) return e;
     // feasible lists longer than WIDE_P positions can come from any unit: the defer pass always runs
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);
   }
@@ -2906,6 +3363,8 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     // nothing can be deferred (host-checked: every unit and cluster is in the
     // lean kernel's range and every feasible list fits its registers)
     if (nch <= 4 && !b.may_defer) return hipSuccess;
+    if (nch > 4)
+      if (hipError_t e = launch_rows(s, b, o, p, st)) return e;
     // the defer list: its length is only known on the device, so the grid
     // strides over it (waves past its end exit at once)
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);

@@ -232,13 +232,14 @@ def make_config(config: str, scale: float = 1.0, seed: Optional[int] = None, W: 
 
 
 # ------------------------------------------------------------------- fuzz
-def gen_fuzz(seed: int, W: int = 60, C: Optional[int] = None):
+def gen_fuzz(seed: int, W: int = 60, C: Optional[int] = None, n_taints: int = 9):
     """Small batch hitting every branch: all operators, invalid requirements, nil/empty terms, fields,
-    sticky, current clusters, scalars, NoExecute on scheduled clusters, ties, weights/min/max/caps."""
+    sticky, current clusters, scalars, NoExecute on scheduled clusters, ties, weights/min/max/caps.
+    n_taints > 64 spreads the taint ids over several 64-bit words (SnapDev::TW > 1)."""
     rng = np.random.default_rng(seed)
     C = C if C is not None else int(rng.integers(1, 40))
-    cl = gen_clusters(rng, C, n_keys=4, n_vals=3, n_int_keys=2, n_taints=9, taints_per=(0, 3), p_gvk=0.8,
-                      gvks=GVKS[:3], scalars=True)
+    cl = gen_clusters(rng, C, n_keys=4, n_vals=3, n_int_keys=2, n_taints=n_taints,
+                      taints_per=(0, 3) if n_taints <= 9 else (1, 12), p_gvk=0.8, gvks=GVKS[:3], scalars=True)
     # make scores tie-heavy: quantise resources on some clusters
     for c in cl:
         if rng.random() < 0.5:
@@ -311,7 +312,8 @@ def gen_fuzz(seed: int, W: int = 60, C: Optional[int] = None):
                                         int(rng.integers(0, 2)) if r() < 0.1 else 0, scal),
             current_clusters=cur, auto_migration=am, scheduling_mode=mode, sticky_cluster=bool(r() < 0.1),
             avoid_disruption=bool(r() < 0.5), cluster_selector=sel, cluster_names=place, affinity=aff,
-            tolerations=_tolerations(rng, 9, 0, 3, allow_wild=True) if r() < 0.8 else None,
+            tolerations=(_tolerations(rng, n_taints, 0, 3 if n_taints <= 9 else 10, allow_wild=True)
+                         if r() < 0.8 else None),
             max_clusters=(int(rng.integers(-1, 8)) if r() < 0.8 else None), min_replicas=mins, max_replicas=maxs,
             weights=weights))
     return cl, units

@@ -279,6 +279,35 @@ def test_config_shaped_gpu_equals_python_oracle(ctx, cfg, W, C):
         assert same(got, want[w]), (cfg, w, got, want[w])
 
 
+@pytest.mark.parametrize("seed,C,n_taints", [(5101, 40, 160), (5102, 300, 180), (5103, 1500, 120),
+                                             (5104, 200, 100), (5105, 5000, 100), (5103, 1500, 200)])
+def test_fuzz_many_taint_words(ctx, seed, C, n_taints):
+    """Taint ids spread over 2-4 words (SnapDev::TW > 1): prep folds TaintToleration from the 8-id group
+    tables of every word (NoExecute table for units with CurrentClusters), for the lean (NCH = 1..4 and 0)
+    and wide kernels, against the C oracle under every fuzz profile; TW > 4 (the last case) runs unfolded."""
+    clusters, units = synth.gen_fuzz(seed, W=120, C=C, n_taints=n_taints)
+    for i in range(len(synth.FUZZ_PROFILES)):
+        fwk = synth.fuzz_framework(i)
+        snap, batch, res = run(ctx, clusters, units, fwk)
+        assert snap.TW >= 2
+        assert_same(res, c_oracle(snap, batch, fwk), f"many taints seed {seed} C={C} profile {i}")
+
+
+@pytest.mark.parametrize("seed,C,prof", [(6101, 9000, 1), (6102, 3000, 2), (6103, 12000, 3), (6104, 1000, 1),
+                                         (6105, 12289, 1)])
+def test_row_kernel_long_feasible_lists(ctx, seed, C, prof):
+    """Feasible lists longer than the lean (256) / wide (512) kernels' registers go to
+    schedule_row_kernel (one workgroup per unit) on folded snapshots: tie-heavy fuzz clusters (half of
+    them share one resource shape) so the k-th largest total cuts ties and wave 0 replays pdqsort over
+    thousands of positions. C = 12289 is past ROW_MAX_C (those rows take the full kernel)."""
+    clusters, units = synth.gen_fuzz(seed, W=300, C=C)
+    fwk = synth.fuzz_framework(prof)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    ok = res.status == pack.ST_OK
+    assert (res.count[ok] > 0).any()
+    assert_same(res, c_oracle(snap, batch, fwk), f"rows seed {seed} C={C} profile {prof}")
+
+
 def test_large_c_global_scratch(ctx):
     """C = 6000 does not fit the per-wave LDS budget: rows run from global scratch slabs."""
     clusters, units = synth.gen_fuzz(4242, W=200, C=6000)
