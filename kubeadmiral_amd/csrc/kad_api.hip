@@ -42,6 +42,9 @@ struct kad_ctx {
   size_t out_w_cap = 0, out_slot_cap = 0;
   uint64_t* d_req_mask = nullptr;
   size_t req_mask_cap = 0;
+  std::vector<int32_t> h_reqseg;  // BatchDev::req_perm [NR][8] then req_seg [n_seg][4] (host copy until the next upload)
+  void* d_reqseg = nullptr;
+  size_t reqseg_cap = 0;
   void* d_rec = nullptr;  // UnitRec[W] (prep_kernel)
   size_t rec_cap = 0;
   void* d_sw = nullptr;   // u64[W][nch] static filter words (prep_kernel)
@@ -342,7 +345,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -720,6 +723,53 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   }
   const size_t nch = (size_t)((c->sd.C + 63) / 64);
   if (int r = grow(c, (void**)&c->d_req_mask, &c->req_mask_cap, (size_t)h.n_reqs * nch * 8)) return r;
+  // requirements grouped by label key (req_mask_kernel: one label-row load per segment and chunk):
+  // a counting sort by key (the label-free ops last, as key -1), cut into segments of <= seg_len ids;
+  // shorter segments when the batch has few requirements, so the grid still fills the chip
+  int n_seg = 0;
+  {
+    const int NR = h.n_reqs, K = c->snap_hdr.n_label_keys;
+    const int32_t* ro = at<int32_t>(blob, h.off, KAD_B_REQ_OFF);
+    const int32_t* rq = at<int32_t>(blob, h.off, KAD_B_REQ);
+    auto group = [&](int r) {
+      const int op = rq[ro[r]] & 0xff;
+      return (op == KAD_OP_TRUE || op == KAD_OP_FALSE || op == KAD_OP_NAME_EQ || op == KAD_OP_NAME_NE) ? K : rq[ro[r] + 1];
+    };
+    std::vector<int32_t> start((size_t)K + 2, 0);
+    for (int r = 0; r < NR; r++) start[(size_t)group(r) + 1]++;
+    for (int g = 0; g <= K; g++) start[(size_t)g + 1] += start[g];
+    const long ngrp = ((long)nch + REQ_SEG_G - 1) / REQ_SEG_G;
+    int seg_len = 64;
+    while (seg_len > 8 && (long)NR * ngrp / seg_len < 16384) seg_len /= 2;
+    long segs = 0;
+    for (int g = 0; g <= K; g++) segs += (start[(size_t)g + 1] - start[g] + seg_len - 1) / seg_len;
+    // entry e of req_perm: 8 words (id, word offset, op | n << 8, key word, payload 0..3) so a lane
+    // fetches its requirement with two 16-B loads, independent of the segment's label-row loads
+    const size_t perm_len = (size_t)NR * 8;
+    c->h_reqseg.assign(perm_len + 4 * (size_t)segs, 0);
+    std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    for (int r = 0; r < NR; r++) {
+      int32_t* e = c->h_reqseg.data() + 8 * (size_t)fill[(size_t)group(r)]++;
+      const int32_t* q = rq + ro[r];
+      const int n = (int)((uint32_t)q[0] >> 8);
+      e[0] = r;
+      e[1] = ro[r];
+      e[2] = q[0];
+      e[3] = q[1];
+      for (int t = 0; t < 4 && t < n; t++) e[4 + t] = q[2 + t];
+    }
+    int32_t* sg = c->h_reqseg.data() + perm_len;
+    for (int g = 0; g <= K; g++)
+      for (int f = start[g]; f < start[(size_t)g + 1]; f += seg_len) {
+        sg[4 * n_seg] = g == K ? -1 : g;
+        sg[4 * n_seg + 1] = f;
+        sg[4 * n_seg + 2] = start[(size_t)g + 1] - f < seg_len ? start[(size_t)g + 1] - f : seg_len;
+        n_seg++;
+      }
+    if (int r = grow(c, &c->d_reqseg, &c->reqseg_cap, c->h_reqseg.size() * 4 + 16)) return r;
+    if (!c->h_reqseg.empty())
+      HIPCHK(c, hipMemcpyAsync(c->d_reqseg, c->h_reqseg.data(), c->h_reqseg.size() * 4, hipMemcpyHostToDevice, c->stream));
+  }
   if (int r = grow(c, &c->d_rec, &c->rec_cap, (size_t)W * sizeof(UnitRec))) return r;
   if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
@@ -768,6 +818,9 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   b.req_off = at<int32_t>(base, h.off, KAD_B_REQ_OFF);
   b.req = at<int32_t>(base, h.off, KAD_B_REQ);
   b.req_mask = c->d_req_mask;
+  b.n_seg = n_seg;
+  b.req_perm = static_cast<const int32_t*>(c->d_reqseg);
+  b.req_seg = reinterpret_cast<const int4*>(static_cast<const int32_t*>(c->d_reqseg) + (size_t)h.n_reqs * 8);
   b.rec = static_cast<UnitRec*>(c->d_rec);
   b.sw = static_cast<uint64_t*>(c->d_sw);
   b.cw = static_cast<uint64_t*>(c->d_cw);

@@ -13,7 +13,8 @@ constexpr int FITFOLD_MAX_C = 16384;
 constexpr int TFOLD_MAX_TW = 4;
 // unit work queue of the schedule kernels: WQ_HEADS counters, one 128-B line apart (BatchDev::wq)
 constexpr int WQ_HEADS = 64, WQ_STRIDE = 32;
-constexpr int FIT_FENCES = 256;  // prep_kernel's LDS copy of every (fit_mp / 256)-th fit value
+constexpr int FIT_FENCES = 256;
+constexpr int REQ_SEG_G = 8;  // chunks per req_mask_kernel wave (kad_kernels.hip REQ_G)  // prep_kernel's LDS copy of every (fit_mp / 256)-th fit value
 
 struct SnapDev {
   int C, GW, TW, K, S;
@@ -66,6 +67,13 @@ struct BatchDev {
   const int64_t* out_off;
   int NR;                   // distinct requirements
   const int32_t *req_off, *req;
+  // requirements grouped by label key (host, at upload): req_perm lists the requirements key by key as
+  // 8-word entries (id, word offset, op | n << 8, key word, payload 0..3); segment i = (key, first entry,
+  // count <= 64, 0), key -1 for the label-free ops (TRUE / FALSE / metadata.name); req_mask_kernel
+  // evaluates one segment per wave
+  int n_seg;
+  const int32_t* req_perm;
+  const int4* req_seg;
   uint64_t* req_mask;       // device workspace [NR][ceil(C/64)]: requirement × cluster bitmask
   // device workspace written by prep_kernel at every launch
   struct UnitRec* rec;      // [W] per-unit records

@@ -46,7 +46,15 @@ __device__ unsigned long long g_phase[256 * 32];
 #define KAD_PFLUSH_PLAN                                                                  \
   if (lane_id() == 0)                                                                    \
     for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 16 + i_], pacc[i_])
+// row kernel (thread 0, block-synchronous phases): slots 9 (units), 20 (compaction), 22 (scores),
+// 23 (normalise), 30 (select: radix + counts), 31 (pdqsort replay)
+#define KAD_PFLUSH_ROW                                                                   \
+  if (threadIdx.x == 0) {                                                                \
+    const int sl_[6] = {9, 20, 22, 23, 30, 31};                                          \
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + sl_[i_]], pacc[i_]); \
+  }
 #else
+#define KAD_PFLUSH_ROW
 #define KAD_PFLUSH_LEAN
 #define KAD_PFLUSH_PLAN
 #define KAD_PT(v)
@@ -95,101 +103,116 @@ __host__ __device__ inline SmallLayout small_layout(int C) {
 }
 
 // ---------------------------------------------------------- predicate programs
-// labels.Requirement.Matches / fields one-term selectors (apimachinery v0.26.6)
-// per interned requirement and cluster: req_group / req_mask_kernel below.
-// Requirement × cluster bitmask rows: M[r][ch] bit l = requirement r holds on
-// cluster 64*ch + l. Every distinct requirement of the batch is evaluated once
-// per cluster here, instead of once per (unit, cluster) pair.
-// One wave per (requirement, group of G consecutive chunks): the requirement
-// is decoded once (scalar loads), each chunk is one coalesced label-row load +
-// compares + ballot, the group's words are gathered in lanes (lane j = chunk
-// g0 + j) and written with one coalesced store. (One wave per (requirement,
-// chunk) made C5 — 50k requirements × 157 chunks — wave-dispatch bound.)
-// U: chunk loads in flight (1 when every wave owns one chunk, G == 1: C2's
-// 1.5k requirements x 4 chunks, where the extra dummy loads only lengthen the chain)
-template <int OPC, int U>  // OPC 0: lval only (IN/NOTIN/EQ/EXISTS/DNE), 1: Gt/Lt
-__device__ __forceinline__ uint64_t req_group(const SnapDev& s, const int32_t* p, int op, int n, int key, int g0,
-                                              int ng) {
+// labels.Requirement.Matches / fields one-term selectors (apimachinery v0.26.6) per interned
+// requirement and cluster. Requirement × cluster bitmask rows: M[r][ch] bit l = requirement r holds on
+// cluster 64*ch + l. Every distinct requirement of the batch is evaluated once per cluster here, instead
+// of once per (unit, cluster) pair.
+// req_mask_kernel: one wave per (segment of <= 64 requirements on ONE label key, group of REQ_G
+// consecutive chunks). The wave loads the key's label-value ids (and, when the segment has Gt/Lt, the
+// parsed integers) of its REQ_G chunks once — one coalesced row load per chunk for the whole segment,
+// not per requirement — and the segment's requirement words into lanes (lane i = requirement i: op,
+// count, first four value ids / the threshold), so the per-requirement loop reads its operands with
+// v_readlane: compares, one ballot per chunk, one coalesced store of the REQ_G words (lane j = chunk).
+constexpr int REQ_G = REQ_SEG_G;
+__global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, int ngrp) {
   const int lane = lane_id();
-  uint64_t acc = 0;
-  const int32_t* lv = s.lval + (size_t)key * s.C;
-  int64_t thr = 0;
-  if (OPC == 1) thr = (int64_t)(((uint64_t)(uint32_t)ldc(p + 3) << 32) | (uint32_t)ldc(p + 2));
-  for (int j0 = 0; j0 < ng; j0 += U) {
-    int32_t v[U];
-    int64_t li[U];
-    uint8_t ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {  // U chunks' loads in flight
-      const int c = (g0 + j0 + u) * WAVE + lane;
-      const uint32_t cc = (j0 + u < ng && c < s.C) ? (uint32_t)c : 0u;
-      v[u] = ldg(lv, cc);
-      if (OPC == 1) {
-        ok[u] = ldg(s.lok + (size_t)key * s.C, cc);
-        li[u] = ldg(s.lint + (size_t)key * s.C, cc);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int c = (g0 + j0 + u) * WAVE + lane;
-      bool r;
-      if (OPC == 1) {
-        r = v[u] >= 0 && ok[u] && (op == KAD_OP_GT ? li[u] > thr : li[u] < thr);
-      } else if (op == KAD_OP_EXISTS) {
-        r = v[u] >= 0;
-      } else if (op == KAD_OP_DNE) {
-        r = v[u] < 0;
-      } else {
-        bool hit = false;
-        for (int i = 0; i < n; i++) hit |= (ldc(p + 2 + i) == v[u]);
-        r = op == KAD_OP_NOTIN ? (v[u] < 0 || !hit) : (v[u] >= 0 && hit);
-      }
-      const uint64_t m = ballot(r && c < s.C);
-      acc = lane == j0 + u ? m : acc;
-    }
-  }
-  return acc;
-}
-
-__global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, int G) {
-  const int lane = lane_id();
-  const int nch = (s.C + 63) >> 6;
-  const int ngrp = (nch + G - 1) / G;
+  const int C = s.C, nch = (C + 63) >> 6;
   const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gw >= (long)b.NR * ngrp) return;
-  const int r = (int)(gw / ngrp), g0 = (int)(gw % ngrp) * G;
-  const int ng = nch - g0 < G ? nch - g0 : G;
-  const int32_t* p = b.req + ldc(b.req_off + r);
-  const int w0 = ldc(p);
-  const int op = w0 & 0xff, n = w0 >> 8, key = ldc(p + 1);
-  uint64_t acc = 0;
-  switch (op) {
-    case KAD_OP_TRUE:
-    case KAD_OP_FALSE:
-    case KAD_OP_NAME_EQ:
-    case KAD_OP_NAME_NE:
-      for (int j = 0; j < ng; ++j) {
+  if (gw >= (long)b.n_seg * ngrp) return;
+  const int sg = (int)(gw / ngrp), g0 = (int)(gw % ngrp) * REQ_G;
+  const int ng = nch - g0 < REQ_G ? nch - g0 : REQ_G;
+  const int key = ldc(&b.req_seg[sg].x), first = ldc(&b.req_seg[sg].y), cnt = ldc(&b.req_seg[sg].z);
+  // lane i < cnt: requirement i of the segment (id, word offset, op | n << 8, key word, payload 0..3)
+  const bool li = lane < cnt;
+  const int4* ent = reinterpret_cast<const int4*>(b.req_perm) + 2 * (size_t)(first + (li ? lane : 0));
+  const int4 e0 = ent[0], e1 = ent[1];
+  const int rid = e0.x, off = e0.y, w0 = li ? e0.z : 0, kw = e0.w;
+  const int pv[4] = {e1.x, e1.y, e1.z, e1.w};
+  uint64_t* out = b.req_mask;
+  if (key < 0) {  // TRUE / FALSE / metadata.name =, != (key word = cluster id): no label rows
+    for (int i = 0; i < cnt; ++i) {
+      const int op = __builtin_amdgcn_readlane(w0, i) & 0xff, ck = __builtin_amdgcn_readlane(kw, i);
+      const int r = __builtin_amdgcn_readlane(rid, i);
+      uint64_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < REQ_G; ++j) {
         const int c = (g0 + j) * WAVE + lane;
-        const bool v = op == KAD_OP_TRUE || (op == KAD_OP_NAME_EQ && c == key) || (op == KAD_OP_NAME_NE && c != key);
-        const uint64_t m = ballot(v && c < s.C);
+        const bool v = op == KAD_OP_TRUE || (op == KAD_OP_NAME_EQ && c == ck) || (op == KAD_OP_NAME_NE && c != ck);
+        const uint64_t m = ballot(v && c < C && j < ng);
         acc = lane == j ? m : acc;
       }
-      break;
-    case KAD_OP_GT:
-    case KAD_OP_LT:
-      acc = G == 1 ? req_group<1, 1>(s, p, op, n, key, g0, ng) : req_group<1, 4>(s, p, op, n, key, g0, ng);
-      break;
-    case KAD_OP_IN:
-    case KAD_OP_NOTIN:
-    case KAD_OP_EQ:
-    case KAD_OP_EXISTS:
-    case KAD_OP_DNE:
-      acc = G == 1 ? req_group<0, 1>(s, p, op, n, key, g0, ng) : req_group<0, 4>(s, p, op, n, key, g0, ng);
-      break;
-    default:
-      break;
+      if (lane < ng) out[(size_t)r * nch + g0 + lane] = acc;
+    }
+    return;
   }
-  if (lane < ng) b.req_mask[(size_t)r * nch + g0 + lane] = acc;
+  int32_t lv[REQ_G];
+#pragma unroll
+  for (int j = 0; j < REQ_G; ++j) {
+    const int c = (g0 + j) * WAVE + lane;
+    lv[j] = (j < ng && c < C) ? ldg(s.lval, (uint32_t)(key * C + c)) : -1;
+  }
+  const int op_l = w0 & 0xff;
+  const bool has_int = ballot(li && (op_l == KAD_OP_GT || op_l == KAD_OP_LT)) != 0;
+  int64_t lint[REQ_G];
+  bool lok[REQ_G];
+#pragma unroll
+  for (int j = 0; j < REQ_G; ++j) {
+    lint[j] = 0;
+    lok[j] = false;
+  }
+  if (has_int) {
+#pragma unroll
+    for (int j = 0; j < REQ_G; ++j) {
+      const int c = (g0 + j) * WAVE + lane;
+      const uint32_t cc = (j < ng && c < C) ? (uint32_t)(key * C + c) : 0u;
+      lint[j] = ldg(s.lint, cc);
+      lok[j] = ldg(s.lok, cc) != 0;
+    }
+  }
+  for (int i = 0; i < cnt; ++i) {
+    const int wi = __builtin_amdgcn_readlane(w0, i);
+    const int op = wi & 0xff, n = (int)((uint32_t)wi >> 8);
+    const int r = __builtin_amdgcn_readlane(rid, i);
+    bool hit[REQ_G];
+    if (op == KAD_OP_GT || op == KAD_OP_LT) {
+      const int64_t thr = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(pv[1], i) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane(pv[0], i));
+#pragma unroll
+      for (int j = 0; j < REQ_G; ++j) hit[j] = lv[j] >= 0 && lok[j] && (op == KAD_OP_GT ? lint[j] > thr : lint[j] < thr);
+    } else if (op == KAD_OP_EXISTS || op == KAD_OP_DNE) {
+#pragma unroll
+      for (int j = 0; j < REQ_G; ++j) hit[j] = (lv[j] >= 0) == (op == KAD_OP_EXISTS);
+    } else {  // IN / NOTIN / EQ: value ids of this key (>= 0; a missing label is -1)
+#pragma unroll
+      for (int j = 0; j < REQ_G; ++j) hit[j] = false;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < n) {
+          const int a = __builtin_amdgcn_readlane(pv[t], i);
+#pragma unroll
+          for (int j = 0; j < REQ_G; ++j) hit[j] |= lv[j] == a;
+        }
+      if (n > 4) {
+        const int offi = __builtin_amdgcn_readlane(off, i);
+        for (int t = 4; t < n; ++t) {
+          const int a = ldc(b.req + offi + 2 + t);
+#pragma unroll
+          for (int j = 0; j < REQ_G; ++j) hit[j] |= lv[j] == a;
+        }
+      }
+      if (op == KAD_OP_NOTIN)
+#pragma unroll
+        for (int j = 0; j < REQ_G; ++j) hit[j] = !hit[j];  // NotIn: a missing label matches too
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < REQ_G; ++j) {
+      const int c = (g0 + j) * WAVE + lane;
+      const uint64_t m = ballot(hit[j] && c < C && j < ng);
+      acc = lane == j ? m : acc;
+    }
+    if (lane < ng) out[(size_t)r * nch + g0 + lane] = acc;
+  }
 }
 
 // A unit's program (filter / score words) held in VGPR lanes: word i < 64 is
@@ -2333,6 +2356,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
 constexpr int ROW_THREADS = 1024;
 constexpr int ROW_WAVES = ROW_THREADS / 64;
 constexpr int ROW_MAX_C = 12288;
+constexpr int ROW_MAX_TERMS = 8;  // preferred terms held as per-chunk words (8 x nch x 8 B <= the pid array)
 struct RowKLayout {
   size_t key, idx, pid, posl, posr, sw, cnt, hist, red, bytes;
 };
@@ -2435,12 +2459,19 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
       sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
   const bool s_tt = sm & BIT(KAD_PL_TAINT_TOLERATION);
 
+  KAD_PACC;
+  // the next unit's list index is dequeued one unit ahead (thread 0), so the returning atomic's latency
+  // overlaps the current unit
+  int ticket = 0;
+  if (tid == 0) ticket = atomicAdd(rargs()->b.rows_head, 1);
   for (;;) {
     __syncthreads();  // the previous unit's LDS reads are done
+    KAD_PT(t0);
     if (tid == 0) {
       RArgs a = rargs();
-      const int i = atomicAdd(a->b.rows_head, 1);
-      bc[0] = i < __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? a->b.rows[i] : -1;
+      const int rn = __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bc[0] = ticket < rn ? a->b.rows[ticket] : -1;
+      if (ticket < rn) ticket = atomicAdd(a->b.rows_head, 1);
     }
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(bc[0]);
@@ -2481,6 +2512,7 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
       const uint64_t m = swl[ch];
       if (lane_on(m)) idx[cnt[ch] + mbcnt(m)] = (uint16_t)(ch * WAVE + lane);
     }
+    KAD_PADD(0, 1);
     if (n == 0) {  // generic_scheduler.go:112-114
       status(KAD_ST_NO_FEASIBLE);
       continue;
@@ -2499,43 +2531,103 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
       if (hm && mc < k) k = (int)mc;
     }
     __syncthreads();
+    KAD_PT(t1);
+    KAD_PADD(1, t1 - t0);
 
     // ---------------- raw scores (RunScorePlugins, framework.go:139-181)
     const int32_t* sp = a->b.sprog + spo;
-    const bool s_aff = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && ldc(sp) > 0;  // no preferred terms: 0 everywhere
+    const int n_terms = ldc(sp);
+    const bool s_aff = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && n_terms > 0;  // no preferred terms: 0 everywhere
+    // ClusterAffinity preferred terms (cluster_affinity.go:96-135) as per-chunk words in LDS (over pid, free
+    // until the replay): word (t, ch) = AND of the term's requirement rows — once per chunk instead of once
+    // per feasible position; a position's raw score is then a sum of weights over LDS bit tests
+    const bool aff_words = s_aff && n_terms <= ROW_MAX_TERMS;
+    uint64_t* termw = (uint64_t*)pid;
+    if (aff_words) {
+      int pc = 1;
+      for (int t = 0; t < n_terms; ++t) {
+        const int ne = ldc(sp + pc + 1);
+        const int32_t* ids = sp + pc + 2;
+        pc += 2 + ne;
+        for (int ch = tid; ch < nch; ch += ROW_THREADS) {
+          uint64_t m = ~0ull;
+          for (int i = 0; i < ne; ++i) m &= ldg(a->b.req_mask, (uint32_t)ldc(ids + i) * (uint32_t)nch + (uint32_t)ch);
+          termw[t * nch + ch] = m;
+        }
+      }
+      __syncthreads();
+    }
     const double rqcd = (double)rqc, rqmd = (double)rqm;
     int ttmax = 0, amax = 0;
-    for (int j = tid; j < n; j += ROW_THREADS) {
+    // two positions per trip: every gather of both is issued before either is used
+    for (int j0 = tid; j0 < n; j0 += 2 * ROW_THREADS) {
       RArgs as = rargs();
-      const uint32_t c = idx[j];
-      int x = 0;
-      if (s_res) {  // the wide kernel's clean path: x = available - request, exact in f64
-        const int64_t ac = ldg(as->s.alloc_cpu, c), uc = ldg(as->s.used_cpu, c);
-        const int64_t am = ldg(as->s.alloc_mem, c), um = ldg(as->s.used_mem, c);
-        const double capc = (double)ac, capm = (double)am;
-        const double xc = (double)(ac - uc) - rqcd, xm = (double)(am - um) - rqmd;
-        const float ivc = (float)(100.0 / capc), ivm = (float)(100.0 / capm);
-        const double xcp = fmax(xc, 0.0), xmp = fmax(xm, 0.0);
-        const int okc = -(int)(xc >= 0.0), okm = -(int)(xm >= 0.0);
-        if (sm & BIT(KAD_PL_LEAST_ALLOCATED)) x += (quot100(xcp, capc, ivc) + quot100(xmp, capm, ivm)) >> 1;
-        if (sm & BIT(KAD_PL_MOST_ALLOCATED))
-          x += ((quot100(capc - xcp, capc, ivc) & okc) + (quot100(capm - xmp, capm, ivm) & okm)) >> 1;
-        if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x += (int)balanced_d((capc - xc) / capc, (capm - xm) / capm);
+      const int j1 = j0 + ROW_THREADS;
+      const bool v1 = j1 < n;
+      const uint32_t c0 = idx[j0], c1 = idx[v1 ? j1 : j0];
+      int64_t ac[2], uc[2], am[2], um[2];
+      uint64_t pn[2][TFOLD_MAX_TW];
+      const uint32_t cs[2] = {c0, c1};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        ac[u] = uc[u] = am[u] = um[u] = 0;
+        if (s_res) {
+          ac[u] = ldg(as->s.alloc_cpu, cs[u]);
+          uc[u] = ldg(as->s.used_cpu, cs[u]);
+          am[u] = ldg(as->s.alloc_mem, cs[u]);
+          um[u] = ldg(as->s.used_mem, cs[u]);
+        }
+#pragma unroll
+        for (int tw = 0; tw < TFOLD_MAX_TW; ++tw)
+          pn[u][tw] = (s_tt && tw < TW) ? ldg(as->s.pns, (uint32_t)(tw * C) + cs[u]) : 0ull;
       }
-      int tc = 0;
-      if (s_tt)  // taint_toleration.go:91-118: PreferNoSchedule taints not tolerated
-        for (int tw = 0; tw < TW; ++tw)
-          tc += popc64(ldg(as->s.pns, (uint32_t)(tw * C) + c) & ~ldc(as->b.tol_pns + (size_t)tsc * TW + tw));
-      key[j] = (uint32_t)x | ((uint32_t)tc << 16);
-      ttmax = tc > ttmax ? tc : ttmax;
-      if (s_aff) {  // cluster_affinity.go:96-135; |raw| <= 2^20 (wider units were deferred above)
-        const int af = (int)affinity_score(as->b.req_mask, sp, nch, (int)c);
-        aff[j] = af;
-        amax = af > amax ? af : amax;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !v1) break;
+        const int j = u == 0 ? j0 : j1;
+        const uint32_t c = cs[u];
+        int x = 0;
+        if (s_res) {  // the wide kernel's clean path: x = available - request, exact in f64
+          const double capc = (double)ac[u], capm = (double)am[u];
+          const double xc = (double)(ac[u] - uc[u]) - rqcd, xm = (double)(am[u] - um[u]) - rqmd;
+          const float ivc = (float)(100.0 / capc), ivm = (float)(100.0 / capm);
+          const double xcp = fmax(xc, 0.0), xmp = fmax(xm, 0.0);
+          const int okc = -(int)(xc >= 0.0), okm = -(int)(xm >= 0.0);
+          if (sm & BIT(KAD_PL_LEAST_ALLOCATED)) x += (quot100(xcp, capc, ivc) + quot100(xmp, capm, ivm)) >> 1;
+          if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+            x += ((quot100(capc - xcp, capc, ivc) & okc) + (quot100(capm - xmp, capm, ivm) & okm)) >> 1;
+          if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x += (int)balanced_d((capc - xc) / capc, (capm - xm) / capm);
+        }
+        int tc = 0;
+        if (s_tt)  // taint_toleration.go:91-118: PreferNoSchedule taints not tolerated
+#pragma unroll
+          for (int tw = 0; tw < TFOLD_MAX_TW; ++tw)
+            if (tw < TW) tc += popc64(pn[u][tw] & ~ldc(as->b.tol_pns + (size_t)tsc * TW + tw));
+        key[j] = (uint32_t)x | ((uint32_t)tc << 16);
+        ttmax = tc > ttmax ? tc : ttmax;
+        if (s_aff) {  // |raw| <= 2^20 (wider units were deferred above)
+          int af;
+          if (aff_words) {
+            af = 0;
+            int pc = 1;
+            for (int t = 0; t < n_terms; ++t) {
+              const int32_t wgt = ldc(sp + pc);
+              pc += 2 + ldc(sp + pc + 1);
+              af += ((termw[t * nch + (c >> 6)] >> (c & 63)) & 1) ? wgt : 0;
+            }
+          } else {
+            af = (int)affinity_score(as->b.req_mask, sp, nch, (int)c);
+          }
+          aff[j] = af;
+          amax = af > amax ? af : amax;
+        }
       }
     }
     if (s_tt) ttmax = row_block_max(ttmax, red);
     if (s_aff) amax = row_block_max(amax, red);
+    __syncthreads();
+    KAD_PT(t2);
+    KAD_PADD(2, t2 - t1);
 
     // ---------------- DefaultNormalizeScore + totals, stored order-preserving as u32 (total ^ 2^31)
     int mn = INT32_MAX, mx = INT32_MIN;
@@ -2554,6 +2646,8 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
     }
     mn = row_block_min(mn, red);
     mx = row_block_max(mx, red);
+    KAD_PT(t3);
+    KAD_PADD(3, t3 - t2);
 
     // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
     // mode: -1 nothing, 0 all, 1 total >= T, 3 replay ranks < k
@@ -2613,6 +2707,8 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
       }
       g = row_block_sum(g, red);
       e = row_block_sum(e, red);
+      KAD_PT(t4);
+      KAD_PADD(4, t4 - t3);
       if (k - g != e) {  // ties straddle the cut: Go's pdqsort decides which tied clusters stay (n > 256)
         rflags = KAD_RF_TIE_STRADDLE;
         mode = 3;
@@ -2627,6 +2723,8 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
         __syncthreads();
         for (int r = tid; r < n; r += ROW_THREADS) inv[pid[r]] = (uint16_t)r;
         __syncthreads();
+        KAD_PT(t5);
+        KAD_PADD(5, t5 - t4);
       }
     }
 
@@ -2672,6 +2770,7 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
       ao->o.flags[w] = rflags;
     }
   }
+  KAD_PFLUSH_ROW;
 }
 
 // ============================================================ plan kernel
@@ -3185,14 +3284,10 @@ static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
-  // chunks per wave: enough waves to fill the chip (~32k), at most 64 (one lane per chunk word)
-  const long pairs = (long)b.NR * nch;
-  int G = 1;
-  while (G < 64 && pairs / (2 * G) >= 32768) G *= 2;
-  const long waves = (long)b.NR * ((nch + G - 1) / G);
+  const int ngrp = (nch + REQ_G - 1) / REQ_G;
+  const long waves = (long)b.n_seg * ngrp;
   if (waves == 0) return hipSuccess;
-  const long grid = (waves + 3) / 4;
-  hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, G);
+  hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, b, ngrp);
   return hipGetLastError();
 }
 

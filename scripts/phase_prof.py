@@ -25,11 +25,11 @@ from kubeadmiral_amd import build as kbuild  # noqa: E402
 
 PROF_LIB = os.path.join(kbuild.HERE, "libkad_prof.so")
 NAMES = ["A_filter", "B_score", "C_normalize", "D_select", "E_output", "n_straddle", "n_select", "sum_feasible",
-         "D_select_straddle", "-", "lean_A_filter", "lean_B_score", "lean_D_select", "lean_E_output",
+         "D_select_straddle", "row_units", "lean_A_filter", "lean_B_score", "lean_D_select", "lean_E_output",
          "lean_n_straddle", "lean_D_select_straddle", "plan_P0_setup", "plan_P1_weights", "plan_P2_plan",
-         "plan_P3_output", "-", "plan_rows", "-", "-",
+         "plan_P3_output", "row_compact", "plan_rows", "row_score", "row_normalize",
          "replay_setup", "replay_partition", "replay_pivot", "replay_insertion", "replay_n_partitions",
-         "replay_sum_n"]
+         "replay_sum_n", "row_select", "row_replay"]
 
 
 def main():
@@ -44,14 +44,18 @@ def main():
         kbuild.build(force=True, extra=["-DKAD_PHASE_PROF"], out=PROF_LIB)
         if a.build:
             return
-    from kubeadmiral_amd import runtime, synth
-    from kubeadmiral_amd.pack import Batch, Snapshot
+    import bench
+    from kubeadmiral_amd import columns, runtime, synth
+    from kubeadmiral_amd.pack import Snapshot
 
     L = runtime.load_library(PROF_LIB)
     L.kad_debug_phase_counters.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    clusters, units, fwk = synth.make_config(a.config, W=a.units or None)
+    W0, C = synth.SIZES[a.config]
+    clusters = bench.make_clusters(a.config, C)
+    fwk = synth.profile_for(a.config)
     snap = Snapshot(clusters)
-    batch = Batch(snap, fwk, units)
+    # the bench's workload (columnar generator + native packer)
+    batch = columns.NativePacker(snap).pack(fwk, bench.make_columns(a.config, 0, a.units or W0, clusters))
     ctx = runtime.Context(0)
     ctx.upload_snapshot(snap)
     ctx.upload_batch(batch)
@@ -71,6 +75,9 @@ def main():
             continue
         if nm.startswith("plan_P"):
             out[nm + "_cycles_per_row"] = round(v / max(1.0, float(cnt[21])), 1)
+            continue
+        if nm.startswith("row_") and nm != "row_units":  # per unit of schedule_row_kernel
+            out[nm + "_cycles_per_row"] = round(v / max(1.0, float(cnt[9])), 1)
             continue
         if nm.startswith("replay_"):  # per straddling unit (wide kernel)
             out[nm + "_per_straddle"] = round(v / max(1.0, float(cnt[14])), 1)
