@@ -45,6 +45,8 @@ struct kad_ctx {
   std::vector<int32_t> h_reqseg;  // BatchDev::req_perm [NR][8] then req_seg [n_seg][4] (host copy until the next upload)
   void* d_reqseg = nullptr;
   size_t reqseg_cap = 0;
+  void* d_rowslab = nullptr;  // BatchDev::row_slabs
+  size_t rowslab_cap = 0;
   void* d_rec = nullptr;  // UnitRec[W] (prep_kernel)
   size_t rec_cap = 0;
   void* d_sw = nullptr;   // u64[W][nch] static filter words (prep_kernel)
@@ -345,7 +347,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -887,6 +889,10 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   // long feasible lists go to schedule_row_kernel when every filter is in the static words
   static const bool no_rows = getenv("KAD_NO_ROWS") && atoi(getenv("KAD_NO_ROWS"));
   c->bd.use_rows = !no_rows && c->sd.clean && c->sd.fold && c->sd.fitfold && row_kernel_fits(c->sd.C);
+  if (c->bd.use_rows) {
+    if (int r = grow(c, &c->d_rowslab, &c->rowslab_cap, (size_t)ROW_MAX_BLOCKS * row_slab_bytes(c->sd.C))) return r;
+    c->bd.row_slabs = static_cast<char*>(c->d_rowslab);
+  }
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[4], c->stream));

@@ -86,6 +86,7 @@ struct BatchDev {
   int32_t* rows;            // [W] units whose feasible list outgrows the lean / wide kernels' registers
   int32_t* rows_n;          // [1] length of rows (reset by prep_kernel)
   int32_t* rows_head;       // [1] schedule_row_kernel's dequeue counter (reset by prep_kernel)
+  char* row_slabs;          // [ROW_MAX_BLOCKS][row_slab_bytes(C)]: long replays' position scratch
   uint32_t* wq;             // [WQ_HEADS * WQ_STRIDE] schedule kernels' work heads (reset by prep_kernel)
 };
 
@@ -155,6 +156,8 @@ hipError_t launch_trigger_objects(const TriggerDev& t, hipStream_t st);
 size_t select_wave_bytes(int C);
 // true if schedule_row_kernel can take the long feasible lists of this snapshot (C <= ROW_MAX_C)
 bool row_kernel_fits(int C);
+constexpr int ROW_MAX_BLOCKS = 1024;  // schedule_row_kernel grid cap (its global slabs are sized for it)
+__host__ __device__ size_t row_slab_bytes(int C);
 size_t plan_wave_bytes(int K);
 
 // phase counters of a -DKAD_PHASE_PROF build (returns 0 in product builds)

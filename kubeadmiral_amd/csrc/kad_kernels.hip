@@ -1373,6 +1373,26 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     auto filter_chunks = [&](auto mode_t) {
       constexpr int MODE = decltype(mode_t)::value;
       constexpr bool FAST = MODE >= 1, FOLD = MODE >= 2, FITF = MODE == 3;
+      if constexpr (NCH == 0 && FITF) {
+        // every filter is in the static words: only the non-zero words of each 64-chunk group (one per
+        // lane) are compacted — C5's median unit has 2 feasible clusters of 10 000
+        for (int g = 0; g < nch; g += WAVE) {
+          if (g > 0) load_words(g);
+          uint64_t nz = ballot(g + lane < nch && dsw != 0);
+          while (nz) {
+            const int l = __builtin_ctzll(nz);
+            nz &= nz - 1;
+            const uint64_t m = readlane64(dsw, l);
+            if (lane_on(m)) {
+              const int pos = n + mbcnt(m);
+              if (pos < P) idx[pos] = (uint16_t)((g + l) * WAVE + lane);  // more than P: deferred
+            }
+            n += popc64(m);
+            if (n > P) return;
+          }
+        }
+        return;
+      }
       const bool ucur = !FAST && use_cur;
       if constexpr (NCH == 0) load_attrs(mode_t, lane);
 #pragma unroll
@@ -2343,32 +2363,39 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
 // schedule_row_kernel — the units whose feasible list is longer than the lean / wide kernels' register
 // positions (C5: 16 % of the units, a few thousand feasible clusters of 10 000), on snapshots where
 // every filter is in the static words (BatchDev::use_rows: clean, SnapDev::fold and ::fitfold,
-// C <= ROW_MAX_C). One 1024-thread workgroup per unit, persistent (units dequeued from BatchDev::rows):
+// C <= ROW_MAX_C). One 512-thread workgroup per unit, two per CU (LDS: 6 B per cluster + the preferred-
+// term words, which the replay scratch reuses), persistent (units dequeued from BatchDev::rows):
 //   * compaction: the unit's static words → per-chunk popcounts → block prefix → cluster ids in LDS
 //     (findClustersThatFitWorkload order, generic_scheduler.go:152-169);
-//   * scores spread over the 16 waves (RunScorePlugins, framework.go:139-181), the clean-snapshot
+//   * scores spread over the 8 waves (RunScorePlugins, framework.go:139-181), the clean-snapshot
 //     arithmetic of the wide kernel (exact f64 quotients, 32-bit totals), block maxima for
 //     DefaultNormalizeScore (framework/util.go:455-483);
 //   * MaxCluster (max_cluster.go:42-66): the k-th largest total by a block-wide 8-bit radix histogram;
-//     the cut takes every tie, or wave 0 replays Go's pdqsort restricted to k (PdqWave) on the LDS keys;
+//     the cut takes every tie, or wave 0 replays Go's pdqsort restricted to k (PdqWave) on the LDS keys,
+//     its position scratch in LDS up to ROW_NREP positions, else in the block's global slab;
 //   * output in ascending cluster id by per-chunk ballots and a block prefix.
-// Units outside the clean-f64 range (requests >= 2^46, wide affinity weights) go on to the defer list.
-constexpr int ROW_THREADS = 1024;
+// Units outside the clean-f64 range (requests >= 2^46, wide affinity weights) or with more than
+// ROW_MAX_TERMS preferred terms go on to the defer list.
+constexpr int ROW_THREADS = 512;
 constexpr int ROW_WAVES = ROW_THREADS / 64;
 constexpr int ROW_MAX_C = 12288;
-constexpr int ROW_MAX_TERMS = 8;  // preferred terms held as per-chunk words (8 x nch x 8 B <= the pid array)
+constexpr int ROW_MAX_TERMS = 8;  // preferred terms held as per-chunk words (8 x nch x 8 B = Cp bytes)
+constexpr int ROW_NREP = 2048;    // replays of up to this many positions keep their scratch in LDS
+static_assert(ROW_MAX_BLOCKS >= 1, "row kernel slabs");
 struct RowKLayout {
-  size_t key, idx, pid, posl, posr, sw, cnt, hist, red, bytes;
+  size_t key, idx, x, pid, posl, posr, sw, cnt, hist, red, bytes;
 };
 __host__ __device__ inline RowKLayout rowk_layout(int C) {
   const size_t Cp = (size_t)((C + 63) & ~63), nch = Cp / 64;
   RowKLayout L;
   L.key = 0;                              // u32[Cp]: fixed | TT raw << 16, then totals (sign-flipped), replay keys
   L.idx = L.key + 4 * Cp;                 // u16[Cp]: position → cluster id
-  L.pid = L.idx + 2 * Cp;                 // u16[Cp]: replay: original position
-  L.posl = L.pid + 2 * Cp;                // u16[Cp + 64] replay scratch, then ranks; with posr: i32 affinity raw
-  L.posr = L.posl + 2 * Cp + 128;         // u16[Cp]
-  L.sw = (L.posr + 2 * Cp + 15) & ~(size_t)15;  // u64[nch]: the unit's static words
+  L.x = L.idx + 2 * Cp;                   // preferred-term words u64[8][nch] while scoring, then the replay
+  L.pid = L.x;                            //   scratch: pid u16[NREP], posl u16[NREP + 64], posr u16[NREP]
+  L.posl = L.pid + 2 * ROW_NREP;
+  L.posr = L.posl + 2 * ROW_NREP + 128;
+  const size_t xb = Cp > 6 * (size_t)ROW_NREP + 128 ? Cp : 6 * (size_t)ROW_NREP + 128;
+  L.sw = (L.x + xb + 15) & ~(size_t)15;   // u64[nch]: the unit's static words
   L.cnt = L.sw + 8 * nch;                 // i32[nch + 1]: chunk counts → exclusive prefix (+ total)
   L.hist = (L.cnt + 4 * (nch + 1) + 15) & ~(size_t)15;  // u32[256]
   L.red = L.hist + 4 * 256;               // i32[4][ROW_WAVES] per-wave partials, i32[8] broadcasts
@@ -2377,12 +2404,15 @@ __host__ __device__ inline RowKLayout rowk_layout(int C) {
 }
 size_t row_kernel_lds(int C) { return rowk_layout(C).bytes; }
 bool row_kernel_fits(int C) { return C > 0 && C <= ROW_MAX_C; }
+// per-block global slab for replays longer than ROW_NREP: pid u16[Cp], posl u16[Cp + 64], posr u16[Cp]
+__host__ __device__ size_t row_slab_bytes(int C) { return ((size_t)6 * ((C + 63) & ~63) + 128 + 255) & ~(size_t)255; }
 
 struct RowArgs {
   SnapDev s;
   BatchDev b;
   OutDev o;
   ProfDev p;
+  char* slabs;  // [grid][row_slab_bytes(C)]
 };
 typedef const __attribute__((address_space(4))) RowArgs* RArgs;
 __device__ __forceinline__ RArgs rargs() {
@@ -2426,7 +2456,7 @@ __device__ __forceinline__ void row_exclusive_scan(int* cnt, int m) {
   if (lane == 0) cnt[m] = carry;
 }
 
-__global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs args) {
+__global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs args) {
   (void)args;  // read through rargs()
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = lane_id();
@@ -2445,11 +2475,12 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
   const RowKLayout L = rowk_layout(C);
   uint32_t* key = (uint32_t*)(smem + L.key);
   uint16_t* idx = (uint16_t*)(smem + L.idx);
-  uint16_t* pid = (uint16_t*)(smem + L.pid);
-  uint16_t* posl = (uint16_t*)(smem + L.posl);
-  uint16_t* posr = (uint16_t*)(smem + L.posr);
-  int32_t* aff = (int32_t*)(smem + L.posl);  // i32[Cp] over posl | posr while scoring
-  uint16_t* inv = posl;                      // ranks after the replay
+  uint16_t* pid_l = (uint16_t*)(smem + L.pid);
+  uint16_t* posl_l = (uint16_t*)(smem + L.posl);
+  uint16_t* posr_l = (uint16_t*)(smem + L.posr);
+  uint64_t* termw = (uint64_t*)(smem + L.x);  // preferred-term words (scoring and normalisation only)
+  uint16_t* pid_g;  // the block's global slab (replays longer than ROW_NREP)
+  pid_g = (uint16_t*)(rargs()->slabs + (size_t)blockIdx.x * row_slab_bytes(C));
   uint64_t* swl = (uint64_t*)(smem + L.sw);
   int32_t* cnt = (int32_t*)(smem + L.cnt);
   uint32_t* hist = (uint32_t*)(smem + L.hist);
@@ -2480,14 +2511,16 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
     const UnitRec* rec = a->b.rec + w;
     const uint32_t fc = ldc(&rec->flags);
     const int64_t rqc = ldc(&rec->req_cpu), rqm = ldc(&rec->req_mem);
-    if ((uint64_t)rqc >= (1ull << 46) || (uint64_t)rqm >= (1ull << 46) || (fc & KAD_W_WIDE_SCORES)) {
+    const int spo = ldc(&rec->sprog_off);
+    const bool many_terms = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && ldc(a->b.sprog + spo) > ROW_MAX_TERMS;
+    if ((uint64_t)rqc >= (1ull << 46) || (uint64_t)rqm >= (1ull << 46) || (fc & KAD_W_WIDE_SCORES) || many_terms) {
       if (tid == 0) {  // outside the exact clean-f64 range: the full kernel
         const int slot = atomicAdd(a->b.defer_n, 1);
         a->b.defer[slot] = w;
       }
       continue;
     }
-    const int tsc = ldc(&rec->tolset), spo = ldc(&rec->sprog_off);
+    const int tsc = ldc(&rec->tolset);
     const int64_t mc = ldc(&rec->maxc), ooff = ldc(&rec->out_off);
     auto status = [&](int32_t st) {
       if (tid == 0) {
@@ -2538,12 +2571,20 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
     const int32_t* sp = a->b.sprog + spo;
     const int n_terms = ldc(sp);
     const bool s_aff = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && n_terms > 0;  // no preferred terms: 0 everywhere
-    // ClusterAffinity preferred terms (cluster_affinity.go:96-135) as per-chunk words in LDS (over pid, free
-    // until the replay): word (t, ch) = AND of the term's requirement rows — once per chunk instead of once
-    // per feasible position; a position's raw score is then a sum of weights over LDS bit tests
-    const bool aff_words = s_aff && n_terms <= ROW_MAX_TERMS;
-    uint64_t* termw = (uint64_t*)pid;
-    if (aff_words) {
+    // ClusterAffinity preferred terms (cluster_affinity.go:96-135) as per-chunk words in LDS (<= ROW_MAX_TERMS,
+    // checked above): word (t, ch) = AND of the term's requirement rows — once per chunk instead of once per
+    // feasible position; a position's raw score is then a sum of weights over LDS bit tests, recomputed
+    // where it is needed (no per-position array)
+    auto raw_aff = [&](uint32_t c) {
+      int af = 0, pc = 1;
+      for (int t = 0; t < n_terms; ++t) {
+        const int32_t wgt = ldc(sp + pc);
+        pc += 2 + ldc(sp + pc + 1);
+        af += ((termw[t * nch + (c >> 6)] >> (c & 63)) & 1) ? wgt : 0;
+      }
+      return af;
+    };
+    if (s_aff) {
       int pc = 1;
       for (int t = 0; t < n_terms; ++t) {
         const int ne = ldc(sp + pc + 1);
@@ -2606,19 +2647,7 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
         key[j] = (uint32_t)x | ((uint32_t)tc << 16);
         ttmax = tc > ttmax ? tc : ttmax;
         if (s_aff) {  // |raw| <= 2^20 (wider units were deferred above)
-          int af;
-          if (aff_words) {
-            af = 0;
-            int pc = 1;
-            for (int t = 0; t < n_terms; ++t) {
-              const int32_t wgt = ldc(sp + pc);
-              pc += 2 + ldc(sp + pc + 1);
-              af += ((termw[t * nch + (c >> 6)] >> (c & 63)) & 1) ? wgt : 0;
-            }
-          } else {
-            af = (int)affinity_score(as->b.req_mask, sp, nch, (int)c);
-          }
-          aff[j] = af;
+          const int af = raw_aff(c);
           amax = af > amax ? af : amax;
         }
       }
@@ -2636,7 +2665,7 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
       int t = (int)(x & 0xFFFFu);
       if (s_tt) t += ttmax == 0 ? 100 : 100 - (int)small_quot(100 * (int)(x >> 16), ttmax);
       if (s_aff) {
-        const int af = aff[j];
+        const int af = raw_aff(idx[j]);
         const int num = 100 * af;
         t += amax == 0 ? af : (num >= 0 && num < (1 << 24) ? (int)small_quot(num, amax) : num / amax);
       }
@@ -2650,6 +2679,7 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
     KAD_PADD(3, t3 - t2);
 
     // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
+    uint16_t* inv = nullptr;  // ranks after a replay (LDS or the block's slab)
     // mode: -1 nothing, 0 all, 1 total >= T, 3 replay ranks < k
     int mode = k >= n ? 0 : (k <= 0 ? -1 : 1);
     uint32_t rflags = 0;
@@ -2712,13 +2742,24 @@ __global__ __launch_bounds__(ROW_THREADS, 1) void schedule_row_kernel(RowArgs ar
       if (k - g != e) {  // ties straddle the cut: Go's pdqsort decides which tied clusters stay (n > 256)
         rflags = KAD_RF_TIE_STRADDLE;
         mode = 3;
+        const bool in_lds = n <= ROW_NREP;
+        const size_t Cp = (size_t)nch * 64;
+        uint16_t* pid = in_lds ? pid_l : pid_g;
+        uint16_t* posl = in_lds ? posl_l : pid_g + Cp;
+        uint16_t* posr = in_lds ? posr_l : pid_g + 2 * Cp + 64;
+        inv = posl;
         for (int j = tid; j < n; j += ROW_THREADS) pid[j] = (uint16_t)j;
         __syncthreads();
         if (wv == 0) {
           const int xs_b = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
           const int xs_c = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
-          PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
-          pw.select(n, k);
+          if (in_lds) {
+            PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
+            pw.select(n, k);
+          } else {  // keys stay in LDS; positions in the slab (workgroup-scope fences order both)
+            PdqWave<uint32_t, true> pw{key, pid, posl, posr, xs_b, xs_c};
+            pw.select(n, k);
+          }
         }
         __syncthreads();
         for (int r = tid; r < n; r += ROW_THREADS) inv[pid[r]] = (uint16_t)r;
@@ -3374,8 +3415,10 @@ static hipError_t launch_rows(const SnapDev& s, const BatchDev& b, const OutDev&
       per_cu < 1)
     per_cu = 1;
   long grid = (long)n_cus() * per_cu;
+  if (grid > ROW_MAX_BLOCKS) grid = ROW_MAX_BLOCKS;
   if (grid > b.W) grid = b.W;
-  const RowArgs A{s, b, o, p};
+  if (!b.row_slabs) return hipErrorInvalidValue;
+  const RowArgs A{s, b, o, p, b.row_slabs};
   hipLaunchKernelGGL(schedule_row_kernel, dim3((unsigned)grid), dim3(ROW_THREADS), lds, st, A);
   return hipGetLastError();
 }
