@@ -2398,8 +2398,8 @@ __host__ __device__ inline RowKLayout rowk_layout(int C) {
   L.sw = (L.x + xb + 15) & ~(size_t)15;   // u64[nch]: the unit's static words
   L.cnt = L.sw + 8 * nch;                 // i32[nch + 1]: chunk counts → exclusive prefix (+ total)
   L.hist = (L.cnt + 4 * (nch + 1) + 15) & ~(size_t)15;  // u32[256]
-  L.red = L.hist + 4 * 256;               // i32[4][ROW_WAVES] per-wave partials, i32[8] broadcasts
-  L.bytes = L.red + 4 * (4 * ROW_WAVES + 8);
+  L.red = L.hist + 4 * 256;               // i32[4][ROW_WAVES] per-wave partials, i32[24] broadcasts
+  L.bytes = L.red + 4 * (4 * ROW_WAVES + 24);
   return L;
 }
 size_t row_kernel_lds(int C) { return rowk_layout(C).bytes; }
@@ -2575,26 +2575,42 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
     // checked above): word (t, ch) = AND of the term's requirement rows — once per chunk instead of once per
     // feasible position; a position's raw score is then a sum of weights over LDS bit tests, recomputed
     // where it is needed (no per-position array)
-    auto raw_aff = [&](uint32_t c) {
-      int af = 0, pc = 1;
-      for (int t = 0; t < n_terms; ++t) {
-        const int32_t wgt = ldc(sp + pc);
-        pc += 2 + ldc(sp + pc + 1);
-        af += ((termw[t * nch + (c >> 6)] >> (c & 63)) & 1) ? wgt : 0;
+    // the term list parsed once: weights in SGPRs (constant indices after unrolling), each term's
+    // expression count and id offset in LDS for the (term, chunk) word pass
+    int32_t wt[ROW_MAX_TERMS];
+    int32_t* tdesc = bc + 4;  // [2][ROW_MAX_TERMS]: expression count, id offset (broadcast slots 4..19)
+    {
+      int pc = 1;
+#pragma unroll
+      for (int t = 0; t < ROW_MAX_TERMS; ++t) {
+        wt[t] = 0;
+        if (t < n_terms) {
+          wt[t] = ldc(sp + pc);
+          const int ne = ldc(sp + pc + 1);
+          if (tid == 0) {
+            tdesc[t] = ne;
+            tdesc[ROW_MAX_TERMS + t] = pc + 2;
+          }
+          pc += 2 + ne;
+        }
       }
+    }
+    auto raw_aff = [&](uint32_t c) {
+      int af = 0;
+#pragma unroll
+      for (int t = 0; t < ROW_MAX_TERMS; ++t)
+        if (t < n_terms) af += ((termw[t * nch + (c >> 6)] >> (c & 63)) & 1) ? wt[t] : 0;
       return af;
     };
     if (s_aff) {
-      int pc = 1;
-      for (int t = 0; t < n_terms; ++t) {
-        const int ne = ldc(sp + pc + 1);
-        const int32_t* ids = sp + pc + 2;
-        pc += 2 + ne;
-        for (int ch = tid; ch < nch; ch += ROW_THREADS) {
-          uint64_t m = ~0ull;
-          for (int i = 0; i < ne; ++i) m &= ldg(a->b.req_mask, (uint32_t)ldc(ids + i) * (uint32_t)nch + (uint32_t)ch);
-          termw[t * nch + ch] = m;
-        }
+      __syncthreads();  // tdesc
+      for (int x = tid; x < n_terms * nch; x += ROW_THREADS) {
+        const int t = x / nch, ch = x - t * nch;
+        const int ne = tdesc[t], io = tdesc[ROW_MAX_TERMS + t];
+        uint64_t m = ~0ull;
+        for (int i = 0; i < ne; ++i)
+          m &= ldg(a->b.req_mask, (uint32_t)ldg(sp, (uint32_t)(io + i)) * (uint32_t)nch + (uint32_t)ch);
+        termw[x] = m;
       }
       __syncthreads();
     }
