@@ -45,6 +45,9 @@ struct kad_ctx {
   std::vector<int32_t> h_reqseg;  // BatchDev::req_perm [NR][8] then req_seg [n_seg][4] (host copy until the next upload)
   void* d_reqseg = nullptr;
   size_t reqseg_cap = 0;
+  int n_seg_reqs = 0;         // requirements on req_mask_kernel's segment path (the rest: value rows)
+  void* d_vrows = nullptr;    // SnapDev::vrows
+  size_t vrows_cap = 0;
   void* d_rowslab = nullptr;  // BatchDev::row_slabs
   size_t rowslab_cap = 0;
   void* d_rec = nullptr;  // UnitRec[W] (prep_kernel)
@@ -347,7 +350,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab, c->d_vrows,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -507,7 +510,21 @@ static int build_fit_table(kad_ctx* c) {
 
 // state derived from the resident snapshot: clean / negative ranges (host shadows) and, with one taint
 // word, the per-id cluster slices prep_kernel folds the taint and API filters from (SnapDev::fold)
+// SnapDev::vrows: per label key, clusters holding value id s < VR_SLOTS, and clusters with the key
+static int build_value_rows(kad_ctx* c) {
+  const int C = c->sd.C, K = c->sd.K;
+  const size_t nch = (size_t)((C + 63) / 64);
+  const size_t bytes = (size_t)K * (VR_SLOTS + 1) * nch * 8;
+  c->sd.vrows = nullptr;
+  if (C <= 0 || K <= 0 || bytes > VR_MAX_BYTES) return 0;
+  if (int r = grow(c, &c->d_vrows, &c->vrows_cap, bytes)) return r;
+  c->sd.vrows = static_cast<const uint64_t*>(c->d_vrows);
+  HIPCHK(c, launch_value_rows(c->sd, static_cast<uint64_t*>(c->d_vrows), c->stream));
+  return 0;
+}
+
 static int refresh_derived(kad_ctx* c) {
+  if (int r = build_value_rows(c)) return r;
   c->snap_negative = res_negative(c->h_res);
   c->sd.clean = res_clean(c->h_res);
   const int C = c->sd.C, TW = c->sd.TW;
@@ -725,35 +742,68 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   }
   const size_t nch = (size_t)((c->sd.C + 63) / 64);
   if (int r = grow(c, (void**)&c->d_req_mask, &c->req_mask_cap, (size_t)h.n_reqs * nch * 8)) return r;
-  // requirements grouped by label key (req_mask_kernel: one label-row load per segment and chunk):
-  // a counting sort by key (the label-free ops last, as key -1), cut into segments of <= seg_len ids;
-  // shorter segments when the batch has few requirements, so the grid still fills the chip
-  int n_seg = 0;
+  // Label requirements whose value ids are all < VR_SLOTS (at most VR_MAX_VALS of them; Exists / DoesNotExist)
+  // read the snapshot's value rows (req_row_kernel: a word is the OR of <= 5 row words). The rest is grouped
+  // by label key (req_mask_kernel: one label-row load per segment and chunk): a counting sort by key (the
+  // label-free ops last, as key -1), cut into segments of <= seg_len ids; shorter segments when the batch
+  // has few requirements, so the grid still fills the chip.
+  int n_seg = 0, n_rowreq = 0;
   {
     const int NR = h.n_reqs, K = c->snap_hdr.n_label_keys;
     const int32_t* ro = at<int32_t>(blob, h.off, KAD_B_REQ_OFF);
     const int32_t* rq = at<int32_t>(blob, h.off, KAD_B_REQ);
+    const bool vr = c->sd.vrows != nullptr;
+    auto by_rows = [&](int r) {
+      const int32_t* q = rq + ro[r];
+      const int op = q[0] & 0xff, n = (int)((uint32_t)q[0] >> 8);
+      if (!vr) return false;
+      if (op == KAD_OP_EXISTS || op == KAD_OP_DNE) return true;
+      if (op != KAD_OP_IN && op != KAD_OP_NOTIN && op != KAD_OP_EQ) return false;
+      if (n > VR_MAX_VALS) return false;
+      for (int t = 0; t < n; t++)
+        if (q[2 + t] < 0 || q[2 + t] >= VR_SLOTS) return false;
+      return true;
+    };
     auto group = [&](int r) {
       const int op = rq[ro[r]] & 0xff;
       return (op == KAD_OP_TRUE || op == KAD_OP_FALSE || op == KAD_OP_NAME_EQ || op == KAD_OP_NAME_NE) ? K : rq[ro[r] + 1];
     };
+    std::vector<uint8_t> rowr((size_t)NR);
     std::vector<int32_t> start((size_t)K + 2, 0);
-    for (int r = 0; r < NR; r++) start[(size_t)group(r) + 1]++;
+    for (int r = 0; r < NR; r++) {
+      rowr[r] = by_rows(r);
+      if (rowr[r])
+        n_rowreq++;
+      else
+        start[(size_t)group(r) + 1]++;
+    }
+    const int NS = NR - n_rowreq;  // requirements on the segment path
     for (int g = 0; g <= K; g++) start[(size_t)g + 1] += start[g];
     const long ngrp = ((long)nch + REQ_SEG_G - 1) / REQ_SEG_G;
     int seg_len = 64;
-    while (seg_len > 8 && (long)NR * ngrp / seg_len < 16384) seg_len /= 2;
+    while (seg_len > 8 && (long)NS * ngrp / seg_len < 16384) seg_len /= 2;
     long segs = 0;
     for (int g = 0; g <= K; g++) segs += (start[(size_t)g + 1] - start[g] + seg_len - 1) / seg_len;
     // entry e of req_perm: 8 words (id, word offset, op | n << 8, key word, payload 0..3) so a lane
-    // fetches its requirement with two 16-B loads, independent of the segment's label-row loads
-    const size_t perm_len = (size_t)NR * 8;
-    c->h_reqseg.assign(perm_len + 4 * (size_t)segs, 0);
+    // fetches its requirement with two 16-B loads, independent of the segment's label-row loads;
+    // value-row entries: (id, op | n << 8, key, value ids 0..4)
+    const size_t perm_len = (size_t)NS * 8, seg_len_w = 4 * (size_t)segs;
+    c->h_reqseg.assign(perm_len + seg_len_w + (size_t)n_rowreq * 8, 0);
     std::vector<int32_t> fill(start.begin(), start.end() - 1);
+    int32_t* rows_e = c->h_reqseg.data() + perm_len + seg_len_w;
+    int nr2 = 0;
     for (int r = 0; r < NR; r++) {
-      int32_t* e = c->h_reqseg.data() + 8 * (size_t)fill[(size_t)group(r)]++;
       const int32_t* q = rq + ro[r];
       const int n = (int)((uint32_t)q[0] >> 8);
+      if (rowr[r]) {
+        int32_t* e = rows_e + 8 * (size_t)nr2++;
+        e[0] = r;
+        e[1] = q[0];
+        e[2] = q[1];
+        for (int t = 0; t < VR_MAX_VALS && t < n; t++) e[3 + t] = q[2 + t];
+        continue;
+      }
+      int32_t* e = c->h_reqseg.data() + 8 * (size_t)fill[(size_t)group(r)]++;
       e[0] = r;
       e[1] = ro[r];
       e[2] = q[0];
@@ -771,7 +821,9 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
     if (int r = grow(c, &c->d_reqseg, &c->reqseg_cap, c->h_reqseg.size() * 4 + 16)) return r;
     if (!c->h_reqseg.empty())
       HIPCHK(c, hipMemcpyAsync(c->d_reqseg, c->h_reqseg.data(), c->h_reqseg.size() * 4, hipMemcpyHostToDevice, c->stream));
+    c->n_seg_reqs = NS;
   }
+
   if (int r = grow(c, &c->d_rec, &c->rec_cap, (size_t)W * sizeof(UnitRec))) return r;
   if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
@@ -822,7 +874,9 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   b.req_mask = c->d_req_mask;
   b.n_seg = n_seg;
   b.req_perm = static_cast<const int32_t*>(c->d_reqseg);
-  b.req_seg = reinterpret_cast<const int4*>(static_cast<const int32_t*>(c->d_reqseg) + (size_t)h.n_reqs * 8);
+  b.req_seg = reinterpret_cast<const int4*>(static_cast<const int32_t*>(c->d_reqseg) + (size_t)c->n_seg_reqs * 8);
+  b.n_rowreq = n_rowreq;
+  b.req_rows = reinterpret_cast<const int4*>(reinterpret_cast<const int32_t*>(b.req_seg) + 4 * (size_t)n_seg);
   b.rec = static_cast<UnitRec*>(c->d_rec);
   b.sw = static_cast<uint64_t*>(c->d_sw);
   b.cw = static_cast<uint64_t*>(c->d_cw);

@@ -14,7 +14,11 @@ constexpr int TFOLD_MAX_TW = 4;
 // unit work queue of the schedule kernels: WQ_HEADS counters, one 128-B line apart (BatchDev::wq)
 constexpr int WQ_HEADS = 64, WQ_STRIDE = 32;
 constexpr int FIT_FENCES = 256;
-constexpr int REQ_SEG_G = 8;  // chunks per req_mask_kernel wave (kad_kernels.hip REQ_G)  // prep_kernel's LDS copy of every (fit_mp / 256)-th fit value
+constexpr int REQ_SEG_G = 8;  // chunks per req_mask_kernel wave (kad_kernels.hip REQ_G)
+// SnapDev::vrows: label value ids below VR_SLOTS get a cluster row; requirements naming at most
+// VR_MAX_VALS such values are ORs of rows (req_row_kernel)
+constexpr int VR_SLOTS = 64, VR_MAX_VALS = 5;
+constexpr size_t VR_MAX_BYTES = (size_t)256 << 20;  // prep_kernel's LDS copy of every (fit_mp / 256)-th fit value
 
 struct SnapDev {
   int C, GW, TW, K, S;
@@ -41,6 +45,9 @@ struct SnapDev {
   const uint64_t* fit_rows[2];
   const int64_t *alloc_cpu, *alloc_mem, *used_cpu, *used_mem, *alloc_s, *used_s, *alloc_cores, *avail_cores;
   const uint64_t *gvk, *nsne, *ne, *pns;
+  // [K][VR_SLOTS + 1][nch]: row (k, s) = clusters whose label k has value id s, row (k, VR_SLOTS) = clusters
+  // with label k (rebuilt at upload / update; null when larger than VR_MAX_BYTES)
+  const uint64_t* vrows;
   const int32_t* lval;
   const int64_t* lint;
   const uint8_t* lok;
@@ -74,6 +81,8 @@ struct BatchDev {
   int n_seg;
   const int32_t* req_perm;
   const int4* req_seg;
+  int n_rowreq;             // requirements evaluated from SnapDev::vrows: 8-word entries (id, op | n << 8,
+  const int4* req_rows;     // key, value ids 0..4)
   uint64_t* req_mask;       // device workspace [NR][ceil(C/64)]: requirement × cluster bitmask
   // device workspace written by prep_kernel at every launch
   struct UnitRec* rec;      // [W] per-unit records
@@ -167,6 +176,7 @@ hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st)
 // per-id cluster bitmask slices of the snapshot (SnapDev::slices) and the taint table over them
 // (SnapDev::taint_tab), rebuilt at upload / update
 hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st);
+hipError_t launch_value_rows(const SnapDev& s, uint64_t* vrows, hipStream_t st);
 // true if the batch runs on schedule_lean_kernel (+ schedule_kernel over its
 // defer list); then launch_prep must run between launch_req_masks and launch_schedule.
 bool fast_path(int C);

@@ -215,6 +215,50 @@ __global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, in
   }
 }
 
+// req_row_kernel: one lane per (value-row requirement, chunk): In / Equals = OR of the value rows, NotIn
+// = its complement (a missing label matches), Exists / DoesNotExist = the key row or its complement.
+__global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b) {
+  const int nch = (s.C + 63) >> 6;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long)b.n_rowreq * nch) return;
+  const int i = (int)(g / nch), ch = (int)(g - (long)i * nch);
+  const int4 e0 = b.req_rows[2 * (size_t)i], e1 = b.req_rows[2 * (size_t)i + 1];
+  const int rid = e0.x, op = e0.y & 0xff, n = (int)((uint32_t)e0.y >> 8), key = e0.z;
+  const int v[VR_MAX_VALS] = {e0.w, e1.x, e1.y, e1.z, e1.w};
+  const uint64_t* kr = s.vrows + (size_t)key * (VR_SLOTS + 1) * nch + ch;
+  uint64_t acc = 0;
+  if (op == KAD_OP_EXISTS || op == KAD_OP_DNE) {
+    acc = kr[(size_t)VR_SLOTS * nch];
+  } else {
+#pragma unroll
+    for (int t = 0; t < VR_MAX_VALS; ++t)
+      if (t < n) acc |= kr[(size_t)v[t] * nch];
+  }
+  if (op == KAD_OP_NOTIN || op == KAD_OP_DNE) acc = ~acc;
+  if (ch == nch - 1 && (s.C & 63)) acc &= (1ull << (s.C & 63)) - 1;  // clusters past C: never
+  b.req_mask[(size_t)rid * nch + ch] = acc;
+}
+
+// SnapDev::vrows: one wave per (key, chunk), lane = cluster; lane s < VR_SLOTS collects value s's word
+__global__ __launch_bounds__(256) void value_rows_kernel(SnapDev s, uint64_t* out) {
+  const int lane = lane_id();
+  const int nch = (s.C + 63) >> 6;
+  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= (long)s.K * nch) return;
+  const int k = (int)(gw / nch), ch = (int)(gw % nch);
+  const int c = ch * WAVE + lane;
+  const int v = c < s.C ? ldg(s.lval, (uint32_t)(k * s.C + c)) : -1;
+  uint64_t mine = 0;
+  for (int t = 0; t < VR_SLOTS; ++t) {
+    const uint64_t m = ballot(v == t);
+    mine = lane == t ? m : mine;
+  }
+  const uint64_t has = ballot(v >= 0);
+  uint64_t* kr = out + (size_t)k * (VR_SLOTS + 1) * nch + ch;
+  kr[(size_t)lane * nch] = mine;
+  if (lane == 0) kr[(size_t)VR_SLOTS * nch] = has;
+}
+
 // A unit's program (filter / score words) held in VGPR lanes: word i < 64 is
 // read with v_readlane (no memory latency on the interpretation chain);
 // longer programs fall back to scalar loads for the tail.
@@ -3341,10 +3385,19 @@ static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
+  const long lanes = (long)b.n_rowreq * nch;
+  if (lanes > 0) hipLaunchKernelGGL(req_row_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, s, b);
   const int ngrp = (nch + REQ_G - 1) / REQ_G;
   const long waves = (long)b.n_seg * ngrp;
+  if (waves > 0) hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, b, ngrp);
+  return hipGetLastError();
+}
+
+hipError_t launch_value_rows(const SnapDev& s, uint64_t* vrows, hipStream_t st) {
+  (void)hipGetLastError();
+  const long waves = (long)s.K * ((s.C + 63) >> 6);
   if (waves == 0) return hipSuccess;
-  hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, b, ngrp);
+  hipLaunchKernelGGL(value_rows_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, vrows);
   return hipGetLastError();
 }
 
