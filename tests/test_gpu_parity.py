@@ -308,6 +308,55 @@ def test_row_kernel_long_feasible_lists(ctx, seed, C, prof):
     assert_same(res, c_oracle(snap, batch, fwk), f"rows seed {seed} C={C} profile {prof}")
 
 
+@pytest.mark.parametrize("seed", [7101, 7102])
+def test_requirement_value_rows_and_segments(ctx, seed):
+    """Requirement masks from both paths: In / NotIn / Exists / DoesNotExist whose value ids are < 64 and
+    at most 5 (snapshot value rows, req_row_kernel) and the rest — value ids >= 64 (a key with 150 distinct
+    values), lists longer than 5, Gt / Lt, metadata.name — through the key-grouped segments
+    (req_mask_kernel); ClusterAffinity filter and score against the C oracle."""
+    rng = np.random.default_rng(seed)
+    C = 700
+    clusters = synth.gen_clusters(rng, C, n_keys=3, n_vals=4, n_int_keys=1)
+    for c in clusters:  # "wide" has 150 distinct values; some clusters lack it
+        if rng.random() < 0.85:
+            c.labels = dict(c.labels or {}, wide=f"w{int(rng.integers(0, 150))}")
+    names = [c.name for c in clusters]
+
+    def req():
+        r = rng.random()
+        if r < 0.35:
+            vals = [f"w{int(v)}" for v in rng.integers(0, 150, int(rng.integers(1, 9)))]
+            return T.ClusterSelectorRequirement("wide", T.OP_IN if rng.random() < 0.5 else T.OP_NOT_IN, vals)
+        if r < 0.5:
+            return T.ClusterSelectorRequirement("wide", T.OP_EXISTS if rng.random() < 0.5 else T.OP_DOES_NOT_EXIST,
+                                                None)
+        if r < 0.6:
+            return T.ClusterSelectorRequirement("num0", T.OP_GT if rng.random() < 0.5 else T.OP_LT,
+                                                [str(int(rng.integers(0, 1000)))])
+        return synth._expr(rng, 3, 4, 1, all_ops=True, p_invalid=0.03)
+
+    units = []
+    for w in range(400):
+        terms = []
+        for _ in range(int(rng.integers(1, 4))):
+            fields = None
+            if rng.random() < 0.2:
+                fields = [T.ClusterSelectorRequirement("metadata.name", T.OP_NOT_IN,
+                                                       [names[int(rng.integers(0, C))]])]
+            terms.append(T.ClusterSelectorTerm([req() for _ in range(int(rng.integers(1, 3)))], fields))
+        prefs = [T.PreferredSchedulingTerm(int(rng.integers(1, 50)), T.ClusterSelectorTerm([req()]))
+                 for _ in range(int(rng.integers(0, 3)))]
+        units.append(T.SchedulingUnit(
+            group="apps", version="v1", kind="Deployment", namespace="default", name=f"vr-{w}", desired_replicas=3,
+            scheduling_mode=T.SCHEDULING_MODE_DUPLICATE, max_clusters=int(rng.integers(1, 9)),
+            affinity=T.Affinity(T.ClusterAffinity(T.ClusterSelector(terms), prefs or None))))
+    for fwk in (F.Framework(F.default_enabled_plugins()),
+                F.Framework(F.EnabledPlugins([F.ClusterAffinity], [F.ClusterAffinity], [F.MaxCluster], []))):
+        snap, batch, res = run(ctx, clusters, units, fwk)
+        assert (res.status == pack.ST_OK).mean() > 0.3
+        assert_same(res, c_oracle(snap, batch, fwk), f"value rows seed {seed}")
+
+
 def test_large_c_global_scratch(ctx):
     """C = 6000 does not fit the per-wave LDS budget: rows run from global scratch slabs."""
     clusters, units = synth.gen_fuzz(4242, W=200, C=6000)
