@@ -29,6 +29,8 @@ namespace kad {
 // 256 stripes (a shared counter per phase would serialise the waves).
 #ifdef KAD_PHASE_PROF
 __device__ unsigned long long g_phase[256 * 32];
+// lean kernel: (start, end) s_memtime of every wave of the last launch, for the wave-lifetime split
+__device__ unsigned long long g_wavetime[8192 * 2];
 #define KAD_PT(v) const unsigned long long v = __builtin_readcyclecounter()
 #define KAD_PACC uint32_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
@@ -1312,6 +1314,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   const uint64_t* sws = largs()->b.sw;
   uint32_t* heads = largs()->b.wq;
   WorkTicket tk = wq_start((int)(blockDim.x >> 6));
+#ifdef KAD_PHASE_PROF
+  const unsigned long long wt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz, device-wide
+#endif
   // the next batch's records are loaded one batch ahead (nrvA/nsvv): the
   // wait at a batch start then only covers the previous unit's stores
   uint32_t rvA = 0, svv = ~0u, nrvA = 0, nsvv = ~0u;
@@ -1843,6 +1848,15 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     KAD_PT(t4);
     KAD_PADD(3, t4 - t3);
   }
+#ifdef KAD_PHASE_PROF
+  {
+    const int gwv = blockIdx.x * (int)(blockDim.x >> 6) + wv;
+    if (lane == 0 && gwv < 8192) {
+      g_wavetime[2 * gwv] = wt_start;
+      g_wavetime[2 * gwv + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+#endif
   KAD_PFLUSH_LEAN;
 }
 
@@ -3362,6 +3376,10 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
 // ================================================================ launchers
 int debug_phase_counters(uint64_t* out, int reset) {
 #ifdef KAD_PHASE_PROF
+  if (reset < 0) {  // the lean kernel's per-wave (start, end) timestamps: out holds 8192 * 2 entries
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavetime), sizeof(unsigned long long) * 8192 * 2) != hipSuccess) return -1;
+    return 8192;
+  }
   static unsigned long long h[256 * 32];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof h) != hipSuccess) return -1;
   for (int i = 0; i < 32; ++i) {

@@ -69,6 +69,35 @@ def main():
     L.kad_debug_phase_counters(cnt.ctypes.data, 1)
     W = batch.W * a.reps
     out = {"config": a.config, "units": batch.W, "reps": a.reps}
+    # lean kernel wave lifetimes of the last launch (s_memtime): mean lifetime / kernel span, start / end spread
+    wt = np.zeros(8192 * 2, dtype=np.uint64)
+    if L.kad_debug_phase_counters(wt.ctypes.data, -1) > 0:
+        st, en = wt[0::2].astype(np.int64), wt[1::2].astype(np.int64)
+        live = np.nonzero(en > 0)[0]
+        if len(live):
+            # s_memrealtime (100 MHz, device-wide); also split by XCD (4-wave blocks round-robin over 8 XCDs)
+            xcd = (live // 4) % 8
+            span_all = float(en[live].max() - st[live].min())
+            out["lean_span_us"] = span_all / 100.0
+            out["lean_wave_lifetime_frac"] = round(float((en[live] - st[live]).mean()) / span_all, 3)
+            out["lean_start_p50_p90_max_frac"] = [round(float(np.percentile(st[live] - st[live].min(), q)) / span_all, 3)
+                                                  for q in (50, 90, 100)]
+            out["lean_end_p10_p50_min_frac"] = [round(float(np.percentile(en[live] - st[live].min(), q)) / span_all, 3)
+                                                for q in (10, 50, 0)]
+            fr, ss, es = [], [], []
+            for x in range(8):
+                sel = live[xcd == x]
+                if not len(sel):
+                    continue
+                s0, e0 = st[sel], en[sel]
+                span = float(e0.max() - s0.min())
+                fr.append(float((e0 - s0).mean()) / span)
+                ss.append(float(s0.max() - s0.min()) / span)
+                es.append(float(e0.max() - e0.min()) / span)
+            out["lean_waves"] = int(len(live))
+            out["lean_wave_lifetime_frac_per_xcd"] = [round(v, 3) for v in fr]
+            out["lean_start_spread_frac_per_xcd"] = [round(v, 3) for v in ss]
+            out["lean_end_spread_frac_per_xcd"] = [round(v, 3) for v in es]
     for i, nm in enumerate(NAMES):
         v = float(cnt[i])
         if nm == "-":
