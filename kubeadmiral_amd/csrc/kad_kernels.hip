@@ -1057,21 +1057,22 @@ struct WorkTicket {
   int x;             // head of the pending ticket
   int i;             // its atomicAdd result (lane 0); batch index = i + static_batches(x)
   int wpb, nblocks;  // waves per block, grid size: the static first round
+  int B;             // units per batch (<= WQ_BATCH): small enough that a wave takes >= ~12 batches
 };
 // the static first-round batches of head x: one per wave of every block b < nblocks with b & 63 == x
 __device__ __forceinline__ int static_batches(const WorkTicket& t, int x) { return t.wpb * ((t.nblocks - x + 63) >> 6); }
-__device__ __forceinline__ WorkTicket wq_start(int wpb) {
+__device__ __forceinline__ WorkTicket wq_start(int wpb, int B = WQ_BATCH) {
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  WorkTicket t{(int)(blockIdx.x & (WQ_HEADS - 1)), 0, wpb, (int)gridDim.x};
+  WorkTicket t{(int)(blockIdx.x & (WQ_HEADS - 1)), 0, wpb, (int)gridDim.x, B};
   t.i = (int)(blockIdx.x >> 6) * wpb + wv - static_batches(t, t.x);
   return t;
 }
 __device__ __forceinline__ void wq_issue(uint32_t* heads, WorkTicket& t) {
   if (lane_id() == 0) t.i = (int)atomicAdd(heads + t.x * WQ_STRIDE, 1u);
 }
-__device__ __forceinline__ int wq_head_batches(int W, int x) {
+__device__ __forceinline__ int wq_head_batches(int W, int x, int B) {
   const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
-  return (s1 - s0 + WQ_BATCH - 1) / WQ_BATCH;
+  return (s1 - s0 + B - 1) / B;
 }
 // the batch [first, first + count) of a ticket; count 0 = queue drained. A drained head costs one
 // wave-wide look at all 64 counters (lane l loads head l, device-coherent) and one atomic on a head
@@ -1081,13 +1082,13 @@ __device__ __forceinline__ int2 wq_resolve(uint32_t* heads, int W, WorkTicket& t
   for (;;) {
     const int x = t.x;
     const int bi = __builtin_amdgcn_readfirstlane(t.i) + static_batches(t, x);
-    if (bi < wq_head_batches(W, x)) {
+    if (bi < wq_head_batches(W, x, t.B)) {
       const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
-      const int first = s0 + bi * WQ_BATCH;
-      return make_int2(first, (s1 - first) < WQ_BATCH ? (s1 - first) : WQ_BATCH);
+      const int first = s0 + bi * t.B;
+      return make_int2(first, (s1 - first) < t.B ? (s1 - first) : t.B);
     }
     const uint32_t taken = __hip_atomic_load(heads + lane * WQ_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t open = ballot((int)taken + static_batches(t, lane) < wq_head_batches(W, lane));
+    const uint64_t open = ballot((int)taken + static_batches(t, lane) < wq_head_batches(W, lane, t.B));
     if (!open) return make_int2(0, 0);
     // same XCD first (heads x & 7 + 8j), in rotation order after x; then the lowest open head
     const uint64_t same = open & (0x0101010101010101ull << (x & 7));
@@ -1160,7 +1161,7 @@ struct LeanArgs {
   BatchDev b;
   OutDev o;
   ProfDev p;
-  int wave_bytes, waves_per_block, units_per_wave;
+  int wave_bytes, waves_per_block, units_per_wave;  // units_per_wave: work-queue batch size (<= LEAN_BATCH)
   int cache_ne, cache_pn;  // optional cache arrays present
 };
 typedef const __attribute__((address_space(4))) LeanArgs* LArgs;
@@ -1313,7 +1314,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   const UnitRec* recs = largs()->b.rec;
   const uint64_t* sws = largs()->b.sw;
   uint32_t* heads = largs()->b.wq;
-  WorkTicket tk = wq_start((int)(blockDim.x >> 6));
+  WorkTicket tk = wq_start((int)(blockDim.x >> 6), largs()->units_per_wave);
 #ifdef KAD_PHASE_PROF
   const unsigned long long wt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz, device-wide
 #endif
@@ -3574,7 +3575,12 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     long grid = (long)n_cu * per_cu;
     const long need = ((long)b.W + wpb - 1) / wpb;  // at least one unit per wave
     if (grid > need) grid = need;
-    const LeanArgs A{s, b, o, p, (int)lb, wpb, LEAN_BATCH, cache_ne, cache_pn};
+    // units per work-queue batch: at most LEAN_BATCH (one VGPR of UnitRecs), small enough that every wave
+    // takes >= 12 batches, so the waves run out of work together (C2: 16 units per wave → 1-unit batches)
+    const long upw = ((long)b.W + grid * wpb - 1) / (grid * wpb);
+    int bsz = (int)(upw / 6);
+    bsz = bsz < 1 ? 1 : (bsz > LEAN_BATCH ? LEAN_BATCH : bsz);
+    const LeanArgs A{s, b, o, p, (int)lb, wpb, bsz, cache_ne, cache_pn};
     switch (nch) {
       case 1: cl ? launch_lean<1, true>(A, (int)grid, lds, st) : launch_lean<1, false>(A, (int)grid, lds, st); break;
       case 2: cl ? launch_lean<2, true>(A, (int)grid, lds, st) : launch_lean<2, false>(A, (int)grid, lds, st); break;
