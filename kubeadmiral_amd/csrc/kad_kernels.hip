@@ -924,7 +924,10 @@ __device__ __forceinline__ int2 fit_ranks(const SnapDev& s, const int64_t (*fenc
   return make_int2(b0, b1);
 }
 
-constexpr int PREP_CPL = 4;                            // chunks per lane
+#ifndef KAD_PREP_CPL
+#define KAD_PREP_CPL 4
+#endif
+constexpr int PREP_CPL = KAD_PREP_CPL;                 // chunks per lane
 __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
   constexpr int CPL = PREP_CPL;
   __shared__ int32_t prog_words[256 * CPL];  // words CPL*l .. CPL*l+CPL-1 of its unit's filter program, per lane
