@@ -14,7 +14,7 @@ step() {  # name, timeout, cmd...
   local rc=$?
   echo "== $name rc=$rc"
   if [ $rc -ne 0 ]; then tail -n 15 "gpurun_out/${tag}_$name.log"; exit $rc; fi
-  python -c "import json; d=json.load(open('gpurun_out/${tag}_$name.json')); print(d['config']['workload'][:40], d['value'], d['ms_per_step'], d['config']['stage_ms'])"
+  python -c "import json; d=json.loads(open('gpurun_out/${tag}_$name.json').read().strip().splitlines()[-1]); print(d['config']['workload'][:40], d['value'], d['ms_per_step'], d['config']['stage_ms'])"
 }
 step bench 600 python bench.py --steps 20 --warmup 5
 step c4 600 python bench.py --config c4 --steps 10 --warmup 2 --cpu-seconds 10
