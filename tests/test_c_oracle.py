@@ -55,6 +55,18 @@ def test_c_oracle_matches_python_oracle_fuzz(seed):
     assert not bad, bad[:3]
 
 
+@pytest.mark.parametrize("seed,n_taints", [(901, 100), (902, 160), (903, 220)])
+def test_c_oracle_matches_python_oracle_many_taint_words(seed, n_taints):
+    """Taint ids over 2-4+ words (the packer's multi-word toleration / taint masks, SnapDev::TW > 1): the C
+    oracle the GPU tests check against agrees with the object-level oracle under every fuzz profile."""
+    from kubeadmiral_amd import pack
+    clusters, units = synth.gen_fuzz(seed, W=40, C=30, n_taints=n_taints)
+    assert pack.Snapshot(clusters).TW >= 2
+    for i in range(len(synth.FUZZ_PROFILES)):
+        bad = compare(clusters, units, synth.fuzz_framework(i))
+        assert not bad, (i, bad[:3])
+
+
 def test_c_oracle_matches_python_oracle_c1():
     clusters, units, fwk = synth.make_config("c1", W=200)
     assert not compare(clusters, units, fwk, n_threads=4)
