@@ -743,7 +743,8 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   const size_t nch = (size_t)((c->sd.C + 63) / 64);
   if (int r = grow(c, (void**)&c->d_req_mask, &c->req_mask_cap, (size_t)h.n_reqs * nch * 8)) return r;
   // Label requirements whose value ids are all < VR_SLOTS (at most VR_MAX_VALS of them; Exists / DoesNotExist)
-  // read the snapshot's value rows (req_row_kernel: a word is the OR of <= 5 row words). The rest is grouped
+  // read the snapshot's value rows (req_row_kernel: a word is the OR of <= 5 row words); so do the label-free
+  // ops (TRUE / FALSE / metadata.name =, !=), whose words are constants or one bit. The rest is grouped
   // by label key (req_mask_kernel: one label-row load per segment and chunk): a counting sort by key (the
   // label-free ops last, as key -1), cut into segments of <= seg_len ids; shorter segments when the batch
   // has few requirements, so the grid still fills the chip.
@@ -756,6 +757,8 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
     auto by_rows = [&](int r) {
       const int32_t* q = rq + ro[r];
       const int op = q[0] & 0xff, n = (int)((uint32_t)q[0] >> 8);
+      // label-free ops: their words need no snapshot data at all
+      if (op == KAD_OP_TRUE || op == KAD_OP_FALSE || op == KAD_OP_NAME_EQ || op == KAD_OP_NAME_NE) return true;
       if (!vr) return false;
       if (op == KAD_OP_EXISTS || op == KAD_OP_DNE) return true;
       if (op != KAD_OP_IN && op != KAD_OP_NOTIN && op != KAD_OP_EQ) return false;

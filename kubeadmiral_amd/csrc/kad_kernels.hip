@@ -218,7 +218,8 @@ __global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, in
 }
 
 // req_row_kernel: one lane per (value-row requirement, chunk): In / Equals = OR of the value rows, NotIn
-// = its complement (a missing label matches), Exists / DoesNotExist = the key row or its complement.
+// = its complement (a missing label matches), Exists / DoesNotExist = the key row or its complement;
+// TRUE / FALSE / metadata.name =, != are constants or one bit (no loads).
 __global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b) {
   const int nch = (s.C + 63) >> 6;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
@@ -227,8 +228,16 @@ __global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b) {
   const int4 e0 = b.req_rows[2 * (size_t)i], e1 = b.req_rows[2 * (size_t)i + 1];
   const int rid = e0.x, op = e0.y & 0xff, n = (int)((uint32_t)e0.y >> 8), key = e0.z;
   const int v[VR_MAX_VALS] = {e0.w, e1.x, e1.y, e1.z, e1.w};
-  const uint64_t* kr = s.vrows + (size_t)key * (VR_SLOTS + 1) * nch + ch;
   uint64_t acc = 0;
+  if (op == KAD_OP_TRUE || op == KAD_OP_FALSE || op == KAD_OP_NAME_EQ || op == KAD_OP_NAME_NE) {
+    // label-free: metadata.name = / != the cluster with snapshot id `key` (-1: no such cluster)
+    const uint64_t one = (key >= 0 && (key >> 6) == ch) ? 1ull << (key & 63) : 0ull;
+    acc = op == KAD_OP_TRUE ? ~0ull : op == KAD_OP_FALSE ? 0ull : op == KAD_OP_NAME_EQ ? one : ~one;
+    if (ch == nch - 1 && (s.C & 63)) acc &= (1ull << (s.C & 63)) - 1;  // clusters past C: never
+    b.req_mask[(size_t)rid * nch + ch] = acc;
+    return;
+  }
+  const uint64_t* kr = s.vrows + (size_t)key * (VR_SLOTS + 1) * nch + ch;
   if (op == KAD_OP_EXISTS || op == KAD_OP_DNE) {
     acc = kr[(size_t)VR_SLOTS * nch];
   } else {
