@@ -105,8 +105,11 @@ def make_columns(cfg: str, lo: int, hi: int, clusters):
     rng = np.random.default_rng([synth.SEEDS[cfg], lo])
     if cfg in ("c2", "c3"):
         return synth.gen_units_c2_columns(rng, hi - lo, prefix=f"su{lo}")
-    gen = {"c1": synth.gen_units_c1, "c4": synth.gen_units_c4, "c5": synth.gen_units_c5}[cfg]
-    units = gen(rng, hi - lo, clusters)
+    if cfg == "c4":  # vectorised generators: 1M C4 units in seconds (the object generator takes minutes)
+        return synth.gen_units_c4_columns(rng, hi - lo, [c.name for c in clusters], prefix=f"c4-{lo}")
+    if cfg == "c5":
+        return synth.gen_units_c5_columns(rng, hi - lo, [c.name for c in clusters], prefix=f"c5-{lo}")
+    units = synth.gen_units_c1(rng, hi - lo, clusters)
     for i, su in enumerate(units):
         su.name = f"{su.name}-{lo + i}"
     return CO.from_units(units)
@@ -124,15 +127,70 @@ def canonical_bytes(n_reqs, n_tols, count, C, TW, divide_counts):
 
 
 def load_pmc(cfg: str, W: int, C: int):
-    """profiles/pmc_<cfg>.json (scripts/profile.sh → scripts/pmc_summary.py) when it matches the workload."""
+    """profiles/pmc_<cfg>.json (scripts/profile.sh → scripts/pmc_summary.py) when it was collected on this
+    workload AND on this code (its ``src_hash`` = build.source_hash() of libkad.so's sources): counters of
+    an older kernel are never reported against today's timing. Returns (pmc | None, path, why-not)."""
+    from kubeadmiral_amd.build import source_hash
+
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
-        return None, path
+        return None, path, "no PMC profile"
     with open(path) as f:
         pmc = json.load(f)
     if pmc.get("units") != W or pmc.get("clusters") != C:
-        return None, path
-    return pmc, path
+        return None, path, f"PMC profile is for {pmc.get('units')} x {pmc.get('clusters')}"
+    if pmc.get("src_hash") != source_hash():
+        return None, path, f"PMC profile is stale (src_hash {pmc.get('src_hash')} != {source_hash()})"
+    return pmc, path, None
+
+
+# stage (kad_stage_timing) → the kernels it launches (rocprofv3 names contain these)
+STAGE_KERNELS = {"req_mask": ("req_row_kernel", "req_mask_kernel"), "prep": ("prep_kernel",),
+                 "main": ("schedule_wide_kernel", "schedule_lean_kernel"), "rows": ("schedule_row_kernel",),
+                 "defer": ("schedule_kernel<",), "planner": ("plan_kernel",)}
+
+
+def pmc_kernel_sum(pmc, stage: str, main_name: str = None):
+    """Per-launch counters of the stage's kernels summed (None without a profile)."""
+    if pmc is None:
+        return None
+    names = (main_name,) if main_name else STAGE_KERNELS[stage]
+    acc = {}
+    for k, d in pmc.get("kernels", {}).items():
+        if any(n in k for n in names):
+            for c, v in d.items():
+                if isinstance(v, (int, float)):
+                    acc[c] = acc.get(c, 0.0) + v
+    return acc or None
+
+
+def roofline_for(stage: str, kernel: str, t_ms: float, compulsory: float, pmc, pmc_path, why_not):
+    """The roofline of one kernel: HBM (compulsory bytes / live time; PMC-measured traffic beside it),
+    VALU issue and SALU issue (PMC instruction counts / live time vs the chip's issue rates). ``bound`` is
+    the largest fraction — the resource that binds — and ``achieved`` / ``peak`` / ``frac`` are its."""
+    t = max(t_ms, 1e-9) * 1e-3
+    d = pmc_kernel_sum(pmc, stage, None if stage != "main" else kernel)
+    traffic = d.get("hbm_bytes_corrected") if d else None
+    hbm_gbs = compulsory / t / 1e9
+    cand = {"hbm": (traffic / t / 1e9 if traffic else hbm_gbs, HBM_PEAK_GBS, "GB/s")}
+    issue = None
+    if d and d.get("SQ_INSTS_VALU") is not None:
+        cand["valu_issue"] = (d["SQ_INSTS_VALU"] / t, VALU_PEAK, "wave-instr/s")
+        cand["salu_issue"] = (d["SQ_INSTS_SALU"] / t, SALU_PEAK, "wave-instr/s")
+        issue = {"valu_insts": d["SQ_INSTS_VALU"], "salu_insts": d["SQ_INSTS_SALU"],
+                 "valu_frac": d["SQ_INSTS_VALU"] / t / VALU_PEAK, "salu_frac": d["SQ_INSTS_SALU"] / t / SALU_PEAK,
+                 "lds_insts": d.get("SQ_INSTS_LDS"),
+                 "wait_frac": (d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]) if d.get("SQ_WAVE_CYCLES") else None,
+                 "peaks": "VALU 1.23e12 wave-instr/s (256 CU x 4 SIMD x 2.4 GHz / 2), SALU 6.1e11 (256 CU x 2.4 GHz)"}
+    bound = max(cand, key=lambda b: cand[b][0] / cand[b][1])
+    ach, peak, unit = cand[bound]
+    return {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak, "traffic": traffic,
+            "kernel": kernel, "time_ms": t_ms, "compulsory_bytes_per_launch": compulsory,
+            "hbm": {"compulsory_gbs": hbm_gbs, "compulsory_frac": hbm_gbs / HBM_PEAK_GBS,
+                    "measured_gbs": traffic / t / 1e9 if traffic else None,
+                    "measured_frac": traffic / t / 1e9 / HBM_PEAK_GBS if traffic else None},
+            "issue": issue,
+            "pmc": os.path.relpath(pmc_path, ROOT) if pmc is not None else why_not}
 
 
 def cpu_baseline(snap, batch, fwk, C, target_s):
@@ -161,7 +219,7 @@ def cpu_baseline(snap, batch, fwk, C, target_s):
 
 
 # ------------------------------------------------------------------------ scheduling bench
-def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, extra_line=False):
+def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, cpu_seconds=None):
     import torch  # noqa: F401  (HIP runtime initialised by torch before libkad.so)
 
     from kubeadmiral_amd import columns as CO
@@ -171,6 +229,7 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, extra_line
     W0, C = synth.SIZES[cfg]
     W_total = W_total if W_total is not None else (args.units if args.units is not None else W0)
     fwk = synth.profile_for(cfg)
+    cpu_seconds = args.cpu_seconds if cpu_seconds is None else cpu_seconds
     lo, hi = shard.shard_range(W_total, rank, world)
     dev = f"cuda:{local}"
     # RCCL moves device tensors over xGMI; the gloo rehearsal mode (--backend gloo) moves host tensors
@@ -249,6 +308,7 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, extra_line
         dist.barrier()
     elapsed = time.perf_counter() - t0
     res = ctx.download()
+    paths = ctx.path_counts()
     # per-stage device time (HIP events on the context's stream), outside the timed region
     ctx.set_timing(True)
     st = []
@@ -263,7 +323,7 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, extra_line
     # placements all-gathered over RCCL (fixed per-rank slot arrays), timed on its own
     allgather = None
     if dist is not None:
-        allgather = gather_placements(ctx, batch, res, dist, world, cdev)
+        allgather = gather_placements(ctx, batch, res, dist, world, cdev, blobs if rank == 0 else None, fwk)
 
     if dist is not None:
         t = torch.tensor([ms] + [stage[k] for k in ctx.STAGES], dtype=torch.float64, device=cdev)
@@ -273,75 +333,136 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, extra_line
 
     out = None
     if rank == 0:
-        value = W_total * C / (ms * 1e-3)
-        W0r = batch.W
-        nch = (C + 63) // 64
-        count = res.count.astype(np.int64)
-        out_bytes = 12 * W0r + 12 * float(count.sum())
-        # dominant kernel (the main schedule kernel): its compulsory bytes per launch — unit records,
-        # static filter words, the cluster columns it caches, its outputs — over its HIP-event time
-        main_bytes = 64 * W0r + 8 * nch * W0r + 56 * C + out_bytes
-        t_main = stage["main"]
-        main_gbs = main_bytes / (t_main * 1e-3) / 1e9
-        # the whole filter/score/select stage: batch blob + snapshot + outputs once
-        fss_ms = stage["req_mask"] + stage["prep"] + stage["main"] + stage["defer"]
-        stage_bytes = batch.blob.nbytes + snap.blob.nbytes + out_bytes
-        cols0, nb0 = stats0
-        divide = (nb0.flags & pack.W_DUPLICATE) == 0 if fwk.replicas_plugin >= 0 else np.zeros(W0r, bool)
-        kbytes, pbytes = canonical_bytes(nb0.n_reqs, nb0.n_tols, count, C, snap.TW, count[divide])
-        pmc, pmc_path = load_pmc(cfg, W0r, C)
-        traffic = issue = None
-        if pmc is not None:
-            k = pmc.get("main_kernel", {})
-            traffic = k.get("hbm_bytes_per_launch")
-            if k.get("SQ_INSTS_VALU") is not None:
-                issue = {"valu_insts": k["SQ_INSTS_VALU"], "salu_insts": k["SQ_INSTS_SALU"],
-                         "valu_frac": k["SQ_INSTS_VALU"] / (t_main * 1e-3 * VALU_PEAK),
-                         "salu_frac": k["SQ_INSTS_SALU"] / (t_main * 1e-3 * SALU_PEAK),
-                         "peaks": "VALU 1.23e12 wave-instr/s (256 CU x 4 SIMD x 2.4 GHz / 2), "
-                                  "SALU 6.1e11 (256 CU x 2.4 GHz)", "source": os.path.relpath(pmc_path, ROOT)}
-        out = {
-            "metric": "scheduling decisions/sec (workload x cluster evals/s)",
-            "value": value,
-            "unit": "decisions/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "int64",
-            "data": "synthetic (seeded SURVEY.md §8(d) generator; no cluster/dataset available)",
-            "config": {"workload": f"{cfg}: {WORKLOAD_DESC[cfg]}", "units_total": W_total, "units_per_gpu": W0r,
-                       "clusters": C, "parallelism": f"dp{world}", "rccl_world_size": world,
-                       "stage_ms": stage},
-            "roofline": {
-                "bound": "hbm", "achieved": main_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": main_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "schedule_wide_kernel" if 4 < nch <= 16 else "schedule_lean_kernel",
-                "time_ms": t_main, "compulsory_bytes_per_launch": main_bytes,
-                "bytes_model": "64 B UnitRec + 8 B x chunks static filter words per unit, 56 B per cached "
-                               "cluster, 12 B per unit + 12 B per placement out",
-                "measured_hbm_gbs": (traffic / (t_main * 1e-3) / 1e9) if traffic else None,
-                "stage": {"time_ms": fss_ms, "compulsory_bytes": stage_bytes,
-                          "frac": stage_bytes / (fss_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                "issue": issue,
-                "algorithmic_bytes_per_launch": kbytes,
-                "algorithmic_model_frac": kbytes / (fss_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "planner": ({"time_ms": stage["planner"], "bytes": pbytes,
-                             "frac": pbytes / (stage["planner"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
-                            if stage["planner"] > 0.001 else None),
-            },
-            "allgather": allgather,
-            "end_to_end": None,
-            "cpu_baseline": None,
-        }
+        out = schedule_line(args, cfg, world, W_total, C, batch, snap, fwk, res, stage, ms, stats0, paths)
+        out["allgather"] = allgather
         if world == 1:
-            out["end_to_end"] = end_to_end(ctx, snap, fwk, cols0, res, C, packer_for=snap)
+            out["end_to_end"] = end_to_end(ctx, snap, fwk, stats0[0], res, C, packer_for=snap)
             if not args.no_cpu_baseline:
                 log(f"[rank 0] timing the CPU baseline (C restatement of the reference) on {cfg}")
-                out["cpu_baseline"] = cpu_baseline(snap, batch, fwk, C, args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(snap, batch, fwk, C, cpu_seconds)
+    ctx.close()
+    return out
+
+
+def stage_bytes_model(stage, W, C, nch, batch, snap, out_bytes, paths, n_distinct_reqs, divide_slots):
+    """Compulsory HBM bytes of one launch of each stage's kernels (inputs read once, outputs written once):
+    * req_mask: every distinct requirement's row words written + the label columns read once;
+    * prep: the batch blob read once + UnitRec (64 B) and static filter words (8 B x chunks) per unit written;
+    * main: UnitRec + static words per unit, 56 B per cached cluster, 12 B per unit + 12 B per placement out;
+    * rows / defer: UnitRec + static words per unit the kernel takes, its cached cluster columns;
+    * planner: SURVEY §8(d) B_plan = 48 B per (Divide unit, selected cluster)."""
+    K = snap.K if hasattr(snap, "K") else 0
+    if stage == "req_mask":
+        return 8.0 * nch * max(0, n_distinct_reqs) + 4.0 * K * C
+    if stage == "prep":
+        return float(batch.blob.nbytes) + (64.0 + 8 * nch) * W
+    if stage == "main":
+        return (64.0 + 8 * nch) * W + 56.0 * C + out_bytes
+    if stage == "rows":
+        return (64.0 + 8 * nch) * paths["row_kernel"] + 56.0 * C
+    if stage == "defer":
+        return (64.0 + 8 * nch) * paths["full_kernel"] + 56.0 * C
+    if stage == "planner":
+        return 48.0 * divide_slots
+    return 0.0
+
+
+def schedule_line(args, cfg, world, W_total, C, batch, snap, fwk, res, stage, ms, stats0, paths):
+    """The bench line of one scheduling config (rank 0): value, stage times, the per-stage rooflines and
+    the dominant kernel's roofline (the stage with the longest live HIP-event time)."""
+    from kubeadmiral_amd import pack
+
+    W0r = batch.W
+    nch = (C + 63) // 64
+    count = res.count.astype(np.int64)
+    out_bytes = 12 * W0r + 12 * float(count.sum())
+    cols0, nb0 = stats0
+    divide = (nb0.flags & pack.W_DUPLICATE) == 0 if fwk.replicas_plugin >= 0 else np.zeros(W0r, bool)
+    divide_slots = float(count[divide].sum())
+    kbytes, pbytes = canonical_bytes(nb0.n_reqs, nb0.n_tols, count, C, snap.TW, count[divide])
+    pmc, pmc_path, why_not = load_pmc(cfg, W0r, C)
+    # the bench snapshots are clean (allocatable >= used >= 0): wide kernel for 5..16 chunks, else lean
+    main_kernel = "schedule_wide_kernel" if 4 < nch <= 16 else "schedule_lean_kernel"
+    kernels = {}
+    for st in ("req_mask", "prep", "main", "rows", "defer", "planner"):
+        t = stage.get(st, 0.0)
+        if t < 0.002:  # not launched (events back to back)
+            continue
+        kname = main_kernel if st == "main" else " + ".join(STAGE_KERNELS[st])
+        cb = stage_bytes_model(st, W0r, C, nch, batch, snap, out_bytes, paths, nb0.n_distinct_reqs, divide_slots)
+        kernels[st] = roofline_for(st, kname, t, cb, pmc, pmc_path, why_not)
+    dom = max(kernels, key=lambda k: kernels[k]["time_ms"])
+    roof = dict(kernels[dom])
+    fss_ms = sum(stage.get(k, 0.0) for k in ("req_mask", "prep", "main", "rows", "defer"))
+    stage_b = batch.blob.nbytes + snap.blob.nbytes + out_bytes
+    roof["stage"] = {"time_ms": fss_ms, "compulsory_bytes": stage_b,
+                     "frac": stage_b / (fss_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    roof["algorithmic_bytes_per_launch"] = kbytes
+    roof["algorithmic_model_frac"] = kbytes / (fss_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    roof["algorithmic_note"] = ("SURVEY §8(d) per-pair model (charges every pair its cluster operands as if "
+                                "streamed from HBM; the kernels serve them from LDS): transparency only")
+    roof["kernels"] = {k: {f: v[f] for f in ("kernel", "time_ms", "bound", "frac", "traffic")} |
+                       {"salu_frac": (v["issue"] or {}).get("salu_frac"), "valu_frac": (v["issue"] or {}).get("valu_frac"),
+                        "hbm_measured_frac": v["hbm"]["measured_frac"], "hbm_compulsory_frac": v["hbm"]["compulsory_frac"]}
+                       for k, v in kernels.items()}
+    return {
+        "metric": "scheduling decisions/sec (workload x cluster evals/s)",
+        "value": W_total * C / (ms * 1e-3),
+        "unit": "decisions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded SURVEY.md §8(d) generator; no cluster/dataset available)",
+        "config": {"workload": f"{cfg}: {WORKLOAD_DESC[cfg]}", "units_total": W_total, "units_per_gpu": W0r,
+                   "clusters": C, "parallelism": f"dp{world}", "rccl_world_size": world,
+                   "stage_ms": stage, "paths": paths},
+        "roofline": roof,
+        "allgather": None,
+        "end_to_end": None,
+        "cpu_baseline": None,
+    }
+
+
+def shard_sweep(args, cfg, local, t1_ms, ns=(2, 4, 8)):
+    """Step time of every rank's shard of the C3 batch for N = 2, 4, 8 ranks, each run alone on this GPU
+    (the shards bench.py --gpus N would hand out: shard.shard_range, the same per-shard generator), and the
+    strong-scaling efficiency they project, t(1 GPU) / (N * max_r t(shard r)), before any RCCL cost (the
+    timed step has no collective)."""
+    from kubeadmiral_amd import columns as CO
+    from kubeadmiral_amd import pack, shard, synth
+    from kubeadmiral_amd.runtime import Context
+
+    W_total, C = synth.SIZES[cfg]
+    fwk = synth.profile_for(cfg)
+    clusters = make_clusters(cfg, C)
+    snap = pack.Snapshot(clusters)
+    packer = CO.NativePacker(snap)
+    ctx = Context(local)
+    ctx.upload_snapshot(snap)
+    out = {"t1_ms": t1_ms, "steps": args.steps, "per_n": {}}
+    for n in ns:
+        ts = []
+        for r in range(n):
+            lo, hi = shard.shard_range(W_total, r, n)
+            ctx.upload_batch(packer.pack(fwk, make_columns(cfg, lo, hi, clusters)))
+            for _ in range(max(2, args.warmup)):
+                ctx.schedule(fwk)
+            ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                ctx.schedule(fwk)
+            ctx.sync()
+            ts.append((time.perf_counter() - t0) / max(1, args.steps) * 1e3)
+        tn = max(ts)
+        out["per_n"][str(n)] = {"units_per_rank": W_total // n, "shard_ms": ts, "max_ms": tn,
+                                "projected_decisions_per_s": W_total * C / (tn * 1e-3),
+                                "projected_efficiency": t1_ms / (n * tn)}
+        log(f"[sweep] N={n}: shard ms {['%.3f' % t for t in ts]} -> efficiency {t1_ms / (n * tn):.3f}")
     ctx.close()
     return out
 
@@ -373,7 +494,7 @@ def end_to_end(ctx, snap, fwk, cols, res, C, packer_for):
                     "host buffers; not the headline value"}
 
 
-def gather_placements(ctx, batch, res, dist, world, dev):
+def gather_placements(ctx, batch, res, dist, world, dev, blobs=None, fwk=None):
     """All-gather of every rank's placements: status / count / flags [W_r] and (cluster, replicas) slots,
     each rank's arrays padded to the largest rank's sizes (fixed per-rank slots). RCCL on device buffers
     filled device-to-device from libkad (kad_results_copy_device); host tensors in the gloo rehearsal."""
@@ -417,9 +538,24 @@ def gather_placements(ctx, batch, res, dist, world, dev):
     r = dist.get_rank()
     assert np.array_equal(g_st[r][:W].cpu().numpy(), res.status[:W]), "all-gathered placements differ"
     assert np.array_equal(g_cl[r][:S].cpu().numpy(), res.cluster[:S]), "all-gathered placements differ"
+    verified = None
+    if r == 0 and blobs is not None:
+        # every rank's gathered part equals a single-rank run of the same shard blob on rank 0
+        for q in range(world):
+            ctx.upload_batch(blobs[q])
+            ctx.schedule(fwk)
+            one = ctx.download()
+            Wq, Sq = blobs[q].W, blobs[q].n_out_slots
+            gs, gc, gr = g_st[q].cpu().numpy(), g_cl[q].cpu().numpy(), g_rp[q].cpu().numpy()
+            for what, got, want in (("status", gs[:Wq], one.status[:Wq]), ("count", gs[Wm:Wm + Wq], one.count[:Wq]),
+                                    ("flags", gs[2 * Wm:2 * Wm + Wq], one.flags[:Wq].view(np.int32)),
+                                    ("cluster", gc[:Sq], one.cluster[:Sq]), ("replicas", gr[:Sq], one.replicas[:Sq])):
+                assert np.array_equal(got, want), f"gathered {what} of rank {q} differs from a single-rank run"
+        verified = f"all {world} ranks' status/count/flags/cluster/replicas == single-rank runs of their shards"
     nbytes = world * (12 * Wm + 12 * Sm)
     return {"ms": float(t[0]) * 1e3, "bytes_gathered": nbytes, "per_rank_slots": Sm, "per_rank_units": Wm,
-            "gbs": nbytes / (float(t[0]) + 1e-12) / 1e9, "backend": "rccl" if dev != "cpu" else "gloo"}
+            "gbs": nbytes / (float(t[0]) + 1e-12) / 1e9, "backend": "rccl" if dev != "cpu" else "gloo",
+            "verified": verified}
 
 
 # ------------------------------------------------------------------------ trigger bench (§8 f4)
@@ -515,7 +651,9 @@ def main():
     ap.add_argument("--units", type=int, default=None, help="total units (default: the config's W)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the embedded C2 line of the default run")
+    ap.add_argument("--no-extra", action="store_true", help="skip the embedded C2/C4/C5 lines of the default run")
+    ap.add_argument("--extras", default="c2,c4,c5", help="configs embedded under `extra` in the default C3 run")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the C3 shard-size sweep of the default run")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse the multi-rank path with host-tensor transfers (e.g. ranks sharing one GPU)")
     ap.add_argument("--share-gpu", action="store_true", help="every rank uses device 0 (rehearsal on a 1-GPU box)")
@@ -552,16 +690,17 @@ def main():
         out = bench_trigger(args, cfg, rank, world, local, dist)
     else:
         out = bench_schedule(args, cfg, rank, world, local, dist)
-        # the default run also measures C2 (100k x 256, one GPU) and embeds it
-        if (cfg == "c3" and world == 1 and args.units is None and not args.no_extra):
-            a2 = argparse.Namespace(**vars(args))
-            a2.no_cpu_baseline = True
-            o2 = bench_schedule(a2, "c2", rank, world, local, dist, W_total=None)
-            if out is not None and o2 is not None:
-                out["extra"] = {"c2": {k: o2[k] for k in ("value", "ms_per_step")} |
-                                {"config": o2["config"], "roofline_frac": o2["roofline"]["frac"],
-                                 "roofline_time_ms": o2["roofline"]["time_ms"],
-                                 "end_to_end": o2["end_to_end"]}}
+        default_run = cfg == "c3" and world == 1 and args.units is None
+        # the default run also measures every other single-GPU config (C2 100k x 256, C4 1M x 512 Divide,
+        # C5 100k x 10k) on the same box and embeds their full lines, sampled CPU baselines included
+        if default_run and not args.no_extra:
+            out["extra"] = {}
+            for c2 in [c for c in args.extras.split(",") if c]:
+                out["extra"][c2] = bench_schedule(args, c2, rank, world, local, dist, W_total=None,
+                                                  cpu_seconds=args.cpu_seconds / 2)
+        # and C3's shard sizes for N = 2, 4, 8 (the 1-GPU projection of strong scaling)
+        if default_run and not args.no_sweep:
+            out["shard_sweep"] = shard_sweep(args, cfg, local, out["ms_per_step"])
     if rank == 0 and out is not None:
         print(json.dumps(out), flush=True)
     if dist is not None:

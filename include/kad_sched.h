@@ -333,10 +333,15 @@ int kad_last_timing(kad_ctx* ctx, float ms[3]);
  * stream carries only the kernels (no marker packets between passes) and
  * kad_last_timing returns KAD_ESTATE.  No reference counterpart (instrumentation). */
 int kad_set_timing(kad_ctx* ctx, int on);
-/* Per-stage device times of the last kad_schedule run with timing on (n <= 6 entries):
+/* Per-stage device times of the last kad_schedule run with timing on (n <= 7 entries):
  * ms[0] req_mask_kernel, [1] prep_kernel, [2] the main schedule kernel (lean / wide / full),
- * [3] the defer pass, [4] the replica planner, [5] the whole pipeline. No reference counterpart. */
+ * [3] the defer pass (schedule_kernel), [4] the replica planner, [5] the whole pipeline,
+ * [6] the long-feasible-list pass (schedule_row_kernel). No reference counterpart. */
 int kad_stage_timing(kad_ctx* ctx, float* ms, int n);
+/* Which kernel took how many units in the last kad_schedule (blocks until it is done): out[0] units,
+ * [1] the full kernel (defer list), [2] the long-feasible-list kernel, [3] planner rows (Divide units).
+ * Measurement only (bench.py's per-kernel byte models). No reference counterpart. */
+int kad_path_counts(kad_ctx* ctx, int32_t* out);
 int kad_results_download(kad_ctx* ctx, const kad_result_view* out);
 /* The same results copied device-to-device into caller DEVICE buffers of the result view's sizes
  * (e.g. the send buffers of an RCCL all-gather of placements across GPUs); blocking. */
@@ -397,6 +402,13 @@ int kad_trigger_hashes(kad_ctx* ctx, int n, const int64_t* prefix_off, const uin
  * counters of the kernels to out (and zero them if reset). Returns 32, or
  * 0 in product builds (no counters compiled in). Not part of the reference. */
 int kad_debug_phase_counters(uint64_t* out, int reset);
+
+/* Tests only: fault injection. where = 1: the next rebuild of the snapshot's
+ * derived state (kad_snapshot_upload / _upload_device / _update) fails with
+ * KAD_ENOMEM, as an allocation failure would. A failed snapshot upload or
+ * update leaves no snapshot and no batch resident (kad_schedule then returns
+ * KAD_ESTATE). where = 0 clears a pending fault. Not part of the reference. */
+int kad_debug_inject_fault(kad_ctx* ctx, int where);
 
 #ifdef __cplusplus
 }

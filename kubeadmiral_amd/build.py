@@ -27,6 +27,18 @@ def _inputs():
         os.path.join(os.path.dirname(HERE), "include", h) for h in ("kad_sched.h", "kad_pack.h")]
 
 
+def source_hash() -> str:
+    """16 hex digits of SHA-256 over libkad.so's sources and headers: profiles/pmc_<cfg>.json records the
+    hash of the code it was collected on, and bench.py uses its counters only when they match."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in _inputs():
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def up_to_date() -> bool:
     if not os.path.exists(LIB):
         return False

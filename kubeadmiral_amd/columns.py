@@ -346,6 +346,34 @@ def _from_blob(blob: np.ndarray, fwk: Framework) -> "NativeBatch":
 NativeBatch.from_blob = staticmethod(_from_blob)
 
 
+def vocab_of(snap, keep: list) -> KadPackVocab:
+    """kad_pack_vocab of a pack.Snapshot (the arrays it points into are appended to ``keep``)."""
+    gvks = sorted(snap.gvk_id, key=snap.gvk_id.get)
+    keys = sorted(snap.label_key_id, key=snap.label_key_id.get)
+    vals, voff = [], [0]
+    for k in keys:
+        d = snap.label_vals[snap.label_key_id[k]]
+        vals += sorted(d, key=d.get)
+        voff.append(len(vals))
+    voff_a = np.asarray(voff, I32)
+    keep.append(voff_a)
+    v = KadPackVocab()
+    v.cluster_names = _strs(snap.names, keep)
+    v.scalar_names = _strs(sorted(snap.scalar_id, key=snap.scalar_id.get), keep)
+    v.gvk_group = _strs([g[0] for g in gvks], keep)
+    v.gvk_version = _strs([g[1] for g in gvks], keep)
+    v.gvk_kind = _strs([g[2] for g in gvks], keep)
+    v.label_keys = _strs(keys, keep)
+    v.label_val_off = voff_a.ctypes.data
+    v.label_vals = _strs(vals, keep)
+    v.taint_key = _strs([t.key for t in snap.taint_defs], keep)
+    v.taint_value = _strs([t.value for t in snap.taint_defs], keep)
+    v.taint_effect = _strs([t.effect for t in snap.taint_defs], keep)
+    v.n_taint_words = snap.TW
+    v.fingerprint = snap.fingerprint
+    return v
+
+
 class NativePacker:
     """kad_packer for one pack.Snapshot's vocabulary."""
 
@@ -361,34 +389,12 @@ class NativePacker:
         L.kad_pack_batch.argtypes = [P, P, P, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), P]
         L.kad_packer_take.argtypes = [P, P, ctypes.c_size_t]
         self.snap = snap
-        keep: list = []
-        gvks = sorted(snap.gvk_id, key=snap.gvk_id.get)
-        keys = sorted(snap.label_key_id, key=snap.label_key_id.get)
-        vals, voff = [], [0]
-        for k in keys:
-            d = snap.label_vals[snap.label_key_id[k]]
-            vals += sorted(d, key=d.get)
-            voff.append(len(vals))
-        voff_a = np.asarray(voff, I32)
-        keep.append(voff_a)
-        v = KadPackVocab()
-        v.cluster_names = _strs(snap.names, keep)
-        v.scalar_names = _strs(sorted(snap.scalar_id, key=snap.scalar_id.get), keep)
-        v.gvk_group = _strs([g[0] for g in gvks], keep)
-        v.gvk_version = _strs([g[1] for g in gvks], keep)
-        v.gvk_kind = _strs([g[2] for g in gvks], keep)
-        v.label_keys = _strs(keys, keep)
-        v.label_val_off = voff_a.ctypes.data
-        v.label_vals = _strs(vals, keep)
-        v.taint_key = _strs([t.key for t in snap.taint_defs], keep)
-        v.taint_value = _strs([t.value for t in snap.taint_defs], keep)
-        v.taint_effect = _strs([t.effect for t in snap.taint_defs], keep)
-        v.n_taint_words = snap.TW
-        v.fingerprint = snap.fingerprint
+        self._keep: list = []
+        v = vocab_of(snap, self._keep)
         h = ctypes.c_void_p()
         rc = L.kad_packer_create(ctypes.byref(v), ctypes.byref(h))
         if rc != 0:
-            raise RuntimeError(f"kad_packer_create failed ({rc})")
+            raise RuntimeError(f"kad_packer_create failed ({rc}): {L.kad_packer_error(None).decode()}")
         self.h = h
 
     def close(self):

@@ -64,6 +64,7 @@ struct kad_ctx {
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   bool have_snapshot = false, have_batch = false, ran = false;
+  int inject_fault = 0;  // kad_debug_inject_fault: 1 = the next refresh_derived fails (tests)
   // HIP event records around the stages (kad_set_timing); timed = the last
   // kad_schedule recorded them
   bool timing = false, timed = false;
@@ -508,8 +509,9 @@ static int build_fit_table(kad_ctx* c) {
   return 0;
 }
 
-// state derived from the resident snapshot: clean / negative ranges (host shadows) and, with one taint
-// word, the per-id cluster slices prep_kernel folds the taint and API filters from (SnapDev::fold)
+// state derived from the resident snapshot: clean / negative ranges (host shadows) and, with up to
+// TFOLD_MAX_TW taint words, the per-id cluster slices + taint table prep_kernel folds the taint and API
+// filters from (SnapDev::fold)
 // SnapDev::vrows: per label key, clusters holding value id s < VR_SLOTS, and clusters with the key
 static int build_value_rows(kad_ctx* c) {
   const int C = c->sd.C, K = c->sd.K;
@@ -524,6 +526,10 @@ static int build_value_rows(kad_ctx* c) {
 }
 
 static int refresh_derived(kad_ctx* c) {
+  if (c->inject_fault == 1) {
+    c->inject_fault = 0;
+    return fail(c, KAD_ENOMEM, "injected refresh_derived failure (kad_debug_inject_fault)");
+  }
   if (int r = build_value_rows(c)) return r;
   c->snap_negative = res_negative(c->h_res);
   c->sd.clean = res_clean(c->h_res);
@@ -535,15 +541,25 @@ static int refresh_derived(kad_ctx* c) {
       for (int x = 0; x < C; x++) present |= c->h_ns[(size_t)t * C + x];
     c->sd.present_taints[t] = present;
   }
-  if (!c->sd.fold) return build_fit_table(c);
   const size_t nch = (size_t)((C + 63) / 64);
   const size_t nc1 = nch ? nch : 1;
   const size_t n_slices = ((size_t)128 * TW + 64) * nc1, n_tab = (size_t)2 * 8 * TW * 256 * nc1;
+  // the table is rebuilt whole on every upload / update: above TTAB_MAX_BYTES (C beyond ~32k clusters at
+  // 4 taint words) the kernels test taints per cluster instead (unfolded path)
+  if (c->sd.fold && (n_slices + n_tab) * 8 > TTAB_MAX_BYTES) c->sd.fold = 0;
+  if (!c->sd.fold) return build_fit_table(c);
   if (int r = grow(c, &c->d_slices, &c->slices_cap, (n_slices + n_tab) * 8)) return r;
   c->sd.slices = static_cast<const uint64_t*>(c->d_slices);
   c->sd.taint_tab = c->sd.slices + n_slices;
   HIPCHK(c, launch_slices(c->sd, static_cast<uint64_t*>(c->d_slices), c->stream));
   return build_fit_table(c);
+}
+
+// nothing resident may be scheduled: the snapshot (and so any batch validated against it) is being replaced
+static void invalidate_snapshot(kad_ctx* c) {
+  c->have_snapshot = false;
+  c->have_batch = false;
+  c->ran = false;
 }
 
 int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
@@ -552,6 +568,9 @@ int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   kad_snapshot_header h;
   std::memcpy(&h, blob, sizeof(h) < nbytes ? sizeof(h) : nbytes);
   if (int r = check_snapshot_header(c, h, nbytes)) return r;
+  // the resident snapshot, its derived state and any batch validated against it are about to be
+  // overwritten: nothing may run on them until every step below has succeeded
+  invalidate_snapshot(c);
   HIPCHK(c, hipSetDevice(c->device));
   if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_snap, blob, nbytes, hipMemcpyHostToDevice, c->stream));
@@ -567,7 +586,6 @@ int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
                 at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + (size_t)h.n_taint_words * h.n_clusters);
   if (int r = refresh_derived(c)) return r;
   c->have_snapshot = true;
-  c->have_batch = false;
   return KAD_OK;
 }
 
@@ -578,6 +596,7 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemcpy(&h, dev_blob, sizeof(h), hipMemcpyDeviceToHost));
   if (int r = check_snapshot_header(c, h, nbytes)) return r;
+  invalidate_snapshot(c);
   if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_snap, dev_blob, nbytes, hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -594,7 +613,6 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
   }
   if (int r = refresh_derived(c)) return r;
   c->have_snapshot = true;
-  c->have_batch = false;
   return KAD_OK;
 }
 
@@ -642,8 +660,14 @@ int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
   d.snap = static_cast<uint8_t*>(c->d_snap);
   d.delta = static_cast<const uint8_t*>(c->d_delta);
   d.idx = reinterpret_cast<const int32_t*>(d.delta + h.idx_off);
-  HIPCHK(c, launch_snapshot_delta(d, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's delta buffer is free on return
+  {
+    hipError_t e = launch_snapshot_delta(d, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the caller's delta buffer is free on return
+    if (e != hipSuccess) {
+      invalidate_snapshot(c);  // the scatter may have run partway
+      return fail(c, KAD_EHIP, std::string("snapshot delta scatter: ") + hipGetErrorString(e));
+    }
+  }
   {
     for (int q = 0; q < 4; q++) {
       const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
@@ -653,7 +677,10 @@ int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
     for (int t = 0; t < sh.n_taint_words; t++)
       for (int j = 0; j < n; j++) c->h_ns[(size_t)t * C + idx[j]] = ns[(size_t)t * n + j];
   }
-  if (int r = refresh_derived(c)) return r;
+  if (int r = refresh_derived(c)) {
+    invalidate_snapshot(c);  // the scattered snapshot no longer matches its derived rows / tables
+    return r;
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KAD_OK;
 }
@@ -745,9 +772,9 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   // Label requirements whose value ids are all < VR_SLOTS (at most VR_MAX_VALS of them; Exists / DoesNotExist)
   // read the snapshot's value rows (req_row_kernel: a word is the OR of <= 5 row words); so do the label-free
   // ops (TRUE / FALSE / metadata.name =, !=), whose words are constants or one bit. The rest is grouped
-  // by label key (req_mask_kernel: one label-row load per segment and chunk): a counting sort by key (the
-  // label-free ops last, as key -1), cut into segments of <= seg_len ids; shorter segments when the batch
-  // has few requirements, so the grid still fills the chip.
+  // by label key (req_mask_kernel: one label-row load per segment and chunk): a counting sort by key, cut
+  // into segments of <= seg_len ids; shorter segments when the batch has few requirements, so the grid
+  // still fills the chip.
   int n_seg = 0, n_rowreq = 0;
   {
     const int NR = h.n_reqs, K = c->snap_hdr.n_label_keys;
@@ -767,10 +794,8 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
         if (q[2 + t] < 0 || q[2 + t] >= VR_SLOTS) return false;
       return true;
     };
-    auto group = [&](int r) {
-      const int op = rq[ro[r]] & 0xff;
-      return (op == KAD_OP_TRUE || op == KAD_OP_FALSE || op == KAD_OP_NAME_EQ || op == KAD_OP_NAME_NE) ? K : rq[ro[r] + 1];
-    };
+    // the segment path sees label requirements only (by_rows takes every label-free op): group = label key
+    auto group = [&](int r) { return rq[ro[r] + 1]; };
     std::vector<uint8_t> rowr((size_t)NR);
     std::vector<int32_t> start((size_t)K + 2, 0);
     for (int r = 0; r < NR; r++) {
@@ -816,7 +841,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
     int32_t* sg = c->h_reqseg.data() + perm_len;
     for (int g = 0; g <= K; g++)
       for (int f = start[g]; f < start[(size_t)g + 1]; f += seg_len) {
-        sg[4 * n_seg] = g == K ? -1 : g;
+        sg[4 * n_seg] = g;
         sg[4 * n_seg + 1] = f;
         sg[4 * n_seg + 2] = start[(size_t)g + 1] - f < seg_len ? start[(size_t)g + 1] - f : seg_len;
         n_seg++;
@@ -944,7 +969,7 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   if (tm) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total || wide_path(c->sd);
   // long feasible lists go to schedule_row_kernel when every filter is in the static words
-  static const bool no_rows = getenv("KAD_NO_ROWS") && atoi(getenv("KAD_NO_ROWS"));
+  static const bool no_rows = tuning_env("KAD_NO_ROWS", 0) != 0;
   c->bd.use_rows = !no_rows && c->sd.clean && c->sd.fold && c->sd.fitfold && row_kernel_fits(c->sd.C);
   if (c->bd.use_rows) {
     if (int r = grow(c, &c->d_rowslab, &c->rowslab_cap, (size_t)ROW_MAX_BLOCKS * row_slab_bytes(c->sd.C))) return r;
@@ -954,7 +979,9 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[5], c->stream));  // re-recorded after the main kernel when it runs
-  HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream, tm ? c->ev[5] : nullptr));
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));  // re-recorded after the long-row kernel
+  HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream, tm ? c->ev[5] : nullptr,
+                            tm ? c->ev[6] : nullptr));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())
     HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, c->d_plan_rows, (int)c->plan_rows.size(), c->batch_hdr.max_row_slots,
@@ -1021,8 +1048,9 @@ int kad_stage_timing(kad_ctx* c, float* ms, int n) {
   if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
   if (!c->timed) return fail(c, KAD_ESTATE, "the last kad_schedule ran with timing off");
   HIPCHK(c, hipEventSynchronize(c->ev[2]));
-  const int pairs[6][2] = {{0, 3}, {3, 4}, {4, 5}, {5, 1}, {1, 2}, {0, 2}};
-  for (int i = 0; i < n && i < 6; i++) HIPCHK(c, hipEventElapsedTime(&ms[i], c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
+  // req_mask, prep, main, defer (schedule_kernel over the defer list), planner, total, rows (schedule_row_kernel)
+  const int pairs[7][2] = {{0, 3}, {3, 4}, {4, 5}, {6, 1}, {1, 2}, {0, 2}, {5, 6}};
+  for (int i = 0; i < n && i < 7; i++) HIPCHK(c, hipEventElapsedTime(&ms[i], c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
   return KAD_OK;
 }
 
@@ -1065,6 +1093,28 @@ int kad_schedule_batch(kad_ctx* c, const kad_profile* p, const void* blob, size_
 }
 
 int kad_debug_phase_counters(uint64_t* out, int reset) { return kad::debug_phase_counters(out, reset); }
+
+int kad_path_counts(kad_ctx* c, int32_t* out) {
+  if (!c || !out) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
+  int32_t h[4] = {0, 0, 0, 0};
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(h, c->d_defer, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  out[0] = c->batch_hdr.n_units;
+  out[1] = h[0];  // defer_n: units the full kernel (schedule_kernel) took
+  out[2] = c->bd.use_rows ? h[2] : 0;  // rows_n: units schedule_row_kernel took
+  out[3] = (int32_t)c->plan_rows.size();  // Divide units handed to the planner
+  return KAD_OK;
+}
+
+int kad_debug_inject_fault(kad_ctx* c, int where) {
+  if (!c || where < 0 || where > 1) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->inject_fault = where;
+  return KAD_OK;
+}
 
 int kad_debug_scores(kad_ctx* c, const kad_profile* p, uint8_t* feasible, int64_t* total) {
   if (!c || !feasible || !total) return KAD_EINVAL;

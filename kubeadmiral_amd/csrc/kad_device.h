@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/kad_sched.h"
 
@@ -11,6 +12,10 @@ namespace kad {
 constexpr int FITFOLD_MAX_C = 16384;
 // taint words (64 ids each) prep_kernel folds into the static filter words (SnapDev::fold): up to 256 ids
 constexpr int TFOLD_MAX_TW = 4;
+// byte cap of the per-id slices + taint table (SnapDev::slices / taint_tab): 2*8*TW*256 words per 64-cluster
+// chunk, 41 MB at C5 (10k clusters, TW = 4), 268 MB at 65535 clusters; above the cap (C > ~32k at TW = 4,
+// ~128k-cluster-equivalents at TW = 1) the snapshot runs unfolded
+constexpr size_t TTAB_MAX_BYTES = (size_t)128 << 20;
 // unit work queue of the schedule kernels: WQ_HEADS counters, one 128-B line apart (BatchDev::wq)
 constexpr int WQ_HEADS = 64, WQ_STRIDE = 32;
 constexpr int FIT_FENCES = 256;
@@ -172,6 +177,20 @@ size_t plan_wave_bytes(int K);
 // phase counters of a -DKAD_PHASE_PROF build (returns 0 in product builds)
 int debug_phase_counters(uint64_t* out, int reset);
 
+// Tuning / measurement knobs read from the environment ONLY in profiling builds (-DKAD_PHASE_PROF,
+// scripts/phase_prof.py): the product library ignores the environment, so no variable set in a
+// controller process can switch it off the reference-exact path (KAD_WIDE_EXPERIMENT, for one,
+// skips the pdqsort replay). Product builds always return the default.
+inline int tuning_env(const char* name, int dflt) {
+#ifdef KAD_PHASE_PROF
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
+
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st);
 // per-id cluster bitmask slices of the snapshot (SnapDev::slices) and the taint table over them
 // (SnapDev::taint_tab), rebuilt at upload / update
@@ -183,9 +202,11 @@ bool fast_path(int C);
 // true if launch_schedule runs schedule_wide_kernel for this snapshot (clean, 5..16 chunks)
 bool wide_path(const SnapDev& s);
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st);
-// after_main (optional): recorded between the main schedule kernel and the defer pass (stage timing)
+// after_main / after_rows (optional): recorded after the main schedule kernel and after the long-row
+// kernel, before the defer pass (stage timing)
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p,
-                           void* global_scratch, size_t scratch_bytes, hipStream_t st, hipEvent_t after_main = nullptr);
+                           void* global_scratch, size_t scratch_bytes, hipStream_t st, hipEvent_t after_main = nullptr,
+                           hipEvent_t after_rows = nullptr);
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,
                        int n_rows, int kmax, void* global_scratch, size_t scratch_bytes, hipStream_t st);
 hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,

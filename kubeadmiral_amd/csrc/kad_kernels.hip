@@ -131,22 +131,8 @@ __global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, in
   const int rid = e0.x, off = e0.y, w0 = li ? e0.z : 0, kw = e0.w;
   const int pv[4] = {e1.x, e1.y, e1.z, e1.w};
   uint64_t* out = b.req_mask;
-  if (key < 0) {  // TRUE / FALSE / metadata.name =, != (key word = cluster id): no label rows
-    for (int i = 0; i < cnt; ++i) {
-      const int op = __builtin_amdgcn_readlane(w0, i) & 0xff, ck = __builtin_amdgcn_readlane(kw, i);
-      const int r = __builtin_amdgcn_readlane(rid, i);
-      uint64_t acc = 0;
-#pragma unroll
-      for (int j = 0; j < REQ_G; ++j) {
-        const int c = (g0 + j) * WAVE + lane;
-        const bool v = op == KAD_OP_TRUE || (op == KAD_OP_NAME_EQ && c == ck) || (op == KAD_OP_NAME_NE && c != ck);
-        const uint64_t m = ballot(v && c < C && j < ng);
-        acc = lane == j ? m : acc;
-      }
-      if (lane < ng) out[(size_t)r * nch + g0 + lane] = acc;
-    }
-    return;
-  }
+  // every segment holds requirements on one label key (key >= 0): the label-free ops (TRUE / FALSE /
+  // metadata.name =, !=) always take req_row_kernel (kad_batch_upload's routing)
   int32_t lv[REQ_G];
 #pragma unroll
   for (int j = 0; j < REQ_G; ++j) {
@@ -3471,7 +3457,7 @@ static int n_cus() {
 // (KAD_WIDE_MIN_NCH overrides the lower bound, for A/B runs of C <= 256)
 static bool use_wide(const SnapDev& s) {
   static int min_nch = -1;
-  if (min_nch < 0) min_nch = getenv("KAD_WIDE_MIN_NCH") ? atoi(getenv("KAD_WIDE_MIN_NCH")) : 5;
+  if (min_nch < 0) min_nch = tuning_env("KAD_WIDE_MIN_NCH", 5);
   const int nch = (s.C + 63) >> 6;
   return s.clean && nch >= min_nch && nch >= 1 && nch <= WIDE_MAX_NCH;
 }
@@ -3524,7 +3510,8 @@ static hipError_t launch_rows(const SnapDev& s, const BatchDev& b, const OutDev&
 }
 
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
-                           size_t scr_bytes, hipStream_t st, hipEvent_t after_main) {
+                           size_t scr_bytes, hipStream_t st, hipEvent_t after_main, hipEvent_t after_rows) {
+  auto rec = [&](hipEvent_t ev) { return ev ? hipEventRecord(ev, st) : hipSuccess; };
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (b.W == 0) return hipSuccess;
   const size_t wb = row_layout(s.C).bytes;
@@ -3548,13 +3535,13 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     long grid = n_cus();
     const long need = ((long)b.W + wpb - 1) / wpb;
     if (grid > need) grid = need;
-    static const int exp = getenv("KAD_WIDE_EXPERIMENT") ? atoi(getenv("KAD_WIDE_EXPERIMENT")) : 0;
+    static const int exp = tuning_env("KAD_WIDE_EXPERIMENT", 0);
     const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, exp};
     hipLaunchKernelGGL(schedule_wide_kernel<WIDE_MAX_NCH>, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
     if (hipError_t e = hipGetLastError()) return e;
-    if (after_main)
-      if (hipError_t e = hipEventRecord(after_main, st)) return e;
+    if (hipError_t e = rec(after_main)) return e;
     if (hipError_t e = launch_rows(s, b, o, p, st)) return e;
+    if (hipError_t e = rec(after_rows)) return e;
     // feasible lists longer than WIDE_P positions can come from any unit: the defer pass always runs
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);
   }
@@ -3583,7 +3570,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     }
 #undef KAD_OCC
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
-    if (getenv("KAD_LEAN_BLOCKS_PER_CU")) per_cu = atoi(getenv("KAD_LEAN_BLOCKS_PER_CU"));
+    per_cu = tuning_env("KAD_LEAN_BLOCKS_PER_CU", per_cu);
     long grid = (long)n_cu * per_cu;
     const long need = ((long)b.W + wpb - 1) / wpb;  // at least one unit per wave
     if (grid > need) grid = need;
@@ -3601,13 +3588,13 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
       default: launch_lean<0, false>(A, (int)grid, lds, st); break;
     }
     if (hipError_t e = hipGetLastError()) return e;
-    if (after_main)
-      if (hipError_t e = hipEventRecord(after_main, st)) return e;
+    if (hipError_t e = rec(after_main)) return e;
     // nothing can be deferred (host-checked: every unit and cluster is in the
     // lean kernel's range and every feasible list fits its registers)
-    if (nch <= 4 && !b.may_defer) return hipSuccess;
+    if (nch <= 4 && !b.may_defer) return rec(after_rows);
     if (nch > 4)
       if (hipError_t e = launch_rows(s, b, o, p, st)) return e;
+    if (hipError_t e = rec(after_rows)) return e;
     // the defer list: its length is only known on the device, so the grid
     // strides over it (waves past its end exit at once)
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);

@@ -297,8 +297,53 @@ static int validate_columns(kad_packer* P, const kad_su_columns* su, int threads
 
 extern "C" {
 
+// kad_packer_create's message for kad_packer_error(NULL) (no packer exists to carry it)
+static thread_local std::string g_create_err;
+
+// one vocabulary string array: n >= 0, offsets from 0, non-decreasing, bytes present when non-empty
+static bool strs_ok(const kad_strs& s) {
+  if (s.n < 0) return false;
+  if (s.n == 0) return true;
+  if (!s.off || s.off[0] != 0) return false;
+  for (int i = 0; i < s.n; i++)
+    if (s.off[i + 1] < s.off[i]) return false;
+  return s.off[s.n] == 0 || s.bytes;
+}
+
+// the vocabulary a caller hands over (cgo / ctypes) is checked as carefully as the unit columns:
+// every array well formed, the GVK and taint triples of equal length, label value ranges in bounds
+static const char* check_vocab(const kad_pack_vocab* v) {
+  const kad_strs* all[] = {&v->cluster_names, &v->scalar_names, &v->gvk_group, &v->gvk_version, &v->gvk_kind,
+                           &v->label_keys, &v->label_vals, &v->taint_key, &v->taint_value, &v->taint_effect};
+  for (const kad_strs* s : all)
+    if (!strs_ok(*s)) return "a vocabulary string array has bad offsets (n < 0, not from 0, decreasing, or no bytes)";
+  if (v->gvk_version.n != v->gvk_group.n || v->gvk_kind.n != v->gvk_group.n)
+    return "gvk_group, gvk_version and gvk_kind must have the same length";
+  if (v->taint_value.n != v->taint_key.n || v->taint_effect.n != v->taint_key.n)
+    return "taint_key, taint_value and taint_effect must have the same length";
+  const int K = v->label_keys.n;
+  if (K > 0 || v->label_val_off) {
+    if (!v->label_val_off) return "label_val_off is null";
+    if (v->label_val_off[0] != 0) return "label_val_off[0] must be 0";
+    for (int k = 0; k < K; k++)
+      if (v->label_val_off[k + 1] < v->label_val_off[k]) return "label_val_off must be non-decreasing";
+    if (v->label_val_off[K] > v->label_vals.n) return "label_val_off[n_keys] exceeds label_vals.n";
+  }
+  if (v->n_taint_words < 1 || (int64_t)v->n_taint_words * 64 < v->taint_key.n)
+    return "n_taint_words must be >= 1 and cover every taint id";
+  return nullptr;
+}
+
 int kad_packer_create(const kad_pack_vocab* v, kad_packer** out) {
-  if (!v || !out) return KAD_EINVAL;
+  if (!v || !out) {
+    g_create_err = "null vocabulary or output pointer";
+    return KAD_EINVAL;
+  }
+  if (const char* e = check_vocab(v)) {
+    g_create_err = e;
+    return KAD_EINVAL;
+  }
+  g_create_err.clear();
   auto* p = new kad_packer();
   const Strs names = strs(v->cluster_names), sc = strs(v->scalar_names), gg = strs(v->gvk_group),
              gv = strs(v->gvk_version), gk = strs(v->gvk_kind), lk = strs(v->label_keys), lv = strs(v->label_vals),
@@ -324,10 +369,6 @@ int kad_packer_create(const kad_pack_vocab* v, kad_packer** out) {
     p->taint_value.emplace_back(tv[i]);
     p->taint_effect.emplace_back(te[i]);
   }
-  if (p->TW < 1 || (int64_t)p->TW * 64 < tk.n) {
-    delete p;
-    return KAD_EINVAL;
-  }
   *out = p;
   return KAD_OK;
 }
@@ -337,7 +378,7 @@ int kad_packer_destroy(kad_packer* p) {
   return KAD_OK;
 }
 
-const char* kad_packer_error(kad_packer* p) { return p ? p->err.c_str() : "null packer"; }
+const char* kad_packer_error(kad_packer* p) { return p ? p->err.c_str() : g_create_err.c_str(); }
 
 int kad_packer_take(kad_packer* p, void* dst, size_t cap) {
   if (!p || (!dst && p->out_n)) return KAD_EINVAL;

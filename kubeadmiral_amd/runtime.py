@@ -79,10 +79,12 @@ def load_library(path: str = LIB_PATH):
     L.kad_results_download.argtypes = [P, P]
     L.kad_results_copy_device.argtypes = [P, P]
     L.kad_stage_timing.argtypes = [P, P, I]
+    L.kad_path_counts.argtypes = [P, P]
     L.kad_schedule_batch.argtypes = [P, P, P, SZ, P]
     L.kad_select_rows.argtypes = [P, I, P, P, P, U32, P, P, P]
     L.kad_plan_rows.argtypes = [P, I, P, P, P, P, P, P, P, P, P, P, P, P]
     L.kad_debug_scores.argtypes = [P, P, P, P]
+    L.kad_debug_inject_fault.argtypes = [P, I]
     L.kad_trigger_suffix_upload.argtypes = [P, P, SZ]
     L.kad_trigger_prefixes_upload.argtypes = [P, I, P, P]
     L.kad_trigger_run.argtypes = [P]
@@ -139,6 +141,11 @@ class Context:
         self._chk(self.L.kad_snapshot_upload_device(self.h, ctypes.c_void_p(dev_ptr), nbytes))
         self.snap = snap
 
+    def inject_fault(self, where: int):
+        """kad_debug_inject_fault (tests): 1 = the next snapshot upload / update fails in its derived-state
+        rebuild."""
+        self._chk(self.L.kad_debug_inject_fault(self.h, where))
+
     def update_snapshot(self, delta: SnapshotDelta):
         """kad_snapshot_update: patch the resident snapshot; the resident batch stays valid."""
         self._chk(self.L.kad_snapshot_update(self.h, _p(delta.blob), delta.blob.nbytes))
@@ -163,13 +170,20 @@ class Context:
         self._chk(self.L.kad_last_timing(self.h, ms))
         return float(ms[0]), float(ms[1]), float(ms[2])
 
-    STAGES = ("req_mask", "prep", "main", "defer", "planner", "total")
+    STAGES = ("req_mask", "prep", "main", "defer", "planner", "total", "rows")
 
     def stage_timing(self) -> dict:
-        """kad_stage_timing: device ms per stage of the last timed schedule()."""
-        ms = (ctypes.c_float * 6)()
-        self._chk(self.L.kad_stage_timing(self.h, ms, 6))
+        """kad_stage_timing: device ms per stage of the last timed schedule() (rows = schedule_row_kernel,
+        defer = schedule_kernel over the defer list)."""
+        ms = (ctypes.c_float * 7)()
+        self._chk(self.L.kad_stage_timing(self.h, ms, 7))
         return {k: float(v) for k, v in zip(self.STAGES, ms)}
+
+    def path_counts(self) -> dict:
+        """kad_path_counts: units per kernel path of the last schedule()."""
+        out = (ctypes.c_int32 * 4)()
+        self._chk(self.L.kad_path_counts(self.h, out))
+        return {"units": out[0], "full_kernel": out[1], "row_kernel": out[2], "planner_rows": out[3]}
 
     def copy_results_device(self, status_ptr: int, count_ptr: int, flags_ptr: int, cluster_ptr: int,
                             replicas_ptr: int):

@@ -523,3 +523,246 @@ def gen_units_c2_columns(rng: np.random.Generator, W: int, n_keys=8, n_vals=8, n
         if kname not in cols:
             cols[kname] = np.zeros(0, dt)
     return CO.SUColumns(W, str_off, str_data, cols)
+
+
+def _tol_columns(rng, st, W: int, n_taints: int, lo: int, hi: int, allow_wild: bool = False):
+    """Columns of :func:`_tolerations` (same distribution, vectorised): lo..hi tolerations per unit; 5 %
+    wildcard (empty key, Exists) with ``allow_wild``; else half Equal (key/value of a pool taint, its effect
+    70 %), half Exists (a pool key, a random effect 70 %)."""
+    from . import columns as CO
+
+    sid = st.id
+    nt = max(1, n_taints)
+    nt3 = max(1, n_taints // 3)
+    tkey = np.array([sid(f"taint-{i % nt3}") for i in range(nt)], np.int32)
+    tval = np.array([sid(f"v{i}") for i in range(nt)], np.int32)
+    eff = np.array([sid(e) for e in EFFECTS], np.int32)
+    empty, equal_id, exists_id = sid(""), sid(T.TOLERATION_OP_EQUAL), sid(T.TOLERATION_OP_EXISTS)
+    n = rng.integers(lo, hi + 1, W).astype(np.int32)
+    TT = int(n.sum())
+    i = rng.integers(0, nt, TT)
+    r = rng.random(TT)
+    with_eff = rng.random(TT) < 0.7
+    wild = (r < 0.05) if allow_wild else np.zeros(TT, bool)
+    eq = ~wild & (r < 0.5)
+    e = np.where(eq, eff[i % 3], eff[rng.integers(0, 3, TT)])
+    return {"tol_off": CO._csr_off(n),
+            "tol_key": np.where(wild, empty, tkey[i]).astype(np.int32),
+            "tol_op": np.where(eq, equal_id, exists_id).astype(np.int32),
+            "tol_value": np.where(eq, tval[i], empty).astype(np.int32),
+            "tol_effect": np.where(wild | ~with_eff, empty, e).astype(np.int32)}
+
+
+def _fill_columns(W: int, st, cols):
+    from . import columns as CO
+
+    zero_off = np.zeros(W + 1, np.int32)
+    for grp in CO.CSR_GROUPS:
+        cols.setdefault(grp + "_off", zero_off)
+    cols.setdefault("rq_val_off", np.zeros(1, np.int32))  # no requirements: one offset
+    for kname, dt in CO.FIELDS:
+        if kname not in cols:
+            cols[kname] = np.zeros(W if kname in ("desired", "max_clusters", "req_cpu", "req_mem", "req_eph")
+                                   else 0, dt)
+    str_off, str_data = st.arrays()
+    return CO.SUColumns(W, str_off, str_data, cols)
+
+
+def _names(st, W: int, prefix: str) -> np.ndarray:
+    name0 = len(st._parts)
+    for w in range(W):
+        st._parts.append(f"{prefix}-{w}".encode())
+    return np.arange(name0, name0 + W, dtype=np.int32)
+
+
+def gen_units_c4_columns(rng: np.random.Generator, W: int, cluster_names, prefix="c4"):
+    """The C4 replica-planner stress workload of :func:`gen_units_c4` (same distributions, its own random
+    stream) as ``columns.SUColumns``: Divide units with ClusterNames of 8-64 distinct clusters (a random
+    start and odd stride over the snapshot, distinct for C a power of two — else rejected and redrawn),
+    static weights U{0..100} on half the units, MinReplicas U{0..5} / MaxReplicas U{0..199} on 30 % and
+    EstimatedCapacity U{0..499} on 20 % of the entries (AutoMigration when any, KeepUnschedulable 50 %),
+    CurrentClusters on 25 % of the units (half the entries, 10 % nil replicas), DesiredReplicas
+    U{1..10 000}, AvoidDisruption 50 %, 0-3 tolerations."""
+    from . import columns as CO
+
+    C = len(cluster_names)
+    st = CO.StringTable()
+    sid = st.id
+    cid = np.array([sid(n) for n in cluster_names], np.int32)
+    g, v, k = sid("apps"), sid("v1"), sid("Deployment")
+    nss = np.array([sid(f"ns{i}") for i in range(7)], np.int32)
+    cols = {"group": np.full(W, g, np.int32), "version": np.full(W, v, np.int32), "kind": np.full(W, k, np.int32),
+            "namespace_": nss[np.arange(W) % 7], "name": _names(st, W, prefix)}
+    kk = np.minimum(rng.integers(8, 65, W), C).astype(np.int32)
+    P = int(kk.sum())
+    place_off = CO._csr_off(kk)
+    unit_of = np.repeat(np.arange(W), kk)
+    j = np.arange(P) - place_off[:-1][unit_of]
+    start = rng.integers(0, C, W)
+    if C & (C - 1) == 0:
+        stride = (2 * rng.integers(0, max(1, C // 2), W) + 1) % C if C > 1 else np.zeros(W, np.int64)
+        pos = (start[unit_of] + stride[unit_of] * j) % max(C, 1)
+    else:  # consecutive clusters from a random start (distinct for k <= C)
+        pos = (start[unit_of] + j) % C
+    cols["place_off"] = place_off
+    cols["place_name"] = cid[pos]
+    has_w = rng.random(W) < 0.5
+    wl = np.where(has_w, kk, 0).astype(np.int32)
+    cols["wt_off"] = CO._csr_off(wl)
+    sel_w = has_w[unit_of]
+    cols["wt_name"] = cid[pos[sel_w]]
+    cols["wt_val"] = rng.integers(0, 101, int(sel_w.sum())).astype(np.int64)
+
+    def sub_map(p, lo, hi, grp):
+        m = rng.random(P) < p
+        cols[grp + "_off"] = CO._csr_off(np.bincount(unit_of[m], minlength=W).astype(np.int32))
+        cols[grp + "_name"] = cid[pos[m]]
+        cols[grp + "_val"] = rng.integers(lo, hi + 1, int(m.sum())).astype(np.int64)
+        return m
+
+    sub_map(0.3, 0, 5, "min")
+    sub_map(0.3, 0, 199, "max")
+    mc = sub_map(0.2, 0, 499, "cap")
+    has_am = np.bincount(unit_of[mc], minlength=W) > 0
+    has_cur = rng.random(W) < 0.25
+    mcur = has_cur[unit_of] & (rng.random(P) < 0.5)
+    cols["cur_off"] = CO._csr_off(np.bincount(unit_of[mcur], minlength=W).astype(np.int32))
+    cols["cur_name"] = cid[pos[mcur]]
+    ncur = int(mcur.sum())
+    hr = rng.random(ncur) < 0.9
+    cols["cur_rep"] = np.where(hr, rng.integers(0, 300, ncur), 0).astype(np.int64)
+    cols["cur_has_rep"] = hr.astype(np.uint8)
+    f = np.full(W, CO.SU_HAS_DESIRED, np.uint32)
+    f |= np.where(rng.random(W) < 0.5, CO.SU_AVOID_DISRUPTION, 0).astype(np.uint32)
+    f |= np.where(has_am, CO.SU_HAS_AUTO_MIGRATION, 0).astype(np.uint32)
+    f |= np.where(has_am & (rng.random(W) < 0.5), CO.SU_KEEP_UNSCHED, 0).astype(np.uint32)
+    cols["flags"] = f
+    cols["desired"] = rng.integers(1, 10_001, W).astype(np.int64)
+    cols.update(_tol_columns(rng, st, W, 16, 0, 3))
+    return _fill_columns(W, st, cols)
+
+
+def _expr_columns(rng, st, R: int, n_keys: int, n_vals: int, n_int_keys: int, p_invalid: float):
+    """R requirements of :func:`_expr` (all_ops=True, vectorised): (rq_key, rq_op, per-requirement value
+    counts, flat value ids)."""
+    sid = st.id
+    keys = np.array([sid(f"key{k}") for k in range(n_keys)], np.int32)
+    ikeys = np.array([sid(f"num{k}") for k in range(max(1, n_int_keys))], np.int32)
+    vals = np.array([sid(f"val{v}") for v in range(n_vals)], np.int32)
+    nums = np.array([sid(str(i)) for i in range(1000)], np.int32)
+    ops = np.array([sid(o) for o in (T.OP_IN, T.OP_NOT_IN, T.OP_EXISTS, T.OP_DOES_NOT_EXIST, T.OP_GT, T.OP_LT)],
+                   np.int32)
+    # the invalid forms of _expr: an invalid label value, an invalid key, an unknown operator, In with no value
+    bad_key = np.array([sid("key0"), sid("bad key/with/slashes"), sid("key1"), sid("key2")], np.int32)
+    bad_op = np.array([ops[0], ops[2], sid("Bogus"), ops[0]], np.int32)
+    bad_nv = np.array([1, 0, 1, 0], np.int32)
+    bad_v = np.array([sid("invalid value: ___@#$%^"), -1, sid("val1"), -1], np.int32)
+    op = rng.integers(0, 6, R)
+    if not n_int_keys:
+        op = np.where(op >= 4, 0, op)
+    rk = np.where(op >= 4, ikeys[rng.integers(0, max(1, n_int_keys), R)], keys[rng.integers(0, n_keys, R)])
+    nv = np.where(op >= 4, 1, np.where(op >= 2, 0, rng.integers(1, 4, R)))
+    rop = ops[op]
+    inv = (rng.random(R) < p_invalid) if p_invalid else np.zeros(R, bool)
+    bad = rng.integers(0, 4, R)
+    rk = np.where(inv, bad_key[bad], rk).astype(np.int32)
+    rop = np.where(inv, bad_op[bad], rop).astype(np.int32)
+    nv = np.where(inv, bad_nv[bad], nv).astype(np.int32)
+    owner = np.repeat(np.arange(R), nv)
+    V = len(owner)
+    rv = np.where(op[owner] >= 4, nums[rng.integers(0, 1000, V)], vals[rng.integers(0, n_vals, V)])
+    rv = np.where(inv[owner], bad_v[bad[owner]], rv).astype(np.int32)
+    return rk, rop, nv, rv
+
+
+def _excl_in_group(lengths, group_first):
+    """Offset of each item within its group: exclusive prefix of ``lengths`` minus that of the group's first
+    item (``group_first[i]`` = index of item i's group's first item)."""
+    excl = np.cumsum(lengths) - lengths
+    return excl - excl[group_first]
+
+
+def gen_units_c5_columns(rng: np.random.Generator, W: int, cluster_names, n_keys=64, n_vals=16, n_int_keys=4,
+                         n_taints=256, prefix="c5"):
+    """The C5 adversarial-filtering workload of :func:`gen_units_c5` (same distributions, its own random
+    stream) as ``columns.SUColumns``: 2-8 required terms of 2-6 expressions over every operator (1 %
+    invalid) with a metadata.name NotIn field on 30 % of the terms, 2-4 preferred terms of 1-3 expressions
+    (weights U{1..100}), GVK = GVKS[w % 8], Divide / Duplicate 50/50, 1-8 tolerations over 256 taints
+    (5 % wildcard), MaxClusters U{1..16}, requests cpu U[0, 64 000] milli, memory U[0, 256 GiB)."""
+    from . import columns as CO
+
+    C = len(cluster_names)
+    st = CO.StringTable()
+    sid = st.id
+    cid = np.array([sid(n) for n in cluster_names], np.int32)
+    gv = [(sid(g[0]), sid("v1"), sid(g[2])) for g in GVKS]
+    gw = np.arange(W) % 8
+    cols = {"group": np.array([gv[i][0] for i in range(8)], np.int32)[gw],
+            "version": np.array([gv[i][1] for i in range(8)], np.int32)[gw],
+            "kind": np.array([gv[i][2] for i in range(8)], np.int32)[gw],
+            "namespace_": np.full(W, sid("default"), np.int32), "name": _names(st, W, prefix)}
+    md_name, notin = sid("metadata.name"), sid(T.OP_NOT_IN)
+    # required terms: 2-8 per unit, 2-6 expressions, 30 % with one metadata.name field
+    nrt = rng.integers(2, 9, W).astype(np.int32)
+    NT = int(nrt.sum())
+    ne = rng.integers(2, 7, NT).astype(np.int32)
+    nf = (rng.random(NT) < 0.3).astype(np.int32)
+    # preferred terms: 2-4 per unit, 1-3 expressions
+    npt = rng.integers(2, 5, W).astype(np.int32)
+    NP = int(npt.sum())
+    pne = rng.integers(1, 4, NP).astype(np.int32)
+    # requirement table: unit by unit, its required terms (exprs then fields), then its preferred terms
+    rt_unit = np.repeat(np.arange(W), nrt)
+    pt_unit = np.repeat(np.arange(W), npt)
+    per_rt = ne + nf
+    req_per_unit = np.bincount(rt_unit, weights=per_rt, minlength=W).astype(np.int64) + \
+        np.bincount(pt_unit, weights=pne, minlength=W).astype(np.int64)
+    unit_base = np.zeros(W + 1, np.int64)
+    unit_base[1:] = np.cumsum(req_per_unit)
+    R = int(unit_base[-1])
+    rterm_off, pterm_off = CO._csr_off(nrt), CO._csr_off(npt)
+    rt_total = np.bincount(rt_unit, weights=per_rt, minlength=W).astype(np.int64)
+    rt_req = (unit_base[:-1][rt_unit] + _excl_in_group(per_rt, rterm_off[:-1][rt_unit])).astype(np.int32)
+    pt_req = (unit_base[:-1][pt_unit] + rt_total[pt_unit] +
+              _excl_in_group(pne, pterm_off[:-1][pt_unit])).astype(np.int32)
+    # which requirement slots are fields (one per term with nf, after its expressions)
+    is_field = np.zeros(R, bool)
+    is_field[(rt_req + ne)[nf == 1]] = True
+    is_pref = np.zeros(R, bool)
+    pref_slots = np.repeat(pt_req.astype(np.int64), pne) + _excl_in_group(
+        np.ones(int(pne.sum()), np.int64), np.repeat(np.cumsum(pne) - pne, pne))
+    is_pref[pref_slots] = True
+    # expressions: required ones with 1 % invalid, preferred ones all valid
+    rk = np.zeros(R, np.int32)
+    rop = np.zeros(R, np.int32)
+    nv = np.zeros(R, np.int32)
+    out_v = []
+    for mask, p_inv in ((~is_field & ~is_pref, 0.01), (is_pref, 0.0)):
+        idx = np.nonzero(mask)[0]
+        k_, o_, n_, v_ = _expr_columns(rng, st, len(idx), n_keys, n_vals, n_int_keys, p_inv)
+        rk[idx], rop[idx], nv[idx] = k_, o_, n_
+        out_v.append((idx, n_, v_))
+    fidx = np.nonzero(is_field)[0]
+    rk[fidx], rop[fidx], nv[fidx] = md_name, notin, 1
+    out_v.append((fidx, np.ones(len(fidx), np.int32), cid[rng.integers(0, C, len(fidx))]))
+    val_off = CO._csr_off(nv)
+    rq_val = np.zeros(int(val_off[-1]), np.int32)
+    for idx, n_, v_ in out_v:
+        if len(v_):
+            dst = np.repeat(val_off[:-1][idx].astype(np.int64), n_) + _excl_in_group(
+                np.ones(int(n_.sum()), np.int64), np.repeat(np.cumsum(n_) - n_, n_))
+            rq_val[dst] = v_
+    cols.update({"rq_key": rk, "rq_op": rop, "rq_val_off": val_off, "rq_val": rq_val,
+                 "rterm_off": rterm_off, "rt_req": rt_req, "rt_n_expr": ne, "rt_n_field": nf,
+                 "pterm_off": pterm_off, "pt_weight": rng.integers(1, 101, NP).astype(np.int32),
+                 "pt_req": pt_req, "pt_n_expr": pne})
+    f = np.full(W, CO.SU_HAS_DESIRED | CO.SU_HAS_MAX_CLUSTERS | CO.SU_HAS_CLUSTER_AFFINITY | CO.SU_HAS_REQUIRED,
+                np.uint32)
+    f |= np.where(rng.random(W) < 0.5, 0, CO.SU_DUPLICATE).astype(np.uint32)
+    cols["flags"] = f
+    cols["desired"] = rng.integers(1, 101, W).astype(np.int64)
+    cols["max_clusters"] = rng.integers(1, 17, W).astype(np.int64)
+    cols["req_cpu"] = rng.integers(0, 64_001, W).astype(np.int64)
+    cols["req_mem"] = rng.integers(0, 256 * GI, W, dtype=np.int64)
+    cols.update(_tol_columns(rng, st, W, n_taints, 1, 8, allow_wild=True))
+    return _fill_columns(W, st, cols)

@@ -16,10 +16,16 @@ import csv
 import glob
 import json
 import os
+import sys
 from collections import defaultdict
 
-STAGE = ("req_mask_kernel", "prep_kernel", "schedule_lean_kernel", "schedule_wide_kernel", "schedule_kernel")
-MAIN = ("schedule_wide_kernel", "schedule_lean_kernel")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kubeadmiral_amd.build import source_hash  # noqa: E402
+
+STAGE = ("req_mask_kernel", "req_row_kernel", "prep_kernel", "schedule_lean_kernel", "schedule_wide_kernel",
+         "schedule_row_kernel", "schedule_kernel")
+# the step's kernels (bench.py picks its roofline kernel among them by live HIP-event time)
+STEP = STAGE + ("plan_kernel",)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("out")
@@ -52,10 +58,10 @@ for k, d in res["kernels"].items():
         stage_bytes += d.get("hbm_bytes_corrected", 0.0)
         stage_ns += d.get("avg_ns", 0.0)
 res["stage"] = {"kernels": list(STAGE), "hbm_bytes_per_launch": stage_bytes, "avg_ns_sum": stage_ns}
-# the dominant kernel of the stage (bench.py's roofline kernel): traffic and instruction counts per launch
+# the longest kernel of the step: traffic and instruction counts per launch
 main = {}
 for k, d in res["kernels"].items():
-    if any(m in k for m in MAIN) and d.get("avg_ns", 0) > main.get("avg_ns", 0):
+    if any(m in k for m in STEP) and d.get("avg_ns", 0) > main.get("avg_ns", 0):
         main = dict(d, name=k)
 if main:
     main["hbm_bytes_per_launch"] = main.get("hbm_bytes_corrected")
@@ -63,7 +69,7 @@ res["main_kernel"] = main
 print(json.dumps(res, indent=1))
 if a.json:
     with open(a.json, "w") as f:
-        json.dump({"config": a.cfg, "units": a.units, "clusters": a.clusters,
+        json.dump({"config": a.cfg, "units": a.units, "clusters": a.clusters, "src_hash": source_hash(),
                    "hbm_bytes_per_launch": stage_bytes, "stage_avg_ns_sum": stage_ns,
                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; (2*FETCH_SIZE + WRITE_SIZE)"
                              " KiB per dispatch summed over the stage kernels (MI355X_MICROARCH.md HBM section)",

@@ -1,0 +1,113 @@
+"""bench.py's host logic on CPU: the JSON line contract, the per-stage rooflines, the shard sweep and the
+gathered-placement verification, with a stand-in for the GPU context whose results come from the C
+restatement (oracle/kad_ref.c). No GPU here: this checks the bookkeeping, never a kernel; the GPU run of
+bench.py (round end, and tests/test_gpu_bench_dist.py) uses the real libkad.so context."""
+import argparse
+import json
+
+import numpy as np
+import pytest
+
+import bench
+from kubeadmiral_amd import runtime, synth
+
+
+class FakeContext:
+    """runtime.Context's surface as bench.py uses it; schedule() runs the C oracle."""
+    STAGES = runtime.Context.STAGES
+
+    def __init__(self, device=0):
+        self.snap = self.batch = None
+        self.res = None
+
+    def upload_snapshot(self, snap):
+        self.snap = snap
+
+    def upload_batch(self, batch):
+        self.batch = batch
+
+    def schedule(self, fwk):
+        from oracle import ref
+        self.res = ref.schedule(self.snap, self.batch, fwk, n_threads=4)
+        self.fwk = fwk
+
+    def sync(self):
+        pass
+
+    def download(self):
+        return self.res
+
+    def path_counts(self):
+        return {"units": self.batch.W, "full_kernel": 3, "row_kernel": 5, "planner_rows": 0}
+
+    def set_timing(self, on):
+        pass
+
+    def stage_timing(self):
+        return {"req_mask": 0.01, "prep": 0.02, "main": 0.2, "defer": 0.003, "planner": 0.0, "total": 0.25,
+                "rows": 0.015}
+
+    def close(self):
+        pass
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    from kubeadmiral_amd import build
+    build.build()
+    monkeypatch.setattr(runtime, "Context", FakeContext)
+    monkeypatch.setitem(synth.SIZES, "c3", (3000, 1000))
+    monkeypatch.setitem(synth.SIZES, "c2", (800, 256))
+
+
+def _args(**kw):
+    a = dict(gpus=1, steps=2, warmup=1, config="c3", units=None, cpu_seconds=0.05, no_cpu_baseline=False,
+             no_extra=True, extras="c2", no_sweep=True, backend="nccl", share_gpu=False)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def test_line_contract_and_rooflines(fake):
+    out = bench.bench_schedule(_args(), "c3", 0, 1, 0, None)
+    json.dumps(out)  # serialisable
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "end_to_end"):
+        assert k in out, k
+    r = out["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    # the dominant kernel is the stage with the longest (stand-in) time: the main kernel
+    assert r["kernel"] == "schedule_wide_kernel" and r["time_ms"] == pytest.approx(0.2)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
+    assert set(r["kernels"]) == {"req_mask", "prep", "main", "rows", "defer"}
+    assert out["cpu_baseline"]["kind"] == "port" and out["cpu_baseline"]["cores"] >= 1
+    assert out["config"]["paths"]["row_kernel"] == 5
+
+
+def test_stale_pmc_is_not_used(fake, tmp_path, monkeypatch):
+    """A PMC profile whose src_hash is not the code's is reported as stale, never mixed with live timing."""
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "pmc_c3.json").write_text(json.dumps({"units": 3000, "clusters": 1000, "src_hash": "0" * 16,
+                                                  "kernels": {"schedule_wide_kernel<16>": {"SQ_INSTS_SALU": 1e9}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    pmc, _, why = bench.load_pmc("c3", 3000, 1000)
+    assert pmc is None and "stale" in why
+    from kubeadmiral_amd.build import source_hash
+    (prof / "pmc_c3.json").write_text(json.dumps({"units": 3000, "clusters": 1000, "src_hash": source_hash(),
+                                                  "kernels": {"kad::schedule_wide_kernel<16>(kad::WideArgs)": {
+                                                      "SQ_INSTS_SALU": 4.0e8, "SQ_INSTS_VALU": 1.0e8,
+                                                      "hbm_bytes_corrected": 1e6}}}))
+    pmc, _, why = bench.load_pmc("c3", 3000, 1000)
+    assert pmc is not None and why is None
+    r = bench.roofline_for("main", "schedule_wide_kernel", 1.0, 5e5, pmc, "x", None)
+    assert r["bound"] == "salu_issue"
+    assert r["frac"] == pytest.approx(4.0e8 / 1e-3 / bench.SALU_PEAK)
+    assert r["traffic"] == 1e6 and r["hbm"]["measured_gbs"] == pytest.approx(1.0)
+
+
+def test_shard_sweep_projection(fake):
+    out = bench.shard_sweep(_args(), "c3", 0, t1_ms=1.0, ns=(2,))
+    p = out["per_n"]["2"]
+    assert len(p["shard_ms"]) == 2 and p["units_per_rank"] == 1500
+    assert p["projected_efficiency"] == pytest.approx(1.0 / (2 * p["max_ms"]))

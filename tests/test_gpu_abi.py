@@ -157,3 +157,44 @@ def test_malformed_batches_are_rejected(ctx):
             ctx.schedule(fwk)
     # the context still works
     assert_same(ctx.run(fwk, batch), c_oracle(snap, batch, fwk), "after rejected blobs")
+
+
+def test_failed_snapshot_refresh_leaves_nothing_resident(ctx):
+    """a snapshot upload / update whose derived-state rebuild fails (kad_debug_inject_fault,
+    standing in for a hipMalloc failure) must not leave a batch validated against the old snapshot
+    resident: kad_schedule returns KAD_ESTATE until a snapshot and a batch are uploaded again."""
+    import copy
+
+    from kubeadmiral_amd.runtime import KadError
+
+    clusters, units = synth.gen_fuzz(4242, W=60, C=96)
+    fwk = synth.fuzz_framework(4)
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, units)
+    ctx.upload_snapshot(snap)
+    want = ctx.run(fwk, batch)
+    # full upload fails in refresh_derived
+    ctx.inject_fault(1)
+    with pytest.raises(KadError) as e:
+        ctx.upload_snapshot(snap)
+    assert e.value.code == -3  # KAD_ENOMEM
+    with pytest.raises(KadError) as e:
+        ctx.schedule(fwk)
+    assert e.value.code == -4  # KAD_ESTATE
+    ctx.upload_snapshot(snap)
+    assert_same(ctx.run(fwk, batch), want, "after a failed upload")
+    # in-place update fails in refresh_derived
+    c2 = copy.deepcopy(clusters)
+    c2[3].available = dict(c2[3].allocatable or {})  # a status event: all of cluster 3 free
+    delta = snap.diff(c2)
+    assert delta is not None and delta.changed
+    ctx.inject_fault(1)
+    with pytest.raises(KadError) as e:
+        ctx.update_snapshot(delta)
+    assert e.value.code == -3
+    with pytest.raises(KadError) as e:
+        ctx.schedule(fwk)
+    assert e.value.code == -4
+    ctx.inject_fault(0)
+    ctx.upload_snapshot(snap)
+    assert_same(ctx.run(fwk, batch), want, "after a failed update")

@@ -1,6 +1,7 @@
 """bench.py's multi-GPU path on the one-GPU box: `--gpus 2` starts two ranks itself (torch.distributed.run),
 `--share-gpu` puts both on device 0 and `--backend gloo` stands in for RCCL (two ranks on one GPU cannot use
-RCCL). Checks the line the driver parses: world size, whole-job value, the timed placement all-gather."""
+RCCL). Checks the line the driver parses: world size, whole-job value, the timed placement all-gather, and
+that the gathered placements of every rank equal a single-rank run of its shard."""
 import json
 import os
 import subprocess
@@ -24,3 +25,5 @@ def test_bench_two_ranks_share_one_gpu():
     assert line["config"]["units_total"] == 20000 and line["config"]["units_per_gpu"] == 10000
     assert line["value"] > 0 and line["scaling"] == "strong"
     assert line["allgather"] is not None and line["allgather"]["ms"] > 0
+    # every gathered field of both ranks was compared with a single-rank run of the same shard blob
+    assert line["allgather"]["verified"] and "2 ranks" in line["allgather"]["verified"]

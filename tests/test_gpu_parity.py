@@ -311,9 +311,9 @@ def test_row_kernel_long_feasible_lists(ctx, seed, C, prof):
 @pytest.mark.parametrize("seed", [7101, 7102])
 def test_requirement_value_rows_and_segments(ctx, seed):
     """Requirement masks from both paths: In / NotIn / Exists / DoesNotExist whose value ids are < 64 and
-    at most 5 (snapshot value rows, req_row_kernel) and the rest — value ids >= 64 (a key with 150 distinct
-    values), lists longer than 5, Gt / Lt, metadata.name — through the key-grouped segments
-    (req_mask_kernel); ClusterAffinity filter and score against the C oracle."""
+    at most 5, and the label-free ops (metadata.name, TRUE / FALSE) through req_row_kernel, and the rest —
+    value ids >= 64 (a key with 150 distinct values), lists longer than 5, Gt / Lt — through the
+    key-grouped segments (req_mask_kernel); ClusterAffinity filter and score against the C oracle."""
     rng = np.random.default_rng(seed)
     C = 700
     clusters = synth.gen_clusters(rng, C, n_keys=3, n_vals=4, n_int_keys=1)
@@ -355,6 +355,51 @@ def test_requirement_value_rows_and_segments(ctx, seed):
         snap, batch, res = run(ctx, clusters, units, fwk)
         assert (res.status == pack.ST_OK).mean() > 0.3
         assert_same(res, c_oracle(snap, batch, fwk), f"value rows seed {seed}")
+
+
+@pytest.mark.parametrize("C", [333, 1000])
+def test_label_free_requirements(ctx, C):
+    """the label-free requirement ops computed on req_row_kernel without label loads —
+    metadata.name In / NotIn on an existing and on an unknown cluster name, ClusterSelector entries on a key
+    no cluster has (the Equals requirement is constant FALSE) and DoesNotExist on such a key (constant
+    TRUE) — with C not a multiple of 64, ClusterAffinity filter + score against the C oracle."""
+    rng = np.random.default_rng(C)
+    clusters = synth.gen_clusters(rng, C, n_keys=3, n_vals=4)
+    names = [c.name for c in clusters]
+
+    def field():
+        op = T.OP_IN if rng.random() < 0.5 else T.OP_NOT_IN
+        name = names[int(rng.integers(0, C))] if rng.random() < 0.7 else "no-such-cluster"
+        return T.ClusterSelectorRequirement("metadata.name", op, [name])
+
+    def expr():
+        r = rng.random()
+        if r < 0.3:
+            return T.ClusterSelectorRequirement("absent-key", T.OP_DOES_NOT_EXIST, None)
+        if r < 0.45:
+            return T.ClusterSelectorRequirement("absent-key", T.OP_IN, ["x"])
+        return synth._expr(rng, 3, 4, 0, all_ops=False, p_invalid=0.0)
+
+    units = []
+    for w in range(500):
+        terms = []
+        for _ in range(int(rng.integers(1, 3))):
+            fields = [field() for _ in range(int(rng.integers(0, 2)))] or None
+            exprs = [expr() for _ in range(int(rng.integers(0, 3)))] or None
+            terms.append(T.ClusterSelectorTerm(exprs, fields))
+        prefs = [T.PreferredSchedulingTerm(int(rng.integers(1, 50)), T.ClusterSelectorTerm(None, [field()]))
+                 for _ in range(int(rng.integers(0, 3)))]
+        sel = {"absent-key": "v"} if rng.random() < 0.1 else None
+        units.append(T.SchedulingUnit(
+            group="apps", version="v1", kind="Deployment", namespace="default", name=f"lf-{w}", desired_replicas=3,
+            scheduling_mode=T.SCHEDULING_MODE_DUPLICATE, max_clusters=int(rng.integers(1, 9)), cluster_selector=sel,
+            affinity=T.Affinity(T.ClusterAffinity(T.ClusterSelector(terms), prefs or None))))
+    for fwk in (F.Framework(F.default_enabled_plugins()),
+                F.Framework(F.EnabledPlugins([F.ClusterAffinity], [F.ClusterAffinity], [F.MaxCluster], []))):
+        snap, batch, res = run(ctx, clusters, units, fwk)
+        st = np.bincount(res.status, minlength=6)
+        assert st[pack.ST_OK] > 50 and st[pack.ST_NO_FEASIBLE] > 10, st
+        assert_same(res, c_oracle(snap, batch, fwk), f"label-free C={C}")
 
 
 def test_large_c_global_scratch(ctx):

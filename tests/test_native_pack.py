@@ -119,3 +119,99 @@ def test_malformed_columns_are_rejected():
         with pytest.raises(RuntimeError, match="kad_pack_batch"):
             P.pack(F.Framework(), bad)
     P.pack(F.Framework(), good)  # still usable
+
+
+def _create(v):
+    import ctypes
+
+    from kubeadmiral_amd.runtime import load_library
+
+    L = load_library()
+    L.kad_packer_create.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+    L.kad_packer_error.argtypes = [ctypes.c_void_p]
+    L.kad_packer_error.restype = ctypes.c_char_p
+    L.kad_packer_destroy.argtypes = [ctypes.c_void_p]
+    h = ctypes.c_void_p()
+    rc = L.kad_packer_create(ctypes.byref(v), ctypes.byref(h))
+    if rc == 0:
+        L.kad_packer_destroy(h)
+        return rc, ""
+    return rc, L.kad_packer_error(None).decode()
+
+
+def _bad_vocab_cases():
+    """(name, mutate(vocab, keep)) — each breaks one rule kad_packer_create checks."""
+    import ctypes
+
+    def offs(v, field, arr):
+        a = np.asarray(arr, np.int64)
+        v._keep.append(a)
+        getattr(v, field).off = a.ctypes.data
+
+    def voff(v, arr):
+        a = np.asarray(arr, np.int32)
+        v._keep.append(a)
+        v.label_val_off = a.ctypes.data
+
+    return [
+        ("gvk_count", lambda v: setattr(v.gvk_version, "n", v.gvk_group.n - 1)),
+        ("taint_count", lambda v: setattr(v.taint_effect, "n", v.taint_key.n - 1)),
+        ("label_val_off_null", lambda v: setattr(v, "label_val_off", None)),
+        ("label_val_off_start", lambda v: voff(v, [1] + [v.label_vals.n] * v.label_keys.n)),
+        ("label_val_off_decreasing", lambda v: voff(v, [0, 3, 2] + [v.label_vals.n] * (v.label_keys.n - 2))),
+        ("label_val_off_past_end", lambda v: voff(v, [0] * v.label_keys.n + [v.label_vals.n + 1])),
+        ("strs_negative_n", lambda v: setattr(v.cluster_names, "n", -1)),
+        ("strs_not_from_zero", lambda v: offs(v, "cluster_names", [5] + [9] * v.cluster_names.n)),
+        ("strs_decreasing", lambda v: offs(v, "label_keys", [0, 4, 2] + [8] * (v.label_keys.n - 2))),
+        ("strs_null_off", lambda v: setattr(v.taint_key, "off", ctypes.c_void_p(None))),
+        ("taint_words", lambda v: setattr(v, "n_taint_words", 0)),
+    ]
+
+
+@pytest.mark.parametrize("case", [c[0] for c in _bad_vocab_cases()])
+def test_packer_create_rejects_malformed_vocab(case):
+    """the vocabulary from a cross-language caller is validated (KAD_EINVAL + message)."""
+    clusters, units, fwk = synth.make_config("c5", W=4, C=64)
+    snap = pack.Snapshot(clusters)
+    assert snap.TW >= 1 and len(snap.label_key_id) >= 3 and len(snap.taint_defs) >= 1 and len(snap.gvk_id) >= 1
+    keep = []
+    v = CO.vocab_of(snap, keep)
+    v._keep = keep
+    assert _create(v) == (0, "")
+    mutate = dict(_bad_vocab_cases())[case]
+    mutate(v)
+    rc, msg = _create(v)
+    assert rc == -1 and msg, (case, rc, msg)
+
+
+@pytest.mark.parametrize("cfg,W,C", [("c4", 1500, 512), ("c4", 400, 100), ("c5", 300, 1500)])
+def test_columnar_generators_blob_identical(cfg, W, C):
+    """synth.gen_units_c4_columns / gen_units_c5_columns (the bench's vectorised C4 / C5 generators): the
+    native packer's blob equals the Python packer's on the same units (columns → objects → pack.Batch)."""
+    rng = np.random.default_rng(C + W)
+    if cfg == "c4":
+        clusters = synth.gen_clusters(rng, C)
+        cols = synth.gen_units_c4_columns(rng, W, [c.name for c in clusters])
+    else:
+        clusters = synth.gen_clusters(rng, C, n_keys=64, n_vals=16, n_int_keys=4, n_taints=256, taints_per=(4, 16),
+                                      p_gvk=0.9, gvks=synth.GVKS)
+        cols = synth.gen_units_c5_columns(rng, W, [c.name for c in clusters])
+    units = CO.to_units(cols)
+    snap = pack.Snapshot(clusters)
+    fwk = synth.profile_for(cfg)
+    want = pack.Batch(snap, fwk, units)
+    got = CO.NativePacker(snap).pack(fwk, cols)
+    assert np.array_equal(got.blob, want.blob)
+    # the distributions the docstrings promise
+    if cfg == "c4":
+        k = np.diff(cols["place_off"])
+        assert k.min() >= min(8, C) and k.max() <= 64
+        assert all(len(u.cluster_names) == n for u, n in zip(units, k))  # distinct clusters
+        assert 0.35 < np.mean([u.weights is not None for u in units]) < 0.65
+        assert 0.15 < np.mean([u.current_clusters is not None for u in units]) < 0.35
+    else:
+        assert all(2 <= len(u.affinity.cluster_affinity.required.cluster_selector_terms) <= 8 for u in units)
+        ops = {r.operator for u in units for t in u.affinity.cluster_affinity.required.cluster_selector_terms
+               for r in (t.match_expressions or [])}
+        assert {"In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt", "Bogus"} <= ops
+        assert any(t.match_fields for u in units for t in u.affinity.cluster_affinity.required.cluster_selector_terms)
