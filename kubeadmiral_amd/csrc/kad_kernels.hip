@@ -1790,16 +1790,27 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
             lean_defer(w);
             continue;
           }
+          if ((uint64_t)rmax - (uint64_t)rmin < 65536u) {  // packed replay: key << 16 | position
 #pragma unroll
-          for (int q = 0; q < Q; ++q)
-            if (q < nq && q * 64 + lane < n) {
-              key[q * 64 + lane] = (uint32_t)((uint64_t)t[q] - (uint64_t)rmin);
-              pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
-            }
-          wave_sync();
-          PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
-          pw.select(n, (int)k);
-          for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
+            for (int q = 0; q < Q; ++q)
+              if (q < nq && q * 64 + lane < n)
+                key[q * 64 + lane] = ((uint32_t)((uint64_t)t[q] - (uint64_t)rmin) << 16) | (uint32_t)(q * 64 + lane);
+            wave_sync();
+            PdqWaveP<> pw{key, posl, posr, xs_b, xs_c};
+            pw.select(n, (int)k);
+            for (int r = lane; r < n; r += WAVE) inv[key[r] & 0xFFFFu] = (uint16_t)r;
+          } else {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq && q * 64 + lane < n) {
+                key[q * 64 + lane] = (uint32_t)((uint64_t)t[q] - (uint64_t)rmin);
+                pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
+              }
+            wave_sync();
+            PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
+            pw.select(n, (int)k);
+            for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
+          }
           wave_sync();
 #pragma unroll
           for (int q = 0; q < Q; ++q)
@@ -2326,28 +2337,45 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
             const int xs_b = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
             const int xs_c = (ad->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
             KAD_PT(r0);
+            if ((uint32_t)mx32 - (uint32_t)mn32 < 65536u) {
+              // packed replay: key << 16 | position (n <= 512), one LDS word per element
 #pragma unroll
-            for (int q = 0; q < Q; ++q)
-              if (q < nq && q * 64 + lane < n) {
-                key[q * 64 + lane] = (uint32_t)(t[q] - mn32);
-                pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
-              }
-            wave_sync();
-            PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
-            KAD_PT(r1);
-            pw.select(n, k);
-            KAD_PT(r2);
-            for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
-            wave_sync();
-            KAD_PT(r3);
-            KAD_PADD(6, (r1 - r0) + (r3 - r2));
+              for (int q = 0; q < Q; ++q)
+                if (q < nq && q * 64 + lane < n)
+                  key[q * 64 + lane] = ((uint32_t)(t[q] - mn32) << 16) | (uint32_t)(q * 64 + lane);
+              wave_sync();
+              PdqWaveP<> pw{key, posl, posr, xs_b, xs_c};
+              KAD_PT(r1);
+              pw.select(n, k);
+              KAD_PT(r2);
+              for (int r = lane; r < n; r += WAVE) inv[key[r] & 0xFFFFu] = (uint16_t)r;
+              wave_sync();
+              KAD_PT(r3);
+              KAD_PADD(6, (r1 - r0) + (r3 - r2));
 #ifdef KAD_PHASE_PROF
-            KAD_PADD(7, pw.pr[0]);
-            KAD_PADD(8, pw.pr[1]);
-            KAD_PADD(9, pw.pr[2]);
-            KAD_PADD(10, pw.pr[3]);
-            KAD_PADD(11, n);
+              KAD_PADD(7, pw.pr[0]);
+              KAD_PADD(8, pw.pr[1]);
+              KAD_PADD(9, pw.pr[2]);
+              KAD_PADD(10, pw.pr[3]);
+              KAD_PADD(11, n);
 #endif
+            } else {
+#pragma unroll
+              for (int q = 0; q < Q; ++q)
+                if (q < nq && q * 64 + lane < n) {
+                  key[q * 64 + lane] = (uint32_t)(t[q] - mn32);
+                  pid[q * 64 + lane] = (uint16_t)(q * 64 + lane);
+                }
+              wave_sync();
+              PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
+              KAD_PT(r1);
+              pw.select(n, k);
+              KAD_PT(r2);
+              for (int r = lane; r < n; r += WAVE) inv[pid[r]] = (uint16_t)r;
+              wave_sync();
+              KAD_PT(r3);
+              KAD_PADD(6, (r1 - r0) + (r3 - r2));
+            }
             mode = 3;
           }
         }
@@ -2821,12 +2849,25 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
         uint16_t* posl = in_lds ? posl_l : pid_g + Cp;
         uint16_t* posr = in_lds ? posr_l : pid_g + 2 * Cp + 64;
         inv = posl;
-        for (int j = tid; j < n; j += ROW_THREADS) pid[j] = (uint16_t)j;
+        // packed replay (key - min << 16 | position: every C5 row, n <= C < 2^16) unless the totals span 2^16
+        const bool packed = (uint32_t)mx - (uint32_t)mn < 65536u;
+        for (int j = tid; j < n; j += ROW_THREADS) {
+          if (packed)
+            key[j] = (((key[j] ^ 0x80000000u) - (uint32_t)mn) << 16) | (uint32_t)j;
+          else
+            pid[j] = (uint16_t)j;
+        }
         __syncthreads();
         if (wv == 0) {
           const int xs_b = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
           const int xs_c = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
-          if (in_lds) {
+          if (packed && in_lds) {
+            PdqWaveP<> pw{key, posl, posr, xs_b, xs_c};
+            pw.select(n, k);
+          } else if (packed) {  // elements stay in LDS; stopper scratch in the slab (workgroup fences order both)
+            PdqWaveP<true> pw{key, posl, posr, xs_b, xs_c};
+            pw.select(n, k);
+          } else if (in_lds) {
             PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
             pw.select(n, k);
           } else {  // keys stay in LDS; positions in the slab (workgroup-scope fences order both)
@@ -2835,7 +2876,7 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
           }
         }
         __syncthreads();
-        for (int r = tid; r < n; r += ROW_THREADS) inv[pid[r]] = (uint16_t)r;
+        for (int r = tid; r < n; r += ROW_THREADS) inv[packed ? (key[r] & 0xFFFFu) : pid[r]] = (uint16_t)r;
         __syncthreads();
         KAD_PT(t5);
         KAD_PADD(5, t5 - t4);

@@ -267,6 +267,17 @@ struct KeyLdsStoreT {
   }
 };
 
+// storage: packed key << 16 | id words (PdqWaveP's heapsort fallback)
+struct PackedLdsStore {
+  uint32_t* e;
+  __device__ __forceinline__ bool gt(int i, int j) const { return (e[i] >> 16) > (e[j] >> 16); }
+  __device__ __forceinline__ void swap(int i, int j) const {
+    const uint32_t a = e[i], b = e[j];
+    e[i] = b;
+    e[j] = a;
+  }
+};
+
 // ------------------------------------------- wave-parallel restricted replay
 // PdqWave runs the same control flow as PdqT::select — Go 1.19 pdqsort_func
 // restricted to the ranges that straddle k — with the whole wave. The scalar
@@ -690,6 +701,352 @@ struct PdqWave {  // GS: key/id/posL/posR live in a global scratch slab
   }
 };
 
+// ------------------------------------- packed wave-parallel restricted replay
+// PdqWaveP: the same restricted pdqsort_func replay as PdqWave, on packed elements
+// e = key << 16 | original position (rows whose key range and length both fit 16 bits: every
+// C3 / C2 row, C5's long rows): a move is one 32-bit LDS access instead of a key and an id.
+// The partition is fused into two LDS passes. Go's partition is
+//   swap(a, pivot); Hoare pairing over [a+1, b); swap(j, a)      (partitionEqual: no final swap)
+// which is one permutation of [a, b). The first pass reads the range through the virtual first
+// swap (position `pivot` reads as old e[a]) and scatters the left / right stopper positions; the
+// second reads each misplaced pair and the few special positions (a, j, pivot) and writes the final
+// arrangement directly: the t-th misplaced left stopper l_t and the t-th misplaced right stopper
+// r_t (from the right) exchange; the element paired into j = a + #R goes to a instead (the final
+// swap), the pivot element to j; position `pivot` gets old e[a] unless a pair or j covers it.
+template <bool GS = false>
+struct PdqWaveP {
+  uint32_t* e;      // [n] packed elements, permuted in place
+  uint16_t* posL;   // [n + 64] stopper scratch (lanes past the range write into the tail)
+  uint16_t* posR;   // [n]
+  int xs_b, xs_c;
+#ifdef KAD_PHASE_PROF
+  mutable uint32_t pr[4] = {0, 0, 0, 0};
+#endif
+
+  __device__ __forceinline__ uint32_t E(int p) const { return (uint32_t)__builtin_amdgcn_readfirstlane((int)e[p]); }
+  __device__ __forceinline__ void swap1(int i, int j) const {
+    const uint32_t vi = e[i], vj = e[j];
+    wsync<GS>();
+    if (lane_id() == 0) {
+      e[i] = vj;
+      e[j] = vi;
+    }
+    wsync<GS>();
+  }
+  // length <= 12: stable rank = #greater + #equal before, from the lanes by readlane
+  __device__ void insertion_sort(int a, int b) const {
+    const int m = b - a, lane = lane_id();
+    const bool in = lane < m;
+    const uint32_t vp = e[in ? a + lane : a];
+    const uint32_t kp = vp >> 16;
+    int r = 0;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      const uint32_t kq = (uint32_t)__builtin_amdgcn_readlane((int)vp, q) >> 16;
+      r += (q < m) & ((int)(kq > kp) | (int)((kq == kp) & (q < lane)));
+    }
+    wsync<GS>();
+    if (in) e[a + r] = vp;
+    wsync<GS>();
+  }
+  __device__ void reverse_range(int a, int b) const {
+    const int h = (b - a) / 2;
+    for (int x0 = 0; x0 < h; x0 += WAVE) {
+      const int x = x0 + lane_id();
+      if (x < h) {
+        const int i = a + x, j = b - 1 - x;
+        const uint32_t vi = e[i], vj = e[j];
+        e[i] = vj;
+        e[j] = vi;
+      }
+    }
+    wsync<GS>();
+  }
+  __device__ void break_patterns(int a, int b) const {
+    const int length = b - a;
+    if (length >= 8) {
+      uint64_t r = (uint64_t)length;
+      const uint64_t modulus = 1ull << (64 - __clzll((unsigned long long)length));
+      const int idx = a + (length / 4) * 2 - 1;
+      for (int i = 0; i < 3; i++) {
+        r ^= r << 13;
+        r ^= r >> xs_b;
+        r ^= r << xs_c;
+        int other = (int)(r & (modulus - 1));
+        if (other >= length) other -= length;
+        swap1(idx - 1 + i, a + other);
+      }
+    }
+  }
+  // choosePivot (Go's medianAdjacent / median order2 sequences, swap counts): lanes 0-2 each read and
+  // order one candidate triple in VALU; lane 3 reads e[a - 1] (the partitionEqual test) in the same
+  // LDS round trip. Returns the pivot position; *pk its key, *prev the key at a - 1 (a > 0).
+  __device__ int choose_pivot(int a, int b, int& hint, uint32_t& pk, uint32_t& prev) const {
+    const int lane = lane_id();
+    const int l = b - a;
+    int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    int swaps = 0;
+    const bool adj = l >= 50;
+    const int g = lane < 3 ? lane : 0;
+    const int base = g == 0 ? i : (g == 1 ? j : k);
+    int pa = adj ? base - 1 : base, pb = base, pc = adj ? base + 1 : base;
+    uint32_t ka = e[pa] >> 16, kb = e[pb] >> 16, kc = e[pc] >> 16;
+    prev = a > 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)e[a - 1]) >> 16 : 0u;
+    if (l >= 8) {
+      int sw = 0;
+      if (adj) {
+        auto o2 = [&](int& p0, uint32_t& k0, int& p1, uint32_t& k1) {  // order2: less(p1, p0) = k1 > k0
+          const bool x = k1 > k0;
+          const int tp = x ? p1 : p0, tq = x ? p0 : p1;
+          const uint32_t tk = x ? k1 : k0, tl = x ? k0 : k1;
+          p0 = tp;
+          p1 = tq;
+          k0 = tk;
+          k1 = tl;
+          sw += x;
+        };
+        o2(pa, ka, pb, kb);
+        o2(pb, kb, pc, kc);
+        o2(pa, ka, pb, kb);
+      }
+      i = __builtin_amdgcn_readlane(pb, 0);
+      j = __builtin_amdgcn_readlane(pb, 1);
+      k = __builtin_amdgcn_readlane(pb, 2);
+      uint32_t ki = (uint32_t)__builtin_amdgcn_readlane((int)kb, 0), kj = (uint32_t)__builtin_amdgcn_readlane((int)kb, 1),
+               kk = (uint32_t)__builtin_amdgcn_readlane((int)kb, 2);
+      if (adj) swaps = __builtin_amdgcn_readlane(sw, 0) + __builtin_amdgcn_readlane(sw, 1) + __builtin_amdgcn_readlane(sw, 2);
+      if (kj > ki) { int tp = i; i = j; j = tp; uint32_t tk = ki; ki = kj; kj = tk; swaps++; }
+      if (kk > kj) { int tp = j; j = k; k = tp; uint32_t tk = kj; kj = kk; kk = tk; swaps++; }
+      if (kj > ki) { int tp = i; i = j; j = tp; uint32_t tk = ki; ki = kj; kj = tk; swaps++; }
+      pk = kj;
+    } else {
+      pk = (uint32_t)__builtin_amdgcn_readlane((int)kb, 1);  // lane 1 read e[j]
+    }
+    hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+    return j;
+  }
+  __device__ int first_descent(int i, int b) const {
+    for (int p0 = i; p0 < b; p0 += WAVE) {
+      const int p = p0 + lane_id();
+      const uint64_t m = ballot(p < b && (e[p] >> 16) > (e[p - 1] >> 16));
+      if (m) return p0 + __ffsll((unsigned long long)m) - 1;
+    }
+    return b;
+  }
+  // the element at j0 moves left while it is less than its left neighbour (down to position 0: Go's
+  // loop bound is 1)
+  __device__ void shift_left(int j0) const {
+    const int lane = lane_id();
+    const uint32_t X = E(j0);
+    int m = 0;
+    for (int q1 = j0; q1 > 0; q1 -= WAVE) {
+      const int q = q1 - 1 - lane;
+      const uint64_t mm = ballot(q >= 0 && (e[q] >> 16) >= (X >> 16));
+      if (mm) {
+        m = q1 - 1 - (__ffsll((unsigned long long)mm) - 1) + 1;
+        break;
+      }
+    }
+    for (int p1 = j0; p1 > m; p1 -= WAVE) {  // [m, j0) → +1, high chunks first
+      const int p = p1 - 1 - lane;
+      const bool in = p >= m;
+      const uint32_t v = in ? e[p] : 0u;
+      wsync<GS>();
+      if (in) e[p + 1] = v;
+      wsync<GS>();
+    }
+    if (lane == 0) e[m] = X;
+    wsync<GS>();
+  }
+  // the element at j0-1 moves right while its right neighbour is less than it
+  __device__ void shift_right(int j0, int b) const {
+    const int lane = lane_id();
+    const uint32_t Y = E(j0 - 1);
+    int mp = b - 1;
+    for (int q0 = j0; q0 < b; q0 += WAVE) {
+      const int q = q0 + lane;
+      const uint64_t mm = ballot(q < b && (e[q] >> 16) <= (Y >> 16));
+      if (mm) {
+        mp = q0 + __ffsll((unsigned long long)mm) - 2;
+        break;
+      }
+    }
+    for (int p0 = j0; p0 <= mp; p0 += WAVE) {  // (j0-1, mp] → -1, low chunks first
+      const int p = p0 + lane;
+      const bool in = p <= mp;
+      const uint32_t v = in ? e[p] : 0u;
+      wsync<GS>();
+      if (in) e[p - 1] = v;
+      wsync<GS>();
+    }
+    if (lane == 0) e[mp] = Y;
+    wsync<GS>();
+  }
+  __device__ bool partial_insertion_sort(int a, int b) const {
+    int i = a + 1;
+    for (int step = 0; step < 5; step++) {
+      i = first_descent(i, b);
+      if (i == b) return true;
+      if (b - a < 50) return false;
+      swap1(i, i - 1);
+      if (i - a >= 2) shift_left(i - 1);
+      if (b - i >= 2) shift_right(i + 1, b);
+    }
+    return false;
+  }
+  // Fused partition / partitionEqual of [a, b) around the element at `pivot` (key P). strict:
+  // right stoppers R = key > P (partition, with the final swap); else R = key >= P (partitionEqual).
+  // Returns #R; *npairs = number of misplaced pairs (Go's swap count in the Hoare loop).
+  __device__ int fused(int a, int b, int pivot, uint32_t P, bool strict, int* npairs) const {
+    const int lane = lane_id();
+    const uint32_t Ea = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[a]);  // S[pivot] = old e[a]
+    // thresholds on packed values: key > P <=> v > P << 16 | 0xFFFF; key >= P <=> v >= P << 16
+    const uint32_t thr = strict ? ((P << 16) | 0xFFFFu) : ((P << 16) - 1u);  // R: v > thr (P = 0: all)
+    const bool P0eq = !strict && P == 0;
+    // pass 1: stoppers of [a+1, b) through the virtual first swap
+    int cL = 0, cR = 0;
+    for (int c0 = a + 1; c0 < b; c0 += WAVE) {
+      const int p = c0 + lane;
+      const bool in = p < b;
+      const uint32_t raw = e[in ? p : b - 1];
+      const uint32_t v = p == pivot ? Ea : raw;
+      const bool isR = in && (P0eq || v > thr);
+      const uint64_t mR = ballot(isR);
+      const int rR = mbcnt(mR);
+      uint16_t* dst = isR ? posR + (cR + rR) : posL + (cL + lane - rR);
+      *dst = (uint16_t)p;
+      const int nin = b - c0 < WAVE ? b - c0 : WAVE;
+      const int nr = popc64(mR);
+      cR += nr;
+      cL += nin - nr;
+    }
+    wsync<GS>();
+    const int m = cR;
+    const int j = a + m;  // partition: the pivot's final position
+    // the special positions, read before any pair is written: S[j] (strict), the pivot element
+    const uint32_t Ep = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[pivot]);  // the pivot element (memory)
+    const uint32_t Sj = j == pivot ? Ea : (j == a ? Ep : (uint32_t)__builtin_amdgcn_readfirstlane((int)e[j]));
+    // a misplaced position holds the wrong kind for its region: L in [a+1, a+m], R in [a+m+1, b)
+    const bool Ea_R = P0eq || Ea > thr;
+    const bool pivot_paired = pivot != a && (pivot <= j ? !Ea_R : Ea_R);
+    const bool j_paired = strict && m > 0 && !(P0eq || Sj > thr);
+    const int np = cL < cR ? cL : cR;
+    int t_n = 0;
+    for (int t0 = 0; t0 < np; t0 += WAVE) {
+      const int t = t0 + lane;
+      const int l = posL[t];  // t < np + 64 <= n + 64: inside posL
+      const int ri = cR - 1 - t;
+      const int r = posR[ri > 0 ? ri : 0];
+      const bool sw = t < np && l < r;
+      const uint64_t mk = ballot(sw);
+      t_n += popc64(mk);
+      if (sw) {
+        const uint32_t el = e[l], er = e[r];
+        const uint32_t vl = l == pivot ? Ea : el, vr = r == pivot ? Ea : er;
+        e[r] = vl;
+        e[strict && l == j ? a : l] = vr;  // the element paired into j takes the final swap to a
+      }
+      if (~mk) break;  // a prefix: once a t fails, every later t fails
+    }
+    if (lane == 0) {
+      if (strict) {
+        if (m > 0 && !j_paired) e[a] = Sj;  // final swap(j, a): S[j] to a ...
+        e[j] = Ep;                          // ... and the pivot element to j (m = 0: j = a)
+      } else if (pivot != a) {
+        e[a] = Ep;  // the first swap: the pivot element to a
+      }
+      if (pivot != a && !pivot_paired && !(strict && pivot == j)) e[pivot] = Ea;  // old e[a] to `pivot`
+    }
+    wsync<GS>();
+    *npairs = t_n;
+    return m;
+  }
+  __device__ void select(int n, int k) const {
+    int a = 0, b = n;
+    int limit = 32 - __clz(n);
+    bool wasBalanced = true, wasPartitioned = true;
+    while (a < k && k < b) {
+      const int length = b - a;
+      if (length <= 12) {
+        PQ_T(i0);
+        insertion_sort(a, b);
+        PQ_T(i1);
+        PQ_ADD(2, i1 - i0);
+        return;
+      }
+      if (limit == 0) {
+        if (lane_id() == 0) {
+          PackedLdsStore st{e};
+          PdqT<PackedLdsStore> s{st, xs_b, xs_c};
+          s.heap_sort(a, b);
+        }
+        wsync<GS>();
+        return;
+      }
+      PQ_T(c0);
+      if (!wasBalanced) {
+        break_patterns(a, b);
+        limit--;
+      }
+      int hint;
+      uint32_t pk, prev;
+      int pivot = choose_pivot(a, b, hint, pk, prev);
+      if (hint == 2) {
+        reverse_range(a, b);
+        pivot = (b - 1) - (pivot - a);
+        hint = 1;
+      }
+      PQ_T(c1);
+      PQ_ADD(1, c1 - c0);
+      if (wasBalanced && wasPartitioned && hint == 1) {
+        const bool done = partial_insertion_sort(a, b);
+        PQ_T(c2);
+        PQ_ADD(2, c2 - c1);
+        if (done) return;
+        // the shifts may have moved another element to the pivot's position, and (Go's shift-left bound
+        // is 1) across a
+        pk = E(pivot) >> 16;
+        if (a > 0) prev = E(a - 1) >> 16;
+      }
+      PQ_T(c3);
+      PQ_ADD(3, 1);
+      int T;
+      if (a > 0 && !(prev > pk)) {  // !less(a-1, pivot): partitionEqual
+        a = a + 1 + fused(a, b, pivot, pk, false, &T);
+        PQ_T(c4);
+        PQ_ADD(0, c4 - c3);
+        continue;
+      }
+      const int mid = a + fused(a, b, pivot, pk, true, &T);
+      PQ_T(c5);
+      PQ_ADD(0, c5 - c3);
+      wasPartitioned = T == 0;
+      const int leftLen = mid - a, rightLen = b - mid, thr = length / 8;
+      if (leftLen < rightLen) {
+        if (k < mid) {  // recursion into the smaller left side
+          b = mid;
+          wasBalanced = wasPartitioned = true;
+        } else if (k > mid + 1) {
+          wasBalanced = leftLen >= thr;
+          a = mid + 1;
+        } else {
+          return;
+        }
+      } else {
+        if (k > mid + 1) {  // recursion into the smaller right side
+          a = mid + 1;
+          wasBalanced = wasPartitioned = true;
+        } else if (k < mid) {
+          wasBalanced = rightLen >= thr;
+          b = mid;
+        } else {
+          return;
+        }
+      }
+    }
+  }
+};
+
 __device__ __forceinline__ uint64_t okey(int64_t x) { return (uint64_t)x ^ 0x8000000000000000ull; }
 
 // Per-wave selection workspace (pointers into LDS or global scratch). The
@@ -790,6 +1147,30 @@ __device__ uint32_t select_topk(const SelWs& ws, int n, int64_t k, int64_t row_m
   }
   // ---- straddle: replay pdqsort on positions (input order) restricted to k,
   // keys permuted in place (tot is not read after the selection)
+  if (range < 65536u && n < 65536) {
+    // packed replay: (total - min) << 16 | position, written over tot in place (chunk c's words overlap
+    // totals 32c..32c+31, read by this or an earlier chunk)
+    uint32_t* e = reinterpret_cast<uint32_t*>(ws.tot);
+    for (int j0 = 0; j0 < n; j0 += WAVE) {
+      const int j = j0 + lane;
+      const uint32_t v = j < n ? ((uint32_t)(okey(ws.tot[j]) - umin) << 16) | (uint32_t)j : 0u;
+      wsync<GSCR>();
+      if (j < n) e[j] = v;
+    }
+    for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
+    wsync<GSCR>();
+    {
+      PdqWaveP<GSCR> pw{e, ws.posl, ws.posr, xs_b, xs_c};
+      pw.select(n, (int)k);
+    }
+    wsync<GSCR>();
+    for (int i = lane; i < k; i += WAVE) {
+      const int j = (int)(e[i] & 0xFFFFu);
+      atomicOr((unsigned long long*)&ws.sel[j >> 6], 1ull << (j & 63));
+    }
+    wsync<GSCR>();
+    return KAD_RF_TIE_STRADDLE;
+  }
   for (int j = lane; j < n; j += WAVE) ws.perm[j] = (uint16_t)j;
   for (int ch = lane; ch < nch; ch += WAVE) ws.sel[ch] = 0;
   wsync<GSCR>();

@@ -196,8 +196,9 @@ def code_of(res):
 
 
 # ------------------------------------------------------------------ table reader
-def read_table(src, func_name, env_funcs, var="tests", pre_env=None):
-    """Evaluate ``<var> := <composite>`` inside ``func_name`` → list of (line, case)."""
+def read_table(src, func_name, env_funcs, var="tests", pre_env=None, with_keys=False):
+    """Evaluate ``<var> := <composite>`` inside ``func_name`` → list of (line, case), or (line, key, case) with
+    ``with_keys`` (map tables keyed by the case name)."""
     body = find_func_body(src, func_name)
     ev = Evaluator(CONSTS, {**BASE_FUNCS, **env_funcs}, pre_env or {})
     p = Parser(body)
@@ -218,9 +219,11 @@ def read_table(src, func_name, env_funcs, var="tests", pre_env=None):
             if name == var:
                 elems = node[2]
                 cases = []
-                for (_, e), epos in zip(elems, node[3]):
+                for (k, e), epos in zip(elems, node[3]):
                     line = line_of(src, func_name, epos - body[0].pos + _body_off(body))
-                    cases.append((line, ev.eval(e, node[1][1] if node[1][0] == "slice" else None)))
+                    et = node[1][1] if node[1][0] == "slice" else (node[1][2] if node[1][0] == "map" else None)
+                    val = ev.eval(e, et)
+                    cases.append((line, ev.eval(k), val) if with_keys else (line, val))
                 break
             try:
                 ev.env[name] = ev.eval(node)
@@ -511,6 +514,175 @@ def extract_core():
     ]
 
 
+# ------------------------------------------------------------------ f2: SchedulingUnit from objects / policies
+def _go_json_tags():
+    """struct name → {Go field: json name} from the reference's API type files (read as text): the
+    fixtures carry objects and policies in the JSON an apiserver would hold."""
+    import re
+    tags = {}
+    for rel in ("pkg/apis/core/v1alpha1/types_propagationpolicy.go", "pkg/apis/core/v1alpha1/types_common.go",
+                "pkg/apis/types/v1alpha1/types_placements.go", "pkg/apis/core/v1alpha1/types_federatedtypeconfig.go"):
+        src = read(rel)
+        for m in re.finditer(r"^type\s+(\w+)\s+struct\s*\{(.*?)^\}", src, re.M | re.S):
+            fields = {}
+            for f in re.finditer(r"^\s*(\w+)\s+[^`\n]*`json:\"([^\"]*)\"", m.group(2), re.M):
+                fields[f.group(1)] = f.group(2).split(",")[0]
+            tags[m.group(1)] = fields
+    return tags
+
+
+_TAGS = None
+
+
+def to_k8s_json(v):
+    """Evaluated Go literal (goliteral dicts with __type__) → the object's JSON form: the reference's json tags
+    for its API types, Kubernetes' lowerCamel names for the k8s types (TypeMeta inline, ObjectMeta →
+    metadata). Fields the literal leaves out stay out."""
+    global _TAGS
+    if _TAGS is None:
+        _TAGS = _go_json_tags()
+    if isinstance(v, list):
+        return [to_k8s_json(x) for x in v]
+    if not isinstance(v, dict):
+        return v
+    if "__type__" not in v:
+        return {k: to_k8s_json(x) for k, x in v.items()}
+    tname = v["__type__"].split(".")[-1]
+    tags = _TAGS.get(tname, {})
+    out = {}
+    for k, x in v.items():
+        if k == "__type__":
+            continue
+        if k == "TypeMeta":
+            out.update(to_k8s_json(x))
+            continue
+        if k == "ObjectMeta":
+            out["metadata"] = to_k8s_json(x)
+            continue
+        name = tags.get(k) or ("apiVersion" if k == "APIVersion" else k[0].lower() + k[1:])
+        out[name] = to_k8s_json(x)
+    return out
+
+
+def go_plain(v):
+    """Evaluated Go literal with the __type__ markers dropped (framework.SchedulingUnit expectations keep their
+    Go field names; the test converts them)."""
+    if isinstance(v, list):
+        return [go_plain(x) for x in v]
+    if isinstance(v, dict):
+        return {k: go_plain(x) for k, x in v.items() if k != "__type__"}
+    return v
+
+
+def _scheduler_consts():
+    """The annotation / label constants of scheduler/constants.go and common/constants.go (read as text)."""
+    import re
+    common = read("pkg/controllers/common/constants.go")
+    prefix = re.search(r'DefaultPrefix\s*=\s*"([^"]*)"', common).group(1)
+    out = {"common.DefaultPrefix": prefix, "common.DeploymentKind": "Deployment"}
+    src = read(SCHED + "/constants.go")
+    for m in re.finditer(r'^\s*(\w+)\s*=\s*common\.DefaultPrefix\s*\+\s*"([^"]*)"', src, re.M):
+        out[m.group(1)] = prefix + m.group(2)
+    for m in re.finditer(r'^\s*(\w+)\s*=\s*"([^"]*)"', src, re.M):
+        out.setdefault(m.group(1), m.group(2))
+    out["DefaultSchedulingMode"] = "Duplicate"  # = fedcorev1a1.SchedulingModeDuplicate (constants.go:45)
+    return out
+
+
+def _tc_json(tc):
+    spec = (tc or {}).get("Spec") or {}
+    tt = spec.get("TargetType") or {}
+    pd = spec.get("PathDefinition") or {}
+    return {"group": tt.get("Group", ""), "version": tt.get("Version", ""), "kind": tt.get("Kind", ""),
+            "plural": tt.get("PluralName", ""), "scope": tt.get("Scope", ""), "replicas_spec": pd.get("ReplicasSpec", "")}
+
+
+F2_FUNCS = {
+    "fedtypesv1a1.SchemeGroupVersion.String": lambda: "types.kubeadmiral.io/v1alpha1",
+    "appsv1.SchemeGroupVersion.String": lambda: "apps/v1",
+    "pointer.Int32": lambda v: v,
+    "pointer.String": lambda v: v,
+    "pointer.Bool": lambda v: v,
+    "string": lambda v: v,
+}
+
+
+def _read_vars(src, func_name, funcs, consts):
+    """Every ``name := <literal>`` of a non-table test, evaluated in order."""
+    body = find_func_body(src, func_name)
+    ev = Evaluator({**CONSTS, **consts}, {**BASE_FUNCS, **funcs})
+    p = Parser(body)
+    expect = None
+    while p.peek().kind != "eof":
+        tok = p.peek()
+        if tok.kind == "ident" and p.peek(1).val == ":=":
+            name = tok.val
+            p.next()
+            p.next()
+            try:
+                node = p.parse_expr()
+                ev.env[name] = ev.eval(node)
+            except (KeyError, SyntaxError):
+                pass
+        elif tok.val == "gomega" and p.peek(1).val == "." and p.peek(2).val == "Equal" and p.peek(3).val == "(":
+            line = line_of(src, func_name, tok.pos - body[0].pos + _body_off(body))
+            for _ in range(4):
+                p.next()
+            expect = (line, ev.eval(p.parse_expr()))
+        else:
+            p.next()
+    return ev.env, expect
+
+
+def extract_schedulingunit():
+    """scheduler_test.go (TestGetSchedulingUnit, TestGetSchedulingUnitWithAnnotationOverrides,
+    TestSchedulingMode) and util_test.go (TestMatchedPolicyKey)."""
+    rel = SCHED + "/scheduler_test.go"
+    src = read(rel)
+    consts = _scheduler_consts()
+    out = []
+    # TestGetSchedulingUnit: the object is fedObj with the template set at spec.template
+    env, (eline, want) = _read_vars(src, "TestGetSchedulingUnit", F2_FUNCS, consts)
+    obj = to_k8s_json(env["fedObj"])
+    obj.setdefault("spec", {})["template"] = to_k8s_json(env["template"])
+    out.append({"source": f"{rel}:{eline}", "test": "TestGetSchedulingUnit", "name": "TestGetSchedulingUnit",
+                "type_config": _tc_json(env["typeConfig"]), "object": obj,
+                "policy": to_k8s_json(env["policy"]), "ignore": [], "want": go_plain(want)})
+    # TestGetSchedulingUnitWithAnnotationOverrides: an empty object with the annotations and an empty template
+    ev_consts = {**consts}
+    CONSTS.update(ev_consts)
+    for line, c in read_table(src, "TestGetSchedulingUnitWithAnnotationOverrides", F2_FUNCS):
+        obj = {"metadata": {"annotations": c.get("annotations")}, "spec": {"template": {}}}
+        out.append({"source": f"{rel}:{line}", "test": "TestGetSchedulingUnitWithAnnotationOverrides",
+                    "name": c["name"], "type_config": {"group": "", "version": "", "kind": "", "plural": "",
+                                                       "scope": "", "replicas_spec": "spec.replicas"},
+                    "object": obj, "policy": to_k8s_json(c["policy"]),
+                    # scheduler_test.go:420-431: the fields the test copies from the expectation before comparing
+                    "ignore": ["GroupVersion", "Kind", "Resource", "Name", "Namespace", "Labels", "Annotations",
+                               "DesiredReplicas", "CurrentClusters", "ResourceRequest", "AvoidDisruption"],
+                    "want": go_plain(c["expectedResult"])})
+    for line, name, c in read_table(src, "TestSchedulingMode", F2_FUNCS, with_keys=True):
+        gvk = c.get("gvk") or {}
+        out.append({"source": f"{rel}:{line}", "test": "TestSchedulingMode", "name": name,
+                    "type_config": {"group": gvk.get("Group", ""), "version": gvk.get("Version", ""),
+                                    "kind": gvk.get("Kind", ""), "plural": "", "scope": "",
+                                    "replicas_spec": c.get("replicasSpecPath", "")},
+                    "object": {"spec": {"template": {}}}, "policy": to_k8s_json(c["policy"]),
+                    "ignore": "all but SchedulingMode", "want": {"SchedulingMode": c["expectedResult"]}})
+    rel2 = SCHED + "/util_test.go"
+    src2 = read(rel2)
+    policy_cases = []
+    for line, name, c in read_table(src2, "TestMatchedPolicyKey", F2_FUNCS, var="testCases", with_keys=True):
+        policy_cases.append({"source": f"{rel2}:{line}", "name": name,
+                             "namespace": c.get("objectNamespace", ""), "pp": c.get("ppLabelValue"),
+                             "cpp": c.get("cppLabelValue"), "found": c.get("expectedPolicyFound", False),
+                             "policy_name": c.get("expectedPolicyName", ""),
+                             "policy_namespace": c.get("expectedPolicyNamespace", ""),
+                             "pp_label": consts["PropagationPolicyNameLabel"],
+                             "cpp_label": consts["ClusterPropagationPolicyNameLabel"]})
+    return out, policy_cases
+
+
 def main():
     outdir = HERE
     fixtures = {
@@ -521,6 +693,9 @@ def main():
         "profile.json": extract_profile(),
         "core.json": extract_core(),
     }
+    su_cases, policy_cases = extract_schedulingunit()
+    fixtures["schedulingunit.json"] = su_cases
+    fixtures["matched_policy.json"] = policy_cases
     wl, atp, plug = extract_rsp()
     fixtures["rsp_weight_limit.json"] = wl
     fixtures["rsp_available_to_percentage.json"] = atp

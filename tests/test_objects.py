@@ -1,11 +1,8 @@
 """Federated object ↔ SchedulingUnit, result application, trigger bytes (CPU).
 
-Known-answer cases transcribed from the reference's own tests:
-* ``pkg/controllers/scheduler/scheduler_test.go:37-163``  TestGetSchedulingUnit
-* ``scheduler_test.go:165-441``  TestGetSchedulingUnitWithAnnotationOverrides
-* ``scheduler_test.go:443-508``  TestSchedulingMode
-* ``pkg/controllers/scheduler/util_test.go:26-114``  TestMatchedPolicyKey
-plus edge cases read from ``schedulingunit.go`` / ``util.go`` /
+The reference's own test tables (scheduler_test.go TestGetSchedulingUnit*, TestSchedulingMode,
+util_test.go TestMatchedPolicyKey) run from extracted fixtures in ``tests/test_objects_golden.py``;
+this file holds edge cases read from ``schedulingunit.go`` / ``util.go`` /
 ``util/overrides.go`` (marked with the lines they follow), and the trigger
 JSON against the independent restatement in oracle/triggers.py.
 """
@@ -36,140 +33,6 @@ def _bare_obj(annotations=None):
     if annotations is not None:
         obj["metadata"] = {"annotations": annotations}
     return obj
-
-
-# ------------------------------------------------------------ scheduler_test.go:37-163
-def test_get_scheduling_unit():
-    fed = {
-        "apiVersion": "types.kubeadmiral.io/v1alpha1", "kind": "FederatedDeployment",
-        "metadata": {"name": "test", "namespace": "default"},
-        "spec": {
-            "placements": [{"controller": "test-controller", "placement": {
-                "clusters": [{"name": "cluster-1"}, {"name": "cluster-2"}, {"name": "cluster-3"}]}}],
-            "template": {
-                "apiVersion": "apps/v1", "kind": "Deployment",
-                "metadata": {"name": "test", "namespace": "default", "labels": {"foo": "bar"},
-                             "annotations": {"baz": "qux"}},
-                "spec": {"replicas": 10, "selector": {"matchLabels": {"name": "test"}},
-                         "template": {"metadata": {"labels": {"name": "test"}},
-                                      "spec": {"containers": [{"name": "main", "image": "nginx"}]}}},
-            },
-        },
-    }
-    pol = _policy(scheduling_mode=T.SCHEDULING_MODE_DUPLICATE,
-                  auto_migration=O.AutoMigration(keep_unschedulable_replicas=False),
-                  replica_rescheduling=O.ReplicaRescheduling(avoid_disruption=False))
-    su = O.scheduling_unit_for_fed_object(DEPLOY_FTC, fed, pol)
-    assert su == T.SchedulingUnit(
-        group="apps", version="v1", kind="Deployment", resource="deployments", namespace="default", name="test",
-        labels={"foo": "bar"}, annotations={"baz": "qux"}, resource_request=T.Resource(), current_clusters={},
-        auto_migration=T.AutoMigrationSpec(None, False), scheduling_mode=T.SCHEDULING_MODE_DUPLICATE,
-        sticky_cluster=False, avoid_disruption=False)
-
-
-# ------------------------------------------------------------ scheduler_test.go:165-441
-AFFINITY_JSON = """{
-    "clusterAffinity": {
-        "requiredDuringSchedulingIgnoredDuringExecution": {
-            "clusterSelectorTerms": [
-                {"matchExpressions": [{"key": "test", "operator": "In", "values": ["value1", "value2"]}]}
-            ]
-        }
-    }
-}"""
-PLACEMENTS_JSON = """[
-    {"cluster": "cluster1", "preferences": {"minReplicas": 5, "maxReplicas": 10, "weight": 2}},
-    {"cluster": "cluster2", "preferences": {"minReplicas": 2, "weight": 1}}
-]"""
-
-OVERRIDE_CASES = [
-    ("scheduling mode override",
-     dict(scheduling_mode=T.SCHEDULING_MODE_DIVIDE, cluster_selector={"label": "value1"}),
-     {O.SCHEDULING_MODE_ANNOTATION: "Duplicate"},
-     dict(scheduling_mode="Duplicate", cluster_selector={"label": "value1"})),
-    ("sticky cluster override",
-     dict(sticky_cluster=True, cluster_selector={"label": "value1"}),
-     {O.STICKY_CLUSTER_ANNOTATION: "false"},
-     dict(scheduling_mode="Duplicate", sticky_cluster=False, cluster_selector={"label": "value1"})),
-    ("Cluster selector override",
-     dict(sticky_cluster=True, cluster_selector={"label": "value1"}),
-     {O.CLUSTER_SELECTOR_ANNOTATIONS: '{"override": "label"}'},
-     dict(scheduling_mode="Duplicate", sticky_cluster=True, cluster_selector={"override": "label"})),
-    ("cluster affinity override",
-     dict(scheduling_mode="Duplicate", sticky_cluster=True, cluster_selector={"label": "value1"}),
-     {O.AFFINITY_ANNOTATIONS: AFFINITY_JSON},
-     dict(scheduling_mode="Duplicate", sticky_cluster=True, cluster_selector={"label": "value1"},
-          affinity=T.Affinity(T.ClusterAffinity(required=T.ClusterSelector([T.ClusterSelectorTerm(
-              [T.ClusterSelectorRequirement("test", "In", ["value1", "value2"])])]))))),
-    ("Tolerations override",
-     dict(sticky_cluster=True, cluster_selector={"label": "value1"},
-          tolerations=[T.Toleration("test", "Exists", "", "NoExecute")]),
-     {O.TOLERATIONS_ANNOTATIONS: '[{"key": "override", "operator": "Exists", "effect": "NoSchedule"}]'},
-     dict(scheduling_mode="Duplicate", sticky_cluster=True, cluster_selector={"label": "value1"},
-          tolerations=[T.Toleration("override", "Exists", "", "NoSchedule")])),
-    ("Max clusters override",
-     dict(cluster_selector={"label": "value1"}, max_clusters=5),
-     {O.MAX_CLUSTERS_ANNOTATIONS: "10"},
-     dict(scheduling_mode="Duplicate", cluster_selector={"label": "value1"}, max_clusters=10)),
-    ("Placements override",
-     dict(cluster_selector={"label": "value1"}, max_clusters=5, placements=[O.Placement("cluster1")]),
-     {O.PLACEMENTS_ANNOTATIONS: PLACEMENTS_JSON},
-     dict(scheduling_mode="Duplicate", cluster_selector={"label": "value1"}, max_clusters=5,
-          cluster_names={"cluster1", "cluster2"}, min_replicas={"cluster1": 5, "cluster2": 2},
-          max_replicas={"cluster1": 10}, weights={"cluster1": 2, "cluster2": 1})),
-]
-
-# the fields scheduler_test.go:406-417 resets before comparing
-_RESET = ("group", "version", "kind", "resource", "name", "namespace", "labels", "annotations", "desired_replicas",
-          "current_clusters", "resource_request", "avoid_disruption")
-
-
-def _compare_overrides(su, expected):
-    want = T.SchedulingUnit(**expected)
-    for f in _RESET:
-        setattr(su, f, getattr(want, f))
-    assert su == want
-
-
-@pytest.mark.parametrize("name,spec,ann,expected", OVERRIDE_CASES, ids=[c[0] for c in OVERRIDE_CASES])
-def test_annotation_overrides(name, spec, ann, expected):
-    ftc = O.FederatedTypeConfig(replicas_spec="spec.replicas")
-    _compare_overrides(O.scheduling_unit_for_fed_object(ftc, _bare_obj(ann), _policy(**spec)), expected)
-
-
-# ------------------------------------------------------------ scheduler_test.go:443-508
-@pytest.mark.parametrize("mode,path,gvk,want", [
-    ("Divide", "spec.replicas", ("apps", "v1", "Deployment"), "Divide"),
-    ("Duplicate", "spec.replicas", ("apps", "v1", "Deployment"), "Duplicate"),
-    ("Divide", "", ("apps", "v1", "StatefulSet"), "Duplicate"),
-])
-def test_scheduling_mode(mode, path, gvk, want):
-    ftc = O.FederatedTypeConfig(*gvk, replicas_spec=path)
-    su = O.scheduling_unit_for_fed_object(ftc, _bare_obj(), _policy(scheduling_mode=mode))
-    assert su.scheduling_mode == want
-
-
-# ------------------------------------------------------------ util_test.go:26-114
-@pytest.mark.parametrize("ns,pp,cpp,want", [
-    ("default", None, None, None),
-    ("", None, None, None),
-    ("default", "pp1", None, ("default", "pp1")),
-    ("default", None, "cpp1", ("", "cpp1")),
-    ("default", "pp1", "cpp1", ("default", "pp1")),
-    ("", "pp1", None, None),
-    ("", None, "cpp1", ("", "cpp1")),
-    ("", "pp1", "cpp1", ("", "cpp1")),
-])
-def test_matched_policy_key(ns, pp, cpp, want):
-    labels = {}
-    if pp is not None:
-        labels[O.PROPAGATION_POLICY_NAME_LABEL] = pp
-    if cpp is not None:
-        labels[O.CLUSTER_PROPAGATION_POLICY_NAME_LABEL] = cpp
-    obj = {"metadata": {"namespace": ns, "labels": labels}}
-    if not ns:
-        del obj["metadata"]["namespace"]
-    assert O.matched_policy_key(obj, ns != "") == want
 
 
 # ------------------------------------------------------------ edge cases read from schedulingunit.go
