@@ -537,7 +537,7 @@ def gather_placements(ctx, batch, res, dist, world, dev, blobs=None, fwk=None):
     # this rank's own part of the gathered arrays equals its download
     r = dist.get_rank()
     assert np.array_equal(g_st[r][:W].cpu().numpy(), res.status[:W]), "all-gathered placements differ"
-    assert np.array_equal(g_cl[r][:S].cpu().numpy(), res.cluster[:S]), "all-gathered placements differ"
+    assert np.array_equal(g_cl[r][:S].cpu().numpy(), res.cluster[:S]), "all-gathered placements differ"  # same buffer
     verified = None
     if r == 0 and blobs is not None:
         # every rank's gathered part equals a single-rank run of the same shard blob on rank 0
@@ -547,9 +547,17 @@ def gather_placements(ctx, batch, res, dist, world, dev, blobs=None, fwk=None):
             one = ctx.download()
             Wq, Sq = blobs[q].W, blobs[q].n_out_slots
             gs, gc, gr = g_st[q].cpu().numpy(), g_cl[q].cpu().numpy(), g_rp[q].cpu().numpy()
+            # the written slots of each unit: [out_off[w], out_off[w] + count[w]) (the rest of a unit's bound
+            # is never written, by either run)
+            cnt = one.count[:Wq].astype(np.int64)
+            valid = np.zeros(Sq, bool)
+            starts = np.asarray(blobs[q].out_off[:Wq], np.int64)
+            idx = np.repeat(starts, cnt) + (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+            valid[idx] = True
             for what, got, want in (("status", gs[:Wq], one.status[:Wq]), ("count", gs[Wm:Wm + Wq], one.count[:Wq]),
                                     ("flags", gs[2 * Wm:2 * Wm + Wq], one.flags[:Wq].view(np.int32)),
-                                    ("cluster", gc[:Sq], one.cluster[:Sq]), ("replicas", gr[:Sq], one.replicas[:Sq])):
+                                    ("cluster", gc[:Sq][valid], one.cluster[:Sq][valid]),
+                                    ("replicas", gr[:Sq][valid], one.replicas[:Sq][valid])):
                 assert np.array_equal(got, want), f"gathered {what} of rank {q} differs from a single-rank run"
         verified = f"all {world} ranks' status/count/flags/cluster/replicas == single-rank runs of their shards"
     nbytes = world * (12 * Wm + 12 * Sm)

@@ -23,6 +23,10 @@ class FakeContext:
     def upload_snapshot(self, snap):
         self.snap = snap
 
+    def upload_snapshot_blob(self, blob, snap=None):
+        import types
+        self.snap = types.SimpleNamespace(blob=np.ascontiguousarray(blob, np.uint8))
+
     def upload_batch(self, batch):
         self.batch = batch
 
@@ -111,3 +115,41 @@ def test_shard_sweep_projection(fake):
     p = out["per_n"]["2"]
     assert len(p["shard_ms"]) == 2 and p["units_per_rank"] == 1500
     assert p["projected_efficiency"] == pytest.approx(1.0 / (2 * p["max_ms"]))
+
+
+def _rank_worker(rank, world, port, outdir):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        runtime.Context = FakeContext
+        synth.SIZES["c2"] = (900, 256)
+        out = bench.bench_schedule(_args(gpus=world, backend="gloo", share_gpu=True, config="c2"), "c2", rank, world,
+                                   0, dist)
+        if rank == 0:
+            with open(os.path.join(outdir, "line.json"), "w") as f:
+                json.dump(out, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_gloo_line_and_gather_verification(tmp_path):
+    """bench.py's N > 1 path on CPU (gloo, world size 2): snapshot broadcast, shard send, the timed steps, the
+    placement all-gather and its check against single-rank runs of every shard, the max-over-ranks line."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from kubeadmiral_amd import build
+    build.build()
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.start_processes(_rank_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    line = json.loads((tmp_path / "line.json").read_text())
+    assert line["n_gpus"] == 2 and line["config"]["units_total"] == 900 and line["config"]["units_per_gpu"] == 450
+    assert line["allgather"]["backend"] == "gloo"
+    assert line["allgather"]["verified"] and "2 ranks" in line["allgather"]["verified"]

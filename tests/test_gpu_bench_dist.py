@@ -19,7 +19,8 @@ def test_bench_two_ranks_share_one_gpu():
            "--config", "c2", "--units", "20000", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-extra"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
-    assert p.returncode == 0, p.stderr[-3000:]
+    r0 = "\n".join(ln for ln in p.stderr.splitlines() if ln.startswith("[rank0]"))
+    assert p.returncode == 0, (r0 or p.stderr)[-4000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["config"]["rccl_world_size"] == 2
     assert line["config"]["units_total"] == 20000 and line["config"]["units_per_gpu"] == 10000
