@@ -373,6 +373,41 @@ int kad_plan_rows(kad_ctx* ctx, int n_rows, const int32_t* row_off, const uint32
  * kad_schedule (feasible: u8[W*C]; total: i64[W*C], meaningful where feasible). */
 int kad_debug_scores(kad_ctx* ctx, const kad_profile* profile, uint8_t* feasible, int64_t* total);
 
+/* ------------------------------------------------ result application (§8 f3)
+ * applySchedulingResult (pkg/controllers/scheduler/scheduler.go:632-695) writes a unit's result into its
+ * federated object: the scheduler controller's placement (util.SetPlacementClusterNames,
+ * util/placement.go:48-59 → SetPlacementNames, types/v1alpha1/extensions_placements.go:78-103) and its
+ * replicas overrides (UpdateReplicasOverride → OverrideUpdateNeeded, scheduler/util.go:71-94, 154-185).
+ * kad_result_diff decides on the device, where the results of the last kad_schedule are, which of the two
+ * would change for every unit, so the caller edits and re-serialises only those objects. The caller
+ * describes each object's CURRENT state with snapshot cluster positions (-1: a name not in the snapshot):
+ *   place_off[W+1] / place_cluster: the clusters of the FIRST placement whose controller is the scheduler
+ *     (any order, duplicates allowed); place_has[W] = 1 if that placement exists (DeletePlacement's
+ *     hasChange when the result is empty);
+ *   ovr_off[W+1] / ovr_cluster / ovr_value / ovr_kind: the scheduler controller's override patches whose
+ *     path is the replicas path (util.GetOverrides, one entry per patch); ovr_kind 0: the value decoded as
+ *     a JSON number (float64) and ovr_value = int64(value) (Go's truncating conversion); 1: any other type.
+ * out_flags[W]: KAD_DIFF_PLACEMENT and / or KAD_DIFF_OVERRIDES as the reference reports them
+ * (placementUpdated, overridesUpdated); KAD_DIFF_SKIP for units whose Schedule returned an error (nothing is
+ * applied, scheduler.go:505-517); KAD_DIFF_STICKY for sticky units (the result is su.CurrentClusters, which
+ * the caller holds and applies itself). The annotation half of applySchedulingResult (follower scheduling,
+ * unschedulable threshold) does not depend on the result and stays with the caller. Blocks until done.  */
+typedef struct kad_result_state {
+  int32_t n_units;              /* = the resident batch's n_units */
+  const int32_t* place_off;     /* [n_units + 1] */
+  const int32_t* place_cluster; /* [place_off[n_units]] */
+  const uint8_t* place_has;     /* [n_units] */
+  const int32_t* ovr_off;       /* [n_units + 1] */
+  const int32_t* ovr_cluster;   /* [ovr_off[n_units]] */
+  const int64_t* ovr_value;     /* [ovr_off[n_units]] */
+  const uint8_t* ovr_kind;      /* [ovr_off[n_units]] */
+} kad_result_state;
+#define KAD_DIFF_PLACEMENT 1u
+#define KAD_DIFF_OVERRIDES 2u
+#define KAD_DIFF_SKIP 4u
+#define KAD_DIFF_STICKY 8u
+int kad_result_diff(kad_ctx* ctx, const kad_result_state* state, uint32_t* out_flags);
+
 /* ------------------------------------------- scheduling-trigger hashes
  * Replaces the FNV-1 half of Scheduler.computeSchedulingTriggerHash
  * (pkg/controllers/scheduler/schedulingtriggers.go:106-147, called per object

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kad_sched.h"
@@ -65,6 +66,8 @@ struct kad_ctx {
   size_t scratch_bytes = 0;
   bool have_snapshot = false, have_batch = false, ran = false;
   int inject_fault = 0;  // kad_debug_inject_fault: 1 = the next refresh_derived fails (tests)
+  void* d_diff = nullptr;  // kad_result_diff: canonical object state + flags
+  size_t diff_cap = 0;
   // HIP event records around the stages (kad_set_timing); timed = the last
   // kad_schedule recorded them
   bool timing = false, timed = false;
@@ -352,7 +355,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
                   (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab, c->d_vrows,
-                  c->t_suffix, c->t_prefix, c->t_work, c->t_tabs})
+                  c->t_suffix, c->t_prefix, c->t_work, c->t_tabs, c->d_diff})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1093,6 +1096,109 @@ int kad_schedule_batch(kad_ctx* c, const kad_profile* p, const void* blob, size_
 }
 
 int kad_debug_phase_counters(uint64_t* out, int reset) { return kad::debug_phase_counters(out, reset); }
+
+// ------------------------------------------------ §8 f3: result application diff
+// per unit [lo, hi) of n on up to 16 host threads
+extern "C++" {
+template <class F>
+static void host_parallel(int n, F f) {
+  const int T = n < 4096 ? 1 : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (T <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++) th.emplace_back([=, &f] { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
+  for (auto& x : th) x.join();
+}
+
+}  // extern "C++"
+
+int kad_result_diff(kad_ctx* c, const kad_result_state* st, uint32_t* out) {
+  if (!c || !st || !out) return KAD_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ran || !c->have_batch) return fail(c, KAD_ESTATE, "no scheduled batch resident");
+  const int W = c->batch_hdr.n_units, C = c->sd.C;
+  if (st->n_units != W) return fail(c, KAD_EINVAL, "state n_units differs from the resident batch");
+  if (W == 0) return KAD_OK;
+  if (!st->place_off || !st->place_has || !st->ovr_off) return fail(c, KAD_EINVAL, "null state array");
+  auto csr_ok = [&](const int32_t* off) {
+    if (off[0] != 0) return false;
+    for (int w = 0; w < W; w++)
+      if (off[w + 1] < off[w]) return false;
+    return true;
+  };
+  if (!csr_ok(st->place_off) || !csr_ok(st->ovr_off)) return fail(c, KAD_EINVAL, "state offsets not monotone from 0");
+  const int64_t NP = st->place_off[W], NO = st->ovr_off[W];
+  if ((NP && !st->place_cluster) || (NO && (!st->ovr_cluster || !st->ovr_value || !st->ovr_kind)))
+    return fail(c, KAD_EINVAL, "null state array");
+  for (int64_t i = 0; i < NP; i++)
+    if (st->place_cluster[i] < -1 || st->place_cluster[i] >= C) return fail(c, KAD_EINVAL, "placement cluster out of range");
+  for (int64_t i = 0; i < NO; i++)
+    if (st->ovr_cluster[i] < -1 || st->ovr_cluster[i] >= C) return fail(c, KAD_EINVAL, "override cluster out of range");
+  // canonical placements: sorted unique snapshot positions; names outside the snapshot → uflag bit 1
+  std::vector<int32_t> cnt((size_t)W + 1, 0);
+  std::vector<uint8_t> uflag((size_t)W);
+  std::vector<int32_t> ids((size_t)NP);
+  host_parallel(W, [&](int lo, int hi) {
+    for (int w = lo; w < hi; w++) {
+      int32_t* b = ids.data() + st->place_off[w];
+      const int m = st->place_off[w + 1] - st->place_off[w];
+      std::copy(st->place_cluster + st->place_off[w], st->place_cluster + st->place_off[w + 1], b);
+      std::sort(b, b + m);
+      const int u = (int)(std::unique(b, b + m) - b);
+      const bool unknown = u > 0 && b[0] < 0;
+      cnt[(size_t)w + 1] = unknown ? u - 1 : u;
+      if (unknown) std::copy(b + 1, b + u, b);  // drop the -1
+      uflag[w] = (uint8_t)((st->place_has[w] ? 1 : 0) | (unknown ? 2 : 0));
+    }
+  });
+  std::vector<int32_t> pl_off((size_t)W + 1, 0);
+  for (int w = 0; w < W; w++) pl_off[(size_t)w + 1] = pl_off[w] + cnt[(size_t)w + 1];
+  std::vector<int32_t> pl_id((size_t)pl_off[W] + 1);
+  host_parallel(W, [&](int lo, int hi) {
+    for (int w = lo; w < hi; w++)
+      std::copy(ids.data() + st->place_off[w], ids.data() + st->place_off[w] + cnt[(size_t)w + 1], pl_id.data() + pl_off[w]);
+  });
+  // one device buffer: [pl_off | pl_id | ov_off | ov_id | ov_val | uflag | ov_kind | out], 256-B aligned parts
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t b_ploff = 0, b_plid = al(b_ploff + 4 * ((size_t)W + 1)), b_ovoff = al(b_plid + 4 * pl_id.size()),
+               b_ovid = al(b_ovoff + 4 * ((size_t)W + 1)), b_ovval = al(b_ovid + 4 * (size_t)(NO + 1)),
+               b_uf = al(b_ovval + 8 * (size_t)(NO + 1)), b_ovk = al(b_uf + (size_t)W), b_out = al(b_ovk + (size_t)NO + 1),
+               total = al(b_out + 4 * (size_t)W);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int r = grow(c, &c->d_diff, &c->diff_cap, total)) return r;
+  char* d = static_cast<char*>(c->d_diff);
+  auto up = [&](size_t off, const void* h, size_t n) {
+    return n ? hipMemcpyAsync(d + off, h, n, hipMemcpyHostToDevice, c->stream) : hipSuccess;
+  };
+  HIPCHK(c, up(b_ploff, pl_off.data(), 4 * ((size_t)W + 1)));
+  HIPCHK(c, up(b_plid, pl_id.data(), 4 * (size_t)pl_off[W]));
+  HIPCHK(c, up(b_ovoff, st->ovr_off, 4 * ((size_t)W + 1)));
+  HIPCHK(c, up(b_ovid, st->ovr_cluster, 4 * (size_t)NO));
+  HIPCHK(c, up(b_ovval, st->ovr_value, 8 * (size_t)NO));
+  HIPCHK(c, up(b_uf, uflag.data(), (size_t)W));
+  HIPCHK(c, up(b_ovk, st->ovr_kind, (size_t)NO));
+  ResultDiffDev dd{};
+  dd.W = W;
+  dd.status = c->d_status;
+  dd.count = c->d_count;
+  dd.cluster = c->d_cluster;
+  dd.replicas = c->d_replicas;
+  dd.out_off = c->bd.out_off;
+  dd.pl_off = reinterpret_cast<const int32_t*>(d + b_ploff);
+  dd.pl_id = reinterpret_cast<const int32_t*>(d + b_plid);
+  dd.uflag = reinterpret_cast<const uint8_t*>(d + b_uf);
+  dd.ov_off = reinterpret_cast<const int32_t*>(d + b_ovoff);
+  dd.ov_id = reinterpret_cast<const int32_t*>(d + b_ovid);
+  dd.ov_val = reinterpret_cast<const int64_t*>(d + b_ovval);
+  dd.ov_kind = reinterpret_cast<const uint8_t*>(d + b_ovk);
+  dd.out = reinterpret_cast<uint32_t*>(d + b_out);
+  HIPCHK(c, launch_result_diff(dd, c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, dd.out, 4 * (size_t)W, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's state arrays are free on return
+  return KAD_OK;
+}
 
 int kad_path_counts(kad_ctx* c, int32_t* out) {
   if (!c || !out) return KAD_EINVAL;

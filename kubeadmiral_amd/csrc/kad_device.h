@@ -228,4 +228,24 @@ struct DeltaDev {
 };
 hipError_t launch_snapshot_delta(const DeltaDev& d, hipStream_t st);
 
+// kad_result_diff (§8 f3): the last kad_schedule's outputs + the callers' current object state, canonical
+// (placement ids sorted and unique per unit, names outside the snapshot folded into uflag bit 1)
+struct ResultDiffDev {
+  int W;
+  const int32_t* status;
+  const int32_t* count;
+  const int32_t* cluster;
+  const int64_t* replicas;
+  const int64_t* out_off;  // [W + 1] (BatchDev::out_off)
+  const int32_t* pl_off;   // [W + 1]
+  const int32_t* pl_id;
+  const uint8_t* uflag;    // bit 0: the scheduler's placement exists, bit 1: it names a cluster outside the snapshot
+  const int32_t* ov_off;   // [W + 1]
+  const int32_t* ov_id;
+  const int64_t* ov_val;
+  const uint8_t* ov_kind;
+  uint32_t* out;           // [W] KAD_DIFF_*
+};
+hipError_t launch_result_diff(const ResultDiffDev& d, hipStream_t st);
+
 }  // namespace kad
