@@ -770,6 +770,60 @@ def update_replicas_override(type_config: FederatedTypeConfig, obj, result: Dict
     return False
 
 
+def result_state_of(type_config: FederatedTypeConfig, obj, index: Dict[str, int]):
+    """One object's current state for kad_result_diff (include/kad_sched.h kad_result_state): whether the
+    scheduler's placement exists and its clusters (the first placement of the controller, as
+    GetOrCreatePlacement / DeletePlacement find it, extensions_placements.go:38-76), and its replicas-path
+    override patches (util.GetOverrides, util/overrides.go:68-112) as (cluster position, int64(value), kind) —
+    kind 1 for a value that is not a JSON number. Positions come from ``index`` (snapshot cluster name →
+    position; -1 for other names). Raises ObjectError where applySchedulingResult would fail on the object."""
+    po = _unmarshal_placements(obj)
+    has, ids = False, []
+    for p in po.spec.placements or []:
+        if p.controller == PREFIXED_GLOBAL_SCHEDULER_NAME:
+            has = True
+            ids = [index.get(c.name, -1) for c in (p.placement.clusters or [])]
+            break
+    path = to_slash_path(type_config.replicas_spec)
+    ov = []
+    for cluster, patches in get_overrides(obj, PREFIXED_GLOBAL_SCHEDULER_NAME).items():
+        for p in patches or []:
+            if p.path != path:
+                continue
+            if isinstance(p.value, float):
+                ov.append((index.get(cluster, -1), f64_to_i64(p.value), 0))
+            else:
+                ov.append((index.get(cluster, -1), 0, 1))
+    return has, ids, ov
+
+
+def result_states(type_config: FederatedTypeConfig, objs, names: List[str]) -> dict:
+    """kad_result_state arrays for a batch of objects (their units in the same order); objects whose state
+    cannot be read (ObjectError) get an empty state and are listed under ``errors``."""
+    import numpy as np
+
+    index = {n: i for i, n in enumerate(names)}
+    has, p_off, p_id, o_off, o_id, o_val, o_kind, errors = [], [0], [], [0], [], [], [], []
+    for w, obj in enumerate(objs):
+        try:
+            h, ids, ov = result_state_of(type_config, obj, index)
+        except ObjectError:
+            h, ids, ov = False, [], []
+            errors.append(w)
+        has.append(1 if h else 0)
+        p_id += ids
+        p_off.append(len(p_id))
+        for cid, val, kind in ov:
+            o_id.append(cid)
+            o_val.append(val)
+            o_kind.append(kind)
+        o_off.append(len(o_id))
+    return {"place_off": np.asarray(p_off, np.int32), "place_cluster": np.asarray(p_id, np.int32),
+            "place_has": np.asarray(has, np.uint8), "ovr_off": np.asarray(o_off, np.int32),
+            "ovr_cluster": np.asarray(o_id, np.int32), "ovr_value": np.asarray(o_val, np.int64),
+            "ovr_kind": np.asarray(o_kind, np.uint8), "errors": errors}
+
+
 def apply_scheduling_result(type_config: FederatedTypeConfig, obj: dict, result: T.ScheduleResult,
                             enable_follower_scheduling: bool, unschedulable_threshold_ns: Optional[int]) -> bool:
     """applySchedulingResult (scheduler.go:632-695): mutates ``obj``; True if anything changed."""

@@ -40,6 +40,12 @@ class ResultView(ctypes.Structure):
                 ("cluster", ctypes.c_void_p), ("replicas", ctypes.c_void_p)]
 
 
+class ResultState(ctypes.Structure):  # kad_result_state
+    _fields_ = [("n_units", ctypes.c_int32), ("place_off", ctypes.c_void_p), ("place_cluster", ctypes.c_void_p),
+                ("place_has", ctypes.c_void_p), ("ovr_off", ctypes.c_void_p), ("ovr_cluster", ctypes.c_void_p),
+                ("ovr_value", ctypes.c_void_p), ("ovr_kind", ctypes.c_void_p)]
+
+
 _lib = None
 
 
@@ -80,6 +86,7 @@ def load_library(path: str = LIB_PATH):
     L.kad_results_copy_device.argtypes = [P, P]
     L.kad_stage_timing.argtypes = [P, P, I]
     L.kad_path_counts.argtypes = [P, P]
+    L.kad_result_diff.argtypes = [P, P, P]
     L.kad_schedule_batch.argtypes = [P, P, P, SZ, P]
     L.kad_select_rows.argtypes = [P, I, P, P, P, U32, P, P, P]
     L.kad_plan_rows.argtypes = [P, I, P, P, P, P, P, P, P, P, P, P, P, P]
@@ -178,6 +185,19 @@ class Context:
         ms = (ctypes.c_float * 7)()
         self._chk(self.L.kad_stage_timing(self.h, ms, 7))
         return {k: float(v) for k, v in zip(self.STAGES, ms)}
+
+    DIFF_PLACEMENT, DIFF_OVERRIDES, DIFF_SKIP, DIFF_STICKY = 1, 2, 4, 8
+
+    def result_diff(self, state: dict) -> np.ndarray:
+        """kad_result_diff: per unit of the last schedule(), which parts of applySchedulingResult would change
+        its object (KAD_DIFF_* flags). ``state``: objects.result_states(...) arrays."""
+        W = len(state["place_has"])
+        keep = {k: np.ascontiguousarray(v) for k, v in state.items() if isinstance(v, np.ndarray)}
+        st = ResultState(W, *(_p(keep[k]) for k in ("place_off", "place_cluster", "place_has", "ovr_off", "ovr_cluster",
+                                                    "ovr_value", "ovr_kind")))
+        out = np.zeros(max(1, W), np.uint32)
+        self._chk(self.L.kad_result_diff(self.h, ctypes.byref(st), _p(out)))
+        return out[:W]
 
     def path_counts(self) -> dict:
         """kad_path_counts: units per kernel path of the last schedule()."""

@@ -766,3 +766,54 @@ def gen_units_c5_columns(rng: np.random.Generator, W: int, cluster_names, n_keys
     cols["req_mem"] = rng.integers(0, 256 * GI, W, dtype=np.int64)
     cols.update(_tol_columns(rng, st, W, n_taints, 1, 8, allow_wild=True))
     return _fill_columns(W, st, cols)
+
+
+# ------------------------------------------------------- result application (§8 f3)
+def gen_result_objects(rng: np.random.Generator, W: int, names: List[str], replicas_path: str = "/spec/replicas"):
+    """W federated objects whose placements / overrides exercise every branch of applySchedulingResult's
+    result-dependent half: the scheduler's placement present or not (other controllers' placements beside
+    it, a second scheduler entry after the first), clusters from the snapshot, unknown names and duplicates,
+    an empty cluster list; replicas-path override patches with integral, fractional and non-numeric values,
+    other paths, other controllers, clusters outside the snapshot."""
+    from . import objects as O
+
+    sched = O.PREFIXED_GLOBAL_SCHEDULER_NAME
+    pool = list(names) + ["ghost-a", "ghost-b"]
+    out = []
+    for w in range(W):
+        r = rng.random
+        pls = []
+        if r() < 0.3:
+            pls.append({"controller": "other-controller", "placement": {"clusters": [{"name": pool[0]}]}})
+        if r() < 0.75:
+            k = int(rng.integers(0, 6))
+            cl = [{"name": pool[int(i)]} for i in rng.integers(0, len(pool) if r() < 0.3 else len(names), k)]
+            pls.append({"controller": sched, "placement": {"clusters": cl} if (cl or r() < 0.5) else {}})
+            if r() < 0.1:
+                pls.append({"controller": sched, "placement": {"clusters": [{"name": pool[1]}]}})
+        ovs = []
+        if r() < 0.6:
+            clusters = []
+            for c in sorted({pool[int(i)] for i in rng.integers(0, len(pool) if r() < 0.2 else len(names),
+                                                                 int(rng.integers(0, 6)))}):
+                paths = []
+                if r() < 0.2:
+                    paths.append({"path": "/spec/template/spec/containers/0/image", "value": "nginx"})
+                if r() < 0.85:
+                    v = r()
+                    val = float(rng.integers(0, 40)) if v < 0.8 else (float(rng.integers(0, 40)) + 0.5 if v < 0.9
+                                                                      else str(int(rng.integers(0, 40))))
+                    paths.append({"path": replicas_path, "value": val})
+                clusters.append({"clusterName": c, "paths": paths})
+            ovs.append({"controller": sched, "clusters": clusters})
+        if r() < 0.2:
+            ovs.append({"controller": "other-controller", "clusters": [{"clusterName": pool[0], "paths": [
+                {"path": replicas_path, "value": 7.0}]}]})
+        obj = {"apiVersion": "types.kubeadmiral.io/v1alpha1", "kind": "FederatedDeployment",
+               "metadata": {"name": f"obj-{w}", "namespace": "default"}, "spec": {"template": {}}}
+        if pls or r() < 0.5:
+            obj["spec"]["placements"] = pls
+        if ovs:
+            obj["spec"]["overrides"] = ovs
+        out.append(obj)
+    return out
