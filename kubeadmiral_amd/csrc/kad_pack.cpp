@@ -499,105 +499,211 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   };
 
   lap("reqs");
-  // ---- 2. interning in unit order (pack.py _Compiler.intern / tol_key), keys are views of stable words
-  std::unordered_map<sv, int32_t> req_id;
-  std::vector<sv> reqs;  // by batch-wide id: the words as bytes
-  std::deque<std::array<int32_t, 3>> extra_words;  // selector words (stable addresses)
-  auto words_sv = [](const int32_t* p, size_t n) { return sv(reinterpret_cast<const char*>(p), 4 * n); };
-  auto intern = [&](sv w) -> int32_t {
-    auto it = req_id.find(w);
-    if (it != req_id.end()) return it->second;
-    const int32_t id = (int32_t)reqs.size();
-    req_id.emplace(w, id);
-    reqs.push_back(w);
-    return id;
-  };
+  // ---- 2. interning in unit order (pack.py _Compiler.intern / tol_key), keys are views of stable words.
+  // Batch-wide ids are the order of first occurrence over the units. In parallel: every chunk of units
+  // interns into its own table (local ids in first-occurrence order within the chunk); the chunks' tables
+  // are then merged in chunk order (only their distinct keys, serially), which assigns exactly the ids one
+  // serial pass would; a last parallel pass rewrites the entries' local ids to batch-wide ones.
   static const int32_t kFalse[2] = {OP_FALSE, -1};
+  auto words_sv = [](const int32_t* p, size_t n) { return sv(reinterpret_cast<const char*>(p), 4 * n); };
   std::vector<int32_t> egid(R, -1), fgid(R, -1);
   std::vector<int32_t> sgid((size_t)n_sel_total);
-  std::unordered_map<int64_t, int32_t> eq_gid;
   std::vector<int32_t> tolset(W);
-  std::unordered_map<uint64_t, int32_t> tol_by_hash;
-  std::unordered_map<std::string, int32_t> tol_collide;  // exact fallback on a 64-bit hash collision
-  std::vector<int> tol_rows;  // first unit of each toleration set
+  // chunks write the entries' local ids in place: an entry two units share (the column format allows it)
+  // forces one chunk
+  bool shared = false;
+  std::vector<int32_t> owner(R, -1);  // the unit whose terms reference each requirement entry
   {
-    std::string key;
-    for (int w = 0; w < W; w++) {
-      // toleration list → set id
-      auto it = tol_by_hash.find(tol_hash[w]);
-      int32_t ts;
-      if (it == tol_by_hash.end()) {
-        ts = (int32_t)tol_rows.size();
-        tol_by_hash.emplace(tol_hash[w], ts);
-        tol_rows.push_back(w);
-      } else if (same_tols(tol_rows[it->second], w)) {
-        ts = it->second;
-      } else {
-        key.clear();
-        for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++)
-          for (const int32_t s2 : {su->tol_key[t], su->tol_op[t], su->tol_value[t], su->tol_effect[t]}) {
-            const sv x = S[s2];
-            const uint32_t n = (uint32_t)x.size();
-            key.append(reinterpret_cast<const char*>(&n), 4).append(x);
+    auto own = [&](int e0, int e1, int w) {
+      for (int e = e0; e < e1 && !shared; e++) {
+        if (owner[e] >= 0 && owner[e] != w) shared = true;
+        owner[e] = w;
+      }
+    };
+    for (int w = 0; w < W && !shared; w++) {
+      for (int t = su->rterm_off[w]; t < su->rterm_off[w + 1]; t++)
+        own(su->rt_req[t], su->rt_req[t] + su->rt_n_expr[t] + su->rt_n_field[t], w);
+      for (int t = su->pterm_off[w]; t < su->pterm_off[w + 1]; t++) own(su->pt_req[t], su->pt_req[t] + su->pt_n_expr[t], w);
+    }
+  }
+  const int NCH = shared ? 1 : std::max(1, std::min(threads, W));
+  lap("owners");
+  struct Chunk {
+    std::unordered_map<sv, int32_t> req_id;
+    std::vector<sv> reqs;                             // local id → words
+    std::deque<std::array<int32_t, 3>> extra_words;   // selector Equals words (stable addresses)
+    std::unordered_map<int64_t, int32_t> eq_gid;
+    std::unordered_map<uint64_t, std::vector<int32_t>> tol_by_hash;  // hash → local sets with that hash
+    std::vector<int> tol_rows;                        // local set → its first unit
+    std::vector<int32_t> req_map, tol_map;            // local → batch-wide id (merge)
+  };
+  std::vector<Chunk> chunks(NCH);
+  auto chunk_lo = [&](int c) { return (int)((int64_t)W * c / NCH); };
+  parallel_for(NCH, NCH, [&](int ca, int cb) {
+    for (int c = ca; c < cb; c++) {
+      Chunk& K = chunks[c];
+      auto intern = [&](sv w) -> int32_t {
+        auto it = K.req_id.find(w);
+        if (it != K.req_id.end()) return it->second;
+        const int32_t id = (int32_t)K.reqs.size();
+        K.req_id.emplace(w, id);
+        K.reqs.push_back(w);
+        return id;
+      };
+      for (int w = chunk_lo(c); w < chunk_lo(c + 1); w++) {
+        // toleration list → local set id (content identity: hash, confirmed against the set's first unit)
+        auto& cand = K.tol_by_hash[tol_hash[w]];
+        int32_t ts = -1;
+        for (int32_t x : cand)
+          if (same_tols(K.tol_rows[x], w)) {
+            ts = x;
+            break;
           }
-        auto jt = tol_collide.find(key);
-        if (jt == tol_collide.end()) {
-          ts = (int32_t)tol_rows.size();
-          tol_collide.emplace(key, ts);
-          tol_rows.push_back(w);
-        } else {
-          ts = jt->second;
+        if (ts < 0) {
+          ts = (int32_t)K.tol_rows.size();
+          K.tol_rows.push_back(w);
+          cand.push_back(ts);
         }
-      }
-      tolset[w] = ts;
-      // filter program: ClusterSelector entries, then required terms
-      for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) {
-        const int64_t code = sel_code[e];
-        if (code < 0) {
-          sgid[e] = intern(words_sv(kFalse, 2));
-          continue;
+        tolset[w] = ts;
+        // filter program: ClusterSelector entries, then required terms
+        for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) {
+          const int64_t code = sel_code[e];
+          if (code < 0) {
+            sgid[e] = intern(words_sv(kFalse, 2));
+            continue;
+          }
+          auto jt = K.eq_gid.find(code);
+          if (jt != K.eq_gid.end()) {
+            sgid[e] = jt->second;
+            continue;
+          }
+          K.extra_words.push_back({OP_EQ | (1 << 8), (int32_t)(code >> 32), (int32_t)(uint32_t)code});
+          sgid[e] = intern(words_sv(K.extra_words.back().data(), 3));
+          K.eq_gid.emplace(code, sgid[e]);
         }
-        auto jt = eq_gid.find(code);
-        if (jt != eq_gid.end()) {
-          sgid[e] = jt->second;
-          continue;
+        const uint32_t f = su->flags[w];
+        if ((f & KAD_SU_HAS_CLUSTER_AFFINITY) && (f & KAD_SU_HAS_REQUIRED)) {
+          for (int t = su->rterm_off[w]; t < su->rterm_off[w + 1]; t++) {
+            const int e0 = su->rt_req[t], e1 = e0 + su->rt_n_expr[t];
+            bool ok = true;
+            for (int e = e0; e < e1; e++) ok = ok && valid[e];
+            if (e1 > e0 && ok)
+              for (int e = e0; e < e1; e++)
+                if (egid[e] < 0) egid[e] = intern(words_sv(wbuf.data() + eoff[e], elen[e]));
+            const int g0 = e1, g1 = e1 + su->rt_n_field[t];
+            bool fok = true;
+            for (int e = g0; e < g1; e++) fok = fok && fvalid[e];
+            if (g1 > g0 && fok)
+              for (int e = g0; e < g1; e++)
+                if (fgid[e] < 0) fgid[e] = intern(words_sv(fw.data() + 2 * (size_t)e, 2));
+          }
         }
-        extra_words.push_back({OP_EQ | (1 << 8), (int32_t)(code >> 32), (int32_t)(uint32_t)code});
-        sgid[e] = intern(words_sv(extra_words.back().data(), 3));
-        eq_gid.emplace(code, sgid[e]);
-      }
-      const uint32_t f = su->flags[w];
-      if ((f & KAD_SU_HAS_CLUSTER_AFFINITY) && (f & KAD_SU_HAS_REQUIRED)) {
-        for (int t = su->rterm_off[w]; t < su->rterm_off[w + 1]; t++) {
-          const int e0 = su->rt_req[t], e1 = e0 + su->rt_n_expr[t];
-          bool ok = true;
-          for (int e = e0; e < e1; e++) ok = ok && valid[e];
-          if (e1 > e0 && ok)
+        // score program: preferred terms
+        if (f & KAD_SU_HAS_CLUSTER_AFFINITY) {
+          for (int t = su->pterm_off[w]; t < su->pterm_off[w + 1]; t++) {
+            if (su->pt_weight[t] == 0) continue;
+            const int e0 = su->pt_req[t], e1 = e0 + su->pt_n_expr[t];
+            if (e1 == e0) continue;
+            bool ok = true;
+            for (int e = e0; e < e1; e++) ok = ok && valid[e];
+            if (!ok) continue;
             for (int e = e0; e < e1; e++)
               if (egid[e] < 0) egid[e] = intern(words_sv(wbuf.data() + eoff[e], elen[e]));
-          const int g0 = e1, g1 = e1 + su->rt_n_field[t];
-          bool fok = true;
-          for (int e = g0; e < g1; e++) fok = fok && fvalid[e];
-          if (g1 > g0 && fok)
-            for (int e = g0; e < g1; e++)
-              if (fgid[e] < 0) fgid[e] = intern(words_sv(fw.data() + 2 * (size_t)e, 2));
-        }
-      }
-      // score program: preferred terms
-      if (f & KAD_SU_HAS_CLUSTER_AFFINITY) {
-        for (int t = su->pterm_off[w]; t < su->pterm_off[w + 1]; t++) {
-          if (su->pt_weight[t] == 0) continue;
-          const int e0 = su->pt_req[t], e1 = e0 + su->pt_n_expr[t];
-          if (e1 == e0) continue;
-          bool ok = true;
-          for (int e = e0; e < e1; e++) ok = ok && valid[e];
-          if (!ok) continue;
-          for (int e = e0; e < e1; e++)
-            if (egid[e] < 0) egid[e] = intern(words_sv(wbuf.data() + eoff[e], elen[e]));
+          }
         }
       }
     }
+  }, 1);
+  lap("intern-A");
+  // merge: batch-wide ids by first occurrence. The chunks' distinct keys, flattened in (chunk, local)
+  // order, are bucketed by hash into shards; each shard (in parallel) finds every key's first occurrence
+  // among equal keys; one serial pass over the flat order then numbers the first occurrences 0, 1, ...
+  // and gives every later occurrence its first's number — the ids of one serial pass over the units.
+  auto first_occurrence = [&](int n_items, auto hash_of, auto same, std::vector<int32_t>& gid) -> int {
+    std::vector<uint64_t> hs((size_t)n_items);
+    parallel_for(n_items, threads, [&](int a, int b) {
+      for (int g = a; g < b; g++) hs[g] = hash_of(g);
+    });
+    const int SH = std::max(1, std::min(4 * threads, 256));
+    std::vector<std::vector<int32_t>> shard(SH);
+    for (int g = 0; g < n_items; g++) shard[hs[g] % SH].push_back(g);
+    std::vector<int32_t> canon((size_t)n_items);
+    parallel_for(SH, threads, [&](int a, int b) {
+      for (int sh = a; sh < b; sh++) {
+        std::unordered_map<uint64_t, std::vector<int32_t>> seen;  // hash → first occurrences
+        for (int32_t g : shard[sh]) {
+          auto& cand = seen[hs[g]];
+          int32_t f = -1;
+          for (int32_t x : cand)
+            if (same(x, g)) {
+              f = x;
+              break;
+            }
+          if (f < 0) {
+            cand.push_back(g);
+            f = g;
+          }
+          canon[g] = f;
+        }
+      }
+    }, 1);
+    gid.resize((size_t)n_items);
+    int next = 0;
+    for (int g = 0; g < n_items; g++) gid[g] = canon[g] == g ? next++ : gid[canon[g]];
+    return next;
+  };
+  std::vector<int32_t> req_base((size_t)NCH + 1, 0), tol_base((size_t)NCH + 1, 0);
+  for (int c = 0; c < NCH; c++) {
+    req_base[c + 1] = req_base[c] + (int32_t)chunks[c].reqs.size();
+    tol_base[c + 1] = tol_base[c] + (int32_t)chunks[c].tol_rows.size();
   }
+  std::vector<int32_t> flat_chunk((size_t)std::max(req_base[NCH], tol_base[NCH]));
+  for (int c = 0; c < NCH; c++) {
+    for (int32_t g = req_base[c]; g < req_base[c + 1]; g++) flat_chunk[g] = c;
+  }
+  auto req_at = [&](int g) -> sv { const int c = flat_chunk[g]; return chunks[c].reqs[g - req_base[c]]; };
+  std::vector<int32_t> req_gid, tol_gid;
+  const int NR0 = first_occurrence(
+      req_base[NCH], [&](int g) { return (uint64_t)std::hash<sv>()(req_at(g)); },
+      [&](int x, int y) { return req_at(x) == req_at(y); }, req_gid);
+  std::vector<sv> reqs((size_t)NR0);  // by batch-wide id: the words as bytes (views into wbuf / fw / chunk words)
+  for (int g = 0; g < req_base[NCH]; g++) reqs[req_gid[g]] = req_at(g);
+  for (int c = 0; c < NCH; c++) {
+    for (int32_t g = tol_base[c]; g < tol_base[c + 1]; g++) flat_chunk[g] = c;
+  }
+  auto tol_unit = [&](int g) { const int c = flat_chunk[g]; return chunks[c].tol_rows[g - tol_base[c]]; };
+  const int NT0 = first_occurrence(
+      tol_base[NCH], [&](int g) { return tol_hash[tol_unit(g)]; },
+      [&](int x, int y) { return same_tols(tol_unit(x), tol_unit(y)); }, tol_gid);
+  std::vector<int> tol_rows((size_t)NT0);  // first unit of each toleration set
+  for (int g = tol_base[NCH] - 1; g >= 0; g--) tol_rows[tol_gid[g]] = tol_unit(g);  // the first occurrence wins
+  for (int c = 0; c < NCH; c++) {
+    Chunk& K = chunks[c];
+    K.req_map.assign(req_gid.begin() + req_base[c], req_gid.begin() + req_base[c + 1]);
+    K.tol_map.assign(tol_gid.begin() + tol_base[c], tol_gid.begin() + tol_base[c + 1]);
+  }
+  lap("merge");
+  // local → batch-wide ids: units (toleration sets, selector entries) per chunk, requirement entries by
+  // their owning unit's chunk
+  std::vector<int32_t> unit_chunk(W);
+  parallel_for(NCH, NCH, [&](int ca, int cb) {
+    for (int c = ca; c < cb; c++) {
+      const Chunk& K = chunks[c];
+      for (int w = chunk_lo(c); w < chunk_lo(c + 1); w++) {
+        unit_chunk[w] = c;
+        tolset[w] = K.tol_map[tolset[w]];
+        for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) sgid[e] = K.req_map[sgid[e]];
+      }
+    }
+  }, 1);
+  parallel_for(R, threads, [&](int a, int b) {
+    for (int e = a; e < b; e++) {
+      if (owner[e] < 0) continue;
+      const Chunk& K = chunks[unit_chunk[owner[e]]];
+      if (egid[e] >= 0) egid[e] = K.req_map[egid[e]];
+      if (fgid[e] >= 0) fgid[e] = K.req_map[fgid[e]];
+    }
+  });
   const int NR = (int)reqs.size();
   const int NT = std::max(1, (int)tol_rows.size());
   lap("intern");

@@ -215,3 +215,25 @@ def test_columnar_generators_blob_identical(cfg, W, C):
                for r in (t.match_expressions or [])}
         assert {"In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt", "Bogus"} <= ops
         assert any(t.match_fields for u in units for t in u.affinity.cluster_affinity.required.cluster_selector_terms)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_shared_requirement_entries(threads):
+    """Units whose terms reference the same requirement entries (the column format allows it): the parallel
+    interning falls back to one chunk and the blob still equals the Python packer's."""
+    clusters, units = synth.gen_fuzz(4321, W=60, C=20)
+    fwk = synth.fuzz_framework(1)
+    cols = CO.from_units(units)
+    c = cols.cols
+    # point every required term of the second half at the first term's entries of unit 0 (when it has one)
+    r0 = int(c["rterm_off"][0])
+    if int(c["rterm_off"][1]) > r0:
+        for w in range(30, 60):
+            for t in range(int(c["rterm_off"][w]), int(c["rterm_off"][w + 1])):
+                c["rt_req"][t] = c["rt_req"][r0]
+                c["rt_n_expr"][t] = c["rt_n_expr"][r0]
+                c["rt_n_field"][t] = c["rt_n_field"][r0]
+    snap = pack.Snapshot(clusters)
+    want = pack.Batch(snap, fwk, CO.to_units(cols))
+    got = CO.NativePacker(snap).pack(fwk, cols, threads=threads)
+    assert np.array_equal(got.blob, want.blob)
