@@ -127,11 +127,15 @@ int kad_packer_create(const kad_pack_vocab* vocab, kad_packer** out);
 int kad_packer_destroy(kad_packer* p);
 const char* kad_packer_error(kad_packer* p);
 /* Pack a batch for `profile` (output slot bounds depend on its filter / select plugins). The blob
- * stays inside the packer until kad_packer_take copies it out; *nbytes = its size. `threads` <= 0:
- * one per hardware thread (the per-unit passes run in parallel, the interning pass is serial). */
+ * stays inside the packer (page-locked host memory, reused by the next pack) until kad_packer_take
+ * copies it out; *nbytes = its size. `threads` <= 0: one per hardware thread (every pass runs in
+ * parallel; the interning's chunk merge is sharded by hash, its ids equal one serial pass's). */
 int kad_pack_batch(kad_packer* p, const kad_profile* profile, const kad_su_columns* su, int threads,
                    size_t* nbytes, kad_pack_stats* stats);
 int kad_packer_take(kad_packer* p, void* dst, size_t cap);
+/* The packed blob in place (no copy): valid until the next kad_pack_batch / kad_packer_take /
+ * kad_packer_destroy; hand it to kad_batch_upload directly (a DMA from page-locked memory). */
+int kad_packer_blob(kad_packer* p, const void** data, size_t* nbytes);
 
 #ifdef __cplusplus
 }

@@ -346,6 +346,20 @@ def _from_blob(blob: np.ndarray, fwk: Framework) -> "NativeBatch":
 NativeBatch.from_blob = staticmethod(_from_blob)
 
 
+def default_threads() -> int:
+    """Packer threads: the process's CPU share — OMP_NUM_THREADS when set (16 on the GPU boxes), else the CPU
+    count — at most 16 (beyond that the interning merge and memory bandwidth stop scaling)."""
+    import os
+
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    if n <= 0:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def vocab_of(snap, keep: list) -> KadPackVocab:
     """kad_pack_vocab of a pack.Snapshot (the arrays it points into are appended to ``keep``)."""
     gvks = sorted(snap.gvk_id, key=snap.gvk_id.get)
@@ -388,6 +402,7 @@ class NativePacker:
         L.kad_packer_error.restype = ctypes.c_char_p
         L.kad_pack_batch.argtypes = [P, P, P, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), P]
         L.kad_packer_take.argtypes = [P, P, ctypes.c_size_t]
+        L.kad_packer_blob.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
         self.snap = snap
         self._keep: list = []
         v = vocab_of(snap, self._keep)
@@ -408,7 +423,12 @@ class NativePacker:
         except Exception:
             pass
 
-    def pack(self, fwk: Framework, cols: SUColumns, threads: int = 0) -> NativeBatch:
+    def pack(self, fwk: Framework, cols: SUColumns, threads: int = 0, take: bool = True) -> NativeBatch:
+        """kad_pack_batch. ``threads`` 0: the process's CPU share (OMP_NUM_THREADS, else the CPU count, at most
+        16). ``take=False`` returns the blob in place (kad_packer_blob: page-locked, no copy), valid until this
+        packer's next pack."""
+        if threads <= 0:
+            threads = default_threads()
         su = KadSUColumns()
         su.n_units = cols.n_units
         su.str = KadStrs(len(cols.str_off) - 1, cols.str_off.ctypes.data, cols.str_data.ctypes.data)
@@ -425,9 +445,16 @@ class NativePacker:
                                    ctypes.byref(st))
         if rc != 0:
             raise RuntimeError(f"kad_pack_batch: {self.L.kad_packer_error(self.h).decode()}")
-        blob = np.empty(n.value, U8)
-        rc = self.L.kad_packer_take(self.h, blob.ctypes.data, blob.nbytes)
-        if rc != 0:
-            raise RuntimeError(f"kad_packer_take: {self.L.kad_packer_error(self.h).decode()}")
+        if take:
+            blob = np.empty(n.value, U8)
+            rc = self.L.kad_packer_take(self.h, blob.ctypes.data, blob.nbytes)
+            if rc != 0:
+                raise RuntimeError(f"kad_packer_take: {self.L.kad_packer_error(self.h).decode()}")
+        else:
+            ptr, nb = ctypes.c_void_p(), ctypes.c_size_t()
+            rc = self.L.kad_packer_blob(self.h, ctypes.byref(ptr), ctypes.byref(nb))
+            if rc != 0:
+                raise RuntimeError(f"kad_packer_blob: {self.L.kad_packer_error(self.h).decode()}")
+            blob = np.ctypeslib.as_array((ctypes.c_uint8 * nb.value).from_address(ptr.value))
         return NativeBatch(self.snap, fwk, blob, nr[:W].astype(np.int64), nt[:W].astype(np.int64),
                            int(st.n_distinct_reqs), int(st.n_tolsets))

@@ -30,6 +30,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/kad_pack.h"
 
 namespace {
@@ -157,9 +159,39 @@ struct kad_packer {
   Map name_id, scalar_id, label_key_id, gvk_id;
   std::vector<Map> label_vals;
   std::vector<std::string> taint_key, taint_value, taint_effect;
-  std::unique_ptr<uint8_t[]> out;  // the last packed blob (kad_packer_take)
-  size_t out_n = 0;
+  // the last packed blob (kad_packer_take / kad_packer_blob): page-locked host memory (one DMA to the GPU),
+  // kept across packs (grown when needed, so repeated packs touch no new pages)
+  uint8_t* out = nullptr;
+  size_t out_n = 0, out_cap = 0;
+  bool out_pinned = false;
   int take_threads = 1;
+
+  uint8_t* reserve(size_t n) {
+    if (n <= out_cap && out) return out;
+    release();
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) == hipSuccess && p) {
+      out_pinned = true;
+    } else {  // no HIP device here (CPU-only hosts, tests): ordinary memory
+      (void)hipGetLastError();
+      p = std::malloc(n);
+      out_pinned = false;
+    }
+    out = static_cast<uint8_t*>(p);
+    out_cap = out ? n : 0;
+    return out;
+  }
+  void release() {
+    if (out) {
+      if (out_pinned)
+        (void)hipHostFree(out);
+      else
+        std::free(out);
+    }
+    out = nullptr;
+    out_cap = 0;
+  }
+  ~kad_packer() { release(); }
 
   int fail(int code, const std::string& m) {
     err = m;
@@ -388,11 +420,18 @@ int kad_packer_take(kad_packer* p, void* dst, size_t cap) {
   parallel_for(pieces, p->take_threads, [&](int a, int b) {
     for (int i = a; i < b; i++) {
       const size_t o = (size_t)i * chunk;
-      std::memcpy(static_cast<uint8_t*>(dst) + o, p->out.get() + o, std::min(chunk, n - o));
+      std::memcpy(static_cast<uint8_t*>(dst) + o, p->out + o, std::min(chunk, n - o));
     }
   }, 1);
-  p->out.reset();
   p->out_n = 0;
+  return KAD_OK;
+}
+
+int kad_packer_blob(kad_packer* p, const void** data, size_t* nbytes) {
+  if (!p || !data || !nbytes) return KAD_EINVAL;
+  if (!p->out_n) return p->fail(KAD_ESTATE, "no packed blob");
+  *data = p->out;
+  *nbytes = p->out_n;
   return KAD_OK;
 }
 
@@ -888,9 +927,9 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   h.n_reqs = NR;
   h.total_bytes = total;
   h.snapshot_fingerprint = P->fingerprint;
-  P->out.reset(new uint8_t[total]);
+  uint8_t* base = P->reserve(total);
+  if (!base) return P->fail(KAD_ENOMEM, "cannot allocate the batch blob");
   P->out_n = total;
-  uint8_t* base = P->out.get();
   // every array is written in full below except the OR-filled toleration masks; zero those, the header
   // region and the alignment padding after each array (the blob must equal pack.py's byte for byte)
   std::memset(base, 0, h.off[0]);
@@ -901,28 +940,38 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
     std::memset(base + h.off[i] + used, 0, end - h.off[i] - used);
   }
   auto A = [&](int i) { return base + h.off[i]; };
-  auto put = [&](int i, const void* src, size_t n) {
-    if (n) std::memcpy(A(i), src, n);
-  };
-  put(KAD_B_FLAGS, flags.data(), 4 * (size_t)W);
-  put(KAD_B_GVK, gvk.data(), 4 * (size_t)W);
-  put(KAD_B_REQ_CPU, su->req_cpu, 8 * (size_t)W);
-  put(KAD_B_REQ_MEM, su->req_mem, 8 * (size_t)W);
-  put(KAD_B_DESIRED, desired.data(), 8 * (size_t)W);
-  put(KAD_B_MAX_CLUSTERS, maxc.data(), 8 * (size_t)W);
-  put(KAD_B_TOLSET, tolset.data(), 4 * (size_t)W);
-  put(KAD_B_SREQ_OFF, o_sreq.data(), 4 * ((size_t)W + 1));
-  put(KAD_B_FPROG_OFF, o_fp.data(), 4 * ((size_t)W + 1));
-  put(KAD_B_SPROG_OFF, o_sp.data(), 4 * ((size_t)W + 1));
-  put(KAD_B_PLACE_OFF, o_place.data(), 4 * ((size_t)W + 1));
-  put(KAD_B_CUR_OFF, o_cur.data(), 4 * ((size_t)W + 1));
-  put(KAD_B_PREF_OFF, o_pref.data(), 4 * ((size_t)W + 1));
-  put(KAD_B_KEY_OFF, o_key.data(), 4 * ((size_t)W + 1));
-  put(KAD_B_OUT_OFF, o_out.data(), 8 * ((size_t)W + 1));
-  put(KAD_B_REQ_OFF, req_off.data(), 4 * ((size_t)NR + 1));
+  {
+    // the per-unit arrays, copied in parallel pieces of <= 4 MiB
+    struct Put {
+      int i;
+      const void* src;
+      size_t n;
+    };
+    const Put puts[] = {{KAD_B_FLAGS, flags.data(), 4 * (size_t)W}, {KAD_B_GVK, gvk.data(), 4 * (size_t)W},
+                        {KAD_B_REQ_CPU, su->req_cpu, 8 * (size_t)W}, {KAD_B_REQ_MEM, su->req_mem, 8 * (size_t)W},
+                        {KAD_B_DESIRED, desired.data(), 8 * (size_t)W}, {KAD_B_MAX_CLUSTERS, maxc.data(), 8 * (size_t)W},
+                        {KAD_B_TOLSET, tolset.data(), 4 * (size_t)W},
+                        {KAD_B_SREQ_OFF, o_sreq.data(), 4 * ((size_t)W + 1)}, {KAD_B_FPROG_OFF, o_fp.data(), 4 * ((size_t)W + 1)},
+                        {KAD_B_SPROG_OFF, o_sp.data(), 4 * ((size_t)W + 1)}, {KAD_B_PLACE_OFF, o_place.data(), 4 * ((size_t)W + 1)},
+                        {KAD_B_CUR_OFF, o_cur.data(), 4 * ((size_t)W + 1)}, {KAD_B_PREF_OFF, o_pref.data(), 4 * ((size_t)W + 1)},
+                        {KAD_B_KEY_OFF, o_key.data(), 4 * ((size_t)W + 1)}, {KAD_B_OUT_OFF, o_out.data(), 8 * ((size_t)W + 1)},
+                        {KAD_B_REQ_OFF, req_off.data(), 4 * ((size_t)NR + 1)}};
+    constexpr size_t PIECE = 4u << 20;
+    std::vector<std::array<size_t, 3>> pieces;  // put, offset, length
+    for (size_t q = 0; q < sizeof(puts) / sizeof(puts[0]); q++)
+      for (size_t o = 0; o < puts[q].n; o += PIECE) pieces.push_back({q, o, std::min(PIECE, puts[q].n - o)});
+    parallel_for((int)pieces.size(), threads, [&](int a, int b) {
+      for (int x = a; x < b; x++) {
+        const Put& pu = puts[pieces[x][0]];
+        std::memcpy(A(pu.i) + pieces[x][1], static_cast<const uint8_t*>(pu.src) + pieces[x][1], pieces[x][2]);
+      }
+    }, 1);
+  }
   {
     int32_t* rq = reinterpret_cast<int32_t*>(A(KAD_B_REQ));
-    for (int r = 0; r < NR; r++) std::memcpy(rq + req_off[r], reqs[r].data(), reqs[r].size());
+    parallel_for(NR, threads, [&](int a, int b) {
+      for (int r = a; r < b; r++) std::memcpy(rq + req_off[r], reqs[r].data(), reqs[r].size());
+    });
   }
 
   lap("layout");
