@@ -94,6 +94,46 @@ class SUColumns:
     def n_reqs(self) -> int:
         return len(self.cols["rq_key"])
 
+    def slice(self, lo: int, hi: int) -> "SUColumns":
+        """Units [lo, hi) as their own columns (CSR offsets rebased; the requirement table cut to the range its
+        terms reference; the string table shared) — e.g. the chunks of a pipelined pack."""
+        c = self.cols
+        out = {}
+        for k in ("group", "version", "kind", "namespace_", "name", "flags", "desired", "max_clusters", "req_cpu",
+                  "req_mem", "req_eph"):
+            out[k] = c[k][lo:hi]
+
+        def cut(grp, fields):
+            off = c[grp + "_off"]
+            a, b = int(off[lo]), int(off[hi])
+            out[grp + "_off"] = (off[lo:hi + 1] - a).astype(I32)
+            for f in fields:
+                out[f] = c[f][a:b]
+
+        cut("scalar", ("scalar_name", "scalar_val"))
+        cut("tol", ("tol_key", "tol_op", "tol_value", "tol_effect"))
+        cut("sel", ("sel_key", "sel_value"))
+        cut("rterm", ("rt_req", "rt_n_expr", "rt_n_field"))
+        cut("pterm", ("pt_weight", "pt_req", "pt_n_expr"))
+        cut("place", ("place_name",))
+        cut("cur", ("cur_name", "cur_rep", "cur_has_rep"))
+        cut("wt", ("wt_name", "wt_val"))
+        cut("min", ("min_name", "min_val"))
+        cut("max", ("max_name", "max_val"))
+        cut("cap", ("cap_name", "cap_val"))
+        # requirement entries the range's terms reference: [r0, r1)
+        starts = np.concatenate([out["rt_req"], out["pt_req"]]).astype(np.int64)
+        ends = np.concatenate([out["rt_req"] + out["rt_n_expr"] + out["rt_n_field"],
+                               out["pt_req"] + out["pt_n_expr"]]).astype(np.int64)
+        r0, r1 = (int(starts.min()), int(ends.max())) if len(starts) else (0, 0)
+        out["rt_req"] = (out["rt_req"] - r0).astype(I32)
+        out["pt_req"] = (out["pt_req"] - r0).astype(I32)
+        vo = c["rq_val_off"]
+        out["rq_key"], out["rq_op"] = c["rq_key"][r0:r1], c["rq_op"][r0:r1]
+        out["rq_val_off"] = (vo[r0:r1 + 1] - vo[r0]).astype(I32)
+        out["rq_val"] = c["rq_val"][int(vo[r0]):int(vo[r1])]
+        return SUColumns(hi - lo, self.str_off, self.str_data, out)
+
     def strings(self) -> List[str]:
         b = self.str_data.tobytes()
         o = self.str_off

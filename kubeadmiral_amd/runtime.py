@@ -110,6 +110,7 @@ class Context:
     """A kad_ctx: one HIP device, one stream, resident snapshot + batch."""
 
     def __init__(self, device: int = 0):
+        self.device = device
         self.L = load_library()
         h = ctypes.c_void_p()
         rc = self.L.kad_ctx_create(device, ctypes.byref(h))

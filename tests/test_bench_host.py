@@ -17,6 +17,7 @@ class FakeContext:
     STAGES = runtime.Context.STAGES
 
     def __init__(self, device=0):
+        self.device = device
         self.snap = self.batch = None
         self.res = None
 
@@ -86,6 +87,8 @@ def test_line_contract_and_rooflines(fake):
     assert set(r["kernels"]) == {"req_mask", "prep", "main", "rows", "defer"}
     assert out["cpu_baseline"]["kind"] == "port" and out["cpu_baseline"]["cores"] >= 1
     assert out["config"]["paths"]["row_kernel"] == 5
+    e2e = out["end_to_end"]
+    assert e2e["pipelined"]["chunks"] == 4 and e2e["sequential"]["units"] == 3000
 
 
 def test_stale_pmc_is_not_used(fake, tmp_path, monkeypatch):

@@ -237,3 +237,22 @@ def test_shared_requirement_entries(threads):
     want = pack.Batch(snap, fwk, CO.to_units(cols))
     got = CO.NativePacker(snap).pack(fwk, cols, threads=threads)
     assert np.array_equal(got.blob, want.blob)
+
+
+@pytest.mark.parametrize("cfg,W,C", [("c3", 2000, 1000), ("c4", 900, 512), ("c5", 300, 1500)])
+def test_columns_slice_packs_like_its_units(cfg, W, C):
+    """SUColumns.slice (the pipelined pack's chunks): a chunk's blob equals the Python packer's blob of the
+    same units."""
+    import bench
+    clusters = bench.make_clusters(cfg, C) if cfg != "c5" else synth.gen_clusters(
+        np.random.default_rng(5), C, n_keys=64, n_vals=16, n_int_keys=4, n_taints=256, taints_per=(4, 16),
+        p_gvk=0.9, gvks=synth.GVKS)
+    cols = bench.make_columns(cfg, 0, W, clusters)
+    snap = pack.Snapshot(clusters)
+    fwk = synth.profile_for(cfg)
+    units = CO.to_units(cols)
+    for lo, hi in ((0, W // 3), (W // 3, W - 7), (W - 7, W)):
+        part = cols.slice(lo, hi)
+        got = CO.NativePacker(snap).pack(fwk, part)
+        want = pack.Batch(snap, fwk, units[lo:hi])
+        assert np.array_equal(got.blob, want.blob), (lo, hi)
