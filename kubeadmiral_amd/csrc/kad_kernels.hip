@@ -2157,8 +2157,12 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            // positions past P (the unit is then deferred) stay inside the wave's region (pid, posl)
-            idx[lane_on(mk[j]) ? n + mbcnt(mk[j]) : P + lane] = (uint16_t)((g + j) * WAVE + lane);
+            // positions past P (the unit is then deferred) stay inside the wave's region (pid, posl); the
+            // rank is computed by every lane (pinned in a VGPR) so the address is one v_cndmask, not an
+            // exec-mask branch
+            int r = n + mbcnt(mk[j]);
+            asm volatile("" : "+v"(r));
+            idx[lane_on(mk[j]) ? r : P + lane] = (uint16_t)((g + j) * WAVE + lane);
             n += popc64(mk[j]);
           }
         }
@@ -2283,8 +2287,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         int mn32, mx32;
         wave_minmax_u_i32(mn, mx, mn32, mx32);
         int lo32 = mn32, hi32 = mx32;
+        int gcount = -1, e = 0;  // #(total > T), #(total == T); -1: count them below
         if ((uint32_t)mx32 - (uint32_t)mn32 < 128u) {
-          // LDS histogram in descending bin order + one wave prefix sum: the k-th largest total
+          // LDS histogram in descending bin order + one wave prefix sum: the k-th largest total, and the
+          // counts above / at it from the same prefix (no per-position ballots)
           uint32_t* hist = key;
           *(uint2*)(hist + 2 * lane) = make_uint2(0u, 0u);
           wave_sync();
@@ -2299,8 +2305,12 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           const int pre = wave_incl_sum_i32((int)(hh.x + hh.y));
           const int l0 = (int)__builtin_ctzll(ballot(pre >= k));
           const int pl = __builtin_amdgcn_readlane(pre, l0);
+          const int h0 = __builtin_amdgcn_readlane((int)hh.x, l0);
           const int h1 = __builtin_amdgcn_readlane((int)hh.y, l0);
-          lo32 = mn32 + (pl - h1 >= k ? 127 - 2 * l0 : 126 - 2 * l0);
+          const bool first = pl - h1 >= k;  // T is the higher bin of lane l0's pair
+          lo32 = mn32 + (first ? 127 - 2 * l0 : 126 - 2 * l0);
+          e = first ? h0 : h1;
+          gcount = first ? pl - h1 - h0 : pl - h1;
           wave_sync();
         } else {
           while (lo32 < hi32) {  // the largest T with #(total >= T) >= k
@@ -2317,14 +2327,16 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           }
         }
         T = lo32;
-        int gcount = 0, e = 0;
+        if (gcount < 0) {
+          gcount = 0;
 #pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if (q < nq) {
-            const bool v = q * 64 + lane < n;
-            gcount += popc64(ballot(v && t[q] > T));
-            e += popc64(ballot(v && t[q] == T));
-          }
+          for (int q = 0; q < Q; ++q)
+            if (q < nq) {
+              const bool v = q * 64 + lane < n;
+              gcount += popc64(ballot(v && t[q] > T));
+              e += popc64(ballot(v && t[q] == T));
+            }
+        }
         need = k - gcount;
         if (need == e) {  // the cut takes every tie: no sort needed
           mode = 1;
@@ -2399,33 +2411,40 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         if ((dup || replicas) && mode >= 0) {
           int32_t* oc = ae->o.cluster + ooff;
           int64_t* orp = ae->o.replicas + ooff;
-          int eq_before = 0;  // mode 2: ties at T in earlier positions
-#pragma unroll
-          for (int q = 0; q < Q; ++q) {
-            if (q >= nq) continue;
-            const int p = q * 64 + lane;
-            const bool v = p < n;
-            bool s;
-            if (mode == 0) {
-              s = v;
-            } else if (mode == 1) {
-              s = v && t[q] >= T;
-            } else if (mode == 2) {
-              const uint64_t eqm = ballot(v && t[q] == T);
-              s = v && (t[q] > T || (t[q] == T && mbcnt(eqm) + eq_before < need));
-              eq_before += popc64(eqm);
-            } else {
-              s = v && inv[p] < k;
-            }
+          const int64_t rv = dup ? -1 : 0;
+          // the selection mode is uniform: one branch per unit, then a branch-free predicate per position
+          auto emit = [&](int q, bool s) {
             const uint64_t sel = ballot(s);
+            const uint32_t at = (uint32_t)(base + mbcnt(sel));
             if (s) {
-              const uint32_t at = (uint32_t)(base + mbcnt(sel));
               stg(oc, at, (int32_t)cid[q]);
-              stg(orp, at, (int64_t)(dup ? -1 : 0));
+              stg(orp, at, rv);
             }
             base += popc64(sel);
+          };
+          if (mode == 3) {  // the replay's ranks
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq) {
+                const int p = q * 64 + lane;
+                emit(q, p < n && inv[p] < k);
+              }
+          } else if (mode == 2) {  // every total > T, then the first `need` ties by position
+            int eq_before = 0;
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq) {
+                const bool v = q * 64 + lane < n;
+                const uint64_t eqm = ballot(v && t[q] == T);
+                emit(q, v && (t[q] > T || (t[q] == T && mbcnt(eqm) + eq_before < need)));
+                eq_before += popc64(eqm);
+              }
+          } else {  // 0: every position; 1: total >= T
+            const int Tlo = mode == 0 ? INT32_MIN : T;
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+              if (q < nq) emit(q, q * 64 + lane < n && t[q] >= Tlo);
           }
-          (void)eq_before;
         }
         if (lane == 0) {
           ae->o.status[w] = KAD_ST_OK;
