@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -139,6 +140,49 @@ static int to_dev(kad_ctx* c, const T* h, size_t n, T** d, std::vector<void*>& o
 // the blob, every CSR offset array to be monotone and to end inside its data
 // array, every id the kernels index with to be in range, and every predicate
 // program to be well formed — the kernels then read only inside the blob.
+// [lo, hi) pieces of n on up to 16 host threads
+template <class F>
+static void host_parallel(int n, F f) {
+  const int T = n < 4096 ? 1 : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (T <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++) th.emplace_back([=, &f] { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
+  for (auto& x : th) x.join();
+}
+// the smallest i in [0, n) with bad(i), or -1: pieces checked on up to 16 host threads, each
+// stopping at its first failure or once an earlier one is known — the same index, so the same
+// error, as one serial pass
+template <class F>
+static int64_t first_bad(int64_t n, F bad) {
+  if (n < 65536) {
+    for (int64_t i = 0; i < n; i++)
+      if (bad(i)) return i;
+    return -1;
+  }
+  std::atomic<int64_t> best{INT64_MAX};
+  const int T = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++)
+    th.emplace_back([&, t] {
+      const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+      for (int64_t i = lo; i < hi; i++) {
+        if ((i & 1023) == 0 && i > best.load(std::memory_order_relaxed)) return;
+        if (bad(i)) {
+          int64_t cur = best.load();
+          while (i < cur && !best.compare_exchange_weak(cur, i)) {
+          }
+          return;
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  const int64_t r = best.load();
+  return r == INT64_MAX ? -1 : r;
+}
+
 namespace {
 struct BatchCheck {
   kad_ctx* c;
@@ -161,8 +205,8 @@ struct BatchCheck {
     if (!extent(off_a, (uint64_t)n + 1, 4, what)) return false;
     const int32_t* o = arr<int32_t>(off_a);
     if (o[0] != 0) return fail(c, KAD_EINVAL, std::string(what) + " offsets must start at 0"), false;
-    for (int i = 0; i < n; i++)
-      if (o[i + 1] < o[i]) return fail(c, KAD_EINVAL, std::string(what) + " offsets must be non-decreasing"), false;
+    if (first_bad(n, [o](int64_t i) { return o[i + 1] < o[i]; }) >= 0)
+      return fail(c, KAD_EINVAL, std::string(what) + " offsets must be non-decreasing"), false;
     *total = o[n];
     return data_a < 0 || extent(data_a, (uint64_t)o[n], esz, what);
   }
@@ -170,13 +214,17 @@ struct BatchCheck {
   bool sorted_ids(int off_a, int ids_a, int n, int lo, int hi, bool unique, const char* what) {
     const int32_t* o = arr<int32_t>(off_a);
     const int32_t* v = arr<int32_t>(ids_a);
-    for (int w = 0; w < n; w++)
+    // 0 ok, 1 out of range, 2 not ascending: the first failing element of row w
+    auto row = [=](int64_t w) {
       for (int j = o[w]; j < o[w + 1]; j++) {
-        if (v[j] < lo || v[j] >= hi) return fail(c, KAD_EINVAL, std::string(what) + " id out of range"), false;
-        if (j > o[w] && (unique ? v[j] <= v[j - 1] : v[j] < v[j - 1]))
-          return fail(c, KAD_EINVAL, std::string(what) + " ids must be ascending"), false;
+        if (v[j] < lo || v[j] >= hi) return 1;
+        if (j > o[w] && (unique ? v[j] <= v[j - 1] : v[j] < v[j - 1])) return 2;
       }
-    return true;
+      return 0;
+    };
+    const int64_t w = first_bad(n, [&](int64_t w) { return row(w) != 0; });
+    if (w < 0) return true;
+    return fail(c, KAD_EINVAL, std::string(what) + (row(w) == 1 ? " id out of range" : " ids must be ascending")), false;
   }
 };
 }  // namespace
@@ -218,53 +266,59 @@ static int validate_batch(kad_ctx* c, const void* blob, size_t nbytes, const kad
   const int64_t* oo = k.arr<int64_t>(KAD_B_OUT_OFF);
   const int32_t* sid = k.arr<int32_t>(KAD_B_SREQ_ID);
   const int32_t* po = k.arr<int32_t>(KAD_B_PLACE_OFF);
-  for (int64_t j = 0; j < n_s; j++)
-    if (sid[j] < -1 || sid[j] >= sh.n_scalar) return fail(c, KAD_EINVAL, "scalar request id out of range");
+  if (first_bad(n_s, [&](int64_t j) { return sid[j] < -1 || sid[j] >= sh.n_scalar; }) >= 0)
+    return fail(c, KAD_EINVAL, "scalar request id out of range");
   // output slot ranges must hold every pair the kernels can write for the packed
   // profile: min(C, MaxClusters, |ClusterNames|) (pack.py Batch), 0 when sticky
   if (oo[0] != 0 || oo[W] != h.n_out_slots) return fail(c, KAD_EINVAL, "out_off must run from 0 to n_out_slots");
   const bool sel_max = h.packed_select_plugin == KAD_PL_MAX_CLUSTER;
   const bool place_on = h.packed_filter_mask & (1u << KAD_PL_PLACEMENT_FILTER);
-  for (int w = 0; w < W; w++) {
-    if (gv[w] < -1 || gv[w] >= 64 * sh.n_gvk_words) return fail(c, KAD_EINVAL, "gvk id out of range");
-    if (ts[w] < 0 || ts[w] >= NT) return fail(c, KAD_EINVAL, "toleration-set id out of range");
+  auto unit_err = [&](int64_t w) -> const char* {
+    if (gv[w] < -1 || gv[w] >= 64 * sh.n_gvk_words) return "gvk id out of range";
+    if (ts[w] < 0 || ts[w] >= NT) return "toleration-set id out of range";
     const int64_t len = oo[w + 1] - oo[w];
-    if (len < 0 || len > h.max_row_slots) return fail(c, KAD_EINVAL, "output slot range exceeds max_row_slots");
+    if (len < 0 || len > h.max_row_slots) return "output slot range exceeds max_row_slots";
     int64_t bound = C;
     if (sel_max && (fl[w] & KAD_W_HAS_MAX_CLUSTERS) && mc[w] >= 0 && mc[w] < bound) bound = mc[w];
     if (place_on && (fl[w] & KAD_W_HAS_PLACEMENT) && po[w + 1] - po[w] < bound) bound = po[w + 1] - po[w];
     if (fl[w] & KAD_W_STICKY) bound = 0;
-    if (len < bound) return fail(c, KAD_EINVAL, "output slot range smaller than the unit's selection bound");
-  }
+    if (len < bound) return "output slot range smaller than the unit's selection bound";
+    return nullptr;
+  };
+  if (const int64_t w = first_bad(W, [&](int64_t w) { return unit_err(w) != nullptr; }); w >= 0)
+    return fail(c, KAD_EINVAL, unit_err(w));
   if (h.max_row_slots < 0 || h.max_row_slots > (C > 0 ? C : 1)) return fail(c, KAD_EINVAL, "bad max_row_slots");
   // requirement table: [op | n << 8, key, payload...]
   const int32_t* ro = k.arr<int32_t>(KAD_B_REQ_OFF);
   const int32_t* rq = k.arr<int32_t>(KAD_B_REQ);
-  for (int r = 0; r < NR; r++) {
+  auto req_err = [&](int64_t r) -> const char* {
     const int len = ro[r + 1] - ro[r];
-    if (len < 2) return fail(c, KAD_EINVAL, "requirement shorter than two words");
+    if (len < 2) return "requirement shorter than two words";
     const int32_t* p = rq + ro[r];
     const int op = p[0] & 0xff, n = (int)((uint32_t)p[0] >> 8), key = p[1];
-    if (len != 2 + n) return fail(c, KAD_EINVAL, "requirement payload length mismatch");
+    if (len != 2 + n) return "requirement payload length mismatch";
     switch (op) {
       case KAD_OP_IN: case KAD_OP_NOTIN: case KAD_OP_EQ:
-        if (key < 0 || key >= sh.n_label_keys || n < 1) return fail(c, KAD_EINVAL, "bad label requirement");
+        if (key < 0 || key >= sh.n_label_keys || n < 1) return "bad label requirement";
         break;
       case KAD_OP_EXISTS: case KAD_OP_DNE:
-        if (key < 0 || key >= sh.n_label_keys || n != 0) return fail(c, KAD_EINVAL, "bad label requirement");
+        if (key < 0 || key >= sh.n_label_keys || n != 0) return "bad label requirement";
         break;
       case KAD_OP_GT: case KAD_OP_LT:
-        if (key < 0 || key >= sh.n_label_keys || n != 2) return fail(c, KAD_EINVAL, "bad Gt/Lt requirement");
+        if (key < 0 || key >= sh.n_label_keys || n != 2) return "bad Gt/Lt requirement";
         break;
       case KAD_OP_NAME_EQ: case KAD_OP_NAME_NE:
-        if (key < -1 || key >= C) return fail(c, KAD_EINVAL, "bad field requirement");
+        if (key < -1 || key >= C) return "bad field requirement";
         break;
       case KAD_OP_TRUE: case KAD_OP_FALSE:
         break;
       default:
-        return fail(c, KAD_EINVAL, "unknown requirement op");
+        return "unknown requirement op";
     }
-  }
+    return nullptr;
+  };
+  if (const int64_t r = first_bad(NR, [&](int64_t r) { return req_err(r) != nullptr; }); r >= 0)
+    return fail(c, KAD_EINVAL, req_err(r));
   // programs: every requirement id in range, structure consumes exactly the unit's words
   const int32_t* fo = k.arr<int32_t>(KAD_B_FPROG_OFF);
   const int32_t* fp = k.arr<int32_t>(KAD_B_FPROG);
@@ -276,7 +330,8 @@ static int validate_batch(kad_ctx* c, const void* blob, size_t nbytes, const kad
       if (p[at + i] < 0 || p[at + i] >= NR) return false;
     return true;
   };
-  for (int w = 0; w < W; w++) {
+  // 0 ok, 1 malformed filter program, 2 malformed score program
+  auto prog_err = [&](int64_t w) {
     const int32_t* p = fp + fo[w];
     const int len = fo[w + 1] - fo[w];
     bool ok = len >= 2;
@@ -299,7 +354,7 @@ static int validate_batch(kad_ctx* c, const void* blob, size_t nbytes, const kad
         }
       }
     }
-    if (!ok || pc != len) return fail(c, KAD_EINVAL, "malformed filter program of unit " + std::to_string(w));
+    if (!ok || pc != len) return 1;
     p = sp + spo[w];
     const int sl = spo[w + 1] - spo[w];
     ok = sl >= 1;
@@ -315,8 +370,12 @@ static int validate_batch(kad_ctx* c, const void* blob, size_t nbytes, const kad
         pc += 2 + (ok ? ne : 0);
       }
     }
-    if (!ok || pc != sl) return fail(c, KAD_EINVAL, "malformed score program of unit " + std::to_string(w));
-  }
+    if (!ok || pc != sl) return 2;
+    return 0;
+
+  };
+  if (const int64_t w = first_bad(W, [&](int64_t w) { return prog_err(w) != 0; }); w >= 0)
+    return fail(c, KAD_EINVAL, std::string(prog_err(w) == 1 ? "malformed filter program of unit " : "malformed score program of unit ") + std::to_string(w));
   return 0;
 }
 
@@ -1098,21 +1157,6 @@ int kad_schedule_batch(kad_ctx* c, const kad_profile* p, const void* blob, size_
 int kad_debug_phase_counters(uint64_t* out, int reset) { return kad::debug_phase_counters(out, reset); }
 
 // ------------------------------------------------ §8 f3: result application diff
-// per unit [lo, hi) of n on up to 16 host threads
-extern "C++" {
-template <class F>
-static void host_parallel(int n, F f) {
-  const int T = n < 4096 ? 1 : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-  if (T <= 1) {
-    f(0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (int t = 0; t < T; t++) th.emplace_back([=, &f] { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
-  for (auto& x : th) x.join();
-}
-
-}  // extern "C++"
 
 int kad_result_diff(kad_ctx* c, const kad_result_state* st, uint32_t* out) {
   if (!c || !st || !out) return KAD_EINVAL;

@@ -165,6 +165,16 @@ struct kad_packer {
   size_t out_n = 0, out_cap = 0;
   bool out_pinned = false;
   int take_threads = 1;
+  // per-pack scratch arrays, kept across packs: resizing a kept vector to the same size touches no new
+  // pages and initialises nothing (every array below is fully written, or explicitly filled, per pack)
+  struct Scratch {
+    std::vector<uint8_t> valid, fvalid, is_field;
+    std::vector<int64_t> eoff, sel_code, maxc, desired, out_len, o_out;
+    std::vector<int32_t> wbuf, elen, fw, egid, fgid, sgid, tolset, owner, unit_chunk, gvk, n_sreq, n_fp, n_sp,
+        n_place, n_cur, n_pref, n_key, nr, o_sreq, o_fp, o_sp, o_place, o_cur, o_pref, o_key, req_off;
+    std::vector<uint64_t> tol_hash;
+    std::vector<uint32_t> flags;
+  } sc;
 
   uint8_t* reserve(size_t n) {
     if (n <= out_cap && out) return out;
@@ -444,10 +454,6 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   if (W < 0) return P->fail(KAD_EINVAL, "n_units < 0");
   const Strs S{su->str.off, su->str.bytes, su->str.n};
   const int C = P->C, TW = P->TW;
-  if (int r = validate_columns(P, su, threads)) return r;
-  const bool select_max = prof->select_plugin == KAD_PL_MAX_CLUSTER;
-  const bool place_on = prof->filter_mask & (1u << KAD_PL_PLACEMENT_FILTER);
-  const int R = su->n_reqs;
   static const bool tm = getenv("KAD_PACK_TIMING") != nullptr;
   auto t_prev = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
@@ -456,13 +462,39 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
     fprintf(stderr, "[kad_pack] %-10s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
     t_prev = t;
   };
+  if (int r = validate_columns(P, su, threads)) return r;
+  lap("validate");
+  const bool select_max = prof->select_plugin == KAD_PL_MAX_CLUSTER;
+  const bool place_on = prof->filter_mask & (1u << KAD_PL_PLACEMENT_FILTER);
+  const int R = su->n_reqs;
 
   // ---- 1. requirement entries (parallel): validity, expression words into one flat buffer (a slot of
   // 2 + max(nv, 2) words per entry), field words only for entries a required term uses as a field
-  std::vector<uint8_t> valid(R), fvalid(R), is_field(R, 0);
-  std::vector<int64_t> eoff((size_t)R + 1, 0);
+  auto& X = P->sc;
+  // fill in parallel (kept scratch: no fresh pages)
+  auto pfill = [&](auto& v, auto x) {
+    parallel_for((int)std::min<size_t>(v.size(), INT32_MAX), threads, [&](int a, int b) {
+      std::fill(v.begin() + a, v.begin() + b, x);
+    }, 1 << 16);
+  };
+  auto& valid = X.valid;
+  auto& fvalid = X.fvalid;
+  auto& is_field = X.is_field;
+  auto& eoff = X.eoff;
+  valid.resize(R);
+  fvalid.resize(R);
+  is_field.resize(R);
+  pfill(is_field, (uint8_t)0);
+  eoff.resize((size_t)R + 1);
+  eoff[0] = 0;
   for (int r = 0; r < R; r++) eoff[r + 1] = eoff[r] + 2 + std::max(2, su->rq_val_off[r + 1] - su->rq_val_off[r]);
-  std::vector<int32_t> wbuf((size_t)eoff[R]), elen(R, 0), fw(2 * (size_t)R, 0);
+  auto& wbuf = X.wbuf;
+  auto& elen = X.elen;
+  auto& fw = X.fw;
+  wbuf.resize((size_t)eoff[R]);
+  elen.resize(R);
+  fw.resize(2 * (size_t)R);
+  lap("eoff");
   {
     const int nterms = W ? su->rterm_off[W] : 0;
     parallel_for(nterms, threads, [&](int a, int b) {
@@ -488,6 +520,7 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
       }
       for (int i = 0; ok && i < nv; i++) ok = is_valid_label_value(S[vals[i]]);
       valid[r] = ok;
+      elen[r] = 0;
       if (ok) {
         P->label_words(key, op, vals, nv, S, tmp);
         std::memcpy(wbuf.data() + eoff[r], tmp.data(), 4 * tmp.size());
@@ -501,9 +534,11 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
       }
     }
   });
+  lap("reqwords");
   // ClusterSelector entries (parallel): SelectorFromSet's Equals as (key id, value id), -1 = absent
   const int64_t n_sel_total = W ? su->sel_off[W] : 0;
-  std::vector<int64_t> sel_code((size_t)n_sel_total);
+  auto& sel_code = X.sel_code;
+  sel_code.resize((size_t)n_sel_total);
   parallel_for((int)n_sel_total, threads, [&](int a, int b) {
     for (int e = a; e < b; e++) {
       const int kid = kad_packer::find(P->label_key_id, S[su->sel_key[e]]);
@@ -512,8 +547,10 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
       sel_code[e] = (kid < 0 || vid < 0) ? -1 : (((int64_t)kid << 32) | (uint32_t)vid);
     }
   });
+  lap("selcodes");
   // toleration lists (parallel): a 64-bit content hash per unit, confirmed against the set's first unit
-  std::vector<uint64_t> tol_hash(W);
+  auto& tol_hash = X.tol_hash;
+  tol_hash.resize(W);
   parallel_for(W, threads, [&](int a, int b) {
     for (int w = a; w < b; w++) {
       uint64_t h = 1469598103934665603ull;
@@ -545,13 +582,22 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   // serial pass would; a last parallel pass rewrites the entries' local ids to batch-wide ones.
   static const int32_t kFalse[2] = {OP_FALSE, -1};
   auto words_sv = [](const int32_t* p, size_t n) { return sv(reinterpret_cast<const char*>(p), 4 * n); };
-  std::vector<int32_t> egid(R, -1), fgid(R, -1);
-  std::vector<int32_t> sgid((size_t)n_sel_total);
-  std::vector<int32_t> tolset(W);
+  auto& egid = X.egid;
+  auto& fgid = X.fgid;
+  auto& sgid = X.sgid;
+  auto& tolset = X.tolset;
+  egid.resize(R);
+  fgid.resize(R);
+  pfill(egid, (int32_t)-1);
+  pfill(fgid, (int32_t)-1);
+  sgid.resize((size_t)n_sel_total);
+  tolset.resize(W);
   // chunks write the entries' local ids in place: an entry two units share (the column format allows it)
   // forces one chunk
   bool shared = false;
-  std::vector<int32_t> owner(R, -1);  // the unit whose terms reference each requirement entry
+  auto& owner = X.owner;  // the unit whose terms reference each requirement entry
+  owner.resize(R);
+  pfill(owner, (int32_t)-1);
   {
     auto own = [&](int e0, int e1, int w) {
       for (int e = e0; e < e1 && !shared; e++) {
@@ -724,7 +770,8 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   lap("merge");
   // local → batch-wide ids: units (toleration sets, selector entries) per chunk, requirement entries by
   // their owning unit's chunk
-  std::vector<int32_t> unit_chunk(W);
+  auto& unit_chunk = X.unit_chunk;
+  unit_chunk.resize(W);
   parallel_for(NCH, NCH, [&](int ca, int cb) {
     for (int c = ca; c < cb; c++) {
       const Chunk& K = chunks[c];
@@ -748,9 +795,24 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   lap("intern");
 
   // ---- 3. per-unit columns and CSR row lengths
-  std::vector<uint32_t> flags(W);
-  std::vector<int32_t> gvk(W), n_sreq(W), n_fp(W), n_sp(W), n_place(W), n_cur(W), n_pref(W), n_key(W), nr(W);
-  std::vector<int64_t> maxc(W), desired(W), out_len(W);
+  auto& flags = X.flags;
+  auto& gvk = X.gvk;
+  auto& n_sreq = X.n_sreq;
+  auto& n_fp = X.n_fp;
+  auto& n_sp = X.n_sp;
+  auto& n_place = X.n_place;
+  auto& n_cur = X.n_cur;
+  auto& n_pref = X.n_pref;
+  auto& n_key = X.n_key;
+  auto& nr = X.nr;
+  auto& maxc = X.maxc;
+  auto& desired = X.desired;
+  auto& out_len = X.out_len;
+  for (auto* v : {&gvk, &n_sreq, &n_fp, &n_sp, &n_place, &n_cur, &n_pref, &n_key, &nr}) v->resize(W);
+  flags.resize(W);
+  maxc.resize(W);
+  desired.resize(W);
+  out_len.resize(W);
   // cluster names → snapshot ids, once per map / set entry
   auto resolve = [&](const int32_t* off, const int32_t* names, std::vector<int32_t>& ids) {
     const int n = W ? off[W] : 0;
@@ -766,6 +828,7 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   resolve(su->min_off, su->min_name, min_c);
   resolve(su->max_off, su->max_name, max_c);
   resolve(su->cap_off, su->cap_name, cap_c);
+  lap("resolve");
   parallel_for(W, threads, [&](int a, int b) {
     std::vector<int32_t> ids;
     std::string gkey;
@@ -875,7 +938,8 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
 
   // ---- layout (pack.py _assemble: header, then 256-B aligned arrays in enum order)
   auto csr_off = [&](const std::vector<int32_t>& len, std::vector<int32_t>& off) -> bool {
-    off.assign((size_t)W + 1, 0);
+    off.resize((size_t)W + 1);
+    off[0] = 0;
     int64_t acc = 0;
     for (int w = 0; w < W; w++) {
       acc += len[w];
@@ -884,17 +948,27 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
     }
     return true;
   };
-  std::vector<int32_t> o_sreq, o_fp, o_sp, o_place, o_cur, o_pref, o_key;
+  auto& o_sreq = X.o_sreq;
+  auto& o_fp = X.o_fp;
+  auto& o_sp = X.o_sp;
+  auto& o_place = X.o_place;
+  auto& o_cur = X.o_cur;
+  auto& o_pref = X.o_pref;
+  auto& o_key = X.o_key;
   if (!csr_off(n_sreq, o_sreq) || !csr_off(n_fp, o_fp) || !csr_off(n_sp, o_sp) || !csr_off(n_place, o_place) ||
       !csr_off(n_cur, o_cur) || !csr_off(n_pref, o_pref) || !csr_off(n_key, o_key))
     return P->fail(KAD_EINVAL, "CSR array exceeds 2^31 entries; split the batch");
-  std::vector<int64_t> o_out((size_t)W + 1, 0);
+  auto& o_out = X.o_out;
+  o_out.resize((size_t)W + 1);
+  o_out[0] = 0;
   int64_t max_row = 0;
   for (int w = 0; w < W; w++) {
     o_out[w + 1] = o_out[w] + out_len[w];
     max_row = std::max(max_row, out_len[w]);
   }
-  std::vector<int32_t> req_off((size_t)NR + 1, 0);
+  auto& req_off = X.req_off;
+  req_off.resize((size_t)NR + 1);
+  req_off[0] = 0;
   for (int r = 0; r < NR; r++) req_off[r + 1] = req_off[r] + (int32_t)(reqs[r].size() / 4);
   const size_t nS = (size_t)o_sreq[W], nF = (size_t)o_fp[W], nSP = (size_t)o_sp[W], nPL = (size_t)o_place[W],
                nC = (size_t)o_cur[W], nP = (size_t)o_pref[W], nK = (size_t)o_key[W], nRQ = (size_t)req_off[NR];
