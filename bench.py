@@ -335,7 +335,7 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, cpu_second
     if rank == 0:
         out = schedule_line(args, cfg, world, W_total, C, batch, snap, fwk, res, stage, ms, stats0, paths)
         out["allgather"] = allgather
-        if world == 1:
+        if world == 1 and not args.no_e2e:
             out["end_to_end"] = end_to_end(ctx, snap, fwk, stats0[0], res, C, packer_for=snap)
             if not args.no_cpu_baseline:
                 log(f"[rank 0] timing the CPU baseline (C restatement of the reference) on {cfg}")
@@ -706,6 +706,7 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="skip the embedded C2/C4/C5 lines of the default run")
     ap.add_argument("--extras", default="c2,c4,c5", help="configs embedded under `extra` in the default C3 run")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 shard-size sweep of the default run")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the pack -> upload -> schedule -> download timing")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse the multi-rank path with host-tensor transfers (e.g. ranks sharing one GPU)")
     ap.add_argument("--share-gpu", action="store_true", help="every rank uses device 0 (rehearsal on a 1-GPU box)")

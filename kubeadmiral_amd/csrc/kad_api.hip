@@ -142,8 +142,8 @@ static int to_dev(kad_ctx* c, const T* h, size_t n, T** d, std::vector<void*>& o
 // program to be well formed — the kernels then read only inside the blob.
 // [lo, hi) pieces of n on up to 16 host threads
 template <class F>
-static void host_parallel(int n, F f) {
-  const int T = n < 4096 ? 1 : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+static void host_parallel(int n, F f, int serial_below = 4096) {
+  const int T = n < serial_below ? 1 : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
   if (T <= 1) {
     f(0, n);
     return;
@@ -769,26 +769,57 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   // rows that need the replica planner: Divide mode, DesiredReplicas > 0, not sticky
   const uint32_t* fl = at<uint32_t>(blob, h.off, KAD_B_FLAGS);
   const int64_t* des = at<int64_t>(blob, h.off, KAD_B_DESIRED);
-  c->plan_rows.clear();
   uint32_t flags_or = 0;
-  // units the lean kernel would defer whatever the profile (prep_kernel's
+  // batch_defer: units the lean kernel would defer whatever the profile (prep_kernel's
   // REC_FULL reasons; wide affinity weights or negative requests can give
   // totals spanning >= 2^32)
-  bool defer = false;
   {
     const int32_t* gv = at<int32_t>(blob, h.off, KAD_B_GVK);
     const int32_t* so = at<int32_t>(blob, h.off, KAD_B_SREQ_OFF);
     const int64_t* rc = at<int64_t>(blob, h.off, KAD_B_REQ_CPU);
     const int64_t* rm = at<int64_t>(blob, h.off, KAD_B_REQ_MEM);
-    for (int w = 0; w < W && !defer; w++)
-      defer = gv[w] >= 64 || so[w] < so[w + 1] || rc[w] < 0 || rm[w] < 0 || rc[w] >= (1ll << 46) ||
-              rm[w] >= (1ll << 46) || (fl[w] & KAD_W_WIDE_SCORES);
+    c->batch_defer = first_bad(W, [&](int64_t w) {
+      return gv[w] >= 64 || so[w] < so[w + 1] || rc[w] < 0 || rm[w] < 0 || rc[w] >= (1ll << 46) ||
+             rm[w] >= (1ll << 46) || (fl[w] & KAD_W_WIDE_SCORES);
+    }) >= 0;
   }
-  c->batch_defer = defer;
-  for (int w = 0; w < W; w++) {
-    const uint32_t f = fl[w];
-    flags_or |= f;
-    if (!(f & KAD_W_DUPLICATE) && !(f & KAD_W_STICKY) && (f & KAD_W_HAS_DESIRED) && des[w] > 0) c->plan_rows.push_back(w);
+  {
+    // plan rows in unit order: per-piece counts, then each piece writes at its prefix
+    constexpr int PIECES = 16;
+    int64_t cnt[PIECES + 1] = {};
+    uint32_t ors[PIECES] = {};
+    auto plan = [&](int w) {
+      const uint32_t f = fl[w];
+      return !(f & KAD_W_DUPLICATE) && !(f & KAD_W_STICKY) && (f & KAD_W_HAS_DESIRED) && des[w] > 0;
+    };
+    auto pieces = [&](auto&& body) {
+      host_parallel(
+          PIECES,
+          [&](int a, int b) {
+            for (int q = a; q < b; q++) body(q, (int)((int64_t)W * q / PIECES), (int)((int64_t)W * (q + 1) / PIECES));
+          },
+          W < 65536 ? PIECES + 1 : 0);
+    };
+    pieces([&](int q, int lo, int hi) {
+      uint32_t o = 0;
+      int64_t n = 0;
+      for (int w = lo; w < hi; w++) {
+        o |= fl[w];
+        n += plan(w);
+      }
+      ors[q] = o;
+      cnt[q + 1] = n;
+    });
+    for (int q = 0; q < PIECES; q++) {
+      flags_or |= ors[q];
+      cnt[q + 1] += cnt[q];
+    }
+    c->plan_rows.resize((size_t)cnt[PIECES]);
+    pieces([&](int q, int lo, int hi) {
+      int32_t* o = c->plan_rows.data() + cnt[q];
+      for (int w = lo; w < hi; w++)
+        if (plan(w)) *o++ = w;
+    });
   }
   if (int r = grow(c, (void**)&c->d_plan_rows, &c->plan_rows_cap, c->plan_rows.size() * 4)) return r;
   if (!c->plan_rows.empty())
@@ -860,8 +891,10 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
     auto group = [&](int r) { return rq[ro[r] + 1]; };
     std::vector<uint8_t> rowr((size_t)NR);
     std::vector<int32_t> start((size_t)K + 2, 0);
+    host_parallel(NR, [&](int lo, int hi) {
+      for (int r = lo; r < hi; r++) rowr[r] = by_rows(r);
+    });
     for (int r = 0; r < NR; r++) {
-      rowr[r] = by_rows(r);
       if (rowr[r])
         n_rowreq++;
       else

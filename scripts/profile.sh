@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 cfg=${1:-c2}; tag=${2:-run}
 out=gpurun_out/prof_${cfg}_${tag}
 mkdir -p "$out"
-B="python bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-extra --no-sweep ${UNITS:+--units $UNITS}"
+B="python bench.py --config $cfg --steps 5 --warmup 1 --no-cpu-baseline --no-extra --no-sweep --no-e2e ${UNITS:+--units $UNITS}"
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$out/$name" -o "$name" -- $B > "$out/$name.log" 2>&1
