@@ -343,6 +343,11 @@ int kad_stage_timing(kad_ctx* ctx, float* ms, int n);
  * Measurement only (bench.py's per-kernel byte models). No reference counterpart. */
 int kad_path_counts(kad_ctx* ctx, int32_t* out);
 int kad_results_download(kad_ctx* ctx, const kad_result_view* out);
+/* Page-locked host memory for the download's (or a batch blob's) buffers, reused across batches: the
+ * copies then DMA straight into / out of it (no staging). kad_host_free(NULL) is a no-op. Caller-side
+ * plumbing, no reference counterpart. */
+int kad_host_alloc(size_t nbytes, void** out);
+int kad_host_free(void* p);
 /* The same results copied device-to-device into caller DEVICE buffers of the result view's sizes
  * (e.g. the send buffers of an RCCL all-gather of placements across GPUs); blocking. */
 int kad_results_copy_device(kad_ctx* ctx, const kad_result_view* dev_out);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -761,10 +762,21 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   if (h.snapshot_fingerprint != c->snap_hdr.fingerprint || h.n_clusters != c->snap_hdr.n_clusters ||
       h.n_taint_words != c->snap_hdr.n_taint_words)
     return fail(c, KAD_EINVAL, "batch was packed against a different snapshot");
+  // KAD_UPLOAD_TIMING: host-side laps of the upload on stderr (measurement only)
+  static const bool tm = getenv("KAD_UPLOAD_TIMING") != nullptr;
+  auto t_prev = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kad_upload] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
+    t_prev = t;
+  };
   if (int r = validate_batch(c, blob, nbytes, h)) return r;
+  lap("validate");
   HIPCHK(c, hipSetDevice(c->device));
   if (int r = grow(c, &c->d_batch, &c->batch_cap, nbytes)) return r;
   HIPCHK(c, hipMemcpyAsync(c->d_batch, blob, nbytes, hipMemcpyHostToDevice, c->stream));
+  lap("dma-issue");
   const int W = h.n_units;
   // rows that need the replica planner: Divide mode, DesiredReplicas > 0, not sticky
   const uint32_t* fl = at<uint32_t>(blob, h.off, KAD_B_FLAGS);
@@ -947,12 +959,14 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
     c->n_seg_reqs = NS;
   }
 
+  lap("segments");
   if (int r = grow(c, &c->d_rec, &c->rec_cap, (size_t)W * sizeof(UnitRec))) return r;
   if (int r = grow(c, &c->d_sw, &c->sw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_cw, &c->cw_cap, (size_t)W * nch * 8)) return r;
   if (int r = grow(c, &c->d_defer, &c->defer_cap, (2 * (size_t)W + 4) * 4)) return r;
   if (int r = grow(c, &c->d_wq, &c->wq_cap, (size_t)WQ_HEADS * WQ_STRIDE * 4)) return r;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  lap("sync");
   c->batch_hdr = h;
   const char* base = static_cast<const char*>(c->d_batch);
   BatchDev& b = c->bd;
@@ -1168,6 +1182,21 @@ int kad_results_copy_device(kad_ctx* c, const kad_result_view* dev_out) {
     HIPCHK(c, hipMemcpyAsync(dev_out->replicas, c->d_replicas, S * 8, hipMemcpyDeviceToDevice, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KAD_OK;
+}
+
+int kad_host_alloc(size_t nbytes, void** out) {
+  if (!out) return KAD_EINVAL;
+  *out = nullptr;
+  if (hipHostMalloc(out, nbytes ? nbytes : 1, hipHostMallocDefault) != hipSuccess) {
+    *out = nullptr;
+    return KAD_ENOMEM;
+  }
+  return KAD_OK;
+}
+
+int kad_host_free(void* p) {
+  if (p && hipHostFree(p) != hipSuccess) return KAD_EHIP;
   return KAD_OK;
 }
 

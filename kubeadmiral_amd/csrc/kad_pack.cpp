@@ -594,23 +594,25 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   tolset.resize(W);
   // chunks write the entries' local ids in place: an entry two units share (the column format allows it)
   // forces one chunk
-  bool shared = false;
+  // (parallel: a compare-and-swap claims each entry for its unit; a second, different unit marks it shared)
+  std::atomic<bool> shared{false};
   auto& owner = X.owner;  // the unit whose terms reference each requirement entry
   owner.resize(R);
   pfill(owner, (int32_t)-1);
-  {
+  parallel_for(W, threads, [&](int a, int b) {
     auto own = [&](int e0, int e1, int w) {
-      for (int e = e0; e < e1 && !shared; e++) {
-        if (owner[e] >= 0 && owner[e] != w) shared = true;
-        owner[e] = w;
+      for (int e = e0; e < e1; e++) {
+        int32_t prev = -1;
+        if (!__atomic_compare_exchange_n(&owner[e], &prev, w, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED) && prev != w)
+          shared.store(true, std::memory_order_relaxed);
       }
     };
-    for (int w = 0; w < W && !shared; w++) {
+    for (int w = a; w < b && !shared.load(std::memory_order_relaxed); w++) {
       for (int t = su->rterm_off[w]; t < su->rterm_off[w + 1]; t++)
         own(su->rt_req[t], su->rt_req[t] + su->rt_n_expr[t] + su->rt_n_field[t], w);
       for (int t = su->pterm_off[w]; t < su->pterm_off[w + 1]; t++) own(su->pt_req[t], su->pt_req[t] + su->pt_n_expr[t], w);
     }
-  }
+  });
   const int NCH = shared ? 1 : std::max(1, std::min(threads, W));
   lap("owners");
   struct Chunk {

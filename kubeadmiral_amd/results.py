@@ -28,6 +28,15 @@ class BatchResult:
         return BatchResult(np.zeros(W, np.int32), np.zeros(W, np.int32), np.zeros(W, np.uint32),
                            np.full(n, -1, np.int32), np.zeros(n, np.int64), batch.out_off)
 
+    @staticmethod
+    def pinned(W: int, n_slots: int) -> "BatchResult":
+        """Page-locked result arrays (kad_host_alloc) for Context.download(out=...): the D2H copies then DMA
+        straight into them. Reuse them across batches of at most W units / n_slots slots."""
+        from .runtime import host_array
+
+        return BatchResult(host_array(W, np.int32), host_array(W, np.int32), host_array(W, np.uint32),
+                           host_array(n_slots, np.int32), host_array(n_slots, np.int64), np.zeros(1, np.int64))
+
     def row(self, w: int):
         """(status, [(cluster_id, replicas), ...]) for unit w, ascending cluster id."""
         o = int(self.out_off[w])

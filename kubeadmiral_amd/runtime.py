@@ -98,8 +98,37 @@ def load_library(path: str = LIB_PATH):
     L.kad_trigger_timing.argtypes = [P, P]
     L.kad_trigger_download.argtypes = [P, P]
     L.kad_trigger_hashes.argtypes = [P, I, P, P, P, SZ, P]
+    L.kad_host_alloc.argtypes = [SZ, ctypes.POINTER(P)]
+    L.kad_host_free.argtypes = [P]
     _lib = L
     return L
+
+
+class _HostBlock:
+    """One kad_host_alloc block; freed when the last array viewing it goes away."""
+
+    def __init__(self, nbytes: int):
+        self.L = load_library()
+        p = ctypes.c_void_p()
+        rc = self.L.kad_host_alloc(nbytes, ctypes.byref(p))
+        if rc != 0 or not p.value:
+            raise KadError(rc, f"kad_host_alloc({nbytes}) failed")
+        self.p = p.value
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            self.L.kad_host_free(self.p)
+            self.p = None
+
+
+def host_array(n: int, dtype) -> np.ndarray:
+    """A page-locked numpy array of n elements (kad_host_alloc): D2H / H2D copies DMA straight into it."""
+    dt = np.dtype(dtype)
+    nbytes = max(1, n) * dt.itemsize
+    blk = _HostBlock(nbytes)
+    buf = (ctypes.c_uint8 * nbytes).from_address(blk.p)
+    buf._owner = blk  # the array's base chain keeps the block alive
+    return np.frombuffer(buf, dtype=dt, count=max(1, n))
 
 
 def _p(a: Optional[np.ndarray]):
@@ -212,8 +241,18 @@ class Context:
         v = ResultView(status_ptr, count_ptr, flags_ptr, cluster_ptr, replicas_ptr)
         self._chk(self.L.kad_results_copy_device(self.h, ctypes.byref(v)))
 
-    def download(self) -> BatchResult:
-        res = BatchResult.empty(self.batch)
+    def download(self, out: Optional[BatchResult] = None) -> BatchResult:
+        """kad_results_download into fresh arrays, or into ``out`` (e.g. page-locked arrays reused across
+        batches: BatchResult.pinned), which must be sized for the uploaded batch."""
+        if out is None:
+            res = BatchResult.empty(self.batch)
+        else:  # views of the batch's sizes
+            W, n = self.batch.W, max(1, self.batch.n_out_slots)
+            arrs = ((out.status, W), (out.count, W), (out.flags, W), (out.cluster, n), (out.replicas, n))
+            for a, m in arrs:
+                if len(a) < m or not a.flags.c_contiguous:
+                    raise ValueError("download buffers smaller than the uploaded batch")
+            res = BatchResult(*(a[:m] for a, m in arrs), self.batch.out_off)
         v = ResultView(res.status.ctypes.data, res.count.ctypes.data, res.flags.ctypes.data, res.cluster.ctypes.data,
                        res.replicas.ctypes.data)
         self._chk(self.L.kad_results_download(self.h, ctypes.byref(v)))

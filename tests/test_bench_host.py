@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import bench
-from kubeadmiral_amd import runtime, synth
+from kubeadmiral_amd import results, runtime, synth
 
 
 class FakeContext:
@@ -39,7 +39,14 @@ class FakeContext:
     def sync(self):
         pass
 
-    def download(self):
+    def download(self, out=None):
+        if out is not None:  # the caller's buffers, as kad_results_download fills them
+            W, n = len(self.res.status), len(self.res.cluster)
+            for a, b in ((out.status, self.res.status), (out.count, self.res.count), (out.flags, self.res.flags),
+                         (out.cluster, self.res.cluster), (out.replicas, self.res.replicas)):
+                a[:len(b)] = b
+            return type(self.res)(out.status[:W], out.count[:W], out.flags[:W], out.cluster[:n], out.replicas[:n],
+                                  self.res.out_off)
         return self.res
 
     def path_counts(self):
@@ -61,13 +68,18 @@ def fake(monkeypatch):
     from kubeadmiral_amd import build
     build.build()
     monkeypatch.setattr(runtime, "Context", FakeContext)
+    # pageable stand-ins for the page-locked result arrays (torch's pinned allocator needs a GPU)
+    monkeypatch.setattr(results.BatchResult, "pinned", staticmethod(
+        lambda W, n: results.BatchResult(np.zeros(max(1, W), np.int32), np.zeros(max(1, W), np.int32),
+                                         np.zeros(max(1, W), np.uint32), np.zeros(max(1, n), np.int32),
+                                         np.zeros(max(1, n), np.int64), np.zeros(1, np.int64))))
     monkeypatch.setitem(synth.SIZES, "c3", (3000, 1000))
     monkeypatch.setitem(synth.SIZES, "c2", (800, 256))
 
 
 def _args(**kw):
     a = dict(gpus=1, steps=2, warmup=1, config="c3", units=None, cpu_seconds=0.05, no_cpu_baseline=False,
-             no_extra=True, extras="c2", no_sweep=True, backend="nccl", share_gpu=False)
+             no_extra=True, extras="c2", no_sweep=True, no_e2e=False, backend="nccl", share_gpu=False)
     a.update(kw)
     return argparse.Namespace(**a)
 
