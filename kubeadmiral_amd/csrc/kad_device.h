@@ -178,11 +178,11 @@ size_t plan_wave_bytes(int K);
 int debug_phase_counters(uint64_t* out, int reset);
 
 // Tuning / measurement knobs read from the environment ONLY in profiling builds (-DKAD_PHASE_PROF,
-// scripts/phase_prof.py): the product library ignores the environment, so no variable set in a
+// scripts/phase_prof.py; -DKAD_TUNING, scripts/wide_exp.py): the product library ignores the environment, so no variable set in a
 // controller process can switch it off the reference-exact path (KAD_WIDE_EXPERIMENT, for one,
 // skips the pdqsort replay). Product builds always return the default.
 inline int tuning_env(const char* name, int dflt) {
-#ifdef KAD_PHASE_PROF
+#if defined(KAD_PHASE_PROF) || defined(KAD_TUNING)
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 #else

@@ -1932,13 +1932,20 @@ struct WideArgs {
   ProfDev p;
   int waves_per_block;
   int cache_ne, cache_pn;
-  int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default): bit 0 skips the
-            // pdqsort replay (ties taken by position; results differ from the reference)
+  int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default; results differ from
+            // the reference): bit 0 skips the pdqsort replay (ties taken by position), bit 1 ends each unit
+            // after the filters, bit 2 after the scores (no selection), bit 3 skips the output pass
 };
 typedef const __attribute__((address_space(4))) WideArgs* WArgs;
 __device__ __forceinline__ WArgs wargs() {
   return (WArgs)opq((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
 }
+// experiment bits: compiled out of product builds
+#if defined(KAD_PHASE_PROF) || defined(KAD_TUNING)
+#define WIDE_EXP(bits) ((wargs()->exp & (bits)) != 0)
+#else
+#define WIDE_EXP(bits) false
+#endif
 
 __device__ __forceinline__ void wide_status(int w, int32_t st) {
   if (lane_id() == 0) {
@@ -2189,6 +2196,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         wide_status(w, KAD_ST_ERR_SCORE);
         break;
       }
+      if (WIDE_EXP(2)) {
+        wide_status(w, KAD_ST_OK);
+        break;
+      }
       wave_sync();
 
       // ---------------- scores of positions 64q + lane (RunScorePlugins, framework.go:139-181)
@@ -2264,7 +2275,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       // ---------------- select (framework.go:183-209, max_cluster.go:42-66)
       WArgs ad = wargs();
       int k = n;
-      if (ad->p.select_plugin == KAD_PL_MAX_CLUSTER) {
+      if (ad->p.select_plugin == KAD_PL_MAX_CLUSTER && !WIDE_EXP(4)) {
         const bool hm = fc & KAD_W_HAS_MAX_CLUSTERS;
         if (hm && mc < 0) {
           wide_status(w, KAD_ST_ERR_SELECT);
@@ -2342,7 +2353,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           mode = 1;
         } else {
           rflags = KAD_RF_TIE_STRADDLE;
-          if (n <= 12 || (ad->exp & 1)) {  // pdqsort_func: a single (stable) insertionSort
+          if (n <= 12 || WIDE_EXP(1)) {  // pdqsort_func: a single (stable) insertionSort
             mode = 2;
           } else {
             // restricted pdqsort replay, wave-parallel, on u32 keys total - min (order-preserving)
@@ -2408,7 +2419,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         const bool replicas =
             !dup && ae->p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (fc & REC_DESIRED_POS) && k > 0;
         int base = 0;
-        if ((dup || replicas) && mode >= 0) {
+        if ((dup || replicas) && mode >= 0 && !WIDE_EXP(8)) {
           int32_t* oc = ae->o.cluster + ooff;
           int64_t* orp = ae->o.replicas + ooff;
           const int64_t rv = dup ? -1 : 0;

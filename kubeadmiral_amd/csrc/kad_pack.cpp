@@ -147,6 +147,85 @@ struct WordsHash {
 
 size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
+// Open-addressing index of (hash, id) slots: no allocation per entry, reset by one fill and kept across
+// packs. On a hash match the caller's predicate compares contents, so distinct keys with equal hashes
+// coexist (each content is inserted once; a probe finds only its equal).
+struct FlatIndex {
+  std::vector<uint64_t> hs;
+  std::vector<int32_t> ids;
+  size_t mask = 0, n = 0;
+  static uint64_t mix(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    return h;
+  }
+  void reset(size_t expect = 32) {
+    size_t cap = 64;
+    while (cap < 2 * expect) cap <<= 1;
+    if (ids.size() < cap) {
+      hs.assign(cap, 0);
+      ids.assign(cap, -1);
+    } else {
+      std::fill(ids.begin(), ids.end(), -1);
+    }
+    mask = ids.size() - 1;
+    n = 0;
+  }
+  // the id of the entry equal to the probe (same(id) on a hash match), else adds make_id()'s
+  template <class Same, class Make>
+  int32_t find_or_add(uint64_t h, Same same, Make make_id) {
+    if (2 * (n + 1) > ids.size()) grow();
+    size_t i = mix(h) & mask;
+    for (; ids[i] >= 0; i = (i + 1) & mask)
+      if (hs[i] == h && same(ids[i])) return ids[i];
+    const int32_t id = make_id();
+    hs[i] = h;
+    ids[i] = id;
+    n++;
+    return id;
+  }
+  void grow() {
+    std::vector<uint64_t> oh;
+    std::vector<int32_t> oi;
+    oh.swap(hs);
+    oi.swap(ids);
+    const size_t cap = std::max<size_t>(64, 2 * oi.size());
+    hs.assign(cap, 0);
+    ids.assign(cap, -1);
+    mask = cap - 1;
+    for (size_t j = 0; j < oi.size(); j++)
+      if (oi[j] >= 0) {
+        size_t i = mix(oh[j]) & mask;
+        while (ids[i] >= 0) i = (i + 1) & mask;
+        hs[i] = oh[j];
+        ids[i] = oi[j];
+      }
+  }
+};
+
+// one chunk of units' interning state (kad_pack_batch step 2), kept across packs
+struct InternChunk {
+  FlatIndex req_ix;
+  std::vector<sv> reqs;                            // local id → words
+  std::deque<std::array<int32_t, 3>> extra_words;  // selector Equals words (stable addresses)
+  FlatIndex eq_ix;
+  std::vector<int64_t> eq_code;                    // selector entry → its (key, value) code
+  std::vector<int32_t> eq_req;                     //   and its local requirement id
+  FlatIndex tol_ix;
+  std::vector<int> tol_rows;                       // local set → its first unit
+  void reset() {
+    req_ix.reset();
+    reqs.clear();
+    extra_words.clear();
+    eq_ix.reset();
+    eq_code.clear();
+    eq_req.clear();
+    tol_ix.reset();
+    tol_rows.clear();
+  }
+};
+
 }  // namespace
 
 struct kad_packer {
@@ -172,8 +251,14 @@ struct kad_packer {
     std::vector<int64_t> eoff, sel_code, maxc, desired, out_len, o_out;
     std::vector<int32_t> wbuf, elen, fw, egid, fgid, sgid, tolset, owner, unit_chunk, gvk, n_sreq, n_fp, n_sp,
         n_place, n_cur, n_pref, n_key, nr, o_sreq, o_fp, o_sp, o_place, o_cur, o_pref, o_key, req_off;
-    std::vector<uint64_t> tol_hash;
+    std::vector<uint64_t> tol_hash, fo_hash;
     std::vector<uint32_t> flags;
+    std::vector<int32_t> fo_canon, req_gid, tol_gid, flat_chunk;
+    // per string id of the batch's string table, filled lazily by the threads that meet it (every writer
+    // stores the same value): 0 unknown, 1 yes, 2 no / label key id + 2 (0 unknown)
+    std::vector<uint8_t> m_qname, m_lvalue, m_op;
+    std::vector<int32_t> m_kid;
+    std::vector<InternChunk> chunks;
   } sc;
 
   uint8_t* reserve(size_t n) {
@@ -504,31 +589,98 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
       }
     });
   }
+  // string facts memoised per string id (keys, ops and values repeat across requirements)
+  const int NSTR = su->str.n;
+  X.m_qname.resize(NSTR);
+  X.m_lvalue.resize(NSTR);
+  X.m_op.resize(NSTR);
+  X.m_kid.resize(NSTR);
+  pfill(X.m_qname, (uint8_t)0);
+  pfill(X.m_lvalue, (uint8_t)0);
+  pfill(X.m_op, (uint8_t)0);
+  pfill(X.m_kid, (int32_t)0);
+  auto memo8 = [](uint8_t* slot, auto compute) -> uint8_t {
+    uint8_t f = __atomic_load_n(slot, __ATOMIC_RELAXED);
+    if (!f) {
+      f = compute();
+      __atomic_store_n(slot, f, __ATOMIC_RELAXED);
+    }
+    return f;
+  };
+  auto qname_ok = [&](int32_t id) {
+    return memo8(&X.m_qname[id], [&] { return (uint8_t)(is_qualified_name(S[id]) ? 1 : 2); }) == 1;
+  };
+  auto lvalue_ok = [&](int32_t id) {
+    return memo8(&X.m_lvalue[id], [&] { return (uint8_t)(is_valid_label_value(S[id]) ? 1 : 2); }) == 1;
+  };
+  auto op_of = [&](int32_t id) { return (int)memo8(&X.m_op[id], [&] { return (uint8_t)(label_op(S[id]) + 1); }) - 1; };
+  auto kid_of = [&](int32_t id) {
+    int32_t k = __atomic_load_n(&X.m_kid[id], __ATOMIC_RELAXED);
+    if (!k) {
+      k = kad_packer::find(P->label_key_id, S[id]) + 2;
+      __atomic_store_n(&X.m_kid[id], k, __ATOMIC_RELAXED);
+    }
+    return k - 2;
+  };
   parallel_for(R, threads, [&](int a, int b) {
     std::vector<int32_t> tmp;
+    // (key id, value string) → value id, a direct-mapped cache per thread (one value string may belong to
+    // several keys' vocabularies: a shared per-string slot would bounce between threads)
+    constexpr int VC = 1 << 14;
+    std::vector<int64_t> vc_key(VC, -1);
+    std::vector<int32_t> vc_val(VC);
+    auto vid_of = [&](int kid, int32_t id) {  // the value's id in key kid's vocabulary (-1: absent)
+      const int64_t k = ((int64_t)kid << 32) | (uint32_t)id;
+      const size_t slot = (size_t)(FlatIndex::mix((uint64_t)k) & (VC - 1));
+      if (vc_key[slot] == k) return vc_val[slot];
+      const int32_t v = kad_packer::find(P->label_vals[kid], S[id]);
+      vc_key[slot] = k;
+      vc_val[slot] = v;
+      return v;
+    };
     for (int r = a; r < b; r++) {
-      const sv key = S[su->rq_key[r]], ops = S[su->rq_op[r]];
+      const int32_t key_id = su->rq_key[r];
       const int v0 = su->rq_val_off[r], nv = su->rq_val_off[r + 1] - v0;
       const int32_t* vals = su->rq_val + v0;
-      const int op = label_op(ops);
-      bool ok = op != 0 && is_qualified_name(key);
+      const int op = op_of(su->rq_op[r]);
+      bool ok = op != 0 && qname_ok(key_id);
       if (ok && (op == OP_IN || op == OP_NOTIN)) ok = nv > 0;
       if (ok && (op == OP_EXISTS || op == OP_DNE)) ok = nv == 0;
       if (ok && (op == OP_GT || op == OP_LT)) {
         int64_t x;
         ok = nv == 1 && parse_int64(S[vals[0]], &x);
       }
-      for (int i = 0; ok && i < nv; i++) ok = is_valid_label_value(S[vals[i]]);
+      for (int i = 0; ok && i < nv; i++) ok = lvalue_ok(vals[i]);
       valid[r] = ok;
       elen[r] = 0;
       if (ok) {
-        P->label_words(key, op, vals, nv, S, tmp);
+        // label_words on memoised ids (same words)
+        const int kid = kid_of(key_id);
+        tmp.clear();
+        if (kid < 0) {
+          tmp = {(op == OP_NOTIN || op == OP_DNE) ? OP_TRUE : OP_FALSE, -1};
+        } else if (op == OP_IN || op == OP_NOTIN) {
+          tmp.push_back(0);
+          tmp.push_back(kid);
+          for (int i = 0; i < nv; i++) {
+            const int32_t v = vid_of(kid, vals[i]);
+            if (v >= 0) tmp.push_back(v);
+          }
+          std::sort(tmp.begin() + 2, tmp.end());
+          tmp.erase(std::unique(tmp.begin() + 2, tmp.end()), tmp.end());
+          if (tmp.size() == 2)
+            tmp = {op == OP_IN ? OP_FALSE : OP_TRUE, -1};
+          else
+            tmp[0] = op | ((int32_t)(tmp.size() - 2) << 8);
+        } else {
+          P->label_words(S[key_id], op, vals, nv, S, tmp);
+        }
         std::memcpy(wbuf.data() + eoff[r], tmp.data(), 4 * tmp.size());
         elen[r] = (int32_t)tmp.size();
       }
-      fvalid[r] = (ops == "In" || ops == "NotIn") && nv == 1;
+      fvalid[r] = (op == OP_IN || op == OP_NOTIN) && nv == 1;
       if (fvalid[r] && is_field[r]) {
-        P->field_words(key, ops, S[vals[0]], tmp);
+        P->field_words(S[key_id], S[su->rq_op[r]], S[vals[0]], tmp);
         fw[2 * (size_t)r] = tmp[0];
         fw[2 * (size_t)r + 1] = tmp[1];
       }
@@ -615,43 +767,29 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   });
   const int NCH = shared ? 1 : std::max(1, std::min(threads, W));
   lap("owners");
-  struct Chunk {
-    std::unordered_map<sv, int32_t> req_id;
-    std::vector<sv> reqs;                             // local id → words
-    std::deque<std::array<int32_t, 3>> extra_words;   // selector Equals words (stable addresses)
-    std::unordered_map<int64_t, int32_t> eq_gid;
-    std::unordered_map<uint64_t, std::vector<int32_t>> tol_by_hash;  // hash → local sets with that hash
-    std::vector<int> tol_rows;                        // local set → its first unit
-    std::vector<int32_t> req_map, tol_map;            // local → batch-wide id (merge)
-  };
-  std::vector<Chunk> chunks(NCH);
+  auto& chunks = X.chunks;
+  if ((int)chunks.size() < NCH) chunks.resize(NCH);
   auto chunk_lo = [&](int c) { return (int)((int64_t)W * c / NCH); };
   parallel_for(NCH, NCH, [&](int ca, int cb) {
     for (int c = ca; c < cb; c++) {
-      Chunk& K = chunks[c];
+      InternChunk& K = chunks[c];
+      K.reset();
       auto intern = [&](sv w) -> int32_t {
-        auto it = K.req_id.find(w);
-        if (it != K.req_id.end()) return it->second;
-        const int32_t id = (int32_t)K.reqs.size();
-        K.req_id.emplace(w, id);
-        K.reqs.push_back(w);
-        return id;
+        return K.req_ix.find_or_add(
+            std::hash<sv>()(w), [&](int32_t x) { return K.reqs[x] == w; },
+            [&] {
+              K.reqs.push_back(w);
+              return (int32_t)K.reqs.size() - 1;
+            });
       };
       for (int w = chunk_lo(c); w < chunk_lo(c + 1); w++) {
         // toleration list → local set id (content identity: hash, confirmed against the set's first unit)
-        auto& cand = K.tol_by_hash[tol_hash[w]];
-        int32_t ts = -1;
-        for (int32_t x : cand)
-          if (same_tols(K.tol_rows[x], w)) {
-            ts = x;
-            break;
-          }
-        if (ts < 0) {
-          ts = (int32_t)K.tol_rows.size();
-          K.tol_rows.push_back(w);
-          cand.push_back(ts);
-        }
-        tolset[w] = ts;
+        tolset[w] = K.tol_ix.find_or_add(
+            tol_hash[w], [&](int32_t x) { return same_tols(K.tol_rows[x], w); },
+            [&] {
+              K.tol_rows.push_back(w);
+              return (int32_t)K.tol_rows.size() - 1;
+            });
         // filter program: ClusterSelector entries, then required terms
         for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) {
           const int64_t code = sel_code[e];
@@ -659,14 +797,15 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
             sgid[e] = intern(words_sv(kFalse, 2));
             continue;
           }
-          auto jt = K.eq_gid.find(code);
-          if (jt != K.eq_gid.end()) {
-            sgid[e] = jt->second;
-            continue;
-          }
-          K.extra_words.push_back({OP_EQ | (1 << 8), (int32_t)(code >> 32), (int32_t)(uint32_t)code});
-          sgid[e] = intern(words_sv(K.extra_words.back().data(), 3));
-          K.eq_gid.emplace(code, sgid[e]);
+          const int32_t x = K.eq_ix.find_or_add(
+              (uint64_t)code, [&](int32_t y) { return K.eq_code[y] == code; },
+              [&] {
+                K.extra_words.push_back({OP_EQ | (1 << 8), (int32_t)(code >> 32), (int32_t)(uint32_t)code});
+                K.eq_code.push_back(code);
+                K.eq_req.push_back(intern(words_sv(K.extra_words.back().data(), 3)));
+                return (int32_t)K.eq_code.size() - 1;
+              });
+          sgid[e] = K.eq_req[x];
         }
         const uint32_t f = su->flags[w];
         if ((f & KAD_SU_HAS_CLUSTER_AFFINITY) && (f & KAD_SU_HAS_REQUIRED)) {
@@ -703,72 +842,88 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   }, 1);
   lap("intern-A");
   // merge: batch-wide ids by first occurrence. The chunks' distinct keys, flattened in (chunk, local)
-  // order, are bucketed by hash into shards; each shard (in parallel) finds every key's first occurrence
-  // among equal keys; one serial pass over the flat order then numbers the first occurrences 0, 1, ...
-  // and gives every later occurrence its first's number — the ids of one serial pass over the units.
+  // order, are split by hash over T threads; each thread (one flat index) finds the first occurrence of
+  // every key of its share among equal keys, scanning in flat order; numbering the first occurrences
+  // 0, 1, ... (a parallel prefix count) and giving every later occurrence its first's number yields the
+  // ids of one serial pass over the units.
   auto first_occurrence = [&](int n_items, auto hash_of, auto same, std::vector<int32_t>& gid) -> int {
-    std::vector<uint64_t> hs((size_t)n_items);
+    auto& hs = X.fo_hash;
+    auto& canon = X.fo_canon;
+    hs.resize((size_t)n_items);
+    canon.resize((size_t)n_items);
+    gid.resize((size_t)n_items);
     parallel_for(n_items, threads, [&](int a, int b) {
       for (int g = a; g < b; g++) hs[g] = hash_of(g);
     });
-    const int SH = std::max(1, std::min(4 * threads, 256));
-    std::vector<std::vector<int32_t>> shard(SH);
-    for (int g = 0; g < n_items; g++) shard[hs[g] % SH].push_back(g);
-    std::vector<int32_t> canon((size_t)n_items);
-    parallel_for(SH, threads, [&](int a, int b) {
-      for (int sh = a; sh < b; sh++) {
-        std::unordered_map<uint64_t, std::vector<int32_t>> seen;  // hash → first occurrences
-        for (int32_t g : shard[sh]) {
-          auto& cand = seen[hs[g]];
-          int32_t f = -1;
-          for (int32_t x : cand)
-            if (same(x, g)) {
-              f = x;
-              break;
-            }
-          if (f < 0) {
-            cand.push_back(g);
-            f = g;
-          }
-          canon[g] = f;
+    const int T = std::max(1, std::min(threads, 64));
+    parallel_for(T, T, [&](int ta, int tb) {
+      for (int t = ta; t < tb; t++) {
+        FlatIndex ix;
+        ix.reset((size_t)n_items / T + 16);
+        for (int g = 0; g < n_items; g++) {
+          if ((int)((FlatIndex::mix(hs[g]) >> 40) % (uint64_t)T) != t) continue;
+          canon[g] = ix.find_or_add(hs[g], [&](int32_t x) { return same(x, g); }, [&] { return (int32_t)g; });
         }
       }
     }, 1);
-    gid.resize((size_t)n_items);
-    int next = 0;
-    for (int g = 0; g < n_items; g++) gid[g] = canon[g] == g ? next++ : gid[canon[g]];
-    return next;
+    const int NB = std::max(1, std::min(threads * 4, (n_items + 4095) / 4096));
+    std::vector<int32_t> cnt((size_t)NB + 1, 0);
+    auto blo = [&](int k) { return (int)((int64_t)n_items * k / NB); };
+    parallel_for(NB, threads, [&](int ka, int kb) {
+      for (int k = ka; k < kb; k++) {
+        int m = 0;
+        for (int g = blo(k); g < blo(k + 1); g++) m += canon[g] == g;
+        cnt[k + 1] = m;
+      }
+    }, 1);
+    for (int k = 0; k < NB; k++) cnt[k + 1] += cnt[k];
+    parallel_for(NB, threads, [&](int ka, int kb) {
+      for (int k = ka; k < kb; k++) {
+        int32_t next = cnt[k];
+        for (int g = blo(k); g < blo(k + 1); g++)
+          if (canon[g] == g) gid[g] = next++;
+      }
+    }, 1);
+    parallel_for(n_items, threads, [&](int a, int b) {  // a later occurrence: its first's number
+      for (int g = a; g < b; g++)
+        if (canon[g] != g) gid[g] = gid[canon[g]];
+    });
+    return cnt[NB];
   };
   std::vector<int32_t> req_base((size_t)NCH + 1, 0), tol_base((size_t)NCH + 1, 0);
   for (int c = 0; c < NCH; c++) {
     req_base[c + 1] = req_base[c] + (int32_t)chunks[c].reqs.size();
     tol_base[c + 1] = tol_base[c] + (int32_t)chunks[c].tol_rows.size();
   }
-  std::vector<int32_t> flat_chunk((size_t)std::max(req_base[NCH], tol_base[NCH]));
-  for (int c = 0; c < NCH; c++) {
-    for (int32_t g = req_base[c]; g < req_base[c + 1]; g++) flat_chunk[g] = c;
-  }
+  auto& flat_chunk = X.flat_chunk;
+  flat_chunk.resize((size_t)std::max(req_base[NCH], tol_base[NCH]));
+  auto fill_chunks = [&](const std::vector<int32_t>& base) {
+    parallel_for(NCH, threads, [&](int ca, int cb) {
+      for (int c = ca; c < cb; c++) std::fill(flat_chunk.begin() + base[c], flat_chunk.begin() + base[c + 1], c);
+    }, 1);
+  };
+  fill_chunks(req_base);
   auto req_at = [&](int g) -> sv { const int c = flat_chunk[g]; return chunks[c].reqs[g - req_base[c]]; };
-  std::vector<int32_t> req_gid, tol_gid;
+  auto& req_gid = X.req_gid;
+  auto& tol_gid = X.tol_gid;
   const int NR0 = first_occurrence(
       req_base[NCH], [&](int g) { return (uint64_t)std::hash<sv>()(req_at(g)); },
       [&](int x, int y) { return req_at(x) == req_at(y); }, req_gid);
   std::vector<sv> reqs((size_t)NR0);  // by batch-wide id: the words as bytes (views into wbuf / fw / chunk words)
-  for (int g = 0; g < req_base[NCH]; g++) reqs[req_gid[g]] = req_at(g);
-  for (int c = 0; c < NCH; c++) {
-    for (int32_t g = tol_base[c]; g < tol_base[c + 1]; g++) flat_chunk[g] = c;
-  }
+  parallel_for(req_base[NCH], threads, [&](int a, int b) {
+    for (int g = a; g < b; g++)
+      if (X.fo_canon[g] == g) reqs[req_gid[g]] = req_at(g);
+  });
+  fill_chunks(tol_base);
   auto tol_unit = [&](int g) { const int c = flat_chunk[g]; return chunks[c].tol_rows[g - tol_base[c]]; };
   const int NT0 = first_occurrence(
       tol_base[NCH], [&](int g) { return tol_hash[tol_unit(g)]; },
       [&](int x, int y) { return same_tols(tol_unit(x), tol_unit(y)); }, tol_gid);
   std::vector<int> tol_rows((size_t)NT0);  // first unit of each toleration set
-  for (int g = tol_base[NCH] - 1; g >= 0; g--) tol_rows[tol_gid[g]] = tol_unit(g);  // the first occurrence wins
-  for (int c = 0; c < NCH; c++) {
-    Chunk& K = chunks[c];
-    K.req_map.assign(req_gid.begin() + req_base[c], req_gid.begin() + req_base[c + 1]);
-    K.tol_map.assign(tol_gid.begin() + tol_base[c], tol_gid.begin() + tol_base[c + 1]);
-  }
+  parallel_for(tol_base[NCH], threads, [&](int a, int b) {
+    for (int g = a; g < b; g++)
+      if (X.fo_canon[g] == g) tol_rows[tol_gid[g]] = tol_unit(g);
+  });
   lap("merge");
   // local → batch-wide ids: units (toleration sets, selector entries) per chunk, requirement entries by
   // their owning unit's chunk
@@ -776,20 +931,21 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   unit_chunk.resize(W);
   parallel_for(NCH, NCH, [&](int ca, int cb) {
     for (int c = ca; c < cb; c++) {
-      const Chunk& K = chunks[c];
+      const int32_t* rmap = req_gid.data() + req_base[c];
+      const int32_t* tmap = tol_gid.data() + tol_base[c];
       for (int w = chunk_lo(c); w < chunk_lo(c + 1); w++) {
         unit_chunk[w] = c;
-        tolset[w] = K.tol_map[tolset[w]];
-        for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) sgid[e] = K.req_map[sgid[e]];
+        tolset[w] = tmap[tolset[w]];
+        for (int64_t e = su->sel_off[w]; e < su->sel_off[w + 1]; e++) sgid[e] = rmap[sgid[e]];
       }
     }
   }, 1);
   parallel_for(R, threads, [&](int a, int b) {
     for (int e = a; e < b; e++) {
       if (owner[e] < 0) continue;
-      const Chunk& K = chunks[unit_chunk[owner[e]]];
-      if (egid[e] >= 0) egid[e] = K.req_map[egid[e]];
-      if (fgid[e] >= 0) fgid[e] = K.req_map[fgid[e]];
+      const int32_t* rmap = req_gid.data() + req_base[unit_chunk[owner[e]]];
+      if (egid[e] >= 0) egid[e] = rmap[egid[e]];
+      if (fgid[e] >= 0) fgid[e] = rmap[fgid[e]];
     }
   });
   const int NR = (int)reqs.size();
@@ -1200,31 +1356,36 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   uint64_t* tol_all = reinterpret_cast<uint64_t*>(A(KAD_B_TOL_ALL));
   uint64_t* tol_pns = reinterpret_cast<uint64_t*>(A(KAD_B_TOL_PNS));
   const int ntaint = (int)P->taint_key.size();
+  // taint ids by key (a toleration with a key only tolerates taints of that key; an empty key, every taint)
+  std::unordered_map<sv, std::vector<int32_t>> taints_of_key;
+  std::vector<int32_t> all_taints(ntaint);
+  for (int tid = 0; tid < ntaint; tid++) {
+    taints_of_key[sv(P->taint_key[tid])].push_back(tid);
+    all_taints[tid] = tid;
+  }
   parallel_for((int)tol_rows.size(), threads, [&](int a, int b) {
     for (int r = a; r < b; r++) {
       const int w = tol_rows[r];
-      for (int tid = 0; tid < ntaint; tid++) {
-        const std::string &tk = P->taint_key[tid], &tv = P->taint_value[tid], &te = P->taint_effect[tid];
-        bool all = false, pns = false;
-        for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++) {
-          const sv key = S[su->tol_key[t]], op = S[su->tol_op[t]], val = S[su->tol_value[t]], eff = S[su->tol_effect[t]];
-          bool ok;
-          if (!eff.empty() && eff != te)
-            ok = false;
-          else if (!key.empty() && key != tk)
-            ok = false;
-          else if (op.empty() || op == "Equal")
-            ok = val == tv;
-          else
-            ok = op == "Exists";
-          if (ok) {
-            all = true;
-            if (eff.empty() || eff == "PreferNoSchedule") pns = true;
-          }
+      uint64_t* ta = tol_all + (size_t)r * TW;
+      uint64_t* tp = tol_pns + (size_t)r * TW;
+      for (int t = su->tol_off[w]; t < su->tol_off[w + 1]; t++) {
+        const sv key = S[su->tol_key[t]], op = S[su->tol_op[t]], val = S[su->tol_value[t]], eff = S[su->tol_effect[t]];
+        const bool equal = op.empty() || op == "Equal";
+        if (!equal && op != "Exists") continue;  // tolerates nothing
+        const std::vector<int32_t>* cand = &all_taints;
+        if (!key.empty()) {
+          auto it = taints_of_key.find(key);
+          if (it == taints_of_key.end()) continue;
+          cand = &it->second;
         }
-        const uint64_t bit = 1ull << (tid % 64);
-        if (all) tol_all[(size_t)r * TW + tid / 64] |= bit;
-        if (pns) tol_pns[(size_t)r * TW + tid / 64] |= bit;
+        const bool pns = eff.empty() || eff == "PreferNoSchedule";
+        for (const int32_t tid : *cand) {
+          if (!eff.empty() && eff != P->taint_effect[tid]) continue;
+          if (equal && val != P->taint_value[tid]) continue;
+          const uint64_t bit = 1ull << (tid % 64);
+          ta[tid / 64] |= bit;
+          if (pns) tp[tid / 64] |= bit;
+        }
       }
     }
   });
