@@ -446,7 +446,7 @@ def shard_sweep(args, cfg, local, t1_ms, ns=(2, 4, 8)):
     ctx.upload_snapshot(snap)
     out = {"t1_ms": t1_ms, "steps": args.steps, "per_n": {}}
     for n in ns:
-        ts = []
+        ts, stages = [], []
         for r in range(n):
             lo, hi = shard.shard_range(W_total, r, n)
             ctx.upload_batch(packer.pack(fwk, make_columns(cfg, lo, hi, clusters)))
@@ -458,8 +458,17 @@ def shard_sweep(args, cfg, local, t1_ms, ns=(2, 4, 8)):
                 ctx.schedule(fwk)
             ctx.sync()
             ts.append((time.perf_counter() - t0) / max(1, args.steps) * 1e3)
+            if r == 0:  # rank 0's per-stage device times (HIP events), outside the timing
+                ctx.set_timing(True)
+                st = []
+                for _ in range(3):
+                    ctx.schedule(fwk)
+                    ctx.sync()
+                    st.append(ctx.stage_timing())
+                ctx.set_timing(False)
+                stages = {k: float(np.mean([x[k] for x in st])) for k in ctx.STAGES}
         tn = max(ts)
-        out["per_n"][str(n)] = {"units_per_rank": W_total // n, "shard_ms": ts, "max_ms": tn,
+        out["per_n"][str(n)] = {"units_per_rank": W_total // n, "shard_ms": ts, "max_ms": tn, "rank0_stage_ms": stages,
                                 "projected_decisions_per_s": W_total * C / (tn * 1e-3),
                                 "projected_efficiency": t1_ms / (n * tn)}
         log(f"[sweep] N={n}: shard ms {['%.3f' % t for t in ts]} -> efficiency {t1_ms / (n * tn):.3f}")

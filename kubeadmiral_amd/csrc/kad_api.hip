@@ -20,6 +20,8 @@ using namespace kad;
 struct kad_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;                   // schedule_row_kernel beside the wide kernel (BatchDev::early_rows)
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // stage events: 0 start, 3 after req_mask, 4 after prep, 5 after the main schedule kernel, 1 after the
   // defer pass, 2 after the planner
   hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -395,14 +397,20 @@ int kad_ctx_create(int hip_device, kad_ctx** out) {
     delete c;
     return KAD_EHIP;
   }
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) {
+    kad_ctx_destroy(c);
+    return KAD_EHIP;
+  }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) {
-      delete c;
+      kad_ctx_destroy(c);
       return KAD_EHIP;
     }
   for (auto& e : c->tev)
     if (hipEventCreate(&e) != hipSuccess) {
-      delete c;
+      kad_ctx_destroy(c);
       return KAD_EHIP;
     }
   *out = c;
@@ -421,7 +429,13 @@ int kad_ctx_destroy(kad_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->tev)
     if (e) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(c->stream);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
+  for (hipEvent_t e : {c->fork_ev, c->join_ev})
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return KAD_OK;
 }
@@ -1080,6 +1094,10 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   // long feasible lists go to schedule_row_kernel when every filter is in the static words
   static const bool no_rows = tuning_env("KAD_NO_ROWS", 0) != 0;
   c->bd.use_rows = !no_rows && c->sd.clean && c->sd.fold && c->sd.fitfold && row_kernel_fits(c->sd.C);
+  static const bool rows_after = tuning_env("KAD_ROWS_AFTER", 0) != 0;
+  const int per = prep_lanes_per_unit(c->sd.C);
+  c->bd.early_rows = c->bd.use_rows && !rows_after && wide_path(c->sd) && (per & (per - 1)) == 0 && per <= 64 &&
+                     !dbg_feas && !dbg_total;
   if (c->bd.use_rows) {
     if (int r = grow(c, &c->d_rowslab, &c->rowslab_cap, (size_t)ROW_MAX_BLOCKS * row_slab_bytes(c->sd.C))) return r;
     c->bd.row_slabs = static_cast<char*>(c->d_rowslab);
@@ -1090,7 +1108,7 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   if (tm) HIPCHK(c, hipEventRecord(c->ev[5], c->stream));  // re-recorded after the main kernel when it runs
   if (tm) HIPCHK(c, hipEventRecord(c->ev[6], c->stream));  // re-recorded after the long-row kernel
   HIPCHK(c, launch_schedule(c->sd, c->bd, o, pd, c->d_scratch, c->scratch_bytes, c->stream, tm ? c->ev[5] : nullptr,
-                            tm ? c->ev[6] : nullptr));
+                            tm ? c->ev[6] : nullptr, c->side, c->fork_ev, c->join_ev));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())
     HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, c->d_plan_rows, (int)c->plan_rows.size(), c->batch_hdr.max_row_slots,

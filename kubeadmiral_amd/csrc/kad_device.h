@@ -97,6 +97,9 @@ struct BatchDev {
   int32_t* defer_n;         // [1] length of defer
   int32_t* work_n;          // [1] lean kernel work queue: next batch of LEAN_BATCH units
   int use_rows;             // host: schedule_row_kernel runs (clean, folded, fit-folded snapshot, C <= ROW_MAX_C)
+  int early_rows;           // host: the wide kernel runs on static words that are the whole filter, so prep_kernel
+                            // routes units with more than WIDE_P feasible clusters to rows (REC_ROW) and the row
+                            // kernel runs beside the wide kernel (a second stream) instead of after it
   int32_t* rows;            // [W] units whose feasible list outgrows the lean / wide kernels' registers
   int32_t* rows_n;          // [1] length of rows (reset by prep_kernel)
   int32_t* rows_head;       // [1] schedule_row_kernel's dequeue counter (reset by prep_kernel)
@@ -121,6 +124,9 @@ struct UnitRec {
 static_assert(sizeof(UnitRec) == 64, "UnitRec is one 64-B line");
 constexpr uint32_t REC_DESIRED_POS = 1u << 31;  // DesiredReplicas != nil && *DesiredReplicas > 0
 constexpr uint32_t REC_FULL = 1u << 30;         // scheduled by schedule_kernel (features the lean kernel omits)
+constexpr uint32_t REC_ROW = 1u << 29;          // routed to schedule_row_kernel by prep_kernel (BatchDev::early_rows)
+constexpr int WIDE_Q = 8;                       // schedule_wide_kernel: positions per lane
+constexpr int WIDE_P = WIDE_Q * 64;             //   and per wave (longer feasible lists: schedule_row_kernel)
 
 struct OutDev {
   int32_t* status;
@@ -201,12 +207,15 @@ hipError_t launch_value_rows(const SnapDev& s, uint64_t* vrows, hipStream_t st);
 bool fast_path(int C);
 // true if launch_schedule runs schedule_wide_kernel for this snapshot (clean, 5..16 chunks)
 bool wide_path(const SnapDev& s);
+// prep_kernel lanes per unit (a power of two <= 64 lets it count a unit's feasible clusters in one wave)
+int prep_lanes_per_unit(int C);
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st);
 // after_main / after_rows (optional): recorded after the main schedule kernel and after the long-row
 // kernel, before the defer pass (stage timing)
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p,
                            void* global_scratch, size_t scratch_bytes, hipStream_t st, hipEvent_t after_main = nullptr,
-                           hipEvent_t after_rows = nullptr);
+                           hipEvent_t after_rows = nullptr, hipStream_t side = nullptr, hipEvent_t fork = nullptr,
+                           hipEvent_t join = nullptr);
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,
                        int n_rows, int kmax, void* global_scratch, size_t scratch_bytes, hipStream_t st);
 hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,

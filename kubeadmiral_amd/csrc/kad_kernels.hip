@@ -966,12 +966,81 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   const int64_t oo = b.out_off[w];
   const int32_t so0 = b.sreq_off[w], so1 = b.sreq_off[w + 1];
   const uint64_t tol0 = b.tol_all[(size_t)tolset * b.TW], tolp0 = b.tol_pns[(size_t)tolset * b.TW];
+  bool full = force_full != 0;
+  if ((fm & (1u << KAD_PL_API_RESOURCES)) && gvk >= 64) full = true;
+  if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && so0 < so1) full = true;
+  const uint32_t rflags = f | (((f & KAD_W_HAS_DESIRED) && desired > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
+  const bool act = ch0 < nch && !(f & KAD_W_STICKY);
+  int cnt = 0;  // feasible clusters among this lane's chunks (early_rows)
+  if (act) {
+    uint64_t m[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; k++) m[k] = ~0ull;
+    if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) {
+      const int32_t* gp = b.fprog + fpo;
+      const int base = ((int)threadIdx.x - (int)l) * CPL;  // the unit's program word 0 in this block (may be < 0)
+      auto word = [&](int i) -> int32_t {
+        const int t = base + i;
+        return (i < (int)(per * CPL) && t >= 0 && t < 256 * CPL) ? prog_words[t] : gp[i];
+      };
+      affinity_words<CPL>(b.req_mask, word, nch, ch0, m);
+    }
+    if (s.fitfold && (fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO)) {
+      // fit.go:73-134 (cpu, memory) by threshold rows: clusters whose available amount >= the request
+      const int2 j = fit_ranks(s, fences, rqc, rqm);
+      const int jc = j.x, jm = j.y;
+#pragma unroll
+      for (int k = 0; k < CPL; k++) {
+        const uint32_t ch = ch0 + k < nch ? ch0 + k : nch - 1;
+        m[k] &= ldg(s.fit_rows[0], (uint32_t)jc * nch + ch) & ldg(s.fit_rows[1], (uint32_t)jm * nch + ch);
+      }
+    }
+    const bool place = (fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
+    const bool curw = (fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
+    uint64_t pw[CPL], cwv[CPL];
+    if (place) {
+      id_list_words<CPL>(b.place, b.place_off[w], b.place_off[w + 1], ch0, pw);
+#pragma unroll
+      for (int k = 0; k < CPL; k++) m[k] &= pw[k];
+    }
+#pragma unroll
+    for (int k = 0; k < CPL; k++) cwv[k] = 0;
+    if (curw) id_list_words<CPL>(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch0, cwv);
+    if (s.fold) {
+      uint32_t cc[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; k++) cc[k] = ch0 + k < nch ? ch0 + k : nch - 1;
+      uint64_t tw[TFOLD_MAX_TW];
+      tw[0] = tol0;
+      for (int t = 1; t < s.TW && t < TFOLD_MAX_TW; t++) tw[t] = b.tol_all[(size_t)tolset * b.TW + t];
+      uint64_t fw[CPL];
+      folded_words<CPL>(s, fm, f, gvk, tw, cwv, nch, cc, fw);
+#pragma unroll
+      for (int k = 0; k < CPL; k++) m[k] &= fw[k];
+    }
+#pragma unroll
+    for (int k = 0; k < CPL; k++) {
+      const uint32_t ch = ch0 + k;
+      if (ch >= nch) break;
+      if (curw) b.cw[(size_t)w * nch + ch] = cwv[k];
+      if (ch == nch - 1 && (s.C & 63)) m[k] &= (1ull << (s.C & 63)) - 1;  // clusters past C: never feasible
+      b.sw[(size_t)w * nch + ch] = m[k];
+      cnt += popc64(m[k]);
+    }
+  }
+  // early_rows: in the wide kernel's FITF mode (fold + fitfold) the static words are the whole filter, so
+  // the unit's feasible count is their popcount (summed over its `per` lanes: a power of two, one wave);
+  // a unit the wide kernel would hand to rows (past its sticky / defer checks, more than WIDE_P clusters)
+  // is routed here, before the wide kernel starts
+  bool route = false;
+  if (b.early_rows) {
+    for (uint32_t o = 1; o < per; o <<= 1) cnt += __shfl_xor(cnt, (int)o);
+    route = act && !(rflags & REC_FULL) && !(f & KAD_W_WIDE_SCORES) && (uint64_t)rqc < (1ull << 46) &&
+            (uint64_t)rqm < (1ull << 46) && cnt > WIDE_P;
+  }
   if (l == 0) {
     UnitRec r;
-    bool full = force_full != 0;
-    if ((fm & (1u << KAD_PL_API_RESOURCES)) && gvk >= 64) full = true;
-    if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && so0 < so1) full = true;
-    r.flags = f | (((f & KAD_W_HAS_DESIRED) && desired > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
+    r.flags = rflags | (route ? REC_ROW : 0u);
     r.gvk = gvk;
     r.tolset = tolset;
     r.sprog_off = sprog;
@@ -982,61 +1051,13 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
     r.tol0 = tol0;
     r.tolp0 = tolp0;
     b.rec[w] = r;
+    if (route) b.rows[atomicAdd(b.rows_n, 1)] = (int32_t)w;
   }
-  if (ch0 >= nch || (f & KAD_W_STICKY)) return;
-  uint64_t m[CPL];
-#pragma unroll
-  for (int k = 0; k < CPL; k++) m[k] = ~0ull;
-  if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) {
-    const int32_t* gp = b.fprog + fpo;
-    const int base = ((int)threadIdx.x - (int)l) * CPL;  // the unit's program word 0 in this block (may be < 0)
-    auto word = [&](int i) -> int32_t {
-      const int t = base + i;
-      return (i < (int)(per * CPL) && t >= 0 && t < 256 * CPL) ? prog_words[t] : gp[i];
-    };
-    affinity_words<CPL>(b.req_mask, word, nch, ch0, m);
-  }
-  if (s.fitfold && (fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO)) {
-    // fit.go:73-134 (cpu, memory) by threshold rows: clusters whose available amount >= the request
-    const int2 j = fit_ranks(s, fences, rqc, rqm);
-    const int jc = j.x, jm = j.y;
-#pragma unroll
-    for (int k = 0; k < CPL; k++) {
-      const uint32_t ch = ch0 + k < nch ? ch0 + k : nch - 1;
-      m[k] &= ldg(s.fit_rows[0], (uint32_t)jc * nch + ch) & ldg(s.fit_rows[1], (uint32_t)jm * nch + ch);
-    }
-  }
-  const bool place = (fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
-  const bool curw = (fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
-  uint64_t pw[CPL], cwv[CPL];
-  if (place) {
-    id_list_words<CPL>(b.place, b.place_off[w], b.place_off[w + 1], ch0, pw);
-#pragma unroll
-    for (int k = 0; k < CPL; k++) m[k] &= pw[k];
-  }
-#pragma unroll
-  for (int k = 0; k < CPL; k++) cwv[k] = 0;
-  if (curw) id_list_words<CPL>(b.cur_id, b.cur_off[w], b.cur_off[w + 1], ch0, cwv);
-  if (s.fold) {
-    uint32_t cc[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; k++) cc[k] = ch0 + k < nch ? ch0 + k : nch - 1;
-    uint64_t tw[TFOLD_MAX_TW];
-    tw[0] = tol0;
-    for (int t = 1; t < s.TW && t < TFOLD_MAX_TW; t++) tw[t] = b.tol_all[(size_t)tolset * b.TW + t];
-    uint64_t fw[CPL];
-    folded_words<CPL>(s, fm, f, gvk, tw, cwv, nch, cc, fw);
-#pragma unroll
-    for (int k = 0; k < CPL; k++) m[k] &= fw[k];
-  }
-#pragma unroll
-  for (int k = 0; k < CPL; k++) {
-    const uint32_t ch = ch0 + k;
-    if (ch >= nch) break;
-    if (curw) b.cw[(size_t)w * nch + ch] = cwv[k];
-    if (ch == nch - 1 && (s.C & 63)) m[k] &= (1ull << (s.C & 63)) - 1;  // clusters past C: never feasible
-    b.sw[(size_t)w * nch + ch] = m[k];
-  }
+}
+
+int prep_lanes_per_unit(int C) {
+  const int nch = (C + 63) >> 6;
+  return nch > 0 ? (nch + PREP_CPL - 1) / PREP_CPL : 1;
 }
 
 // ====================================================== unit work queue
@@ -1896,8 +1917,6 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 //     lean kernel (all ties / n <= 12 insertionSort / PdqWave replay).
 // Units with more than WIDE_P feasible clusters, REC_FULL units and requests
 // outside the exact-f64 range go to the defer list (schedule_kernel).
-constexpr int WIDE_Q = 8;
-constexpr int WIDE_P = WIDE_Q * 64;
 constexpr int WIDE_MAX_NCH = 16;
 constexpr int WIDE_THREADS = 1024;
 
@@ -1966,7 +1985,7 @@ __device__ __forceinline__ void wide_defer(int w) {
 __device__ __forceinline__ void wide_row_or_defer(int w) {
   if (lane_id() == 0) {
     WArgs a = wargs();
-    if (a->b.use_rows) {
+    if (a->b.use_rows && !a->b.early_rows) {  // (early_rows: the row kernel may already be done)
       const int slot = atomicAdd(a->b.rows_n, 1);
       a->b.rows[slot] = w;
     } else {
@@ -2093,6 +2112,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     const int64_t rqc = fld64(4), rqm = fld64(6);
     const uint64_t tolc = (uint64_t)fld64(12);
     do {  // one unit; `break` = done with it
+      if (fc & REC_ROW) break;  // prep_kernel routed it to schedule_row_kernel
       if (fc & KAD_W_STICKY) {  // generic_scheduler.go:101-104
         wide_status(w, KAD_ST_STICKY);
         break;
@@ -3581,7 +3601,8 @@ static hipError_t launch_rows(const SnapDev& s, const BatchDev& b, const OutDev&
 }
 
 hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, void* gscr,
-                           size_t scr_bytes, hipStream_t st, hipEvent_t after_main, hipEvent_t after_rows) {
+                           size_t scr_bytes, hipStream_t st, hipEvent_t after_main, hipEvent_t after_rows,
+                           hipStream_t side, hipEvent_t fork, hipEvent_t join) {
   auto rec = [&](hipEvent_t ev) { return ev ? hipEventRecord(ev, st) : hipSuccess; };
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (b.W == 0) return hipSuccess;
@@ -3608,10 +3629,21 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (grid > need) grid = need;
     static const int exp = tuning_env("KAD_WIDE_EXPERIMENT", 0);
     const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, exp};
+    const bool beside = b.early_rows && b.use_rows && side && fork && join;
+    if (beside) {  // the row kernel on the side stream, from the end of prep_kernel, beside the wide kernel
+      if (hipError_t e = hipEventRecord(fork, st)) return e;
+      if (hipError_t e = hipStreamWaitEvent(side, fork, 0)) return e;
+      if (hipError_t e = launch_rows(s, b, o, p, side)) return e;
+      if (hipError_t e = hipEventRecord(join, side)) return e;
+    }
     hipLaunchKernelGGL(schedule_wide_kernel<WIDE_MAX_NCH>, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
     if (hipError_t e = hipGetLastError()) return e;
     if (hipError_t e = rec(after_main)) return e;
-    if (hipError_t e = launch_rows(s, b, o, p, st)) return e;
+    if (beside) {
+      if (hipError_t e = hipStreamWaitEvent(st, join, 0)) return e;
+    } else if (hipError_t e = launch_rows(s, b, o, p, st)) {
+      return e;
+    }
     if (hipError_t e = rec(after_rows)) return e;
     // feasible lists longer than WIDE_P positions can come from any unit: the defer pass always runs
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);

@@ -240,6 +240,28 @@ def test_c3_clusters_1000(ctx):
     assert_same(res, c_oracle(snap, batch, fwk), "c3 20k x 1000")
 
 
+@pytest.mark.parametrize("seed", [0xC31, 0xC32])
+def test_c3_long_lists_routed_beside_the_wide_kernel(ctx, seed):
+    """C = 1000 units whose feasible lists pass WIDE_P = 512 positions (a third of them: no selector, an
+    Exists expression only, light requests): prep_kernel routes them to schedule_row_kernel, which runs on
+    the side stream beside the wide kernel (BatchDev::early_rows); every row must equal the C oracle's and
+    the row path must have taken units."""
+    rng = np.random.default_rng(seed)
+    clusters = synth.gen_clusters(rng, 1000)
+    units = synth.gen_units_c2(rng, 3000)
+    for i, su in enumerate(units):
+        if i % 3 == 0:
+            su.cluster_selector = None
+            su.affinity = T.Affinity(T.ClusterAffinity(required=T.ClusterSelector([T.ClusterSelectorTerm(
+                [T.ClusterSelectorRequirement(f"key{i % 8}", T.OP_EXISTS, [])])])))
+            su.tolerations = [T.Toleration(operator=T.TOLERATION_OP_EXISTS)]
+            su.resource_request = T.Resource(int(rng.integers(0, 100)), int(rng.integers(0, 1 << 20)))
+    fwk = synth.profile_for("c3")
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert ctx.path_counts()["row_kernel"] > 100
+    assert_same(res, c_oracle(snap, batch, fwk), f"c3 long lists seed {seed}")
+
+
 def test_c3_default_set_divide_subrun(ctx):
     """'a parity sub-run with the full default plugin set in Divide mode' (C = 1000)."""
     rng = np.random.default_rng(synth.SEEDS["c3"] + 1)
