@@ -894,6 +894,41 @@ struct PdqWaveP {
     }
     return false;
   }
+  // fused() on ranges of at most 64 positions, in registers: lane x holds position a + x (one LDS read, one
+  // LDS write). The virtual first swap puts the pivot element at lane 0 and old e[a] at the pivot's lane;
+  // among lanes 1.. the t-th L stopper from the left and the t-th R stopper from the right exchange while
+  // the L is left of the R (a prefix of t: Go's Hoare loop); each lane pulls its partner's element
+  // (ds_bpermute); strict then swaps lanes j = #R and 0.
+  __device__ int fused64(int a, int b, int pivot, uint32_t P, bool strict, int* npairs) const {
+    const int lane = lane_id(), len = b - a, px = pivot - a;
+    const bool in = lane < len;
+    const uint32_t raw = e[in ? a + lane : a];
+    const uint32_t Ea = (uint32_t)__builtin_amdgcn_readlane((int)raw, 0);
+    const uint32_t Ep = (uint32_t)__builtin_amdgcn_readlane((int)raw, px);
+    const uint32_t v = lane == 0 ? Ep : (lane == px ? Ea : raw);
+    const uint32_t thr = strict ? ((P << 16) | 0xFFFFu) : ((P << 16) - 1u);
+    const bool P0eq = !strict && P == 0;
+    const bool scan = in && lane >= 1;
+    const bool isR = scan && (P0eq || v > thr);
+    const uint64_t mR = ballot(isR), mL = ballot(scan && !isR);
+    const int cR = popc64(mR), cL = popc64(mL);
+    const int np = cL < cR ? cL : cR;
+    // rank: an L lane's from the left, an R lane's from the right; the partner is the other kind's same rank
+    const int t = isR ? cR - 1 - mbcnt(mR) : mbcnt(mL);
+    const bool paired = scan && t < np;
+    const int partner = isR ? nth_bit(mL, t) : nth_bit(mR, cR - 1 - t);
+    const bool sw = paired && (isR ? partner < lane : lane < partner);
+    uint32_t nv = (uint32_t)__builtin_amdgcn_ds_bpermute((sw ? partner : lane) << 2, (int)v);
+    if (strict) {  // swap(j, a): j = a + #R
+      const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)nv, cR);
+      const uint32_t v0 = (uint32_t)__builtin_amdgcn_readlane((int)nv, 0);
+      nv = lane == 0 ? vj : (lane == cR ? v0 : nv);
+    }
+    if (in) e[a + lane] = nv;
+    wsync<GS>();
+    *npairs = popc64(ballot(sw && !isR));
+    return cR;
+  }
   // Fused partition / partitionEqual of [a, b) around the element at `pivot` (key P). strict:
   // right stoppers R = key > P (partition, with the final swap); else R = key >= P (partitionEqual).
   // Returns #R; *npairs = number of misplaced pairs (Go's swap count in the Hoare loop).
@@ -1012,12 +1047,12 @@ struct PdqWaveP {
       PQ_ADD(3, 1);
       int T;
       if (a > 0 && !(prev > pk)) {  // !less(a-1, pivot): partitionEqual
-        a = a + 1 + fused(a, b, pivot, pk, false, &T);
+        a = a + 1 + (length <= WAVE ? fused64(a, b, pivot, pk, false, &T) : fused(a, b, pivot, pk, false, &T));
         PQ_T(c4);
         PQ_ADD(0, c4 - c3);
         continue;
       }
-      const int mid = a + fused(a, b, pivot, pk, true, &T);
+      const int mid = a + (length <= WAVE ? fused64(a, b, pivot, pk, true, &T) : fused(a, b, pivot, pk, true, &T));
       PQ_T(c5);
       PQ_ADD(0, c5 - c3);
       wasPartitioned = T == 0;

@@ -63,6 +63,26 @@ __device__ __forceinline__ void wsync() {
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
 __device__ __forceinline__ int popc64(uint64_t x) { return __popcll(x); }
+// position of the s-th (0-based) set bit of m (per lane; s < popc(m)), by halving popcounts
+__device__ __forceinline__ int nth_bit(uint64_t m, int s) {
+  uint32_t w = (uint32_t)m;
+  int pos = 0, c = __builtin_popcount(w);
+  if (s >= c) {
+    s -= c;
+    w = (uint32_t)(m >> 32);
+    pos = 32;
+  }
+#pragma unroll
+  for (int half = 16; half >= 1; half >>= 1) {
+    c = __builtin_popcount(w & ((1u << half) - 1u));
+    if (s >= c) {
+      s -= c;
+      w >>= half;
+      pos += half;
+    }
+  }
+  return pos;
+}
 
 // number of set bits of m in lanes below this lane
 // this lane's bit of a wave-uniform mask: the mask's SGPR pair is the lane predicate (v_cndmask
