@@ -1102,6 +1102,9 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
     if (int r = grow(c, &c->d_rowslab, &c->rowslab_cap, (size_t)ROW_MAX_BLOCKS * row_slab_bytes(c->sd.C))) return r;
     c->bd.row_slabs = static_cast<char*>(c->d_rowslab);
   }
+  // early_rows: prep_kernel appends to the row list from all its blocks, so the list is emptied before it
+  // starts (rows_n, rows_head: two adjacent words)
+  if (c->bd.early_rows) HIPCHK(c, hipMemsetAsync(c->bd.rows_n, 0, 2 * sizeof(int32_t), c->stream));
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[4], c->stream));

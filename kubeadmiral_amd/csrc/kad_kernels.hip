@@ -932,8 +932,10 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   if (g == 0) {
     *b.defer_n = 0;
     *b.work_n = 0;
-    *b.rows_n = 0;
-    *b.rows_head = 0;
+    if (!b.early_rows) {  // early_rows: this kernel appends to rows (the host zeroes both before it runs)
+      *b.rows_n = 0;
+      *b.rows_head = 0;
+    }
   }
   if (g < (uint32_t)WQ_HEADS) b.wq[g * WQ_STRIDE] = 0u;  // the schedule kernels' work heads
   const bool live = g < (uint32_t)b.W * per;
