@@ -53,6 +53,8 @@ struct kad_ctx {
   int n_seg_reqs = 0;         // requirements on req_mask_kernel's segment path (the rest: value rows)
   void* d_vrows = nullptr;    // SnapDev::vrows
   size_t vrows_cap = 0;
+  void* d_rescols = nullptr;  // SnapDev::res4 / res_iv
+  size_t rescols_cap = 0;
   void* d_rowslab = nullptr;  // BatchDev::row_slabs
   size_t rowslab_cap = 0;
   void* d_rec = nullptr;  // UnitRec[W] (prep_kernel)
@@ -422,7 +424,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
-                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab, c->d_vrows,
+                  (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab, c->d_vrows, c->d_rescols,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs, c->d_diff})
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
@@ -611,6 +613,14 @@ static int refresh_derived(kad_ctx* c) {
   c->snap_negative = res_negative(c->h_res);
   c->sd.clean = res_clean(c->h_res);
   const int C = c->sd.C, TW = c->sd.TW;
+  c->sd.res4 = nullptr;
+  c->sd.res_iv = nullptr;
+  if (c->sd.clean && C > 0) {
+    if (int r = grow(c, &c->d_rescols, &c->rescols_cap, (size_t)40 * C)) return r;
+    HIPCHK(c, launch_res_cols(c->sd, c->d_rescols, c->stream));
+    c->sd.res4 = static_cast<const double4*>(c->d_rescols);
+    c->sd.res_iv = reinterpret_cast<const float2*>(c->sd.res4 + C);
+  }
   c->sd.fold = TW >= 1 && TW <= TFOLD_MAX_TW;
   for (int t = 0; t < TFOLD_MAX_TW; t++) {
     uint64_t present = 0;
@@ -1087,9 +1097,6 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   o.dbg_feas = dbg_feas;
   o.dbg_total = dbg_total;
   const bool tm = c->timing;
-  if (tm) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream));
-  if (tm) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
   c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total || wide_path(c->sd);
   // long feasible lists go to schedule_row_kernel when every filter is in the static words
   static const bool no_rows = tuning_env("KAD_NO_ROWS", 0) != 0;
@@ -1103,8 +1110,12 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
     c->bd.row_slabs = static_cast<char*>(c->d_rowslab);
   }
   // early_rows: prep_kernel appends to the row list from all its blocks, so the list is emptied before it
-  // starts (rows_n, rows_head: two adjacent words)
-  if (c->bd.early_rows) HIPCHK(c, hipMemsetAsync(c->bd.rows_n, 0, 2 * sizeof(int32_t), c->stream));
+  // starts (rows_n, rows_head: two adjacent words) — by req_row_kernel when it runs, else a memset
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  bool zeroed = false;
+  HIPCHK(c, launch_req_masks(c->sd, c->bd, c->stream, c->bd.early_rows, &zeroed));
+  if (tm) HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  if (c->bd.early_rows && !zeroed) HIPCHK(c, hipMemsetAsync(c->bd.rows_n, 0, 2 * sizeof(int32_t), c->stream));
   if (fast_path(c->sd.C))
     HIPCHK(c, launch_prep(c->sd, c->bd, pd, dbg_feas || dbg_total, c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[4], c->stream));

@@ -57,6 +57,12 @@ struct SnapDev {
   const int64_t* lint;
   const uint8_t* lok;
   const uint32_t* name_fnv;
+  // clean snapshots: the score operands of the exact clean-f64 path per cluster, rebuilt at upload / update
+  // (res_cols_kernel) so that kernels gathering them per feasible position (schedule_row_kernel) do one
+  // 32-B + one 8-B load instead of four i64 loads and two f64 divisions: res4[c] = (alloc_cpu - used_cpu,
+  // alloc_mem - used_mem, alloc_cpu, alloc_mem) as f64, res_iv[c] = (float)(100 / alloc) per resource
+  const double4* res4;
+  const float2* res_iv;
 };
 
 struct BatchDev {
@@ -197,11 +203,15 @@ inline int tuning_env(const char* name, int dflt) {
 #endif
 }
 
-hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st);
+// zero_rows: also empty the row list (BatchDev::rows_n, rows_head) before prep_kernel; *zeroed says whether
+// a launched kernel did (else the caller clears it)
+hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st, bool zero_rows, bool* zeroed);
 // per-id cluster bitmask slices of the snapshot (SnapDev::slices) and the taint table over them
 // (SnapDev::taint_tab), rebuilt at upload / update
 hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st);
 hipError_t launch_value_rows(const SnapDev& s, uint64_t* vrows, hipStream_t st);
+// SnapDev::res4 / res_iv of a clean snapshot (buf: 40 B per cluster, res4 first)
+hipError_t launch_res_cols(const SnapDev& s, void* buf, hipStream_t st);
 // true if the batch runs on schedule_lean_kernel (+ schedule_kernel over its
 // defer list); then launch_prep must run between launch_req_masks and launch_schedule.
 bool fast_path(int C);

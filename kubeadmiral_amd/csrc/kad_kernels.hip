@@ -31,6 +31,9 @@ namespace kad {
 __device__ unsigned long long g_phase[256 * 32];
 // lean kernel: (start, end) s_memtime of every wave of the last launch, for the wave-lifetime split
 __device__ unsigned long long g_wavetime[8192 * 2];
+// wide kernel: per wave (units taken, the longest unit's s_memtime cycles, realtime of the last dequeue, units
+// that straddled a tie)
+__device__ unsigned long long g_wavex[8192 * 4];
 #define KAD_PT(v) const unsigned long long v = __builtin_readcyclecounter()
 #define KAD_PACC uint32_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
@@ -206,9 +209,12 @@ __global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, in
 // req_row_kernel: one lane per (value-row requirement, chunk): In / Equals = OR of the value rows, NotIn
 // = its complement (a missing label matches), Exists / DoesNotExist = the key row or its complement;
 // TRUE / FALSE / metadata.name =, != are constants or one bit (no loads).
-__global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b) {
+__global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b, int zero_rows) {
   const int nch = (s.C + 63) >> 6;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  // the row list (rows_n, rows_head) emptied before prep_kernel appends to it (early routing): here
+  // instead of a separate memset launch
+  if (zero_rows && g < 2) b.rows_n[g] = 0;
   if (g >= (long)b.n_rowreq * nch) return;
   const int i = (int)(g / nch), ch = (int)(g - (long)i * nch);
   const int4 e0 = b.req_rows[2 * (size_t)i], e1 = b.req_rows[2 * (size_t)i + 1];
@@ -234,6 +240,15 @@ __global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b) {
   if (op == KAD_OP_NOTIN || op == KAD_OP_DNE) acc = ~acc;
   if (ch == nch - 1 && (s.C & 63)) acc &= (1ull << (s.C & 63)) - 1;  // clusters past C: never
   b.req_mask[(size_t)rid * nch + ch] = acc;
+}
+
+// SnapDev::res4 / res_iv (clean snapshots): the same expressions as the wide kernel's block cache
+__global__ __launch_bounds__(256) void res_cols_kernel(SnapDev s, double4* r4, float2* iv) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= s.C) return;
+  const int64_t ac = s.alloc_cpu[c], uc = s.used_cpu[c], am = s.alloc_mem[c], um = s.used_mem[c];
+  r4[c] = make_double4((double)(ac - uc), (double)(am - um), (double)ac, (double)am);
+  iv[c] = make_float2((float)(100.0 / (double)ac), (float)(100.0 / (double)am));
 }
 
 // SnapDev::vrows: one wave per (key, chunk), lane = cluster; lane s < VR_SLOTS collects value s's word
@@ -1074,26 +1089,37 @@ static_assert(WQ_HEADS == 64, "drained-head set is one u64; heads map to XCDs by
 // batch of work. Every wave's first batch is static (no atomic): wave wv of block b takes batch
 // (b >> 6) * wpb + wv of head b & 63, and that head's atomics count on from its static_batches.
 // Every wave ends once all heads are drained.
+// Guided tail: the last `tail` units of every head go out one per batch, so the waves that drain the
+// queue last finish within about one unit of each other instead of one B-unit batch (a batch of B
+// tie-straddling units is ~4x an average unit: at C3 / 125k units per GPU that batch tail was the bulk of
+// the wide kernel's ~60 us fixed cost).
 struct WorkTicket {
   int x;             // head of the pending ticket
   int i;             // its atomicAdd result (lane 0); batch index = i + static_batches(x)
   int wpb, nblocks;  // waves per block, grid size: the static first round
   int B;             // units per batch (<= WQ_BATCH): small enough that a wave takes >= ~12 batches
+  int tail;          // single-unit batches at the end of each head
 };
+// head x's units [s0, s1): nb B-unit batches, then single units; returns the batch count
+__device__ __forceinline__ int wq_head_split(int W, int x, int B, int tail, int& s0, int& nb) {
+  s0 = (int)((int64_t)W * x / WQ_HEADS);
+  const int s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
+  const int U = s1 - s0;
+  int t1 = U < tail ? U : tail;
+  t1 += (U - t1) % B;  // the B-unit part is whole batches
+  nb = (U - t1) / B;
+  return nb + t1;
+}
 // the static first-round batches of head x: one per wave of every block b < nblocks with b & 63 == x
 __device__ __forceinline__ int static_batches(const WorkTicket& t, int x) { return t.wpb * ((t.nblocks - x + 63) >> 6); }
-__device__ __forceinline__ WorkTicket wq_start(int wpb, int B = WQ_BATCH) {
+__device__ __forceinline__ WorkTicket wq_start(int wpb, int B, int tail) {
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  WorkTicket t{(int)(blockIdx.x & (WQ_HEADS - 1)), 0, wpb, (int)gridDim.x, B};
+  WorkTicket t{(int)(blockIdx.x & (WQ_HEADS - 1)), 0, wpb, (int)gridDim.x, B, tail};
   t.i = (int)(blockIdx.x >> 6) * wpb + wv - static_batches(t, t.x);
   return t;
 }
 __device__ __forceinline__ void wq_issue(uint32_t* heads, WorkTicket& t) {
   if (lane_id() == 0) t.i = (int)atomicAdd(heads + t.x * WQ_STRIDE, 1u);
-}
-__device__ __forceinline__ int wq_head_batches(int W, int x, int B) {
-  const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
-  return (s1 - s0 + B - 1) / B;
 }
 // the batch [first, first + count) of a ticket; count 0 = queue drained. A drained head costs one
 // wave-wide look at all 64 counters (lane l loads head l, device-coherent) and one atomic on a head
@@ -1103,13 +1129,12 @@ __device__ __forceinline__ int2 wq_resolve(uint32_t* heads, int W, WorkTicket& t
   for (;;) {
     const int x = t.x;
     const int bi = __builtin_amdgcn_readfirstlane(t.i) + static_batches(t, x);
-    if (bi < wq_head_batches(W, x, t.B)) {
-      const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
-      const int first = s0 + bi * t.B;
-      return make_int2(first, (s1 - first) < t.B ? (s1 - first) : t.B);
-    }
+    int s0, nb;
+    if (bi < wq_head_split(W, x, t.B, t.tail, s0, nb))
+      return bi < nb ? make_int2(s0 + bi * t.B, t.B) : make_int2(s0 + nb * t.B + (bi - nb), 1);
     const uint32_t taken = __hip_atomic_load(heads + lane * WQ_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t open = ballot((int)taken + static_batches(t, lane) < wq_head_batches(W, lane, t.B));
+    int ls0, lnb;
+    const uint64_t open = ballot((int)taken + static_batches(t, lane) < wq_head_split(W, lane, t.B, t.tail, ls0, lnb));
     if (!open) return make_int2(0, 0);
     // same XCD first (heads x & 7 + 8j), in rotation order after x; then the lowest open head
     const uint64_t same = open & (0x0101010101010101ull << (x & 7));
@@ -1184,6 +1209,7 @@ struct LeanArgs {
   ProfDev p;
   int wave_bytes, waves_per_block, units_per_wave;  // units_per_wave: work-queue batch size (<= LEAN_BATCH)
   int cache_ne, cache_pn;  // optional cache arrays present
+  int wq_tail;             // single-unit batches at the end of each work head (WorkTicket)
 };
 typedef const __attribute__((address_space(4))) LeanArgs* LArgs;
 __device__ __forceinline__ LArgs largs() {
@@ -1335,7 +1361,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   const UnitRec* recs = largs()->b.rec;
   const uint64_t* sws = largs()->b.sw;
   uint32_t* heads = largs()->b.wq;
-  WorkTicket tk = wq_start((int)(blockDim.x >> 6), largs()->units_per_wave);
+  WorkTicket tk = wq_start((int)(blockDim.x >> 6), largs()->units_per_wave, largs()->wq_tail);
 #ifdef KAD_PHASE_PROF
   const unsigned long long wt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz, device-wide
 #endif
@@ -1953,6 +1979,7 @@ struct WideArgs {
   ProfDev p;
   int waves_per_block;
   int cache_ne, cache_pn;
+  int wq_tail;  // single-unit batches at the end of each work head (WorkTicket)
   int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default; results differ from
             // the reference): bit 0 skips the pdqsort replay (ties taken by position), bit 1 ends each unit
             // after the filters, bit 2 after the scores (no selection), bit 3 skips the output pass
@@ -2076,7 +2103,11 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     recs = a->b.rec;
     sws = a->b.sw;
   }
-  WorkTicket tk = wq_start(nwaves);
+  WorkTicket tk = wq_start(nwaves, WQ_BATCH, wargs()->wq_tail);
+#ifdef KAD_PHASE_PROF
+  const unsigned long long wt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz, device-wide
+  unsigned long long wx_units = 0, wx_max = 0, wx_deq = wt_start, wx_str = 0;
+#endif
   // one VGPR per unit: lanes 0-15 its UnitRec dwords, lanes 16..16+2*nch its static filter words
   auto fetch = [&](int w) -> uint32_t {
     if (w < 0) return 0u;
@@ -2101,6 +2132,9 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         wn = nb.x;
         bend = nb.x + nb.y;
         wq_issue(heads, tk);  // resolved one batch later
+#ifdef KAD_PHASE_PROF
+        wx_deq = __builtin_amdgcn_s_memrealtime();
+#endif
       }
     }
     const uint32_t nxt = fetch(wn);
@@ -2489,9 +2523,29 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       KAD_PT(t4);
       KAD_PADD(3, t4 - t3);
     } while (false);
+#ifdef KAD_PHASE_PROF
+    {
+      KAD_PT(tz);
+      wx_units++;
+      wx_max = (tz - t0) > wx_max ? (tz - t0) : wx_max;
+    }
+#endif
     cur = nxt;
     w = wn;
   }
+#ifdef KAD_PHASE_PROF
+  {
+    const int gwv = blockIdx.x * nwaves + wv;
+    if (lane == 0 && gwv < 8192) {
+      g_wavetime[2 * gwv] = wt_start;
+      g_wavetime[2 * gwv + 1] = __builtin_amdgcn_s_memrealtime();
+      g_wavex[4 * gwv] = wx_units;
+      g_wavex[4 * gwv + 1] = wx_max;
+      g_wavex[4 * gwv + 2] = wx_deq;
+      g_wavex[4 * gwv + 3] = pacc[4];
+    }
+  }
+#endif
   KAD_PFLUSH_LEAN;
 }
 
@@ -2518,6 +2572,7 @@ constexpr int ROW_WAVES = ROW_THREADS / 64;
 constexpr int ROW_MAX_C = 12288;
 constexpr int ROW_MAX_TERMS = 8;  // preferred terms held as per-chunk words (8 x nch x 8 B = Cp bytes)
 constexpr int ROW_NREP = 2048;    // replays of up to this many positions keep their scratch in LDS
+constexpr int ROW_BLOCK_PART = 256;  // replay partitions of longer ranges run on every wave of the block
 static_assert(ROW_MAX_BLOCKS >= 1, "row kernel slabs");
 struct RowKLayout {
   size_t key, idx, x, pid, posl, posr, sw, cnt, hist, red, bytes;
@@ -2759,17 +2814,17 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
       const int j1 = j0 + ROW_THREADS;
       const bool v1 = j1 < n;
       const uint32_t c0 = idx[j0], c1 = idx[v1 ? j1 : j0];
-      int64_t ac[2], uc[2], am[2], um[2];
+      double4 r4[2];
+      float2 iv[2];
       uint64_t pn[2][TFOLD_MAX_TW];
       const uint32_t cs[2] = {c0, c1};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        ac[u] = uc[u] = am[u] = um[u] = 0;
-        if (s_res) {
-          ac[u] = ldg(as->s.alloc_cpu, cs[u]);
-          uc[u] = ldg(as->s.used_cpu, cs[u]);
-          am[u] = ldg(as->s.alloc_mem, cs[u]);
-          um[u] = ldg(as->s.used_mem, cs[u]);
+        r4[u] = make_double4(0.0, 0.0, 1.0, 1.0);
+        iv[u] = make_float2(0.f, 0.f);
+        if (s_res) {  // (available cpu, available mem, cap cpu, cap mem) as f64, f32 100 / cap
+          r4[u] = as->s.res4[cs[u]];
+          iv[u] = as->s.res_iv[cs[u]];
         }
 #pragma unroll
         for (int tw = 0; tw < TFOLD_MAX_TW; ++tw)
@@ -2782,9 +2837,9 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
         const uint32_t c = cs[u];
         int x = 0;
         if (s_res) {  // the wide kernel's clean path: x = available - request, exact in f64
-          const double capc = (double)ac[u], capm = (double)am[u];
-          const double xc = (double)(ac[u] - uc[u]) - rqcd, xm = (double)(am[u] - um[u]) - rqmd;
-          const float ivc = (float)(100.0 / capc), ivm = (float)(100.0 / capm);
+          const double capc = r4[u].z, capm = r4[u].w;
+          const double xc = r4[u].x - rqcd, xm = r4[u].y - rqmd;
+          const float ivc = iv[u].x, ivm = iv[u].y;
           const double xcp = fmax(xc, 0.0), xmp = fmax(xm, 0.0);
           const int okc = -(int)(xc >= 0.0), okm = -(int)(xm >= 0.0);
           if (sm & BIT(KAD_PL_LEAST_ALLOCATED)) x += (quot100(xcp, capc, ivc) + quot100(xmp, capm, ivm)) >> 1;
@@ -2910,16 +2965,20 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
             pid[j] = (uint16_t)j;
         }
         __syncthreads();
-        if (wv == 0) {
-          const int xs_b = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
-          const int xs_c = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
-          if (packed && in_lds) {
-            PdqWaveP<> pw{key, posl, posr, xs_b, xs_c};
-            pw.select(n, k);
-          } else if (packed) {  // elements stay in LDS; stopper scratch in the slab (workgroup fences order both)
-            PdqWaveP<true> pw{key, posl, posr, xs_b, xs_c};
-            pw.select(n, k);
-          } else if (in_lds) {
+        const int xs_b = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 7 : 17;
+        const int xs_c = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
+        // packed: the partitions of ranges longer than ROW_BLOCK_PART run on all 8 waves, then wave 0 goes
+        // on alone (red[] is free scratch here)
+        if (packed && in_lds) {
+          PdqWaveP<> pw{key, posl, posr, xs_b, xs_c};
+          const auto st = pw.select_block(n, k, ROW_BLOCK_PART, ROW_WAVES, wv, red);
+          if (wv == 0) pw.select_from(st, k);
+        } else if (packed) {  // elements stay in LDS; stopper scratch in the slab (workgroup fences order both)
+          PdqWaveP<true> pw{key, posl, posr, xs_b, xs_c};
+          const auto st = pw.select_block(n, k, ROW_BLOCK_PART, ROW_WAVES, wv, red);
+          if (wv == 0) pw.select_from(st, k);
+        } else if (wv == 0) {
+          if (in_lds) {
             PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
             pw.select(n, k);
           } else {  // keys stay in LDS; positions in the slab (workgroup-scope fences order both)
@@ -3468,6 +3527,10 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
 // ================================================================ launchers
 int debug_phase_counters(uint64_t* out, int reset) {
 #ifdef KAD_PHASE_PROF
+  if (reset == -2) {  // the wide kernel's per-wave extras: out holds 8192 * 4 entries
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavex), sizeof(unsigned long long) * 8192 * 4) != hipSuccess) return -1;
+    return 8192;
+  }
   if (reset < 0) {  // the lean kernel's per-wave (start, end) timestamps: out holds 8192 * 2 entries
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavetime), sizeof(unsigned long long) * 8192 * 2) != hipSuccess) return -1;
     return 8192;
@@ -3492,11 +3555,13 @@ int debug_phase_counters(uint64_t* out, int reset) {
 
 static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 
-hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st) {
+hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st, bool zero_rows, bool* zeroed) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
   const long lanes = (long)b.n_rowreq * nch;
-  if (lanes > 0) hipLaunchKernelGGL(req_row_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, s, b);
+  *zeroed = zero_rows && lanes > 0;
+  if (lanes > 0)
+    hipLaunchKernelGGL(req_row_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, s, b, zero_rows ? 1 : 0);
   const int ngrp = (nch + REQ_G - 1) / REQ_G;
   const long waves = (long)b.n_seg * ngrp;
   if (waves > 0) hipLaunchKernelGGL(req_mask_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, b, ngrp);
@@ -3508,6 +3573,15 @@ hipError_t launch_value_rows(const SnapDev& s, uint64_t* vrows, hipStream_t st) 
   const long waves = (long)s.K * ((s.C + 63) >> 6);
   if (waves == 0) return hipSuccess;
   hipLaunchKernelGGL(value_rows_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, vrows);
+  return hipGetLastError();
+}
+
+hipError_t launch_res_cols(const SnapDev& s, void* buf, hipStream_t st) {
+  (void)hipGetLastError();
+  if (s.C <= 0) return hipSuccess;
+  double4* r4 = static_cast<double4*>(buf);
+  hipLaunchKernelGGL(res_cols_kernel, dim3((unsigned)((s.C + 255) / 256)), dim3(256), 0, st, s, r4,
+                     reinterpret_cast<float2*>(r4 + s.C));
   return hipGetLastError();
 }
 
@@ -3544,6 +3618,12 @@ static int n_cus() {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
   }
   return n_cu;
+}
+
+// single-unit batches at the end of each work head: KAD_WQ_TAIL (profiling builds) per wave of the head
+static int wq_tail(int total_waves) {
+  static const int per_wave = tuning_env("KAD_WQ_TAIL", 0);
+  return per_wave * ((total_waves + WQ_HEADS - 1) / WQ_HEADS);
 }
 
 // the wide kernel takes clean snapshots with WIDE_MIN_NCH <= nch <= WIDE_MAX_NCH
@@ -3630,7 +3710,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const long need = ((long)b.W + wpb - 1) / wpb;
     if (grid > need) grid = need;
     static const int exp = tuning_env("KAD_WIDE_EXPERIMENT", 0);
-    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, exp};
+    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, wq_tail((int)grid * wpb), exp};
     const bool beside = b.early_rows && b.use_rows && side && fork && join;
     if (beside) {  // the row kernel on the side stream, from the end of prep_kernel, beside the wide kernel
       if (hipError_t e = hipEventRecord(fork, st)) return e;
@@ -3684,7 +3764,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const long upw = ((long)b.W + grid * wpb - 1) / (grid * wpb);
     int bsz = (int)(upw / 6);
     bsz = bsz < 1 ? 1 : (bsz > LEAN_BATCH ? LEAN_BATCH : bsz);
-    const LeanArgs A{s, b, o, p, (int)lb, wpb, bsz, cache_ne, cache_pn};
+    const LeanArgs A{s, b, o, p, (int)lb, wpb, bsz, cache_ne, cache_pn, bsz > 1 ? wq_tail((int)grid * wpb) : 0};
     switch (nch) {
       case 1: cl ? launch_lean<1, true>(A, (int)grid, lds, st) : launch_lean<1, false>(A, (int)grid, lds, st); break;
       case 2: cl ? launch_lean<2, true>(A, (int)grid, lds, st) : launch_lean<2, false>(A, (int)grid, lds, st); break;

@@ -996,10 +996,199 @@ struct PdqWaveP {
     *npairs = t_n;
     return m;
   }
-  __device__ void select(int n, int k) const {
-    int a = 0, b = n;
-    int limit = 32 - __clz(n);
-    bool wasBalanced = true, wasPartitioned = true;
+  // ---- workgroup-wide replay of the long ranges (schedule_row_kernel): every wave of the block runs the
+  // same scalar control flow on the same LDS data; partitions of ranges longer than `thr` are split over
+  // the waves, the rare O(1) / rare-path steps run on wave 0 between barriers. The state is then handed to
+  // wave 0 (select_from) for the short ranges.
+  struct State {
+    int a, b, limit;
+    bool wasBalanced, wasPartitioned, done;
+  };
+  // partition / partitionEqual of [a, b) over nw waves (fused(), same permutation): pass 1 counts each
+  // wave's stoppers over its contiguous chunk segment, scatters them at the block offsets; pass 2 hands
+  // t-chunks of the stopper pairs round-robin to the waves. sh: LDS ints [3 * nw]. Returns #R; *swapped:
+  // some misplaced pair was exchanged (Go's alreadyPartitioned is its negation). Callers barrier before
+  // (every wave's earlier reads of e are done); returns after a barrier.
+  __device__ int fused_block(int a, int b, int pivot, uint32_t P, bool strict, bool* swapped, int nw, int wv,
+                             int* sh) const {
+    const int lane = lane_id();
+    const uint32_t Ea = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[a]);
+    const uint32_t thr = strict ? ((P << 16) | 0xFFFFu) : ((P << 16) - 1u);
+    const bool P0eq = !strict && P == 0;
+    const int first = a + 1;
+    const int nchunk = (b - first + WAVE - 1) / WAVE;
+    const int per = (nchunk + nw - 1) / nw;
+    const int c_lo = wv * per, c_hi = (c_lo + per) < nchunk ? (c_lo + per) : nchunk;
+    auto classify = [&](int c, int& p) -> bool {
+      p = first + c * WAVE + lane;
+      const bool in = p < b;
+      const uint32_t raw = e[in ? p : b - 1];
+      const uint32_t v = p == pivot ? Ea : raw;
+      return in && (P0eq || v > thr);
+    };
+    int myR = 0, myL = 0;
+    for (int c = c_lo; c < c_hi; ++c) {
+      int p;
+      const int nr = popc64(ballot(classify(c, p)));
+      const int nin = b - (first + c * WAVE) < WAVE ? b - (first + c * WAVE) : WAVE;
+      myR += nr;
+      myL += nin - nr;
+    }
+    if (lane == 0) {
+      sh[wv] = myR;
+      sh[nw + wv] = myL;
+    }
+    __syncthreads();
+    int offR = 0, offL = 0, cR = 0, cL = 0;
+    for (int i = 0; i < nw; ++i) {
+      const int r = sh[i], l = sh[nw + i];
+      offR += i < wv ? r : 0;
+      offL += i < wv ? l : 0;
+      cR += r;
+      cL += l;
+    }
+    for (int c = c_lo; c < c_hi; ++c) {  // only the range's last chunk has lanes past b: into posL's tail
+      int p;
+      const bool isR = classify(c, p);
+      const uint64_t mR = ballot(isR);
+      const int rR = mbcnt(mR);
+      uint16_t* dst = isR ? posR + (offR + rR) : posL + (offL + lane - rR);
+      *dst = (uint16_t)p;
+      const int nin = b - (first + c * WAVE) < WAVE ? b - (first + c * WAVE) : WAVE;
+      const int nr = popc64(mR);
+      offR += nr;
+      offL += nin - nr;
+    }
+    __syncthreads();
+    const int m = cR;
+    const int j = a + m;
+    const uint32_t Ep = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[pivot]);
+    const uint32_t Sj = j == pivot ? Ea : (j == a ? Ep : (uint32_t)__builtin_amdgcn_readfirstlane((int)e[j]));
+    __syncthreads();  // every wave read the special positions before any pair is written
+    const bool Ea_R = P0eq || Ea > thr;
+    const bool pivot_paired = pivot != a && (pivot <= j ? !Ea_R : Ea_R);
+    const bool j_paired = strict && m > 0 && !(P0eq || Sj > thr);
+    const int np = cL < cR ? cL : cR;
+    bool any = false;
+    for (int t0 = wv * WAVE; t0 < np; t0 += nw * WAVE) {
+      const int t = t0 + lane;
+      const int l = posL[t];  // t < np + 64 <= n + 64: inside posL
+      const int ri = cR - 1 - t;
+      const int r = posR[ri > 0 ? ri : 0];
+      const bool sw = t < np && l < r;
+      const uint64_t mk = ballot(sw);
+      any |= mk != 0;
+      if (sw) {
+        const uint32_t el = e[l], er = e[r];
+        const uint32_t vl = l == pivot ? Ea : el, vr = r == pivot ? Ea : er;
+        e[r] = vl;
+        e[strict && l == j ? a : l] = vr;
+      }
+      if (~mk) break;  // a prefix: every later t fails
+    }
+    if (lane == 0) sh[2 * nw + wv] = any ? 1 : 0;
+    __syncthreads();
+    if (wv == 0 && lane == 0) {
+      if (strict) {
+        if (m > 0 && !j_paired) e[a] = Sj;
+        e[j] = Ep;
+      } else if (pivot != a) {
+        e[a] = Ep;
+      }
+      if (pivot != a && !pivot_paired && !(strict && pivot == j)) e[pivot] = Ea;
+    }
+    int anyall = 0;
+    for (int i = 0; i < nw; ++i) anyall |= sh[2 * nw + i];
+    __syncthreads();
+    *swapped = anyall != 0;
+    return m;
+  }
+  __device__ State select_block(int n, int k, int thr, int nw, int wv, int* sh) const {
+    State s{0, n, 32 - __clz(n), true, true, false};
+    while (s.a < k && k < s.b && s.b - s.a > thr) {  // thr >= 12: no insertion sort here
+      const int a = s.a, b = s.b, length = b - a;
+      if (s.limit == 0) {
+        if (wv == 0 && lane_id() == 0) {
+          PackedLdsStore st{e};
+          PdqT<PackedLdsStore> hs{st, xs_b, xs_c};
+          hs.heap_sort(a, b);
+        }
+        __syncthreads();
+        s.done = true;
+        return s;
+      }
+      if (!s.wasBalanced) {
+        if (wv == 0) break_patterns(a, b);
+        __syncthreads();
+        s.limit--;
+      }
+      int hint;
+      uint32_t pk, prev;
+      int pivot = choose_pivot(a, b, hint, pk, prev);
+      if (hint == 2) {
+        __syncthreads();
+        if (wv == 0) reverse_range(a, b);
+        __syncthreads();
+        pivot = (b - 1) - (pivot - a);
+        hint = 1;
+      }
+      if (s.wasBalanced && s.wasPartitioned && hint == 1) {
+        __syncthreads();
+        if (wv == 0) {
+          const bool d = partial_insertion_sort(a, b);
+          if (lane_id() == 0) sh[0] = d ? 1 : 0;
+        }
+        __syncthreads();
+        const bool d = __builtin_amdgcn_readfirstlane(sh[0]) != 0;
+        if (d) {
+          __syncthreads();
+          s.done = true;
+          return s;
+        }
+        pk = E(pivot) >> 16;
+        if (a > 0) prev = E(a - 1) >> 16;
+      }
+      __syncthreads();  // every wave's reads of e are done before the partition writes
+      bool swapped;
+      if (a > 0 && !(prev > pk)) {  // !less(a-1, pivot): partitionEqual
+        s.a = a + 1 + fused_block(a, b, pivot, pk, false, &swapped, nw, wv, sh);
+        continue;
+      }
+      const int mid = a + fused_block(a, b, pivot, pk, true, &swapped, nw, wv, sh);
+      s.wasPartitioned = !swapped;
+      const int leftLen = mid - a, rightLen = b - mid, bt = length / 8;
+      if (leftLen < rightLen) {
+        if (k < mid) {
+          s.b = mid;
+          s.wasBalanced = s.wasPartitioned = true;
+        } else if (k > mid + 1) {
+          s.wasBalanced = leftLen >= bt;
+          s.a = mid + 1;
+        } else {
+          s.done = true;
+          return s;
+        }
+      } else {
+        if (k > mid + 1) {
+          s.a = mid + 1;
+          s.wasBalanced = s.wasPartitioned = true;
+        } else if (k < mid) {
+          s.wasBalanced = rightLen >= bt;
+          s.b = mid;
+        } else {
+          s.done = true;
+          return s;
+        }
+      }
+    }
+    return s;
+  }
+  __device__ void select(int n, int k) const { select_from(State{0, n, 32 - __clz(n), true, true, false}, k); }
+  __device__ void select_from(State st, int k) const {
+    if (st.done) return;
+    int a = st.a, b = st.b;
+    int limit = st.limit;
+    bool wasBalanced = st.wasBalanced, wasPartitioned = st.wasPartitioned;
     while (a < k && k < b) {
       const int length = b - a;
       if (length <= 12) {

@@ -76,7 +76,8 @@ def main():
         live = np.nonzero(en > 0)[0]
         if len(live):
             # s_memrealtime (100 MHz, device-wide); also split by XCD (4-wave blocks round-robin over 8 XCDs)
-            xcd = (live // 4) % 8
+            wpb = 16 if a.config == "c3" else 4  # wide kernel: 16-wave blocks; lean: 4
+            xcd = (live // wpb) % 8
             span_all = float(en[live].max() - st[live].min())
             out["lean_span_us"] = span_all / 100.0
             out["lean_wave_lifetime_frac"] = round(float((en[live] - st[live]).mean()) / span_all, 3)
@@ -95,6 +96,20 @@ def main():
                 ss.append(float(s0.max() - s0.min()) / span)
                 es.append(float(e0.max() - e0.min()) / span)
             out["lean_waves"] = int(len(live))
+            wx = np.zeros(8192 * 4, dtype=np.uint64)
+            if a.config == "c3" and L.kad_debug_phase_counters(wx.ctypes.data, -2) > 0:
+                # wide kernel: late waves (last 10 % of ends) vs the rest — units, longest unit, last dequeue
+                units, umax, deq = wx[0::4].astype(np.int64), wx[1::4].astype(np.int64), wx[2::4].astype(np.int64)
+                endf = (en[live] - st[live].min()) / span_all
+                late = live[endf >= np.percentile(endf, 90)]
+                rest = live[endf < np.percentile(endf, 90)]
+                for nm, sel in (("late", late), ("rest", rest)):
+                    out[f"wide_{nm}_units_mean"] = round(float(units[sel].mean()), 2)
+                    out[f"wide_{nm}_maxunit_cycles_mean"] = round(float(umax[sel].mean()), 1)
+                    out[f"wide_{nm}_last_dequeue_frac_mean"] = round(float((deq[sel] - st[live].min()).mean()) / span_all, 3)
+                    out[f"wide_{nm}_end_frac_mean"] = round(float((en[sel] - st[live].min()).mean()) / span_all, 3)
+                out["wide_units_p10_p50_p90"] = [int(np.percentile(units[live], q)) for q in (10, 50, 90)]
+                out["wide_end_frac_hist10"] = np.histogram(endf, bins=10, range=(0, 1))[0].tolist()
             out["lean_wave_lifetime_frac_per_xcd"] = [round(v, 3) for v in fr]
             out["lean_start_spread_frac_per_xcd"] = [round(v, 3) for v in ss]
             out["lean_end_spread_frac_per_xcd"] = [round(v, 3) for v in es]
