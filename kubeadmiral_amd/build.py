@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libkad.so")
 SOURCES = ["kad_kernels.hip", "kad_trigger.hip", "kad_delta.hip", "kad_diff.hip", "kad_api.hip", "kad_pack.cpp"]
-HEADERS = ["kad_device.h", "kad_wave.h", "kad_select.h", "kad_plan.h"]
+HEADERS = ["kad_device.h", "kad_wave.h", "kad_select.h", "kad_plan.h", "kad_pool.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KAD_OFFLOAD_ARCH", "gfx950")
 

@@ -14,6 +14,7 @@
 
 #include "../../include/kad_sched.h"
 #include "kad_device.h"
+#include "kad_pool.h"
 
 using namespace kad;
 
@@ -148,14 +149,12 @@ static int to_dev(kad_ctx* c, const T* h, size_t n, T** d, std::vector<void*>& o
 // [lo, hi) pieces of n on up to 16 host threads
 template <class F>
 static void host_parallel(int n, F f, int serial_below = 4096) {
-  const int T = n < serial_below ? 1 : (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  const int T = n < serial_below ? 1 : kadpool::pool().threads();
   if (T <= 1) {
     f(0, n);
     return;
   }
-  std::vector<std::thread> th;
-  for (int t = 0; t < T; t++) th.emplace_back([=, &f] { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
-  for (auto& x : th) x.join();
+  kadpool::pool().run(T, [&](int t) { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
 }
 // the smallest i in [0, n) with bad(i), or -1: pieces checked on up to 16 host threads, each
 // stopping at its first failure or once an earlier one is known — the same index, so the same
@@ -168,22 +167,19 @@ static int64_t first_bad(int64_t n, F bad) {
     return -1;
   }
   std::atomic<int64_t> best{INT64_MAX};
-  const int T = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-  std::vector<std::thread> th;
-  for (int t = 0; t < T; t++)
-    th.emplace_back([&, t] {
-      const int64_t lo = n * t / T, hi = n * (t + 1) / T;
-      for (int64_t i = lo; i < hi; i++) {
-        if ((i & 1023) == 0 && i > best.load(std::memory_order_relaxed)) return;
-        if (bad(i)) {
-          int64_t cur = best.load();
-          while (i < cur && !best.compare_exchange_weak(cur, i)) {
-          }
-          return;
+  const int T = kadpool::pool().threads();
+  kadpool::pool().run(T, [&](int t) {
+    const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+    for (int64_t i = lo; i < hi; i++) {
+      if ((i & 1023) == 0 && i > best.load(std::memory_order_relaxed)) return;
+      if (bad(i)) {
+        int64_t cur = best.load();
+        while (i < cur && !best.compare_exchange_weak(cur, i)) {
         }
+        return;
       }
-    });
-  for (auto& x : th) x.join();
+    }
+  });
   const int64_t r = best.load();
   return r == INT64_MAX ? -1 : r;
 }

@@ -32,8 +32,8 @@ __device__ unsigned long long g_phase[256 * 32];
 // lean kernel: (start, end) s_memtime of every wave of the last launch, for the wave-lifetime split
 __device__ unsigned long long g_wavetime[8192 * 2];
 // wide kernel: per wave (units taken, the longest unit's s_memtime cycles, realtime of the last dequeue, units
-// that straddled a tie)
-__device__ unsigned long long g_wavex[8192 * 4];
+// that straddled a tie, HW_ID, XCC_ID)
+__device__ unsigned long long g_wavex[8192 * 6];
 #define KAD_PT(v) const unsigned long long v = __builtin_readcyclecounter()
 #define KAD_PACC uint32_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
@@ -1089,37 +1089,26 @@ static_assert(WQ_HEADS == 64, "drained-head set is one u64; heads map to XCDs by
 // batch of work. Every wave's first batch is static (no atomic): wave wv of block b takes batch
 // (b >> 6) * wpb + wv of head b & 63, and that head's atomics count on from its static_batches.
 // Every wave ends once all heads are drained.
-// Guided tail: the last `tail` units of every head go out one per batch, so the waves that drain the
-// queue last finish within about one unit of each other instead of one B-unit batch (a batch of B
-// tie-straddling units is ~4x an average unit: at C3 / 125k units per GPU that batch tail was the bulk of
-// the wide kernel's ~60 us fixed cost).
 struct WorkTicket {
   int x;             // head of the pending ticket
   int i;             // its atomicAdd result (lane 0); batch index = i + static_batches(x)
   int wpb, nblocks;  // waves per block, grid size: the static first round
   int B;             // units per batch (<= WQ_BATCH): small enough that a wave takes >= ~12 batches
-  int tail;          // single-unit batches at the end of each head
 };
-// head x's units [s0, s1): nb B-unit batches, then single units; returns the batch count
-__device__ __forceinline__ int wq_head_split(int W, int x, int B, int tail, int& s0, int& nb) {
-  s0 = (int)((int64_t)W * x / WQ_HEADS);
-  const int s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
-  const int U = s1 - s0;
-  int t1 = U < tail ? U : tail;
-  t1 += (U - t1) % B;  // the B-unit part is whole batches
-  nb = (U - t1) / B;
-  return nb + t1;
-}
 // the static first-round batches of head x: one per wave of every block b < nblocks with b & 63 == x
 __device__ __forceinline__ int static_batches(const WorkTicket& t, int x) { return t.wpb * ((t.nblocks - x + 63) >> 6); }
-__device__ __forceinline__ WorkTicket wq_start(int wpb, int B, int tail) {
+__device__ __forceinline__ WorkTicket wq_start(int wpb, int B = WQ_BATCH) {
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  WorkTicket t{(int)(blockIdx.x & (WQ_HEADS - 1)), 0, wpb, (int)gridDim.x, B, tail};
+  WorkTicket t{(int)(blockIdx.x & (WQ_HEADS - 1)), 0, wpb, (int)gridDim.x, B};
   t.i = (int)(blockIdx.x >> 6) * wpb + wv - static_batches(t, t.x);
   return t;
 }
 __device__ __forceinline__ void wq_issue(uint32_t* heads, WorkTicket& t) {
   if (lane_id() == 0) t.i = (int)atomicAdd(heads + t.x * WQ_STRIDE, 1u);
+}
+__device__ __forceinline__ int wq_head_batches(int W, int x, int B) {
+  const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
+  return (s1 - s0 + B - 1) / B;
 }
 // the batch [first, first + count) of a ticket; count 0 = queue drained. A drained head costs one
 // wave-wide look at all 64 counters (lane l loads head l, device-coherent) and one atomic on a head
@@ -1129,12 +1118,13 @@ __device__ __forceinline__ int2 wq_resolve(uint32_t* heads, int W, WorkTicket& t
   for (;;) {
     const int x = t.x;
     const int bi = __builtin_amdgcn_readfirstlane(t.i) + static_batches(t, x);
-    int s0, nb;
-    if (bi < wq_head_split(W, x, t.B, t.tail, s0, nb))
-      return bi < nb ? make_int2(s0 + bi * t.B, t.B) : make_int2(s0 + nb * t.B + (bi - nb), 1);
+    if (bi < wq_head_batches(W, x, t.B)) {
+      const int s0 = (int)((int64_t)W * x / WQ_HEADS), s1 = (int)((int64_t)W * (x + 1) / WQ_HEADS);
+      const int first = s0 + bi * t.B;
+      return make_int2(first, (s1 - first) < t.B ? (s1 - first) : t.B);
+    }
     const uint32_t taken = __hip_atomic_load(heads + lane * WQ_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ls0, lnb;
-    const uint64_t open = ballot((int)taken + static_batches(t, lane) < wq_head_split(W, lane, t.B, t.tail, ls0, lnb));
+    const uint64_t open = ballot((int)taken + static_batches(t, lane) < wq_head_batches(W, lane, t.B));
     if (!open) return make_int2(0, 0);
     // same XCD first (heads x & 7 + 8j), in rotation order after x; then the lowest open head
     const uint64_t same = open & (0x0101010101010101ull << (x & 7));
@@ -1209,7 +1199,6 @@ struct LeanArgs {
   ProfDev p;
   int wave_bytes, waves_per_block, units_per_wave;  // units_per_wave: work-queue batch size (<= LEAN_BATCH)
   int cache_ne, cache_pn;  // optional cache arrays present
-  int wq_tail;             // single-unit batches at the end of each work head (WorkTicket)
 };
 typedef const __attribute__((address_space(4))) LeanArgs* LArgs;
 __device__ __forceinline__ LArgs largs() {
@@ -1361,7 +1350,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   const UnitRec* recs = largs()->b.rec;
   const uint64_t* sws = largs()->b.sw;
   uint32_t* heads = largs()->b.wq;
-  WorkTicket tk = wq_start((int)(blockDim.x >> 6), largs()->units_per_wave, largs()->wq_tail);
+  WorkTicket tk = wq_start((int)(blockDim.x >> 6), largs()->units_per_wave);
 #ifdef KAD_PHASE_PROF
   const unsigned long long wt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz, device-wide
 #endif
@@ -1979,7 +1968,6 @@ struct WideArgs {
   ProfDev p;
   int waves_per_block;
   int cache_ne, cache_pn;
-  int wq_tail;  // single-unit batches at the end of each work head (WorkTicket)
   int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default; results differ from
             // the reference): bit 0 skips the pdqsort replay (ties taken by position), bit 1 ends each unit
             // after the filters, bit 2 after the scores (no selection), bit 3 skips the output pass
@@ -2103,7 +2091,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     recs = a->b.rec;
     sws = a->b.sw;
   }
-  WorkTicket tk = wq_start(nwaves, WQ_BATCH, wargs()->wq_tail);
+  WorkTicket tk = wq_start(nwaves);
 #ifdef KAD_PHASE_PROF
   const unsigned long long wt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz, device-wide
   unsigned long long wx_units = 0, wx_max = 0, wx_deq = wt_start, wx_str = 0;
@@ -2539,10 +2527,12 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     if (lane == 0 && gwv < 8192) {
       g_wavetime[2 * gwv] = wt_start;
       g_wavetime[2 * gwv + 1] = __builtin_amdgcn_s_memrealtime();
-      g_wavex[4 * gwv] = wx_units;
-      g_wavex[4 * gwv + 1] = wx_max;
-      g_wavex[4 * gwv + 2] = wx_deq;
-      g_wavex[4 * gwv + 3] = pacc[4];
+      g_wavex[6 * gwv] = wx_units;
+      g_wavex[6 * gwv + 1] = wx_max;
+      g_wavex[6 * gwv + 2] = wx_deq;
+      g_wavex[6 * gwv + 3] = pacc[4];
+      g_wavex[6 * gwv + 4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      g_wavex[6 * gwv + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     }
   }
 #endif
@@ -2587,9 +2577,10 @@ __host__ __device__ inline RowKLayout rowk_layout(int C) {
   L.posl = L.pid + 2 * ROW_NREP;
   L.posr = L.posl + 2 * ROW_NREP + 128;
   const size_t xb = Cp > 6 * (size_t)ROW_NREP + 128 ? Cp : 6 * (size_t)ROW_NREP + 128;
-  L.sw = (L.x + xb + 15) & ~(size_t)15;   // u64[nch]: the unit's static words
-  L.cnt = L.sw + 8 * nch;                 // i32[nch + 1]: chunk counts → exclusive prefix (+ total)
-  L.hist = (L.cnt + 4 * (nch + 1) + 15) & ~(size_t)15;  // u32[256]
+  L.sw = (L.x + xb + 15) & ~(size_t)15;   // u64[2][nch]: the unit's static words (two buffers: the next
+  L.cnt = L.sw + 16 * nch;                //   unit's are prefetched); i32[2][nch + 1]: chunk counts →
+                                          //   exclusive prefix (+ total)
+  L.hist = (L.cnt + 8 * (nch + 1) + 15) & ~(size_t)15;  // u32[256]
   L.red = L.hist + 4 * 256;               // i32[4][ROW_WAVES] per-wave partials, i32[24] broadcasts
   L.bytes = L.red + 4 * (4 * ROW_WAVES + 24);
   return L;
@@ -2605,6 +2596,8 @@ struct RowArgs {
   OutDev o;
   ProfDev p;
   char* slabs;  // [grid][row_slab_bytes(C)]
+  int exp;      // measurement-only variants (profiling builds, KAD_ROW_EXPERIMENT; results differ): bit 0 no
+                // resource scores, bit 1 no PreferNoSchedule counts, bit 2 no affinity scores
 };
 typedef const __attribute__((address_space(4))) RowArgs* RArgs;
 __device__ __forceinline__ RArgs rargs() {
@@ -2633,9 +2626,9 @@ __device__ __forceinline__ int row_block_sum(int v, int* red) {
   __syncthreads();
   return m;
 }
-// exclusive prefix of cnt[0..m) in place by wave 0, total in cnt[m]; callers sync before and after
-__device__ __forceinline__ void row_exclusive_scan(int* cnt, int m) {
-  if ((threadIdx.x >> 6) != 0) return;
+// exclusive prefix of cnt[0..m) in place by wave `by`, total in cnt[m]; callers sync before and after
+__device__ __forceinline__ void row_exclusive_scan(int* cnt, int m, int by = 0) {
+  if ((int)(threadIdx.x >> 6) != by) return;
   const int lane = lane_id();
   int carry = 0;
   for (int c0 = 0; c0 < m; c0 += WAVE) {
@@ -2673,32 +2666,70 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
   uint64_t* termw = (uint64_t*)(smem + L.x);  // preferred-term words (scoring and normalisation only)
   uint16_t* pid_g;  // the block's global slab (replays longer than ROW_NREP)
   pid_g = (uint16_t*)(rargs()->slabs + (size_t)blockIdx.x * row_slab_bytes(C));
-  uint64_t* swl = (uint64_t*)(smem + L.sw);
-  int32_t* cnt = (int32_t*)(smem + L.cnt);
+  uint64_t* const swl0 = (uint64_t*)(smem + L.sw);
+  int32_t* const cnt0 = (int32_t*)(smem + L.cnt);
   uint32_t* hist = (uint32_t*)(smem + L.hist);
   int32_t* red = (int32_t*)(smem + L.red);
   int32_t* bc = red + 4 * ROW_WAVES;  // broadcasts
+#if defined(KAD_PHASE_PROF) || defined(KAD_TUNING)
+  const int rexp = rargs()->exp;
+#else
+  constexpr int rexp = 0;
+#endif
   const bool s_res =
-      sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION));
-  const bool s_tt = sm & BIT(KAD_PL_TAINT_TOLERATION);
+      (sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION))) && !(rexp & 1);
+  const bool s_tt = (sm & BIT(KAD_PL_TAINT_TOLERATION)) && !(rexp & 2);
 
   KAD_PACC;
-  // the next unit's list index is dequeued one unit ahead (thread 0), so the returning atomic's latency
-  // overlaps the current unit
+  // the next unit's list index is dequeued one unit ahead (thread 64, wave 1's lane 0), so the returning
+  // atomic's latency overlaps the current unit. While wave 0 replays (or before the output pass) wave 1
+  // also prefetches the next unit: its static words, chunk counts and their prefix into the other LDS
+  // buffer (bc[20]: the prefetched unit, -1 the list is drained, -2 nothing prefetched); the list is
+  // complete before this kernel starts (prep_kernel's early routing, or the lean kernel before it)
   int ticket = 0;
-  if (tid == 0) ticket = atomicAdd(rargs()->b.rows_head, 1);
+  if (tid == 64) ticket = atomicAdd(rargs()->b.rows_head, 1);
+  if (tid == 0) bc[20] = -2;
+  int par = 0;  // the current unit's buffers
+  auto next_unit = [&]() -> int {  // thread 64 only
+    RArgs a = rargs();
+    const int rn = __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int nx = ticket < rn ? a->b.rows[ticket] : -1;
+    if (ticket < rn) ticket = atomicAdd(a->b.rows_head, 1);
+    return nx;
+  };
+  auto prefetch = [&]() {  // wave 1
+    if (lane == 0) bc[20] = next_unit();
+    wave_sync();
+    const int nx = __builtin_amdgcn_readfirstlane(bc[20]);
+    if (nx < 0) return;
+    uint64_t* sw2 = swl0 + (size_t)(par ^ 1) * nch;
+    int32_t* c2 = cnt0 + (size_t)(par ^ 1) * (nch + 1);
+    const uint64_t* src = rargs()->b.sw + (size_t)nx * nch;
+    for (int ch = lane; ch < nch; ch += WAVE) {
+      const uint64_t m = ldg(src, (uint32_t)ch);
+      sw2[ch] = m;
+      c2[ch] = popc64(m);
+    }
+    wave_sync();
+    row_exclusive_scan(c2, nch, 1);
+  };
   for (;;) {
-    __syncthreads();  // the previous unit's LDS reads are done
+    __syncthreads();  // the previous unit's LDS reads (and wave 1's prefetch) are done
     KAD_PT(t0);
-    if (tid == 0) {
-      RArgs a = rargs();
-      const int rn = __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bc[0] = ticket < rn ? a->b.rows[ticket] : -1;
-      if (ticket < rn) ticket = atomicAdd(a->b.rows_head, 1);
+    if (tid == 64) {
+      const int pf = bc[20];
+      bc[21] = pf != -2 ? 1 : 0;
+      bc[0] = pf != -2 ? pf : next_unit();
+      bc[20] = -2;
     }
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(bc[0]);
+    const bool pre = __builtin_amdgcn_readfirstlane(bc[21]) != 0;
     if (w < 0) break;
+    if (pre) par ^= 1;
+    uint64_t* const swl = swl0 + (size_t)par * nch;
+    int32_t* const cnt = cnt0 + (size_t)par * (nch + 1);
+    bool did_pf = false;  // wave 1 prefetched the next unit during this one (uniform)
     RArgs a = rargs();
     const UnitRec* rec = a->b.rec + w;
     const uint32_t fc = ldc(&rec->flags);
@@ -2724,13 +2755,15 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
     };
 
     // ---------------- compaction of the static words (every filter folded by prep_kernel)
-    for (int ch = tid; ch < nch; ch += ROW_THREADS) {
-      const uint64_t m = ldg(a->b.sw, (uint32_t)(w * nch + ch));
-      swl[ch] = m;
-      cnt[ch] = popc64(m);
+    if (!pre) {
+      for (int ch = tid; ch < nch; ch += ROW_THREADS) {
+        const uint64_t m = ldg(a->b.sw, (uint32_t)(w * nch + ch));
+        swl[ch] = m;
+        cnt[ch] = popc64(m);
+      }
+      __syncthreads();
+      row_exclusive_scan(cnt, nch);
     }
-    __syncthreads();
-    row_exclusive_scan(cnt, nch);
     __syncthreads();
     const int n = __builtin_amdgcn_readfirstlane(cnt[nch]);
     for (int ch = wv; ch < nch; ch += ROW_WAVES) {
@@ -2762,7 +2795,7 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
     // ---------------- raw scores (RunScorePlugins, framework.go:139-181)
     const int32_t* sp = a->b.sprog + spo;
     const int n_terms = ldc(sp);
-    const bool s_aff = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && n_terms > 0;  // no preferred terms: 0 everywhere
+    const bool s_aff = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && n_terms > 0 && !(rexp & 4);  // no terms: 0 everywhere
     // ClusterAffinity preferred terms (cluster_affinity.go:96-135) as per-chunk words in LDS (<= ROW_MAX_TERMS,
     // checked above): word (t, ch) = AND of the term's requirement rows — once per chunk instead of once per
     // feasible position; a position's raw score is then a sum of weights over LDS bit tests, recomputed
@@ -2969,14 +3002,19 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
         const int xs_c = (a->p.flags & KAD_PROFILE_XORSHIFT_GO121) ? 17 : 5;
         // packed: the partitions of ranges longer than ROW_BLOCK_PART run on all 8 waves, then wave 0 goes
         // on alone (red[] is free scratch here)
+        did_pf = true;  // wave 1 prefetches the next unit while wave 0 finishes the replay alone
         if (packed && in_lds) {
           PdqWaveP<> pw{key, posl, posr, xs_b, xs_c};
           const auto st = pw.select_block(n, k, ROW_BLOCK_PART, ROW_WAVES, wv, red);
           if (wv == 0) pw.select_from(st, k);
+          else if (wv == 1) prefetch();
         } else if (packed) {  // elements stay in LDS; stopper scratch in the slab (workgroup fences order both)
           PdqWaveP<true> pw{key, posl, posr, xs_b, xs_c};
           const auto st = pw.select_block(n, k, ROW_BLOCK_PART, ROW_WAVES, wv, red);
           if (wv == 0) pw.select_from(st, k);
+          else if (wv == 1) prefetch();
+        } else if (wv == 1) {
+          prefetch();
         } else if (wv == 0) {
           if (in_lds) {
             PdqWave<uint32_t> pw{key, pid, posl, posr, xs_b, xs_c};
@@ -2995,6 +3033,7 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
     }
 
     // ---------------- output, ascending cluster id (= ascending position)
+    if (!did_pf && wv == 1) prefetch();  // (into the other buffers: the output pass uses this unit's cnt)
     const bool dup = fc & KAD_W_DUPLICATE;
     const bool replicas =
         !dup && a->p.replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && (fc & REC_DESIRED_POS) && k > 0;
@@ -3527,8 +3566,8 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
 // ================================================================ launchers
 int debug_phase_counters(uint64_t* out, int reset) {
 #ifdef KAD_PHASE_PROF
-  if (reset == -2) {  // the wide kernel's per-wave extras: out holds 8192 * 4 entries
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavex), sizeof(unsigned long long) * 8192 * 4) != hipSuccess) return -1;
+  if (reset == -2) {  // the wide kernel's per-wave extras: out holds 8192 * 6 entries
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavex), sizeof(unsigned long long) * 8192 * 6) != hipSuccess) return -1;
     return 8192;
   }
   if (reset < 0) {  // the lean kernel's per-wave (start, end) timestamps: out holds 8192 * 2 entries
@@ -3620,12 +3659,6 @@ static int n_cus() {
   return n_cu;
 }
 
-// single-unit batches at the end of each work head: KAD_WQ_TAIL (profiling builds) per wave of the head
-static int wq_tail(int total_waves) {
-  static const int per_wave = tuning_env("KAD_WQ_TAIL", 0);
-  return per_wave * ((total_waves + WQ_HEADS - 1) / WQ_HEADS);
-}
-
 // the wide kernel takes clean snapshots with WIDE_MIN_NCH <= nch <= WIDE_MAX_NCH
 // (KAD_WIDE_MIN_NCH overrides the lower bound, for A/B runs of C <= 256)
 static bool use_wide(const SnapDev& s) {
@@ -3677,7 +3710,8 @@ static hipError_t launch_rows(const SnapDev& s, const BatchDev& b, const OutDev&
   if (grid > ROW_MAX_BLOCKS) grid = ROW_MAX_BLOCKS;
   if (grid > b.W) grid = b.W;
   if (!b.row_slabs) return hipErrorInvalidValue;
-  const RowArgs A{s, b, o, p, b.row_slabs};
+  static const int exp = tuning_env("KAD_ROW_EXPERIMENT", 0);
+  const RowArgs A{s, b, o, p, b.row_slabs, exp};
   hipLaunchKernelGGL(schedule_row_kernel, dim3((unsigned)grid), dim3(ROW_THREADS), lds, st, A);
   return hipGetLastError();
 }
@@ -3710,7 +3744,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const long need = ((long)b.W + wpb - 1) / wpb;
     if (grid > need) grid = need;
     static const int exp = tuning_env("KAD_WIDE_EXPERIMENT", 0);
-    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, wq_tail((int)grid * wpb), exp};
+    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, exp};
     const bool beside = b.early_rows && b.use_rows && side && fork && join;
     if (beside) {  // the row kernel on the side stream, from the end of prep_kernel, beside the wide kernel
       if (hipError_t e = hipEventRecord(fork, st)) return e;
@@ -3764,7 +3798,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const long upw = ((long)b.W + grid * wpb - 1) / (grid * wpb);
     int bsz = (int)(upw / 6);
     bsz = bsz < 1 ? 1 : (bsz > LEAN_BATCH ? LEAN_BATCH : bsz);
-    const LeanArgs A{s, b, o, p, (int)lb, wpb, bsz, cache_ne, cache_pn, bsz > 1 ? wq_tail((int)grid * wpb) : 0};
+    const LeanArgs A{s, b, o, p, (int)lb, wpb, bsz, cache_ne, cache_pn};
     switch (nch) {
       case 1: cl ? launch_lean<1, true>(A, (int)grid, lds, st) : launch_lean<1, false>(A, (int)grid, lds, st); break;
       case 2: cl ? launch_lean<2, true>(A, (int)grid, lds, st) : launch_lean<2, false>(A, (int)grid, lds, st); break;

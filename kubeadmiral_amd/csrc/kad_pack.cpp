@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/kad_pack.h"
+#include "kad_pool.h"
 
 namespace {
 
@@ -128,13 +129,8 @@ void parallel_for(int n, int threads, F f, int grain = 1024) {
     return;
   }
   const int T = std::min(threads, (n + grain - 1) / grain);
-  std::vector<std::thread> th;
-  th.reserve(T);
-  for (int t = 0; t < T; t++) {
-    const int a = (int)((int64_t)n * t / T), b = (int)((int64_t)n * (t + 1) / T);
-    th.emplace_back([=, &f] { f(a, b); });
-  }
-  for (auto& x : th) x.join();
+  // the library's persistent workers (kad_pool.h): T ranges, run by at most pool().threads() at a time
+  kadpool::pool().run(T, [&](int t) { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
 }
 
 struct WordsHash {

@@ -96,10 +96,23 @@ def main():
                 ss.append(float(s0.max() - s0.min()) / span)
                 es.append(float(e0.max() - e0.min()) / span)
             out["lean_waves"] = int(len(live))
-            wx = np.zeros(8192 * 4, dtype=np.uint64)
+            wx = np.zeros(8192 * 6, dtype=np.uint64)
             if a.config == "c3" and L.kad_debug_phase_counters(wx.ctypes.data, -2) > 0:
                 # wide kernel: late waves (last 10 % of ends) vs the rest — units, longest unit, last dequeue
-                units, umax, deq = wx[0::4].astype(np.int64), wx[1::4].astype(np.int64), wx[2::4].astype(np.int64)
+                units, umax, deq = wx[0::6].astype(np.int64), wx[1::6].astype(np.int64), wx[2::6].astype(np.int64)
+                hwid, xcc = wx[4::6].astype(np.int64), wx[5::6].astype(np.int64)
+                # per CU (XCC, SE, SH, CU from HW_ID): the CU's last wave end and its waves' mean end
+                cu_key = (xcc[live] & 0xF) * 4096 + ((hwid[live] >> 13) & 7) * 512 + ((hwid[live] >> 12) & 1) * 16 + \
+                    ((hwid[live] >> 8) & 15)
+                endf_all = (en[live] - st[live].min()) / span_all
+                keys = np.unique(cu_key)
+                cu_last = np.array([endf_all[cu_key == k].max() for k in keys])
+                cu_mean = np.array([endf_all[cu_key == k].mean() for k in keys])
+                out["wide_cus"] = int(len(keys))
+                out["wide_cu_last_end_p10_p50_p90_max"] = [round(float(np.percentile(cu_last, q)), 3) for q in (10, 50, 90, 100)]
+                out["wide_cu_mean_end_p10_p50_p90_max"] = [round(float(np.percentile(cu_mean, q)), 3) for q in (10, 50, 90, 100)]
+                out["wide_cu_of_last_wave"] = int(keys[np.argmax(cu_last)])
+                out["wide_xcc_last_end"] = [round(float(endf_all[(xcc[live] & 0xF) == x].max()), 3) for x in range(8)]
                 endf = (en[live] - st[live].min()) / span_all
                 late = live[endf >= np.percentile(endf, 90)]
                 rest = live[endf < np.percentile(endf, 90)]
