@@ -2563,6 +2563,13 @@ constexpr int ROW_MAX_C = 12288;
 constexpr int ROW_MAX_TERMS = 8;  // preferred terms held as per-chunk words (8 x nch x 8 B = Cp bytes)
 constexpr int ROW_NREP = 2048;    // replays of up to this many positions keep their scratch in LDS
 constexpr int ROW_BLOCK_PART = 256;  // replay partitions of longer ranges run on every wave of the block
+#ifndef KAD_ROW_RU
+#define KAD_ROW_RU 3
+#endif
+#ifndef KAD_ROW_MINW
+#define KAD_ROW_MINW 2  // waves per SIMD the row kernel's VGPR budget is sized for (2 blocks of 8 waves / CU: 4)
+#endif
+constexpr int ROW_RU = KAD_ROW_RU;   // scoring: positions per thread trip, their gathers issued together
 static_assert(ROW_MAX_BLOCKS >= 1, "row kernel slabs");
 struct RowKLayout {
   size_t key, idx, x, pid, posl, posr, sw, cnt, hist, red, bytes;
@@ -2641,7 +2648,7 @@ __device__ __forceinline__ void row_exclusive_scan(int* cnt, int m, int by = 0) 
   if (lane == 0) cnt[m] = carry;
 }
 
-__global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs args) {
+__global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel(RowArgs args) {
   (void)args;  // read through rargs()
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = lane_id();
@@ -2841,18 +2848,26 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
     }
     const double rqcd = (double)rqc, rqmd = (double)rqm;
     int ttmax = 0, amax = 0;
-    // two positions per trip: every gather of both is issued before either is used
-    for (int j0 = tid; j0 < n; j0 += 2 * ROW_THREADS) {
-      RArgs as = rargs();
-      const int j1 = j0 + ROW_THREADS;
-      const bool v1 = j1 < n;
-      const uint32_t c0 = idx[j0], c1 = idx[v1 ? j1 : j0];
-      double4 r4[2];
-      float2 iv[2];
-      uint64_t pn[2][TFOLD_MAX_TW];
-      const uint32_t cs[2] = {c0, c1};
+    // the unit's tolerated PreferNoSchedule words, once (scalar)
+    uint64_t tpn[TFOLD_MAX_TW];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+    for (int tw = 0; tw < TFOLD_MAX_TW; ++tw) tpn[tw] = (s_tt && tw < TW) ? ldc(a->b.tol_pns + (size_t)tsc * TW + tw) : 0ull;
+    // ROW_RU positions per trip: every gather of all of them is issued before any is used (the phase is
+    // latency-bound: its resource, taint and affinity parts cost cycles in proportion to their load chains)
+    constexpr int RU = ROW_RU;
+    for (int j0 = tid; j0 < n; j0 += RU * ROW_THREADS) {
+      RArgs as = rargs();
+      double4 r4[RU];
+      float2 iv[RU];
+      uint64_t pn[RU][TFOLD_MAX_TW];
+      uint32_t cs[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int j = j0 + u * ROW_THREADS;
+        cs[u] = idx[j < n ? j : j0];
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
         r4[u] = make_double4(0.0, 0.0, 1.0, 1.0);
         iv[u] = make_float2(0.f, 0.f);
         if (s_res) {  // (available cpu, available mem, cap cpu, cap mem) as f64, f32 100 / cap
@@ -2864,9 +2879,9 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
           pn[u][tw] = (s_tt && tw < TW) ? ldg(as->s.pns, (uint32_t)(tw * C) + cs[u]) : 0ull;
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (u == 1 && !v1) break;
-        const int j = u == 0 ? j0 : j1;
+      for (int u = 0; u < RU; ++u) {
+        const int j = j0 + u * ROW_THREADS;
+        if (j >= n) break;
         const uint32_t c = cs[u];
         int x = 0;
         if (s_res) {  // the wide kernel's clean path: x = available - request, exact in f64
@@ -2884,7 +2899,7 @@ __global__ __launch_bounds__(ROW_THREADS, 2) void schedule_row_kernel(RowArgs ar
         if (s_tt)  // taint_toleration.go:91-118: PreferNoSchedule taints not tolerated
 #pragma unroll
           for (int tw = 0; tw < TFOLD_MAX_TW; ++tw)
-            if (tw < TW) tc += popc64(pn[u][tw] & ~ldc(as->b.tol_pns + (size_t)tsc * TW + tw));
+            if (tw < TW) tc += popc64(pn[u][tw] & ~tpn[tw]);
         key[j] = (uint32_t)x | ((uint32_t)tc << 16);
         ttmax = tc > ttmax ? tc : ttmax;
         if (s_aff) {  // |raw| <= 2^20 (wider units were deferred above)
