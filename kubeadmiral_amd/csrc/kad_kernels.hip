@@ -2564,12 +2564,15 @@ constexpr int ROW_MAX_TERMS = 8;  // preferred terms held as per-chunk words (8 
 constexpr int ROW_NREP = 2048;    // replays of up to this many positions keep their scratch in LDS
 constexpr int ROW_BLOCK_PART = 256;  // replay partitions of longer ranges run on every wave of the block
 #ifndef KAD_ROW_RU
-#define KAD_ROW_RU 3
+#define KAD_ROW_RU 2
 #endif
 #ifndef KAD_ROW_MINW
 #define KAD_ROW_MINW 2  // waves per SIMD the row kernel's VGPR budget is sized for (2 blocks of 8 waves / CU: 4)
 #endif
-constexpr int ROW_RU = KAD_ROW_RU;   // scoring: positions per thread trip, their gathers issued together
+// scoring: positions per thread trip, their gathers issued together. 3 cut the score phase's cycles per row
+// by 29 % (profiling build, profiles/r03/q6_c5_ru*.json) but at 127 VGPRs the kernel ran 1.5 % longer (C5
+// rows 1.28 -> 1.30 ms, two product builds on one box); 4 spills and drops to one block per CU
+constexpr int ROW_RU = KAD_ROW_RU;
 static_assert(ROW_MAX_BLOCKS >= 1, "row kernel slabs");
 struct RowKLayout {
   size_t key, idx, x, pid, posl, posr, sw, cnt, hist, red, bytes;
