@@ -567,6 +567,8 @@ def gather_placements(ctx, batch, res, dist, world, dev, blobs=None, fwk=None):
     cl = torch.full((Sm,), -1, dtype=torch.int32, device=dev)
     rp = torch.zeros(Sm, dtype=torch.int64, device=dev)
     if dev != "cpu":
+        # the fills above run on torch's stream, libkad's copy on its own: the fills must land first
+        torch.cuda.synchronize()
         ctx.copy_results_device(st.data_ptr(), st.data_ptr() + 4 * Wm, st.data_ptr() + 8 * Wm, cl.data_ptr(),
                                 rp.data_ptr())
     else:
