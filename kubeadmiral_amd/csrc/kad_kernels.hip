@@ -2698,6 +2698,10 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
   // complete before this kernel starts (prep_kernel's early routing, or the lean kernel before it)
   int ticket = 0;
   if (tid == 64) ticket = atomicAdd(rargs()->b.rows_head, 1);
+#ifdef KAD_PHASE_PROF
+  const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+  unsigned long long rt_units = 0;
+#endif
   if (tid == 0) bc[20] = -2;
   int par = 0;  // the current unit's buffers
   auto next_unit = [&]() -> int {  // thread 64 only
@@ -2736,6 +2740,9 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     const int w = __builtin_amdgcn_readfirstlane(bc[0]);
     const bool pre = __builtin_amdgcn_readfirstlane(bc[21]) != 0;
     if (w < 0) break;
+#ifdef KAD_PHASE_PROF
+    rt_units++;
+#endif
     if (pre) par ^= 1;
     uint64_t* const swl = swl0 + (size_t)par * nch;
     int32_t* const cnt = cnt0 + (size_t)par * (nch + 1);
@@ -3093,6 +3100,14 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
       ao->o.flags[w] = rflags;
     }
   }
+#ifdef KAD_PHASE_PROF
+  // per-block (start, end, units) of the last launch in g_wavetime / g_wavex (the wide kernel's slots)
+  if (tid == 0 && blockIdx.x < 8192) {
+    g_wavetime[2 * blockIdx.x] = rt_start;
+    g_wavetime[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    g_wavex[6 * blockIdx.x] = rt_units;
+  }
+#endif
   KAD_PFLUSH_ROW;
 }
 

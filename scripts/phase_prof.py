@@ -126,6 +126,26 @@ def main():
             out["lean_wave_lifetime_frac_per_xcd"] = [round(v, 3) for v in fr]
             out["lean_start_spread_frac_per_xcd"] = [round(v, 3) for v in ss]
             out["lean_end_spread_frac_per_xcd"] = [round(v, 3) for v in es]
+    if a.config == "c5" or os.environ.get("KAD_ROW_STAMPS"):
+        # schedule_row_kernel blocks of the last launch (they overwrite the lean kernel's first slots): lifetime
+        # over the row kernel's own span, and the end spread
+        wt2 = np.zeros(8192 * 2, dtype=np.uint64)
+        wx2 = np.zeros(8192 * 6, dtype=np.uint64)
+        ctx.schedule(fwk)
+        ctx.sync()
+        L.kad_debug_phase_counters(wt2.ctypes.data, -1)
+        L.kad_debug_phase_counters(wx2.ctypes.data, -2)
+        nb = int(os.environ.get("KAD_ROW_BLOCKS", "512"))
+        st2, en2 = wt2[0:2 * nb:2].astype(np.int64), wt2[1:2 * nb:2].astype(np.int64)
+        ok = (en2 > st2)
+        if ok.any():
+            span = float(en2[ok].max() - st2[ok].min())
+            out["row_blocks"] = int(ok.sum())
+            out["row_span_us"] = span / 100.0
+            out["row_block_lifetime_frac"] = round(float((en2[ok] - st2[ok]).mean()) / span, 3)
+            out["row_block_end_p10_p50_p90_frac"] = [round(float(np.percentile(en2[ok] - st2[ok].min(), q)) / span, 3)
+                                                     for q in (10, 50, 90)]
+            out["row_block_units_p10_p50_p90"] = [int(np.percentile(wx2[0:6 * nb:6][ok], q)) for q in (10, 50, 90)]
     for i, nm in enumerate(NAMES):
         v = float(cnt[i])
         if nm == "-":
