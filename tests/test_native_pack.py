@@ -65,6 +65,32 @@ def test_threads_do_not_change_the_blob():
     assert all(np.array_equal(blobs[0], b) for b in blobs[1:])
 
 
+def test_concurrent_packers_share_the_worker_pool():
+    """Packs from several host threads at once (a Go shim's goroutines): every packer's parallel loops go
+    through libkad's one persistent worker pool (csrc/kad_pool.h), one job at a time, and each blob stays
+    byte-identical to a serial pack of the same units — no deadlock, no cross-talk between jobs."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    clusters, units = synth.gen_fuzz(4343, W=8000, C=60)
+    snap = pack.Snapshot(clusters)
+    fwk = F.Framework()
+    parts = [CO.from_units(units[i::4]) for i in range(4)]
+    want = [CO.NativePacker(snap).pack(fwk, p, threads=1).blob.copy() for p in parts]
+
+    def job(i):
+        P = CO.NativePacker(snap)
+        out = []
+        for _ in range(3):
+            out.append(P.pack(fwk, parts[i], threads=0).blob.copy())
+        return out
+
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        got = list(ex.map(job, range(4)))
+    for i in range(4):
+        for b in got[i]:
+            assert np.array_equal(b, want[i])
+
+
 def test_empty_batch():
     clusters, _ = synth.gen_fuzz(3, W=1, C=10)
     _same(pack.Snapshot(clusters), F.Framework(), [])
