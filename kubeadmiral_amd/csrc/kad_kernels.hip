@@ -206,40 +206,65 @@ __global__ __launch_bounds__(256) void req_mask_kernel(SnapDev s, BatchDev b, in
   }
 }
 
-// req_row_kernel: one lane per (value-row requirement, chunk): In / Equals = OR of the value rows, NotIn
-// = its complement (a missing label matches), Exists / DoesNotExist = the key row or its complement;
-// TRUE / FALSE / metadata.name =, != are constants or one bit (no loads).
+// req_row_kernel: one lane per (value-row requirement, REQ_RC consecutive chunks): In / Equals = OR of the
+// value rows, NotIn = its complement (a missing label matches), Exists / DoesNotExist = the key row or its
+// complement; TRUE / FALSE / metadata.name =, != are constants or one bit (no loads). The requirement's
+// 32-B entry is read once per lane for its REQ_RC words (C5: 100k requirements x 157 chunks).
+constexpr int REQ_RC = 4;
 __global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b, int zero_rows) {
   const int nch = (s.C + 63) >> 6;
+  const int nq = (nch + REQ_RC - 1) / REQ_RC;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
   // the row list (rows_n, rows_head) emptied before prep_kernel appends to it (early routing): here
   // instead of a separate memset launch
   if (zero_rows && g < 2) b.rows_n[g] = 0;
-  if (g >= (long)b.n_rowreq * nch) return;
-  const int i = (int)(g / nch), ch = (int)(g - (long)i * nch);
+  if (g >= (long)b.n_rowreq * nq) return;
+  const int i = (int)(g / nq), ch0 = (int)(g - (long)i * nq) * REQ_RC;
   const int4 e0 = b.req_rows[2 * (size_t)i], e1 = b.req_rows[2 * (size_t)i + 1];
   const int rid = e0.x, op = e0.y & 0xff, n = (int)((uint32_t)e0.y >> 8), key = e0.z;
   const int v[VR_MAX_VALS] = {e0.w, e1.x, e1.y, e1.z, e1.w};
-  uint64_t acc = 0;
+  const uint64_t tail = (s.C & 63) ? (1ull << (s.C & 63)) - 1 : ~0ull;  // clusters past C: never
+  uint64_t* out = b.req_mask + (size_t)rid * nch;
   if (op == KAD_OP_TRUE || op == KAD_OP_FALSE || op == KAD_OP_NAME_EQ || op == KAD_OP_NAME_NE) {
     // label-free: metadata.name = / != the cluster with snapshot id `key` (-1: no such cluster)
-    const uint64_t one = (key >= 0 && (key >> 6) == ch) ? 1ull << (key & 63) : 0ull;
-    acc = op == KAD_OP_TRUE ? ~0ull : op == KAD_OP_FALSE ? 0ull : op == KAD_OP_NAME_EQ ? one : ~one;
-    if (ch == nch - 1 && (s.C & 63)) acc &= (1ull << (s.C & 63)) - 1;  // clusters past C: never
-    b.req_mask[(size_t)rid * nch + ch] = acc;
+#pragma unroll
+    for (int k = 0; k < REQ_RC; ++k) {
+      const int ch = ch0 + k;
+      if (ch >= nch) break;
+      const uint64_t one = (key >= 0 && (key >> 6) == ch) ? 1ull << (key & 63) : 0ull;
+      uint64_t acc = op == KAD_OP_TRUE ? ~0ull : op == KAD_OP_FALSE ? 0ull : op == KAD_OP_NAME_EQ ? one : ~one;
+      if (ch == nch - 1) acc &= tail;
+      out[ch] = acc;
+    }
     return;
   }
-  const uint64_t* kr = s.vrows + (size_t)key * (VR_SLOTS + 1) * nch + ch;
+  const uint64_t* kr = s.vrows + (size_t)key * (VR_SLOTS + 1) * nch;
+  uint64_t acc[REQ_RC];
+#pragma unroll
+  for (int k = 0; k < REQ_RC; ++k) acc[k] = 0;
+  auto or_row = [&](const uint64_t* row) {  // the lane's REQ_RC words of one value row, loads issued together
+    uint64_t w[REQ_RC];
+#pragma unroll
+    for (int k = 0; k < REQ_RC; ++k) w[k] = ch0 + k < nch ? row[ch0 + k] : 0ull;
+#pragma unroll
+    for (int k = 0; k < REQ_RC; ++k) acc[k] |= w[k];
+  };
   if (op == KAD_OP_EXISTS || op == KAD_OP_DNE) {
-    acc = kr[(size_t)VR_SLOTS * nch];
+    or_row(kr + (size_t)VR_SLOTS * nch);
   } else {
 #pragma unroll
     for (int t = 0; t < VR_MAX_VALS; ++t)
-      if (t < n) acc |= kr[(size_t)v[t] * nch];
+      if (t < n) or_row(kr + (size_t)v[t] * nch);
   }
-  if (op == KAD_OP_NOTIN || op == KAD_OP_DNE) acc = ~acc;
-  if (ch == nch - 1 && (s.C & 63)) acc &= (1ull << (s.C & 63)) - 1;  // clusters past C: never
-  b.req_mask[(size_t)rid * nch + ch] = acc;
+  const bool neg = op == KAD_OP_NOTIN || op == KAD_OP_DNE;
+#pragma unroll
+  for (int k = 0; k < REQ_RC; ++k) {
+    const int ch = ch0 + k;
+    if (ch >= nch) break;
+    uint64_t x = neg ? ~acc[k] : acc[k];
+    if (ch == nch - 1) x &= tail;
+    out[ch] = x;
+  }
 }
 
 // SnapDev::res4 / res_iv (clean snapshots): the same expressions as the wide kernel's block cache
@@ -3630,7 +3655,7 @@ static constexpr int MAX_RESIDENT_WAVES = 256 * 32;
 hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st, bool zero_rows, bool* zeroed) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
-  const long lanes = (long)b.n_rowreq * nch;
+  const long lanes = (long)b.n_rowreq * ((nch + REQ_RC - 1) / REQ_RC);
   *zeroed = zero_rows && lanes > 0;
   if (lanes > 0)
     hipLaunchKernelGGL(req_row_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, s, b, zero_rows ? 1 : 0);
