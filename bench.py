@@ -194,17 +194,20 @@ def roofline_for(stage: str, kernel: str, t_ms: float, compulsory: float, pmc, p
 
 
 def cpu_baseline(snap, batch, fwk, C, target_s):
+    """The C restatement timed on the host (kind "port") over the first n units, n sized for ~target_s of
+    work. Returns (line, oracle result of units [0, n), n) — the result doubles as the parity check of
+    the GPU rows (verify_rows)."""
     from oracle import ref
 
     threads = min(16, os.cpu_count() or 1)
     n = min(batch.W, 2000)
     t0 = time.perf_counter()
-    ref.schedule(snap, batch, fwk, 0, n, threads)
+    want = ref.schedule(snap, batch, fwk, 0, n, threads)
     dt = time.perf_counter() - t0
     n2 = int(min(batch.W, max(n, n * target_s / max(dt, 1e-6))))
     if n2 > n:
         t0 = time.perf_counter()
-        ref.schedule(snap, batch, fwk, 0, n2, threads)
+        want = ref.schedule(snap, batch, fwk, 0, n2, threads)
         dt = time.perf_counter() - t0
         n = n2
     reps = max(1, int(target_s / max(dt, 1e-6)))
@@ -213,9 +216,51 @@ def cpu_baseline(snap, batch, fwk, C, target_s):
         for _ in range(reps):
             ref.schedule(snap, batch, fwk, 0, n, threads)
         dt = time.perf_counter() - t0
-    return {"value": reps * n * C / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} pass(es) over the first {n} of {batch.W} units x {C} clusters, oracle/kad_ref.c "
+    line = {"value": reps * n * C / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} pass(es) over units [0, {n}) of {batch.W} x {C} clusters, oracle/kad_ref.c "
                       f"(C restatement of the Go reference, one unit per worker thread), {dt:.2f}s wall"}
+    return line, want, n
+
+
+def verify_rows(snap, batch, fwk, res, want=None, n_want=0, max_units=200_000):
+    """Parity of the timed run's rows against the C oracle (oracle/kad_ref.c), outside every timed region:
+    units [0, n_want) from the CPU baseline's own oracle pass when there was one, else 16 equal windows
+    spread over the batch holding ~max_units units. Rows compare status, count, (cluster, replicas) pairs
+    and result flags."""
+    from oracle import ref
+
+    W = batch.W
+    threads = min(16, os.cpu_count() or 1)
+    if want is not None and n_want > 0:
+        wins = [(0, n_want)]
+    else:
+        want = None
+        if W <= max_units:
+            wins = [(0, W)]
+        else:
+            span = max_units // 16
+            wins = [(W * i // 16, W * i // 16 + span) for i in range(16)]
+    bad = 0
+    first = None
+    for lo, hi in wins:
+        w = want if want is not None else ref.schedule(snap, batch, fwk, lo, hi, threads)
+        sl = slice(lo, hi)
+        eq = np.ones(hi - lo, bool)
+        eq &= (res.status[sl] == w.status[sl]) & (res.count[sl] == w.count[sl]) & (res.flags[sl] == w.flags[sl])
+        # slot contents within each row's written range
+        cnt = w.count[sl].astype(np.int64)
+        starts = np.asarray(batch.out_off[lo:hi], np.int64)
+        idx = np.repeat(starts, cnt) + (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+        rows = np.repeat(np.arange(hi - lo), cnt)
+        d = (res.cluster[idx] != w.cluster[idx]) | (res.replicas[idx] != w.replicas[idx])
+        eq[rows[d]] = False
+        nb = int((~eq).sum())
+        if nb and first is None:
+            first = lo + int(np.nonzero(~eq)[0][0])
+        bad += nb
+    checked = sum(hi - lo for lo, hi in wins)
+    return {"units_checked": checked, "of": W, "mismatches": bad, "first_mismatch": first,
+            "oracle": "oracle/kad_ref.c", "windows": len(wins)}
 
 
 # ------------------------------------------------------------------------ scheduling bench
@@ -337,9 +382,14 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, cpu_second
         out["allgather"] = allgather
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = end_to_end(ctx, snap, fwk, stats0[0], res, C, packer_for=snap)
-            if not args.no_cpu_baseline:
-                log(f"[rank 0] timing the CPU baseline (C restatement of the reference) on {cfg}")
-                out["cpu_baseline"] = cpu_baseline(snap, batch, fwk, C, cpu_seconds)
+        want, n_want = None, 0
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"], want, n_want = cpu_baseline(snap, batch, fwk, C, cpu_seconds)
+        # rank 0's rows (its shard) against the C oracle; the other ranks' rows are checked against
+        # single-rank runs of their shards in gather_placements
+        out["parity"] = verify_rows(snap, batch, fwk, res, want, n_want)
+        if out["parity"]["mismatches"]:
+            log(f"[rank 0] {cfg}: PARITY FAILURE {out['parity']}")
     ctx.close()
     return out
 
@@ -426,6 +476,116 @@ def schedule_line(args, cfg, world, W_total, C, batch, snap, fwk, res, stage, ms
         "end_to_end": None,
         "cpu_baseline": None,
     }
+
+
+HEADLINE_MAX = 3000  # bytes of the last stdout line (the driver keeps a ~9 KB tail of stdout + stderr)
+EXTRA_MAX = 1500
+
+
+def _sig(x, n=4):
+    """Floats to n significant digits (recursively); keeps the printed line short."""
+    if isinstance(x, float):
+        return float(f"{x:.{n}g}")
+    if isinstance(x, dict):
+        return {k: _sig(v, n) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_sig(v, n) for v in x]
+    return x
+
+
+def compact_line(out: dict, headline: bool = True) -> dict:
+    """The printed form of a bench result: the driver's contract fields, a flat ``roofline`` for the
+    dominant kernel (+ one [ms, bound, frac] triple per stage), ``cpu_baseline``, the parity count and
+    short end-to-end / shard-sweep / extra-config summaries. The full result (per-stage kernel dicts,
+    sweep shards, embedded configs) goes to a file (write_full)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: out.get(k) for k in keep}
+    c = out.get("config", {})
+    if "stage_ms" in c:
+        line["config"] = {k: c.get(k) for k in ("workload", "units_total", "units_per_gpu", "clusters", "parallelism")}
+        line["config"]["stage_ms"] = {k: v for k, v in c["stage_ms"].items() if v >= 0.002}
+        if headline:
+            line["config"]["paths"] = c.get("paths")
+    else:  # trigger lines: their config is already short
+        line["config"] = c
+    r = out.get("roofline")
+    if r:
+        issue = r.get("issue") or {}
+        hbm = r.get("hbm") or {}
+        roof = {k: r.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "time_ms")}
+        roof.update({"compulsory_bytes": r.get("compulsory_bytes_per_launch"),
+                     "hbm_measured_frac": hbm.get("measured_frac"), "hbm_compulsory_frac": hbm.get("compulsory_frac"),
+                     "salu_frac": issue.get("salu_frac"), "valu_frac": issue.get("valu_frac"),
+                     "wait_frac": issue.get("wait_frac"), "pmc": r.get("pmc")})
+        if headline:
+            roof["algorithmic_bytes_per_launch"] = r.get("algorithmic_bytes_per_launch")
+            roof["stages"] = {k: [v["time_ms"], v["bound"], v["frac"]] for k, v in (r.get("kernels") or {}).items()}
+        line["roofline"] = roof
+    cb = out.get("cpu_baseline")
+    line["cpu_baseline"] = dict(cb) if cb else None
+    if cb and not headline:
+        line["cpu_baseline"]["sample"] = cb["sample"].split(",")[0]
+    p = out.get("parity")
+    line["parity"] = {k: p[k] for k in ("units_checked", "of", "mismatches")} if p else None
+    e = out.get("end_to_end")
+    if e:
+        s = e["sequential"]
+        line["end_to_end"] = {"decisions_per_s": e["decisions_per_s"],
+                              "seq_ms": {k[:-3]: s[k] for k in ("pack_ms", "h2d_ms", "schedule_ms", "d2h_ms")},
+                              "blob_mb": s["blob_mb"], "pipelined_decisions_per_s": e["pipelined"]["decisions_per_s"]}
+    if out.get("allgather"):
+        a = out["allgather"]
+        line["allgather"] = {"ms": a["ms"], "gbs": a["gbs"], "backend": a["backend"], "verified": bool(a["verified"])}
+    sw = out.get("shard_sweep")
+    if sw:
+        line["shard_sweep"] = {n: {"max_ms": v["max_ms"], "eff": v["projected_efficiency"]}
+                               for n, v in sw["per_n"].items()}
+    ex = out.get("extra")
+    if ex:
+        line["extra"] = {k: {"value": v["value"], "ms_per_step": v["ms_per_step"],
+                             "parity_mismatches": (v.get("parity") or {}).get("mismatches")} for k, v in ex.items()}
+    if out.get("detail"):
+        line["detail"] = out["detail"]
+    return _sig(line)
+
+
+def write_full(out: dict, cfg: str):
+    """The full result as one JSON file under gpurun_out/ (what the compact line leaves out)."""
+    d = os.path.join(ROOT, "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, f"bench_full_{cfg}.json")
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return os.path.relpath(path, ROOT)
+    except OSError:
+        return None
+
+
+def emit(out: dict, cfg: str):
+    """Rank 0's stdout: one compact line per extra config, then the headline line LAST (≤ HEADLINE_MAX)."""
+    out["detail"] = write_full(out, cfg)
+    lines = []
+    for k, v in (out.get("extra") or {}).items():
+        s = json.dumps(compact_line(v, headline=False))
+        if len(s) > EXTRA_MAX:
+            s = json.dumps({f: compact_line(v, headline=False)[f] for f in ("metric", "value", "unit", "ms_per_step",
+                                                                            "config", "parity")})
+        lines.append(s)
+    head = json.dumps(compact_line(out))
+    if len(head) > HEADLINE_MAX:  # never let the headline outgrow the driver's capture
+        h = compact_line(out)
+        for f in ("extra", "shard_sweep", "end_to_end", "detail"):
+            h.pop(f, None)
+            head = json.dumps(h)
+            if len(head) <= HEADLINE_MAX:
+                break
+    sys.stderr.flush()
+    for s in lines:
+        print(s, flush=True)
+    print(head, flush=True)
+    return head
 
 
 def shard_sweep(args, cfg, local, t1_ms, ns=(2, 4, 8)):
@@ -771,7 +931,7 @@ def main():
         if default_run and not args.no_sweep:
             out["shard_sweep"] = shard_sweep(args, cfg, local, out["ms_per_step"])
     if rank == 0 and out is not None:
-        print(json.dumps(out), flush=True)
+        emit(out, cfg)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

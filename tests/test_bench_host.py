@@ -103,6 +103,62 @@ def test_line_contract_and_rooflines(fake):
     assert e2e["pipelined"]["chunks"] == 4 and e2e["sequential"]["units"] == 3000
 
 
+def test_printed_lines_fit_the_driver_tail(fake, capsys, tmp_path, monkeypatch):
+    """bench.py's stdout ends with the headline line, ≤ 3 KB and parseable, after one ≤ 1.5 KB line per extra
+    config; the full result goes to a file. Built from a real bench result (c3 + embedded c2 + sweep) whose
+    per-stage dicts are what made round 3's single 21 KB line unparseable."""
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    args = _args(no_extra=False, no_sweep=False)
+    out = bench.bench_schedule(args, "c3", 0, 1, 0, None)
+    out["extra"] = {"c2": bench.bench_schedule(args, "c2", 0, 1, 0, None),
+                    "c4": bench.bench_schedule(args, "c2", 0, 1, 0, None)}
+    out["shard_sweep"] = bench.shard_sweep(args, "c3", 0, out["ms_per_step"])
+    assert len(json.dumps(out)) > 6000  # the uncompacted result would not fit
+    bench.emit(out, "c3")
+    lines = capsys.readouterr().out.strip().split("\n")
+    assert len(lines) == 3
+    head = lines[-1]
+    assert len(head) <= bench.HEADLINE_MAX, len(head)
+    h = json.loads(head)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "parity"):
+        assert k in h, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in h["roofline"], k
+    assert h["cpu_baseline"]["kind"] == "port" and h["cpu_baseline"]["cores"] >= 1
+    assert h["parity"]["mismatches"] == 0 and h["parity"]["units_checked"] == 3000
+    assert set(h["shard_sweep"]) == {"2", "4", "8"} and set(h["extra"]) == {"c2", "c4"}
+    assert h["value"] == pytest.approx(out["value"], rel=1e-3)
+    for s in lines[:-1]:
+        assert len(s) <= bench.EXTRA_MAX, len(s)
+        assert json.loads(s)["metric"] == h["metric"]
+    full = json.loads((tmp_path / h["detail"]).read_text())
+    assert "kernels" in full["roofline"]
+
+
+def test_verify_rows_reports_mismatches(fake):
+    """The bench's parity count catches a changed row (windows over the batch when no CPU pass is reused)."""
+    out = bench.bench_schedule(_args(no_cpu_baseline=True, no_e2e=True), "c3", 0, 1, 0, None)
+    assert out["parity"]["mismatches"] == 0 and out["parity"]["units_checked"] == 3000
+    ctx = FakeContext()
+    from kubeadmiral_amd import columns as CO
+    from kubeadmiral_amd import pack
+    clusters = bench.make_clusters("c3", 1000)
+    snap = pack.Snapshot(clusters)
+    fwk = synth.profile_for("c3")
+    nb = CO.NativePacker(snap).pack(fwk, bench.make_columns("c3", 0, 3000, clusters))
+    ctx.upload_snapshot(snap)
+    ctx.upload_batch(nb)
+    ctx.schedule(fwk)
+    res = ctx.download()
+    w = int(np.nonzero(res.count > 0)[0][7])
+    res.cluster[nb.out_off[w]] += 1
+    p = bench.verify_rows(snap, nb, fwk, res, max_units=1000)
+    assert p["windows"] == 16 and p["units_checked"] == 16 * (1000 // 16)
+    p = bench.verify_rows(snap, nb, fwk, res, max_units=10_000)
+    assert p["mismatches"] == 1 and p["first_mismatch"] == w
+
+
 def test_stale_pmc_is_not_used(fake, tmp_path, monkeypatch):
     """A PMC profile whose src_hash is not the code's is reported as stale, never mixed with live timing."""
     prof = tmp_path / "profiles"
