@@ -376,6 +376,18 @@ class NativeBatch:
         self.n_reqs, self.n_tols = n_reqs, n_tols
         self.n_distinct_reqs, self.n_tolsets = n_distinct_reqs, n_tolsets
         self.units = None
+        self.in_place = None  # (packer, generation) for a blob that lives in the packer's buffer
+
+    def check_current(self):
+        """An in-place blob (pack(take=False)) is the packer's buffer, which its next pack rewrites and its
+        close() frees: refuse to hand a stale or freed one to the device."""
+        if self.in_place is not None:
+            packer, gen = self.in_place
+            if not getattr(packer, "h", None):
+                raise ValueError("in-place batch: its NativePacker was closed")
+            if packer.gen != gen:
+                raise ValueError("in-place batch: its NativePacker has packed another batch since (pack with "
+                                 "take=True to keep a batch)")
 
 
 def _from_blob(blob: np.ndarray, fwk: Framework) -> "NativeBatch":
@@ -451,6 +463,7 @@ class NativePacker:
         if rc != 0:
             raise RuntimeError(f"kad_packer_create failed ({rc}): {L.kad_packer_error(None).decode()}")
         self.h = h
+        self.gen = 0  # packs so far: an in-place batch is valid only while it is the latest
 
     def close(self):
         if getattr(self, "h", None):
@@ -481,6 +494,9 @@ class NativePacker:
         st = KadPackStats(nr.ctypes.data, nt.ctypes.data, 0, 0)
         prof = fwk.to_c()
         n = ctypes.c_size_t()
+        if not self.h:
+            raise RuntimeError("NativePacker is closed")
+        self.gen += 1
         rc = self.L.kad_pack_batch(self.h, ctypes.byref(prof), ctypes.byref(su), threads, ctypes.byref(n),
                                    ctypes.byref(st))
         if rc != 0:
@@ -495,6 +511,11 @@ class NativePacker:
             rc = self.L.kad_packer_blob(self.h, ctypes.byref(ptr), ctypes.byref(nb))
             if rc != 0:
                 raise RuntimeError(f"kad_packer_blob: {self.L.kad_packer_error(self.h).decode()}")
-            blob = np.ctypeslib.as_array((ctypes.c_uint8 * nb.value).from_address(ptr.value))
-        return NativeBatch(self.snap, fwk, blob, nr[:W].astype(np.int64), nt[:W].astype(np.int64),
-                           int(st.n_distinct_reqs), int(st.n_tolsets))
+            buf = (ctypes.c_uint8 * nb.value).from_address(ptr.value)
+            buf._owner = self  # the array's base chain keeps the packer (and its page-locked buffer) alive
+            blob = np.frombuffer(buf, dtype=U8)
+        nbatch = NativeBatch(self.snap, fwk, blob, nr[:W].astype(np.int64), nt[:W].astype(np.int64),
+                             int(st.n_distinct_reqs), int(st.n_tolsets))
+        if not take:
+            nbatch.in_place = (self, self.gen)
+        return nbatch

@@ -73,6 +73,7 @@ struct kad_ctx {
   size_t scratch_bytes = 0;
   bool have_snapshot = false, have_batch = false, ran = false;
   int inject_fault = 0;  // kad_debug_inject_fault: 1 = the next refresh_derived fails (tests)
+  int plan_force_ws = 0;  // kad_debug_plan_force_workspace: kad_plan_rows through the workspace planner (tests)
   void* d_diff = nullptr;  // kad_result_diff: canonical object state + flags
   size_t diff_cap = 0;
   // HIP event records around the stages (kad_set_timing); timed = the last
@@ -114,6 +115,19 @@ static int fail(kad_ctx* c, int code, const std::string& msg) {
     hipError_t e_ = (x);                                                                           \
     if (e_ != hipSuccess) return fail(ctx, KAD_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
+
+// Nothing unwinds through the C ABI: a host-side exception (std::bad_alloc from a check's or a planner
+// row's vectors, rethrown by the worker pool once all its workers are done) becomes an error code.
+template <class F>
+static int guarded(kad_ctx* c, F f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return fail(c, KAD_ENOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(c, KAD_ENOMEM, std::string("host error: ") + e.what());
+  }
+}
 
 template <class T>
 static const T* at(const void* base, const uint64_t* off, int i) {
@@ -419,6 +433,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   if (!c) return KAD_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->side) (void)hipStreamSynchronize(c->side);  // the row kernel may run there: drain it before any free
   for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
                   (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab, c->d_vrows, c->d_rescols,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs, c->d_diff})
@@ -646,126 +661,132 @@ static void invalidate_snapshot(kad_ctx* c) {
 }
 
 int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
-  if (!c || !blob) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  kad_snapshot_header h;
-  std::memcpy(&h, blob, sizeof(h) < nbytes ? sizeof(h) : nbytes);
-  if (int r = check_snapshot_header(c, h, nbytes)) return r;
-  // the resident snapshot, its derived state and any batch validated against it are about to be
-  // overwritten: nothing may run on them until every step below has succeeded
-  invalidate_snapshot(c);
-  HIPCHK(c, hipSetDevice(c->device));
-  if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
-  HIPCHK(c, hipMemcpyAsync(c->d_snap, blob, nbytes, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->snap_hdr = h;
-  if (int r = bind_snapshot(c, h)) return r;
-  c->h_res.assign((size_t)4 * h.n_clusters, 0);
-  {
-    for (int q = 0; q < 4; q++)
-      if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
-  }
-  c->h_ns.assign(at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE),
-                at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + (size_t)h.n_taint_words * h.n_clusters);
-  if (int r = refresh_derived(c)) return r;
-  c->have_snapshot = true;
-  return KAD_OK;
+  return guarded(c, [&]() -> int {
+    if (!c || !blob) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    kad_snapshot_header h;
+    std::memcpy(&h, blob, sizeof(h) < nbytes ? sizeof(h) : nbytes);
+    if (int r = check_snapshot_header(c, h, nbytes)) return r;
+    // the resident snapshot, its derived state and any batch validated against it are about to be
+    // overwritten: nothing may run on them until every step below has succeeded
+    invalidate_snapshot(c);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
+    HIPCHK(c, hipMemcpyAsync(c->d_snap, blob, nbytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->snap_hdr = h;
+    if (int r = bind_snapshot(c, h)) return r;
+    c->h_res.assign((size_t)4 * h.n_clusters, 0);
+    {
+      for (int q = 0; q < 4; q++)
+        if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
+    }
+    c->h_ns.assign(at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE),
+                  at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + (size_t)h.n_taint_words * h.n_clusters);
+    if (int r = refresh_derived(c)) return r;
+    c->have_snapshot = true;
+    return KAD_OK;
+  });
 }
 
 int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) {
-  if (!c || !dev_blob) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  kad_snapshot_header h;
-  HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemcpy(&h, dev_blob, sizeof(h), hipMemcpyDeviceToHost));
-  if (int r = check_snapshot_header(c, h, nbytes)) return r;
-  invalidate_snapshot(c);
-  if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
-  HIPCHK(c, hipMemcpyAsync(c->d_snap, dev_blob, nbytes, hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->snap_hdr = h;
-  if (int r = bind_snapshot(c, h)) return r;
-  c->h_res.assign((size_t)4 * h.n_clusters, 0);
-  c->h_ns.assign((size_t)h.n_taint_words * h.n_clusters, 0);
-  if (h.n_clusters) {
-    for (int q = 0; q < 4; q++)
-      HIPCHK(c, hipMemcpy(c->h_res.data() + (size_t)q * h.n_clusters, static_cast<const char*>(dev_blob) + h.off[kResArrays[q]],
-                          (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemcpy(c->h_ns.data(), static_cast<const char*>(dev_blob) + h.off[KAD_S_TAINT_NSNE],
-                        (size_t)h.n_taint_words * h.n_clusters * 8, hipMemcpyDeviceToHost));
-  }
-  if (int r = refresh_derived(c)) return r;
-  c->have_snapshot = true;
-  return KAD_OK;
+  return guarded(c, [&]() -> int {
+    if (!c || !dev_blob) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    kad_snapshot_header h;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(&h, dev_blob, sizeof(h), hipMemcpyDeviceToHost));
+    if (int r = check_snapshot_header(c, h, nbytes)) return r;
+    invalidate_snapshot(c);
+    if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
+    HIPCHK(c, hipMemcpyAsync(c->d_snap, dev_blob, nbytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->snap_hdr = h;
+    if (int r = bind_snapshot(c, h)) return r;
+    c->h_res.assign((size_t)4 * h.n_clusters, 0);
+    c->h_ns.assign((size_t)h.n_taint_words * h.n_clusters, 0);
+    if (h.n_clusters) {
+      for (int q = 0; q < 4; q++)
+        HIPCHK(c, hipMemcpy(c->h_res.data() + (size_t)q * h.n_clusters, static_cast<const char*>(dev_blob) + h.off[kResArrays[q]],
+                            (size_t)h.n_clusters * 8, hipMemcpyDeviceToHost));
+      HIPCHK(c, hipMemcpy(c->h_ns.data(), static_cast<const char*>(dev_blob) + h.off[KAD_S_TAINT_NSNE],
+                          (size_t)h.n_taint_words * h.n_clusters * 8, hipMemcpyDeviceToHost));
+    }
+    if (int r = refresh_derived(c)) return r;
+    c->have_snapshot = true;
+    return KAD_OK;
+  });
 }
 
 int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
-  if (!c || !delta) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot uploaded");
-  kad_snapshot_delta_header h;
-  if (nbytes < sizeof(h)) return fail(c, KAD_EINVAL, "delta too small");
-  std::memcpy(&h, delta, sizeof(h));
-  const kad_snapshot_header& sh = c->snap_hdr;
-  if (h.magic != KAD_DELTA_MAGIC) return fail(c, KAD_EINVAL, "bad delta magic");
-  if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "delta ABI version mismatch");
-  if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "delta size mismatch");
-  if (h.n_clusters != sh.n_clusters || h.fingerprint != sh.fingerprint)
-    return fail(c, KAD_EINVAL, "delta was packed against a different snapshot vocabulary");
-  const int n = h.n_changed, C = sh.n_clusters;
-  if (n < 0 || n > C) return fail(c, KAD_EINVAL, "bad n_changed");
-  if (n == 0) return KAD_OK;
-  if (h.idx_off > nbytes || (h.idx_off & 3) || h.idx_off + (uint64_t)n * 4 > nbytes)
-    return fail(c, KAD_EINVAL, "bad delta index offset");
-  const int32_t* idx = reinterpret_cast<const int32_t*>(static_cast<const char*>(delta) + h.idx_off);
-  for (int j = 0; j < n; j++)
-    if (idx[j] < 0 || idx[j] >= C || (j && idx[j] <= idx[j - 1]))
-      return fail(c, KAD_EINVAL, "delta cluster indices must be strictly increasing snapshot positions");
-  DeltaDev d{};
-  d.n = n;
-  d.C = C;
-  d.start[0] = 0;
-  for (int a = 0; a < KAD_S_NARRAYS; a++) {
-    int64_t rows;
-    int esz;
-    snapshot_array_shape(sh, a, &rows, &esz);
-    const uint64_t len = (uint64_t)rows * n * esz;
-    if (h.off[a] > nbytes || (h.off[a] % esz) || h.off[a] + len > nbytes)
-      return fail(c, KAD_EINVAL, "bad delta array offset");
-    d.s_off[a] = sh.off[a];
-    d.d_off[a] = h.off[a];
-    d.esz[a] = esz;
-    d.start[a + 1] = d.start[a] + rows * n;
-  }
-  HIPCHK(c, hipSetDevice(c->device));
-  if (int r = grow(c, &c->d_delta, &c->delta_cap, nbytes)) return r;
-  HIPCHK(c, hipMemcpyAsync(c->d_delta, delta, nbytes, hipMemcpyHostToDevice, c->stream));
-  d.snap = static_cast<uint8_t*>(c->d_snap);
-  d.delta = static_cast<const uint8_t*>(c->d_delta);
-  d.idx = reinterpret_cast<const int32_t*>(d.delta + h.idx_off);
-  {
-    hipError_t e = launch_snapshot_delta(d, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the caller's delta buffer is free on return
-    if (e != hipSuccess) {
-      invalidate_snapshot(c);  // the scatter may have run partway
-      return fail(c, KAD_EHIP, std::string("snapshot delta scatter: ") + hipGetErrorString(e));
+  return guarded(c, [&]() -> int {
+    if (!c || !delta) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot uploaded");
+    kad_snapshot_delta_header h;
+    if (nbytes < sizeof(h)) return fail(c, KAD_EINVAL, "delta too small");
+    std::memcpy(&h, delta, sizeof(h));
+    const kad_snapshot_header& sh = c->snap_hdr;
+    if (h.magic != KAD_DELTA_MAGIC) return fail(c, KAD_EINVAL, "bad delta magic");
+    if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "delta ABI version mismatch");
+    if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "delta size mismatch");
+    if (h.n_clusters != sh.n_clusters || h.fingerprint != sh.fingerprint)
+      return fail(c, KAD_EINVAL, "delta was packed against a different snapshot vocabulary");
+    const int n = h.n_changed, C = sh.n_clusters;
+    if (n < 0 || n > C) return fail(c, KAD_EINVAL, "bad n_changed");
+    if (n == 0) return KAD_OK;
+    if (h.idx_off > nbytes || (h.idx_off & 3) || h.idx_off + (uint64_t)n * 4 > nbytes)
+      return fail(c, KAD_EINVAL, "bad delta index offset");
+    const int32_t* idx = reinterpret_cast<const int32_t*>(static_cast<const char*>(delta) + h.idx_off);
+    for (int j = 0; j < n; j++)
+      if (idx[j] < 0 || idx[j] >= C || (j && idx[j] <= idx[j - 1]))
+        return fail(c, KAD_EINVAL, "delta cluster indices must be strictly increasing snapshot positions");
+    DeltaDev d{};
+    d.n = n;
+    d.C = C;
+    d.start[0] = 0;
+    for (int a = 0; a < KAD_S_NARRAYS; a++) {
+      int64_t rows;
+      int esz;
+      snapshot_array_shape(sh, a, &rows, &esz);
+      const uint64_t len = (uint64_t)rows * n * esz;
+      if (h.off[a] > nbytes || (h.off[a] % esz) || h.off[a] + len > nbytes)
+        return fail(c, KAD_EINVAL, "bad delta array offset");
+      d.s_off[a] = sh.off[a];
+      d.d_off[a] = h.off[a];
+      d.esz[a] = esz;
+      d.start[a + 1] = d.start[a] + rows * n;
     }
-  }
-  {
-    for (int q = 0; q < 4; q++) {
-      const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
-      for (int j = 0; j < n; j++) c->h_res[(size_t)q * C + idx[j]] = v[j];
+    HIPCHK(c, hipSetDevice(c->device));
+    if (int r = grow(c, &c->d_delta, &c->delta_cap, nbytes)) return r;
+    HIPCHK(c, hipMemcpyAsync(c->d_delta, delta, nbytes, hipMemcpyHostToDevice, c->stream));
+    d.snap = static_cast<uint8_t*>(c->d_snap);
+    d.delta = static_cast<const uint8_t*>(c->d_delta);
+    d.idx = reinterpret_cast<const int32_t*>(d.delta + h.idx_off);
+    {
+      hipError_t e = launch_snapshot_delta(d, c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the caller's delta buffer is free on return
+      if (e != hipSuccess) {
+        invalidate_snapshot(c);  // the scatter may have run partway
+        return fail(c, KAD_EHIP, std::string("snapshot delta scatter: ") + hipGetErrorString(e));
+      }
     }
-    const uint64_t* ns = at<uint64_t>(delta, h.off, KAD_S_TAINT_NSNE);  // [TW][n_changed]
-    for (int t = 0; t < sh.n_taint_words; t++)
-      for (int j = 0; j < n; j++) c->h_ns[(size_t)t * C + idx[j]] = ns[(size_t)t * n + j];
-  }
-  if (int r = refresh_derived(c)) {
-    invalidate_snapshot(c);  // the scattered snapshot no longer matches its derived rows / tables
-    return r;
-  }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return KAD_OK;
+    {
+      for (int q = 0; q < 4; q++) {
+        const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
+        for (int j = 0; j < n; j++) c->h_res[(size_t)q * C + idx[j]] = v[j];
+      }
+      const uint64_t* ns = at<uint64_t>(delta, h.off, KAD_S_TAINT_NSNE);  // [TW][n_changed]
+      for (int t = 0; t < sh.n_taint_words; t++)
+        for (int j = 0; j < n; j++) c->h_ns[(size_t)t * C + idx[j]] = ns[(size_t)t * n + j];
+    }
+    if (int r = refresh_derived(c)) {
+      invalidate_snapshot(c);  // the scattered snapshot no longer matches its derived rows / tables
+      return r;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KAD_OK;
+  });
 }
 
 static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
@@ -1050,9 +1071,11 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
 }
 
 int kad_batch_upload(kad_ctx* c, const void* blob, size_t nbytes) {
-  if (!c || !blob) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  return batch_upload_locked(c, blob, nbytes);
+  return guarded(c, [&]() -> int {
+    if (!c || !blob) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return batch_upload_locked(c, blob, nbytes);
+  });
 }
 
 static int validate_profile(kad_ctx* c, const kad_profile* p) {
@@ -1130,9 +1153,11 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
 }
 
 int kad_schedule(kad_ctx* c, const kad_profile* p) {
-  if (!c) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  return schedule_locked(c, p, nullptr, nullptr);
+  return guarded(c, [&]() -> int {
+    if (!c) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return schedule_locked(c, p, nullptr, nullptr);
+  });
 }
 
 int kad_sync(kad_ctx* c) {
@@ -1229,19 +1254,23 @@ int kad_host_free(void* p) {
 }
 
 int kad_results_download(kad_ctx* c, const kad_result_view* out) {
-  if (!c || !out) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  return results_download_locked(c, out);
+  return guarded(c, [&]() -> int {
+    if (!c || !out) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return results_download_locked(c, out);
+  });
 }
 
 // One critical section from upload to download: worker goroutines sharing the
 // ctx cannot interleave and schedule / download each other's batches.
 int kad_schedule_batch(kad_ctx* c, const kad_profile* p, const void* blob, size_t nbytes, const kad_result_view* out) {
-  if (!c || !blob || !out) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (int r = batch_upload_locked(c, blob, nbytes)) return r;
-  if (int r = schedule_locked(c, p, nullptr, nullptr)) return r;
-  return results_download_locked(c, out);
+  return guarded(c, [&]() -> int {
+    if (!c || !blob || !out) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (int r = batch_upload_locked(c, blob, nbytes)) return r;
+    if (int r = schedule_locked(c, p, nullptr, nullptr)) return r;
+    return results_download_locked(c, out);
+  });
 }
 
 int kad_debug_phase_counters(uint64_t* out, int reset) { return kad::debug_phase_counters(out, reset); }
@@ -1249,89 +1278,91 @@ int kad_debug_phase_counters(uint64_t* out, int reset) { return kad::debug_phase
 // ------------------------------------------------ §8 f3: result application diff
 
 int kad_result_diff(kad_ctx* c, const kad_result_state* st, uint32_t* out) {
-  if (!c || !st || !out) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (!c->ran || !c->have_batch) return fail(c, KAD_ESTATE, "no scheduled batch resident");
-  const int W = c->batch_hdr.n_units, C = c->sd.C;
-  if (st->n_units != W) return fail(c, KAD_EINVAL, "state n_units differs from the resident batch");
-  if (W == 0) return KAD_OK;
-  if (!st->place_off || !st->place_has || !st->ovr_off) return fail(c, KAD_EINVAL, "null state array");
-  auto csr_ok = [&](const int32_t* off) {
-    if (off[0] != 0) return false;
-    for (int w = 0; w < W; w++)
-      if (off[w + 1] < off[w]) return false;
-    return true;
-  };
-  if (!csr_ok(st->place_off) || !csr_ok(st->ovr_off)) return fail(c, KAD_EINVAL, "state offsets not monotone from 0");
-  const int64_t NP = st->place_off[W], NO = st->ovr_off[W];
-  if ((NP && !st->place_cluster) || (NO && (!st->ovr_cluster || !st->ovr_value || !st->ovr_kind)))
-    return fail(c, KAD_EINVAL, "null state array");
-  for (int64_t i = 0; i < NP; i++)
-    if (st->place_cluster[i] < -1 || st->place_cluster[i] >= C) return fail(c, KAD_EINVAL, "placement cluster out of range");
-  for (int64_t i = 0; i < NO; i++)
-    if (st->ovr_cluster[i] < -1 || st->ovr_cluster[i] >= C) return fail(c, KAD_EINVAL, "override cluster out of range");
-  // canonical placements: sorted unique snapshot positions; names outside the snapshot → uflag bit 1
-  std::vector<int32_t> cnt((size_t)W + 1, 0);
-  std::vector<uint8_t> uflag((size_t)W);
-  std::vector<int32_t> ids((size_t)NP);
-  host_parallel(W, [&](int lo, int hi) {
-    for (int w = lo; w < hi; w++) {
-      int32_t* b = ids.data() + st->place_off[w];
-      const int m = st->place_off[w + 1] - st->place_off[w];
-      std::copy(st->place_cluster + st->place_off[w], st->place_cluster + st->place_off[w + 1], b);
-      std::sort(b, b + m);
-      const int u = (int)(std::unique(b, b + m) - b);
-      const bool unknown = u > 0 && b[0] < 0;
-      cnt[(size_t)w + 1] = unknown ? u - 1 : u;
-      if (unknown) std::copy(b + 1, b + u, b);  // drop the -1
-      uflag[w] = (uint8_t)((st->place_has[w] ? 1 : 0) | (unknown ? 2 : 0));
-    }
+  return guarded(c, [&]() -> int {
+    if (!c || !st || !out) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->ran || !c->have_batch) return fail(c, KAD_ESTATE, "no scheduled batch resident");
+    const int W = c->batch_hdr.n_units, C = c->sd.C;
+    if (st->n_units != W) return fail(c, KAD_EINVAL, "state n_units differs from the resident batch");
+    if (W == 0) return KAD_OK;
+    if (!st->place_off || !st->place_has || !st->ovr_off) return fail(c, KAD_EINVAL, "null state array");
+    auto csr_ok = [&](const int32_t* off) {
+      if (off[0] != 0) return false;
+      for (int w = 0; w < W; w++)
+        if (off[w + 1] < off[w]) return false;
+      return true;
+    };
+    if (!csr_ok(st->place_off) || !csr_ok(st->ovr_off)) return fail(c, KAD_EINVAL, "state offsets not monotone from 0");
+    const int64_t NP = st->place_off[W], NO = st->ovr_off[W];
+    if ((NP && !st->place_cluster) || (NO && (!st->ovr_cluster || !st->ovr_value || !st->ovr_kind)))
+      return fail(c, KAD_EINVAL, "null state array");
+    for (int64_t i = 0; i < NP; i++)
+      if (st->place_cluster[i] < -1 || st->place_cluster[i] >= C) return fail(c, KAD_EINVAL, "placement cluster out of range");
+    for (int64_t i = 0; i < NO; i++)
+      if (st->ovr_cluster[i] < -1 || st->ovr_cluster[i] >= C) return fail(c, KAD_EINVAL, "override cluster out of range");
+    // canonical placements: sorted unique snapshot positions; names outside the snapshot → uflag bit 1
+    std::vector<int32_t> cnt((size_t)W + 1, 0);
+    std::vector<uint8_t> uflag((size_t)W);
+    std::vector<int32_t> ids((size_t)NP);
+    host_parallel(W, [&](int lo, int hi) {
+      for (int w = lo; w < hi; w++) {
+        int32_t* b = ids.data() + st->place_off[w];
+        const int m = st->place_off[w + 1] - st->place_off[w];
+        std::copy(st->place_cluster + st->place_off[w], st->place_cluster + st->place_off[w + 1], b);
+        std::sort(b, b + m);
+        const int u = (int)(std::unique(b, b + m) - b);
+        const bool unknown = u > 0 && b[0] < 0;
+        cnt[(size_t)w + 1] = unknown ? u - 1 : u;
+        if (unknown) std::copy(b + 1, b + u, b);  // drop the -1
+        uflag[w] = (uint8_t)((st->place_has[w] ? 1 : 0) | (unknown ? 2 : 0));
+      }
+    });
+    std::vector<int32_t> pl_off((size_t)W + 1, 0);
+    for (int w = 0; w < W; w++) pl_off[(size_t)w + 1] = pl_off[w] + cnt[(size_t)w + 1];
+    std::vector<int32_t> pl_id((size_t)pl_off[W] + 1);
+    host_parallel(W, [&](int lo, int hi) {
+      for (int w = lo; w < hi; w++)
+        std::copy(ids.data() + st->place_off[w], ids.data() + st->place_off[w] + cnt[(size_t)w + 1], pl_id.data() + pl_off[w]);
+    });
+    // one device buffer: [pl_off | pl_id | ov_off | ov_id | ov_val | uflag | ov_kind | out], 256-B aligned parts
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t b_ploff = 0, b_plid = al(b_ploff + 4 * ((size_t)W + 1)), b_ovoff = al(b_plid + 4 * pl_id.size()),
+                 b_ovid = al(b_ovoff + 4 * ((size_t)W + 1)), b_ovval = al(b_ovid + 4 * (size_t)(NO + 1)),
+                 b_uf = al(b_ovval + 8 * (size_t)(NO + 1)), b_ovk = al(b_uf + (size_t)W), b_out = al(b_ovk + (size_t)NO + 1),
+                 total = al(b_out + 4 * (size_t)W);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (int r = grow(c, &c->d_diff, &c->diff_cap, total)) return r;
+    char* d = static_cast<char*>(c->d_diff);
+    auto up = [&](size_t off, const void* h, size_t n) {
+      return n ? hipMemcpyAsync(d + off, h, n, hipMemcpyHostToDevice, c->stream) : hipSuccess;
+    };
+    HIPCHK(c, up(b_ploff, pl_off.data(), 4 * ((size_t)W + 1)));
+    HIPCHK(c, up(b_plid, pl_id.data(), 4 * (size_t)pl_off[W]));
+    HIPCHK(c, up(b_ovoff, st->ovr_off, 4 * ((size_t)W + 1)));
+    HIPCHK(c, up(b_ovid, st->ovr_cluster, 4 * (size_t)NO));
+    HIPCHK(c, up(b_ovval, st->ovr_value, 8 * (size_t)NO));
+    HIPCHK(c, up(b_uf, uflag.data(), (size_t)W));
+    HIPCHK(c, up(b_ovk, st->ovr_kind, (size_t)NO));
+    ResultDiffDev dd{};
+    dd.W = W;
+    dd.status = c->d_status;
+    dd.count = c->d_count;
+    dd.cluster = c->d_cluster;
+    dd.replicas = c->d_replicas;
+    dd.out_off = c->bd.out_off;
+    dd.pl_off = reinterpret_cast<const int32_t*>(d + b_ploff);
+    dd.pl_id = reinterpret_cast<const int32_t*>(d + b_plid);
+    dd.uflag = reinterpret_cast<const uint8_t*>(d + b_uf);
+    dd.ov_off = reinterpret_cast<const int32_t*>(d + b_ovoff);
+    dd.ov_id = reinterpret_cast<const int32_t*>(d + b_ovid);
+    dd.ov_val = reinterpret_cast<const int64_t*>(d + b_ovval);
+    dd.ov_kind = reinterpret_cast<const uint8_t*>(d + b_ovk);
+    dd.out = reinterpret_cast<uint32_t*>(d + b_out);
+    HIPCHK(c, launch_result_diff(dd, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, dd.out, 4 * (size_t)W, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's state arrays are free on return
+    return KAD_OK;
   });
-  std::vector<int32_t> pl_off((size_t)W + 1, 0);
-  for (int w = 0; w < W; w++) pl_off[(size_t)w + 1] = pl_off[w] + cnt[(size_t)w + 1];
-  std::vector<int32_t> pl_id((size_t)pl_off[W] + 1);
-  host_parallel(W, [&](int lo, int hi) {
-    for (int w = lo; w < hi; w++)
-      std::copy(ids.data() + st->place_off[w], ids.data() + st->place_off[w] + cnt[(size_t)w + 1], pl_id.data() + pl_off[w]);
-  });
-  // one device buffer: [pl_off | pl_id | ov_off | ov_id | ov_val | uflag | ov_kind | out], 256-B aligned parts
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t b_ploff = 0, b_plid = al(b_ploff + 4 * ((size_t)W + 1)), b_ovoff = al(b_plid + 4 * pl_id.size()),
-               b_ovid = al(b_ovoff + 4 * ((size_t)W + 1)), b_ovval = al(b_ovid + 4 * (size_t)(NO + 1)),
-               b_uf = al(b_ovval + 8 * (size_t)(NO + 1)), b_ovk = al(b_uf + (size_t)W), b_out = al(b_ovk + (size_t)NO + 1),
-               total = al(b_out + 4 * (size_t)W);
-  HIPCHK(c, hipSetDevice(c->device));
-  if (int r = grow(c, &c->d_diff, &c->diff_cap, total)) return r;
-  char* d = static_cast<char*>(c->d_diff);
-  auto up = [&](size_t off, const void* h, size_t n) {
-    return n ? hipMemcpyAsync(d + off, h, n, hipMemcpyHostToDevice, c->stream) : hipSuccess;
-  };
-  HIPCHK(c, up(b_ploff, pl_off.data(), 4 * ((size_t)W + 1)));
-  HIPCHK(c, up(b_plid, pl_id.data(), 4 * (size_t)pl_off[W]));
-  HIPCHK(c, up(b_ovoff, st->ovr_off, 4 * ((size_t)W + 1)));
-  HIPCHK(c, up(b_ovid, st->ovr_cluster, 4 * (size_t)NO));
-  HIPCHK(c, up(b_ovval, st->ovr_value, 8 * (size_t)NO));
-  HIPCHK(c, up(b_uf, uflag.data(), (size_t)W));
-  HIPCHK(c, up(b_ovk, st->ovr_kind, (size_t)NO));
-  ResultDiffDev dd{};
-  dd.W = W;
-  dd.status = c->d_status;
-  dd.count = c->d_count;
-  dd.cluster = c->d_cluster;
-  dd.replicas = c->d_replicas;
-  dd.out_off = c->bd.out_off;
-  dd.pl_off = reinterpret_cast<const int32_t*>(d + b_ploff);
-  dd.pl_id = reinterpret_cast<const int32_t*>(d + b_plid);
-  dd.uflag = reinterpret_cast<const uint8_t*>(d + b_uf);
-  dd.ov_off = reinterpret_cast<const int32_t*>(d + b_ovoff);
-  dd.ov_id = reinterpret_cast<const int32_t*>(d + b_ovid);
-  dd.ov_val = reinterpret_cast<const int64_t*>(d + b_ovval);
-  dd.ov_kind = reinterpret_cast<const uint8_t*>(d + b_ovk);
-  dd.out = reinterpret_cast<uint32_t*>(d + b_out);
-  HIPCHK(c, launch_result_diff(dd, c->stream));
-  HIPCHK(c, hipMemcpyAsync(out, dd.out, 4 * (size_t)W, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's state arrays are free on return
-  return KAD_OK;
 }
 
 int kad_path_counts(kad_ctx* c, int32_t* out) {
@@ -1356,131 +1387,144 @@ int kad_debug_inject_fault(kad_ctx* c, int where) {
   return KAD_OK;
 }
 
-int kad_debug_scores(kad_ctx* c, const kad_profile* p, uint8_t* feasible, int64_t* total) {
-  if (!c || !feasible || !total) return KAD_EINVAL;
+int kad_debug_plan_force_workspace(kad_ctx* c, int on) {
+  if (!c) return KAD_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  const size_t n = (size_t)c->batch_hdr.n_units * c->sd.C;
-  uint8_t* df = nullptr;
-  int64_t* dt = nullptr;
-  HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMalloc(&df, n ? n : 1));
-  HIPCHK(c, hipMalloc(&dt, (n ? n : 1) * 8));
-  HIPCHK(c, hipMemsetAsync(df, 0, n ? n : 1, c->stream));
-  HIPCHK(c, hipMemsetAsync(dt, 0, (n ? n : 1) * 8, c->stream));
-  int r = schedule_locked(c, p, df, dt);
-  if (r == 0 && n) {
-    HIPCHK(c, hipMemcpyAsync(feasible, df, n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(total, dt, n * 8, hipMemcpyDeviceToHost, c->stream));
-  }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  (void)hipFree(df);
-  (void)hipFree(dt);
-  return r;
+  c->plan_force_ws = on != 0;
+  return KAD_OK;
+}
+
+int kad_debug_scores(kad_ctx* c, const kad_profile* p, uint8_t* feasible, int64_t* total) {
+  return guarded(c, [&]() -> int {
+    if (!c || !feasible || !total) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    const size_t n = (size_t)c->batch_hdr.n_units * c->sd.C;
+    uint8_t* df = nullptr;
+    int64_t* dt = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMalloc(&df, n ? n : 1));
+    HIPCHK(c, hipMalloc(&dt, (n ? n : 1) * 8));
+    HIPCHK(c, hipMemsetAsync(df, 0, n ? n : 1, c->stream));
+    HIPCHK(c, hipMemsetAsync(dt, 0, (n ? n : 1) * 8, c->stream));
+    int r = schedule_locked(c, p, df, dt);
+    if (r == 0 && n) {
+      HIPCHK(c, hipMemcpyAsync(feasible, df, n, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(total, dt, n * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(df);
+    (void)hipFree(dt);
+    return r;
+  });
 }
 
 
 int kad_select_rows(kad_ctx* c, int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,
                     uint32_t pflags, int32_t* out_count, int32_t* out_sel, int32_t* out_status) {
-  if (!c || n_rows < 0) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(c, hipSetDevice(c->device));
-  const size_t tot = row_off[n_rows];
-  int kmax = 1;
-  for (int r = 0; r < n_rows; r++) {
-    const int k = row_off[r + 1] - row_off[r];
-    if (k > 65535) return fail(c, KAD_EINVAL, "row longer than 65535");
-    kmax = k > kmax ? k : kmax;
-  }
-  std::vector<void*> owned;
-  int32_t *d_off, *d_cnt, *d_sel, *d_st;
-  int64_t *d_sc, *d_mc;
-  int r = 0;
-  if ((r = to_dev(c, row_off, n_rows + 1, &d_off, owned)) || (r = to_dev(c, scores, tot, &d_sc, owned)) ||
-      (r = to_dev(c, maxc, n_rows, &d_mc, owned)) || (r = to_dev<int32_t>(c, nullptr, n_rows, &d_cnt, owned)) ||
-      (r = to_dev<int32_t>(c, nullptr, tot, &d_sel, owned)) || (r = to_dev<int32_t>(c, nullptr, n_rows, &d_st, owned))) {
+  return guarded(c, [&]() -> int {
+    if (!c || n_rows < 0) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t tot = row_off[n_rows];
+    int kmax = 1;
+    for (int r = 0; r < n_rows; r++) {
+      const int k = row_off[r + 1] - row_off[r];
+      if (k > 65535) return fail(c, KAD_EINVAL, "row longer than 65535");
+      kmax = k > kmax ? k : kmax;
+    }
+    std::vector<void*> owned;
+    int32_t *d_off, *d_cnt, *d_sel, *d_st;
+    int64_t *d_sc, *d_mc;
+    int r = 0;
+    if ((r = to_dev(c, row_off, n_rows + 1, &d_off, owned)) || (r = to_dev(c, scores, tot, &d_sc, owned)) ||
+        (r = to_dev(c, maxc, n_rows, &d_mc, owned)) || (r = to_dev<int32_t>(c, nullptr, n_rows, &d_cnt, owned)) ||
+        (r = to_dev<int32_t>(c, nullptr, tot, &d_sel, owned)) || (r = to_dev<int32_t>(c, nullptr, n_rows, &d_st, owned))) {
+      for (void* p : owned) (void)hipFree(p);
+      return r;
+    }
+    void* scr = nullptr;
+    size_t scr_bytes = 0;
+    const size_t wb = select_wave_bytes(kmax);
+    if (wb > 64 * 1024) {
+      scr_bytes = wb * (size_t)(n_rows < 4096 ? n_rows : 4096);
+      HIPCHK(c, hipMalloc(&scr, scr_bytes));
+      owned.push_back(scr);
+    }
+    hipError_t e = launch_select_rows(n_rows, d_off, d_sc, d_mc, pflags, kmax, d_cnt, d_sel, d_st, scr, scr_bytes, c->stream);
+    if (e == hipSuccess) {
+      (void)hipMemcpyAsync(out_count, d_cnt, n_rows * 4, hipMemcpyDeviceToHost, c->stream);
+      if (tot) (void)hipMemcpyAsync(out_sel, d_sel, tot * 4, hipMemcpyDeviceToHost, c->stream);
+      (void)hipMemcpyAsync(out_status, d_st, n_rows * 4, hipMemcpyDeviceToHost, c->stream);
+      e = hipStreamSynchronize(c->stream);
+    }
     for (void* p : owned) (void)hipFree(p);
-    return r;
-  }
-  void* scr = nullptr;
-  size_t scr_bytes = 0;
-  const size_t wb = select_wave_bytes(kmax);
-  if (wb > 64 * 1024) {
-    scr_bytes = wb * (size_t)(n_rows < 4096 ? n_rows : 4096);
-    HIPCHK(c, hipMalloc(&scr, scr_bytes));
-    owned.push_back(scr);
-  }
-  hipError_t e = launch_select_rows(n_rows, d_off, d_sc, d_mc, pflags, kmax, d_cnt, d_sel, d_st, scr, scr_bytes, c->stream);
-  if (e == hipSuccess) {
-    (void)hipMemcpyAsync(out_count, d_cnt, n_rows * 4, hipMemcpyDeviceToHost, c->stream);
-    if (tot) (void)hipMemcpyAsync(out_sel, d_sel, tot * 4, hipMemcpyDeviceToHost, c->stream);
-    (void)hipMemcpyAsync(out_status, d_st, n_rows * 4, hipMemcpyDeviceToHost, c->stream);
-    e = hipStreamSynchronize(c->stream);
-  }
-  for (void* p : owned) (void)hipFree(p);
-  if (e != hipSuccess) return fail(c, KAD_EHIP, hipGetErrorString(e));
-  return KAD_OK;
+    if (e != hipSuccess) return fail(c, KAD_EHIP, hipGetErrorString(e));
+    return KAD_OK;
+  });
 }
 
 int kad_plan_rows(kad_ctx* c, int n_rows, const int32_t* row_off, const uint32_t* hash, const int64_t* weight,
                   const int64_t* min_r, const int64_t* max_r, const int64_t* cap, const int64_t* current,
                   const uint32_t* elem_flags, const int64_t* total, const uint32_t* row_flags, int64_t* out_plan,
                   int64_t* out_overflow) {
-  if (!c || n_rows < 0) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(c, hipSetDevice(c->device));
-  const size_t tot = row_off[n_rows];
-  int kmax = 1;
-  for (int r = 0; r < n_rows; r++) {
-    const int k = row_off[r + 1] - row_off[r];
-    kmax = k > kmax ? k : kmax;
-  }
-  std::vector<void*> owned;
-  PlanRowsDev R{};
-  R.n_rows = n_rows;
-  int32_t* d_off;
-  uint32_t *d_hash, *d_ef, *d_rf;
-  int64_t *d_w, *d_mn, *d_mx, *d_cap, *d_cur, *d_tot, *d_plan, *d_over;
-  int r = 0;
-  if ((r = to_dev(c, row_off, n_rows + 1, &d_off, owned)) || (r = to_dev(c, hash, tot, &d_hash, owned)) ||
-      (r = to_dev(c, weight, tot, &d_w, owned)) || (r = to_dev(c, min_r, tot, &d_mn, owned)) ||
-      (r = to_dev(c, max_r, tot, &d_mx, owned)) || (r = to_dev(c, cap, tot, &d_cap, owned)) ||
-      (r = to_dev(c, current, tot, &d_cur, owned)) || (r = to_dev(c, elem_flags, tot, &d_ef, owned)) ||
-      (r = to_dev(c, total, n_rows, &d_tot, owned)) || (r = to_dev(c, row_flags, n_rows, &d_rf, owned)) ||
-      (r = to_dev<int64_t>(c, nullptr, tot, &d_plan, owned)) || (r = to_dev<int64_t>(c, nullptr, tot, &d_over, owned))) {
-    for (void* p : owned) (void)hipFree(p);
-    return r;
-  }
-  R.row_off = d_off;
-  R.hash = d_hash;
-  R.weight = d_w;
-  R.min_r = d_mn;
-  R.max_r = d_mx;
-  R.cap = d_cap;
-  R.current = d_cur;
-  R.elem_flags = d_ef;
-  R.total = d_tot;
-  R.row_flags = d_rf;
-  R.out_plan = d_plan;
-  R.out_overflow = d_over;
-  void* scr = nullptr;
-  size_t scr_bytes = 0;
-  const size_t wb = plan_wave_bytes(kmax);
-  if (wb > 64 * 1024) {
-    scr_bytes = wb * (size_t)(n_rows < 4096 ? n_rows : 4096);
-    HIPCHK(c, hipMalloc(&scr, scr_bytes));
-    owned.push_back(scr);
-  }
-  hipError_t e = launch_plan_rows(R, kmax, scr, scr_bytes, c->stream);
-  if (e == hipSuccess) {
-    if (tot) {
-      (void)hipMemcpyAsync(out_plan, d_plan, tot * 8, hipMemcpyDeviceToHost, c->stream);
-      (void)hipMemcpyAsync(out_overflow, d_over, tot * 8, hipMemcpyDeviceToHost, c->stream);
+  return guarded(c, [&]() -> int {
+    if (!c || n_rows < 0) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t tot = row_off[n_rows];
+    int kmax = 1;
+    for (int r = 0; r < n_rows; r++) {
+      const int k = row_off[r + 1] - row_off[r];
+      kmax = k > kmax ? k : kmax;
     }
-    e = hipStreamSynchronize(c->stream);
-  }
-  for (void* p : owned) (void)hipFree(p);
-  if (e != hipSuccess) return fail(c, KAD_EHIP, hipGetErrorString(e));
-  return KAD_OK;
+    std::vector<void*> owned;
+    PlanRowsDev R{};
+    R.n_rows = n_rows;
+    int32_t* d_off;
+    uint32_t *d_hash, *d_ef, *d_rf;
+    int64_t *d_w, *d_mn, *d_mx, *d_cap, *d_cur, *d_tot, *d_plan, *d_over;
+    int r = 0;
+    if ((r = to_dev(c, row_off, n_rows + 1, &d_off, owned)) || (r = to_dev(c, hash, tot, &d_hash, owned)) ||
+        (r = to_dev(c, weight, tot, &d_w, owned)) || (r = to_dev(c, min_r, tot, &d_mn, owned)) ||
+        (r = to_dev(c, max_r, tot, &d_mx, owned)) || (r = to_dev(c, cap, tot, &d_cap, owned)) ||
+        (r = to_dev(c, current, tot, &d_cur, owned)) || (r = to_dev(c, elem_flags, tot, &d_ef, owned)) ||
+        (r = to_dev(c, total, n_rows, &d_tot, owned)) || (r = to_dev(c, row_flags, n_rows, &d_rf, owned)) ||
+        (r = to_dev<int64_t>(c, nullptr, tot, &d_plan, owned)) || (r = to_dev<int64_t>(c, nullptr, tot, &d_over, owned))) {
+      for (void* p : owned) (void)hipFree(p);
+      return r;
+    }
+    R.row_off = d_off;
+    R.hash = d_hash;
+    R.weight = d_w;
+    R.min_r = d_mn;
+    R.max_r = d_mx;
+    R.cap = d_cap;
+    R.current = d_cur;
+    R.elem_flags = d_ef;
+    R.total = d_tot;
+    R.row_flags = d_rf;
+    R.out_plan = d_plan;
+    R.out_overflow = d_over;
+    void* scr = nullptr;
+    size_t scr_bytes = 0;
+    const size_t wb = plan_wave_bytes(kmax);
+    if (wb > 64 * 1024) {
+      scr_bytes = wb * (size_t)(n_rows < 4096 ? n_rows : 4096);
+      HIPCHK(c, hipMalloc(&scr, scr_bytes));
+      owned.push_back(scr);
+    }
+    hipError_t e = launch_plan_rows(R, kmax, c->plan_force_ws, scr, scr_bytes, c->stream);
+    if (e == hipSuccess) {
+      if (tot) {
+        (void)hipMemcpyAsync(out_plan, d_plan, tot * 8, hipMemcpyDeviceToHost, c->stream);
+        (void)hipMemcpyAsync(out_overflow, d_over, tot * 8, hipMemcpyDeviceToHost, c->stream);
+      }
+      e = hipStreamSynchronize(c->stream);
+    }
+    for (void* p : owned) (void)hipFree(p);
+    if (e != hipSuccess) return fail(c, KAD_EHIP, hipGetErrorString(e));
+    return KAD_OK;
+  });
 }
 
 /* ------------------------------------------------ scheduling-trigger hashes */
@@ -1562,15 +1606,19 @@ static int trigger_download_locked(kad_ctx* c, uint32_t* out_hash) {
 }
 
 int kad_trigger_suffix_upload(kad_ctx* c, const uint8_t* suffix, size_t nbytes) {
-  if (!c || (!suffix && nbytes)) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  return trigger_suffix_upload_locked(c, suffix, nbytes);
+  return guarded(c, [&]() -> int {
+    if (!c || (!suffix && nbytes)) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return trigger_suffix_upload_locked(c, suffix, nbytes);
+  });
 }
 
 int kad_trigger_prefixes_upload(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix) {
-  if (!c || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  return trigger_prefixes_upload_locked(c, n, prefix_off, prefix);
+  return guarded(c, [&]() -> int {
+    if (!c || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    return trigger_prefixes_upload_locked(c, n, prefix_off, prefix);
+  });
 }
 
 int kad_trigger_run(kad_ctx* c) {
@@ -1588,13 +1636,15 @@ int kad_trigger_download(kad_ctx* c, uint32_t* out_hash) {
 // one critical section (see kad_schedule_batch)
 int kad_trigger_hashes(kad_ctx* c, int n, const int64_t* prefix_off, const uint8_t* prefix, const uint8_t* suffix,
                        size_t suffix_len, uint32_t* out_hash) {
-  if (!c || (!suffix && suffix_len) || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  int r = trigger_suffix_upload_locked(c, suffix, suffix_len);
-  if (!r) r = trigger_prefixes_upload_locked(c, n, prefix_off, prefix);
-  if (!r) r = trigger_run_locked(c);
-  if (!r) r = trigger_download_locked(c, out_hash);
-  return r;
+  return guarded(c, [&]() -> int {
+    if (!c || (!suffix && suffix_len) || n < 0 || !prefix_off || prefix_off[0] != 0) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    int r = trigger_suffix_upload_locked(c, suffix, suffix_len);
+    if (!r) r = trigger_prefixes_upload_locked(c, n, prefix_off, prefix);
+    if (!r) r = trigger_run_locked(c);
+    if (!r) r = trigger_download_locked(c, out_hash);
+    return r;
+  });
 }
 
 }  // extern "C"

@@ -231,7 +231,7 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
 hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,
                               uint32_t pflags, int kmax, int32_t* out_count, int32_t* out_sel, int32_t* out_status,
                               void* global_scratch, size_t scratch_bytes, hipStream_t st);
-hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, void* global_scratch, size_t scratch_bytes,
+hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, int force_ws, void* global_scratch, size_t scratch_bytes,
                             hipStream_t st);
 
 // kad_snapshot_update: scatter the changed clusters' columns of every snapshot

@@ -3811,14 +3811,18 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
       if (hipError_t e = hipEventRecord(join, side)) return e;
     }
     hipLaunchKernelGGL(schedule_wide_kernel<WIDE_MAX_NCH>, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
-    if (hipError_t e = hipGetLastError()) return e;
-    if (hipError_t e = rec(after_main)) return e;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = rec(after_main);
     if (beside) {
-      if (hipError_t e = hipStreamWaitEvent(st, join, 0)) return e;
-    } else if (hipError_t e = launch_rows(s, b, o, p, st)) {
-      return e;
+      // joined even when the wide launch failed: the row kernel on the side stream must finish before
+      // anything later on st (the next batch upload) can overwrite what it reads
+      const hipError_t j = hipStreamWaitEvent(st, join, 0);
+      if (e == hipSuccess) e = j;
+    } else if (e == hipSuccess) {
+      e = launch_rows(s, b, o, p, st);
     }
-    if (hipError_t e = rec(after_rows)) return e;
+    if (e != hipSuccess) return e;
+    if (hipError_t e2 = rec(after_rows)) return e2;
     // feasible lists longer than WIDE_P positions can come from any unit: the defer pass always runs
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);
   }
@@ -3956,12 +3960,12 @@ hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t*
   return hipGetLastError();
 }
 
-hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, void* gscr, size_t scr_bytes, hipStream_t st) {
+hipError_t launch_plan_rows(const PlanRowsDev& r, int kmax, int force_ws, void* gscr, size_t scr_bytes,
+                            hipStream_t st) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   if (r.n_rows == 0 || kmax <= 0) return hipSuccess;
   const size_t wb = plan_layout(kmax).bytes;
-  // KAD_PLAN_FORCE_WS=1 (tests): rows of K <= 64 through the LDS-workspace planner too
-  const int force_ws = getenv("KAD_PLAN_FORCE_WS") ? atoi(getenv("KAD_PLAN_FORCE_WS")) : 0;
+  // force_ws (kad_debug_plan_force_workspace, tests): rows of K <= 64 through the LDS-workspace planner too
   if (wb <= (size_t)LDS_BUDGET) {
     hipLaunchKernelGGL(plan_rows_kernel<false>, dim3(r.n_rows), dim3(64), wb, st, r, (char*)nullptr, (int)wb,
                        r.n_rows, force_ws);

@@ -457,7 +457,7 @@ static const char* check_vocab(const kad_pack_vocab* v) {
   return nullptr;
 }
 
-int kad_packer_create(const kad_pack_vocab* v, kad_packer** out) {
+static int packer_create_impl(const kad_pack_vocab* v, kad_packer** out) {
   if (!v || !out) {
     g_create_err = "null vocabulary or output pointer";
     return KAD_EINVAL;
@@ -503,7 +503,7 @@ int kad_packer_destroy(kad_packer* p) {
 
 const char* kad_packer_error(kad_packer* p) { return p ? p->err.c_str() : g_create_err.c_str(); }
 
-int kad_packer_take(kad_packer* p, void* dst, size_t cap) {
+static int packer_take_impl(kad_packer* p, void* dst, size_t cap) {
   if (!p || (!dst && p->out_n)) return KAD_EINVAL;
   if (cap < p->out_n) return p->fail(KAD_EINVAL, "destination smaller than the packed blob");
   const size_t n = p->out_n, chunk = 4u << 20;
@@ -526,8 +526,8 @@ int kad_packer_blob(kad_packer* p, const void** data, size_t* nbytes) {
   return KAD_OK;
 }
 
-int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns* su, int threads, size_t* nbytes,
-                   kad_pack_stats* stats) {
+static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_columns* su, int threads,
+                           size_t* nbytes, kad_pack_stats* stats) {
   if (!P || !prof || !su || !nbytes) return KAD_EINVAL;
   if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
   P->take_threads = threads;
@@ -1396,6 +1396,35 @@ int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns*
   }
   *nbytes = total;
   return KAD_OK;
+}
+
+// The entry points: nothing may unwind through the C ABI. An exception out of the packer (std::bad_alloc
+// from a task's vectors, rethrown by the worker pool after every worker has finished) becomes KAD_ENOMEM.
+int kad_packer_create(const kad_pack_vocab* v, kad_packer** out) {
+  try {
+    return packer_create_impl(v, out);
+  } catch (const std::exception& e) {
+    g_create_err = std::string("packer creation failed: ") + e.what();
+    return KAD_ENOMEM;
+  }
+}
+
+int kad_packer_take(kad_packer* p, void* dst, size_t cap) {
+  try {
+    return packer_take_impl(p, dst, cap);
+  } catch (const std::exception& e) {
+    return p->fail(KAD_ENOMEM, std::string("copy-out failed: ") + e.what());
+  }
+}
+
+int kad_pack_batch(kad_packer* P, const kad_profile* prof, const kad_su_columns* su, int threads, size_t* nbytes,
+                   kad_pack_stats* stats) {
+  try {
+    return pack_batch_impl(P, prof, su, threads, nbytes, stats);
+  } catch (const std::exception& e) {
+    if (!P) return KAD_ENOMEM;
+    return P->fail(KAD_ENOMEM, std::string("packing failed: ") + e.what());
+  }
 }
 
 }  // extern "C"

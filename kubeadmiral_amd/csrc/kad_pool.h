@@ -6,14 +6,25 @@
 // range runs on its own thread as with per-call threads. Between jobs a worker spins for ~0.2 ms before it
 // sleeps on a condition variable: the packer's and the checks' back-to-back parallel loops do not pay a
 // wake-up each. A parallel call made from inside a task runs serially (no nested jobs).
+//
+// fork(): a child has none of the parent's workers (and may have inherited a locked mutex), so a
+// pthread_atfork child handler drops the pool (it is leaked, never touched again) and the child's first
+// parallel call builds a fresh one.
+// Exceptions: a task that throws (e.g. std::bad_alloc in the packer) is caught on whichever thread ran it;
+// run() still waits for every worker to finish the job before it rethrows the first one, so no worker
+// can touch the caller's unwound frame. The extern "C" entry points turn it into an error code.
 #pragma once
+#include <pthread.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <exception>
 #include <functional>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -34,7 +45,7 @@ class Pool {
     for (auto& t : th_) t.join();
   }
   int threads() const { return (int)th_.size() + 1; }
-  // f(t) for every t in [0, n); returns when all have run
+  // f(t) for every t in [0, n); returns when all have run; rethrows the first exception a task threw
   void run(int n, const std::function<void(int)>& f) {
     if (n <= 0) return;
     if (n == 1 || in_task() || th_.empty()) {
@@ -43,6 +54,7 @@ class Pool {
     }
     std::lock_guard<std::mutex> rg(run_mu_);  // one job at a time
     const int P = std::min(n, threads());
+    err_ = nullptr;
     pending_.store(P - 1, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> g(mu_);  // a worker reads (gen, job) together under mu_
@@ -52,16 +64,33 @@ class Pool {
       gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
-    in_task() = true;
-    for (int t = 0; t < n; t += P) f(t);
-    in_task() = false;
+    {
+      struct InTask {  // reset even when a task throws
+        InTask() { in_task() = true; }
+        ~InTask() { in_task() = false; }
+      } guard;
+      run_tasks(f, 0, n, P);
+    }
     while (pending_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    if (err_) {
+      std::exception_ptr e = err_;
+      err_ = nullptr;
+      std::rethrow_exception(e);
+    }
   }
 
  private:
   static bool& in_task() {
     static thread_local bool flag = false;
     return flag;
+  }
+  void run_tasks(const std::function<void(int)>& f, int j, int ntask, int nthr) {
+    try {
+      for (int t = j; t < ntask; t += nthr) f(t);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(err_mu_);
+      if (!err_) err_ = std::current_exception();
+    }
   }
   void loop(int j) {
     uint64_t seen = 0;
@@ -88,14 +117,14 @@ class Pool {
       }
       if (j < nthr && job) {
         in_task() = true;
-        for (int t = j; t < ntask; t += nthr) (*job)(t);
+        run_tasks(*job, j, ntask, nthr);
         in_task() = false;
         pending_.fetch_sub(1, std::memory_order_acq_rel);
       }
     }
   }
   std::vector<std::thread> th_;
-  std::mutex mu_, run_mu_;
+  std::mutex mu_, run_mu_, err_mu_;
   std::condition_variable cv_;
   std::atomic<uint64_t> gen_{0};
   std::atomic<int> pending_{0};
@@ -103,12 +132,34 @@ class Pool {
   // written by run() before gen_ is bumped (release), read by workers after they see the bump (acquire)
   const std::function<void(int)>* job_ = nullptr;
   int ntask_ = 0, nthr_ = 0;
+  std::exception_ptr err_;
 };
 
-// up to 16 threads (the GPU box's CPU share), created on first use
+struct Holder {
+  std::mutex mu;
+  Pool* p = nullptr;
+};
+
+inline Holder& holder() {
+  static Holder h;
+  return h;
+}
+
+// fork() child: only the forking thread exists; forget the parent's pool and reset the creation lock
+inline void on_fork_child() {
+  Holder& h = holder();
+  new (&h.mu) std::mutex();
+  h.p = nullptr;
+}
+
+// up to 16 threads (the GPU box's CPU share), created on first use (per process)
 inline Pool& pool() {
-  static Pool p((int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())) - 1);
-  return p;
+  static std::once_flag once;
+  std::call_once(once, [] { pthread_atfork(nullptr, nullptr, &on_fork_child); });
+  Holder& h = holder();
+  std::lock_guard<std::mutex> g(h.mu);
+  if (!h.p) h.p = new Pool((int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())) - 1);
+  return *h.p;
 }
 
 }  // namespace kadpool

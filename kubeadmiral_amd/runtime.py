@@ -92,6 +92,7 @@ def load_library(path: str = LIB_PATH):
     L.kad_plan_rows.argtypes = [P, I, P, P, P, P, P, P, P, P, P, P, P, P]
     L.kad_debug_scores.argtypes = [P, P, P, P]
     L.kad_debug_inject_fault.argtypes = [P, I]
+    L.kad_debug_plan_force_workspace.argtypes = [P, I]
     L.kad_trigger_suffix_upload.argtypes = [P, P, SZ]
     L.kad_trigger_prefixes_upload.argtypes = [P, I, P, P]
     L.kad_trigger_run.argtypes = [P]
@@ -183,11 +184,18 @@ class Context:
         rebuild."""
         self._chk(self.L.kad_debug_inject_fault(self.h, where))
 
+    def plan_force_workspace(self, on: bool):
+        """kad_debug_plan_force_workspace (tests): plan_rows through the LDS-workspace planner."""
+        self._chk(self.L.kad_debug_plan_force_workspace(self.h, int(bool(on))))
+
     def update_snapshot(self, delta: SnapshotDelta):
         """kad_snapshot_update: patch the resident snapshot; the resident batch stays valid."""
         self._chk(self.L.kad_snapshot_update(self.h, _p(delta.blob), delta.blob.nbytes))
 
     def upload_batch(self, batch: Batch):
+        chk = getattr(batch, "check_current", None)
+        if chk is not None:
+            chk()
         self._chk(self.L.kad_batch_upload(self.h, _p(batch.blob), batch.blob.nbytes))
         self.batch = batch
 
@@ -249,7 +257,9 @@ class Context:
         else:  # views of the batch's sizes
             W, n = self.batch.W, max(1, self.batch.n_out_slots)
             arrs = ((out.status, W), (out.count, W), (out.flags, W), (out.cluster, n), (out.replicas, n))
-            for a, m in arrs:
+            for (a, m), dt in zip(arrs, (np.int32, np.int32, np.uint32, np.int32, np.int64)):
+                if a.dtype != dt:  # kad_results_download copies 4 or 8 bytes per element
+                    raise ValueError(f"download buffer dtype {a.dtype}, kad_results_download writes {np.dtype(dt)}")
                 if len(a) < m or not a.flags.c_contiguous:
                     raise ValueError("download buffers smaller than the uploaded batch")
             res = BatchResult(*(a[:m] for a, m in arrs), self.batch.out_off)
@@ -260,6 +270,9 @@ class Context:
 
     def schedule_batch(self, fwk: Framework, batch: Batch) -> BatchResult:
         """kad_schedule_batch: upload, schedule and download under one hold of the context lock."""
+        chk = getattr(batch, "check_current", None)
+        if chk is not None:
+            chk()
         res = BatchResult.empty(batch)
         v = ResultView(res.status.ctypes.data, res.count.ctypes.data, res.flags.ctypes.data, res.cluster.ctypes.data,
                        res.replicas.ctypes.data)

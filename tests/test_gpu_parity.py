@@ -111,12 +111,14 @@ def _gpu_plan(ctx, rsp, replicas, clusters, existing, est, avoid, keep):
                                             for c in PLANNER])
 def test_golden_planner_on_gpu(ctx, c, path, monkeypatch):
     """planner_test.go's cases through kad_plan_rows: the register planner (rows of K <= 64, plan_row_lanes)
-    and the LDS-workspace planner (KAD_PLAN_FORCE_WS=1, the path of rows with K > 64)."""
+    and the LDS-workspace planner (kad_debug_plan_force_workspace, the path of rows with K > 64)."""
     from test_oracle_golden import run_planner_case
-    if path == "ws":
-        monkeypatch.setenv("KAD_PLAN_FORCE_WS", "1")
-    converged, plan, over = run_planner_case(
-        c, lambda rsp, r, cl, ex, est, key, av, kp: _gpu_plan(ctx, rsp, r, cl, ex, est, av, kp))
+    ctx.plan_force_workspace(path == "ws")
+    try:
+        converged, plan, over = run_planner_case(
+            c, lambda rsp, r, cl, ex, est, key, av, kp: _gpu_plan(ctx, rsp, r, cl, ex, est, av, kp))
+    finally:
+        ctx.plan_force_workspace(False)
     assert converged
     if plan or c["want_plan"]:
         assert plan == c["want_plan"]
@@ -143,8 +145,11 @@ def test_plan_rows_lanes_equal_workspace(ctx, seed, monkeypatch):
         rows.append({"elems": elems, "total": int(rng.integers(0, 20_000)), "avoid": bool(rng.random() < 0.5),
                      "keep": bool(rng.random() < 0.5)})
     lanes = ctx.plan_rows(rows)
-    monkeypatch.setenv("KAD_PLAN_FORCE_WS", "1")
-    ws = ctx.plan_rows(rows)
+    ctx.plan_force_workspace(True)
+    try:
+        ws = ctx.plan_rows(rows)
+    finally:
+        ctx.plan_force_workspace(False)
     assert lanes == ws
 
 

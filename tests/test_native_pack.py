@@ -91,6 +91,99 @@ def test_concurrent_packers_share_the_worker_pool():
             assert np.array_equal(b, want[i])
 
 
+def test_pack_after_fork_in_the_child():
+    """The worker pool is per process (kad_pool.h): a child forked after the parent's pool exists packs with a
+    fresh pool (its parent's workers do not exist in it) — the same blob, no hang. Forked while another
+    thread of the parent is packing, too (that thread's locks are not the child's)."""
+    import os
+    import threading
+
+    clusters, units = synth.gen_fuzz(4545, W=9000, C=40)
+    snap = pack.Snapshot(clusters)
+    fwk = F.Framework()
+    cols = CO.from_units(units)
+    want = CO.NativePacker(snap).pack(fwk, cols, threads=8).blob.copy()  # the pool now exists
+    stop = threading.Event()
+
+    def busy():
+        P = CO.NativePacker(snap)
+        while not stop.is_set():
+            P.pack(fwk, cols, threads=8)
+
+    t = threading.Thread(target=busy)
+    t.start()
+    try:
+        for _ in range(3):
+            r, w = os.pipe()
+            pid = os.fork()
+            if pid == 0:  # child: pack twice, report, leave without running the parent's atexit handlers
+                ok = 1
+                try:
+                    for _ in range(2):
+                        ok &= int(np.array_equal(CO.NativePacker(snap).pack(fwk, cols, threads=8).blob, want))
+                finally:
+                    os.write(w, bytes([ok]))
+                    os._exit(0)
+            os.close(w)
+            import select
+            ready, _, _ = select.select([r], [], [], 60)
+            assert ready, "child packer hung after fork"
+            assert os.read(r, 1) == b"\x01"
+            os.close(r)
+            os.waitpid(pid, 0)
+    finally:
+        stop.set()
+        t.join()
+
+
+def test_in_place_batch_is_refused_once_stale():
+    """pack(take=False) returns the packer's own buffer: the batch keeps the packer alive, and a batch the
+    packer has since overwritten (or freed by close) is refused before any upload."""
+    import gc
+
+    clusters, units = synth.gen_fuzz(4646, W=300, C=20)
+    snap = pack.Snapshot(clusters)
+    fwk = F.Framework()
+    cols = CO.from_units(units)
+    want = CO.NativePacker(snap).pack(fwk, cols).blob.copy()
+    P = CO.NativePacker(snap)
+    nb = P.pack(fwk, cols, take=False)
+    nb.check_current()
+    del P
+    gc.collect()
+    assert np.array_equal(nb.blob, want)  # still the packer's live buffer
+    P = nb.in_place[0]
+    nb2 = P.pack(fwk, cols, take=False)
+    nb2.check_current()
+    with pytest.raises(ValueError, match="packed another batch"):
+        nb.check_current()
+    P.close()
+    with pytest.raises(ValueError, match="closed"):
+        nb2.check_current()
+
+
+def test_download_refuses_wrong_dtypes():
+    """kad_results_download writes 4 / 8 bytes per element: a caller buffer of another dtype is refused
+    before the copy (checked on the host, no GPU needed)."""
+    from kubeadmiral_amd import results, runtime
+
+    clusters, units = synth.gen_fuzz(4747, W=50, C=20)
+    snap = pack.Snapshot(clusters)
+    fwk = F.Framework()
+    nb = CO.NativePacker(snap).pack(fwk, CO.from_units(units))
+    ctx = object.__new__(runtime.Context)
+    ctx.h, ctx.batch = None, nb
+    good = results.BatchResult.empty(nb)
+    bad = results.BatchResult(good.status, good.count, good.flags, good.cluster, good.replicas.astype(np.int32),
+                              good.out_off)
+    with pytest.raises(ValueError, match="dtype"):
+        ctx.download(out=bad)
+    bad = results.BatchResult(good.status.astype(np.int16), good.count, good.flags, good.cluster, good.replicas,
+                              good.out_off)
+    with pytest.raises(ValueError, match="dtype"):
+        ctx.download(out=bad)
+
+
 def test_empty_batch():
     clusters, _ = synth.gen_fuzz(3, W=1, C=10)
     _same(pack.Snapshot(clusters), F.Framework(), [])
