@@ -56,7 +56,14 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) 
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+        subprocess.run(cmd, check=True)
+    else:
+        # compiler warnings would flood the caller's stderr (bench.py's tail is what the driver keeps): shown
+        # only when the build fails
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout.decode(errors="replace")[-20000:])
+            raise subprocess.CalledProcessError(r.returncode, cmd)
     os.replace(out + ".tmp", out)
     return out
 

@@ -1118,9 +1118,9 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   const bool tm = c->timing;
   c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total || wide_path(c->sd);
   // long feasible lists go to schedule_row_kernel when every filter is in the static words
-  static const bool no_rows = tuning_env("KAD_NO_ROWS", 0) != 0;
+  const bool no_rows = tuning_env("KAD_NO_ROWS", 0) != 0;  // (read per launch: tuning builds only)
   c->bd.use_rows = !no_rows && c->sd.clean && c->sd.fold && c->sd.fitfold && row_kernel_fits(c->sd.C);
-  static const bool rows_after = tuning_env("KAD_ROWS_AFTER", 0) != 0;
+  const bool rows_after = tuning_env("KAD_ROWS_AFTER", 0) != 0;
   const int per = prep_lanes_per_unit(c->sd.C);
   c->bd.early_rows = c->bd.use_rows && !rows_after && wide_path(c->sd) && (per & (per - 1)) == 0 && per <= 64 &&
                      !dbg_feas && !dbg_total;

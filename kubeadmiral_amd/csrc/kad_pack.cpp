@@ -142,6 +142,77 @@ struct WordsHash {
 };
 
 size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
+struct IdSet;
+const std::vector<int32_t>& sorted_unique(const std::vector<int32_t>& cs, int i0, int i1, IdSet& set,
+                                          std::vector<int32_t>& out);
+
+// A per-thread set of snapshot cluster ids in [0, C): a bitmap whose touched words are scanned in order,
+// so sort + unique of a unit's few dozen ids costs one pass plus (max - min) / 64 words. Used when that
+// range is short next to the list (else the caller sorts).
+struct IdSet {
+  std::vector<uint64_t> bm;
+  int lo = INT32_MAX, hi = -1;
+  explicit IdSet(int C) : bm(((size_t)(C > 0 ? C : 1) + 63) / 64, 0ull) {}
+  static bool worth(int lo_id, int hi_id, size_t n) { return hi_id < lo_id || (size_t)((hi_id >> 6) - (lo_id >> 6)) <= 2 * n + 8; }
+  void add(int c) {
+    bm[(size_t)c >> 6] |= 1ull << (c & 63);
+    lo = c < lo ? c : lo;
+    hi = c > hi ? c : hi;
+  }
+  // f(id) for every member in ascending order; the set is empty afterwards
+  template <class F>
+  void drain(F f) {
+    if (hi >= 0)
+      for (int wd = lo >> 6; wd <= (hi >> 6); wd++) {
+        uint64_t x = bm[wd];
+        bm[wd] = 0;
+        while (x) {
+          f(wd * 64 + __builtin_ctzll(x));
+          x &= x - 1;
+        }
+      }
+    lo = INT32_MAX;
+    hi = -1;
+  }
+  // the sorted distinct ids >= 0 among cs[i0, i1) into out
+  static void sorted_unique_into(const std::vector<int32_t>& cs, int i0, int i1, IdSet& set, std::vector<int32_t>& out) {
+    out.clear();
+    int lo_id = INT32_MAX, hi_id = -1;
+    size_t nn = 0;
+    for (int i = i0; i < i1; i++)
+      if (cs[i] >= 0) {
+        lo_id = std::min(lo_id, cs[i]);
+        hi_id = std::max(hi_id, cs[i]);
+        nn++;
+      }
+    if (worth(lo_id, hi_id, nn)) {
+      for (int i = i0; i < i1; i++)
+        if (cs[i] >= 0) set.add(cs[i]);
+      set.drain([&](int c) { out.push_back(c); });
+      return;
+    }
+    for (int i = i0; i < i1; i++)
+      if (cs[i] >= 0) out.push_back(cs[i]);
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+  }
+  int count_and_clear() {
+    int n = 0;
+    if (hi >= 0)
+      for (int wd = lo >> 6; wd <= (hi >> 6); wd++) {
+        n += __builtin_popcountll(bm[wd]);
+        bm[wd] = 0;
+      }
+    lo = INT32_MAX;
+    hi = -1;
+    return n;
+  }
+};
+const std::vector<int32_t>& sorted_unique(const std::vector<int32_t>& cs, int i0, int i1, IdSet& set,
+                                          std::vector<int32_t>& out) {
+  IdSet::sorted_unique_into(cs, i0, i1, set, out);
+  return out;
+}
 
 // Open-addressing index of (hash, id) slots: no allocation per entry, reset by one fill and kept across
 // packs. On a hash match the caller's predicate compares contents, so distinct keys with equal hashes
@@ -253,7 +324,7 @@ struct kad_packer {
     // per string id of the batch's string table, filled lazily by the threads that meet it (every writer
     // stores the same value): 0 unknown, 1 yes, 2 no / label key id + 2 (0 unknown)
     std::vector<uint8_t> m_qname, m_lvalue, m_op;
-    std::vector<int32_t> m_kid;
+    std::vector<int32_t> m_kid, m_cid;  // m_cid: cluster-name string → snapshot id + 2 (0 unknown)
     std::vector<InternChunk> chunks;
   } sc;
 
@@ -591,6 +662,8 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   X.m_lvalue.resize(NSTR);
   X.m_op.resize(NSTR);
   X.m_kid.resize(NSTR);
+  X.m_cid.resize(NSTR);
+  pfill(X.m_cid, (int32_t)0);
   pfill(X.m_qname, (uint8_t)0);
   pfill(X.m_lvalue, (uint8_t)0);
   pfill(X.m_op, (uint8_t)0);
@@ -967,12 +1040,21 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   maxc.resize(W);
   desired.resize(W);
   out_len.resize(W);
-  // cluster names → snapshot ids, once per map / set entry
+  // cluster names → snapshot ids, once per map / set entry; the name lookup itself once per string id of
+  // the batch's table (a Go shim interns: the ~90 map entries per C4 unit name a few hundred clusters)
+  auto cid_of = [&](int32_t id) {
+    int32_t k = __atomic_load_n(&X.m_cid[id], __ATOMIC_RELAXED);
+    if (!k) {
+      k = kad_packer::find(P->name_id, S[id]) + 2;
+      __atomic_store_n(&X.m_cid[id], k, __ATOMIC_RELAXED);
+    }
+    return k - 2;
+  };
   auto resolve = [&](const int32_t* off, const int32_t* names, std::vector<int32_t>& ids) {
     const int n = W ? off[W] : 0;
     ids.resize(n);
     parallel_for(n, threads, [&](int a, int b) {
-      for (int i = a; i < b; i++) ids[i] = kad_packer::find(P->name_id, S[names[i]]);
+      for (int i = a; i < b; i++) ids[i] = cid_of(names[i]);
     });
   };
   std::vector<int32_t> place_c, cur_c, wt_c, min_c, max_c, cap_c;
@@ -986,6 +1068,8 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   parallel_for(W, threads, [&](int a, int b) {
     std::vector<int32_t> ids;
     std::string gkey;
+    IdSet set(C);
+    int32_t lg = -1, lv = -1, lk = -1, lgvk = -1;  // the last (group, version, kind) string ids and their GVK id
     for (int w = a; w < b; w++) {
       const uint32_t sf = su->flags[w];
       uint32_t f = 0;
@@ -1011,8 +1095,14 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
       int nsr = 0;
       for (int i = ns0; i < ns1; i++) nsr += su->scalar_val[i] > 0;
       n_sreq[w] = nsr;
-      kad_packer::gvk_key(gkey, S[su->group[w]], S[su->version[w]], S[su->kind[w]]);
-      gvk[w] = kad_packer::find(P->gvk_id, gkey);
+      if (su->group[w] != lg || su->version[w] != lv || su->kind[w] != lk) {
+        lg = su->group[w];
+        lv = su->version[w];
+        lk = su->kind[w];
+        kad_packer::gvk_key(gkey, S[lg], S[lv], S[lk]);
+        lgvk = kad_packer::find(P->gvk_id, gkey);
+      }
+      gvk[w] = lgvk;
       // filter program length and R_w
       int fl = 1 + (su->sel_off[w + 1] - su->sel_off[w]) + 1, rw = su->sel_off[w + 1] - su->sel_off[w];
       const bool ca = sf & KAD_SU_HAS_CLUSTER_AFFINITY;
@@ -1057,27 +1147,47 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
       // placement (a set: sorted unique snapshot ids)
       const int np_all = su->place_off[w + 1] - su->place_off[w];
       if (np_all > 0) f |= KAD_W_HAS_PLACEMENT;
-      ids.clear();
-      for (int i = su->place_off[w]; i < su->place_off[w + 1]; i++)
-        if (place_c[i] >= 0) ids.push_back(place_c[i]);
-      std::sort(ids.begin(), ids.end());
-      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-      n_place[w] = (int)ids.size();
+      n_place[w] = (int)sorted_unique(place_c, su->place_off[w], su->place_off[w + 1], set, ids).size();
       int ncur = 0;
       for (int i = su->cur_off[w]; i < su->cur_off[w + 1]; i++) ncur += cur_c[i] >= 0;
       n_cur[w] = ncur;
       if (su->wt_off[w + 1] == su->wt_off[w]) f |= KAD_W_DYNAMIC_WEIGHTS;
       // preferences: union of the Weights / Min / Max / EstimatedCapacity (>= 0) names in the snapshot
-      ids.clear();
-      for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++) ids.push_back(wt_c[i]);
-      for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++) ids.push_back(min_c[i]);
-      for (int i = su->max_off[w]; i < su->max_off[w + 1]; i++) ids.push_back(max_c[i]);
-      if (am)
-        for (int i = su->cap_off[w]; i < su->cap_off[w + 1]; i++)
-          if (su->cap_val[i] >= 0) ids.push_back(cap_c[i]);
-      std::sort(ids.begin(), ids.end());
-      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-      n_pref[w] = (int)(ids.size() - (size_t)(!ids.empty() && ids[0] < 0));
+      {
+        int lo_id = INT32_MAX, hi_id = -1;
+        size_t nn = 0;
+        auto scan = [&](const std::vector<int32_t>& cs, const int32_t* off, const int64_t* val) {
+          for (int i = off[w]; i < off[w + 1]; i++)
+            if (cs[i] >= 0 && (!val || val[i] >= 0)) {
+              lo_id = std::min(lo_id, cs[i]);
+              hi_id = std::max(hi_id, cs[i]);
+              nn++;
+            }
+        };
+        scan(wt_c, su->wt_off, nullptr);
+        scan(min_c, su->min_off, nullptr);
+        scan(max_c, su->max_off, nullptr);
+        if (am) scan(cap_c, su->cap_off, su->cap_val);
+        auto each = [&](auto put) {
+          auto one = [&](const std::vector<int32_t>& cs, const int32_t* off, const int64_t* val) {
+            for (int i = off[w]; i < off[w + 1]; i++)
+              if (cs[i] >= 0 && (!val || val[i] >= 0)) put(cs[i]);
+          };
+          one(wt_c, su->wt_off, nullptr);
+          one(min_c, su->min_off, nullptr);
+          one(max_c, su->max_off, nullptr);
+          if (am) one(cap_c, su->cap_off, su->cap_val);
+        };
+        if (IdSet::worth(lo_id, hi_id, nn)) {
+          each([&](int c) { set.add(c); });
+          n_pref[w] = set.count_and_clear();
+        } else {
+          ids.clear();
+          each([&](int c) { ids.push_back(c); });
+          std::sort(ids.begin(), ids.end());
+          n_pref[w] = (int)(std::unique(ids.begin(), ids.end()) - ids.begin());
+        }
+      }
       const size_t ln = S[su->name[w]].size(), lns = S[su->namespace_[w]].size();
       n_key[w] = (int)(lns ? lns + 1 + ln : ln);
       int64_t bound = C;
@@ -1225,6 +1335,11 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
     std::vector<int32_t> ids;
     std::vector<std::pair<int32_t, int64_t>> cl;
     std::vector<PrefEntry> pe;
+    IdSet set(C);
+    // dense per-cluster merge of the four preference maps (small snapshots): values and a map-present mask
+    const bool dense = C <= (1 << 16);
+    std::vector<int64_t> dv(dense ? 4 * (size_t)C : 0);
+    std::vector<uint8_t> dm(dense ? (size_t)C : 0, 0);
     for (int w = a; w < b; w++) {
       const uint32_t sf = su->flags[w];
       // scalar requests with value > 0, in map order (snapshot id or -1)
@@ -1281,11 +1396,7 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
       }
       sp[0] = nt;
       // placement
-      ids.clear();
-      for (int i = su->place_off[w]; i < su->place_off[w + 1]; i++)
-        if (place_c[i] >= 0) ids.push_back(place_c[i]);
-      std::sort(ids.begin(), ids.end());
-      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      sorted_unique(place_c, su->place_off[w], su->place_off[w + 1], set, ids);
       if (!ids.empty()) std::memcpy(place + o_place[w], ids.data(), 4 * ids.size());
       // current clusters (nil replicas → DesiredReplicas, rsp.go:119-126), by snapshot id
       cl.clear();
@@ -1300,6 +1411,35 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
       // preferences sorted by snapshot id: (cluster, map, entry) triples, merged per cluster;
       // a repeated map key keeps its last entry, as a Go map holds one
       const bool am = sf & KAD_SU_HAS_AUTO_MIGRATION;
+      if (dense) {  // maps in order, entries in order: a repeated key's last entry wins, as in the sort below
+        auto put = [&](int c, int m, int64_t v) {
+          dv[(size_t)m * C + c] = v;
+          dm[c] |= (uint8_t)(1u << m);
+          set.add(c);
+        };
+        for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++)
+          if (wt_c[i] >= 0) put(wt_c[i], 0, su->wt_val[i]);
+        for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++)
+          if (min_c[i] >= 0) put(min_c[i], 1, su->min_val[i]);
+        for (int i = su->max_off[w]; i < su->max_off[w + 1]; i++)
+          if (max_c[i] >= 0) put(max_c[i], 2, su->max_val[i]);
+        if (am)
+          for (int i = su->cap_off[w]; i < su->cap_off[w + 1]; i++)
+            if (cap_c[i] >= 0 && su->cap_val[i] >= 0) put(cap_c[i], 3, su->cap_val[i]);
+        int j = o_pref[w];
+        set.drain([&](int c) {
+          const uint8_t m = dm[c];
+          dm[c] = 0;
+          pref_id[j] = c;
+          pref_w[j] = (m & 1) ? dv[c] : 0;
+          pref_min[j] = (m & 2) ? dv[(size_t)C + c] : 0;
+          pref_max[j] = (m & 4) ? dv[2 * (size_t)C + c] : 0;
+          pref_cap[j] = (m & 8) ? dv[3 * (size_t)C + c] : 0;
+          pref_fl[j] = ((m & 1) ? KAD_PREF_HAS_WEIGHT : 0u) | ((m & 4) ? KAD_PREF_HAS_MAX : 0u) |
+                       ((m & 8) ? KAD_PREF_HAS_CAP : 0u);
+          j++;
+        });
+      } else {
       pe.clear();
       for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++)
         if (wt_c[i] >= 0) pe.push_back({wt_c[i], 0, i});
@@ -1334,6 +1474,7 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
         pref_cap[j] = cp;
         pref_fl[j] = fl;
         j++;
+      }
       }
       // su.Key()
       uint8_t* kb = keyb + o_key[w];

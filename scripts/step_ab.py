@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Step-time A/B of tuning knobs (a -DKAD_TUNING build, libkad_tune.so: scripts/wide_exp.py --build) on one
+workload, variants alternating within one process so that box-to-box spread cancels.
+
+    python scripts/step_ab.py --config c3 --units 125000 --variants "base;KAD_ROWS_AFTER=1" [--rounds 3]
+
+Each variant is ';'-separated, its knobs ','-separated NAME=VALUE pairs (tuning_env reads them per launch
+for the knobs that are not cached; cached knobs need their own process — the script re-execs nothing).
+Prints one JSON line: mean / min step ms per variant and rank-0 stage times."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--units", type=int, default=0)
+    ap.add_argument("--variants", default="base")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "kubeadmiral_amd", "libkad_tune.so"))
+    a = ap.parse_args()
+    import torch  # noqa: F401
+
+    import bench
+    from kubeadmiral_amd import columns, runtime, synth
+    from kubeadmiral_amd.pack import Snapshot
+
+    runtime.load_library(a.lib)
+    W0, C = synth.SIZES[a.config]
+    clusters = bench.make_clusters(a.config, C)
+    fwk = synth.profile_for(a.config)
+    snap = Snapshot(clusters)
+    batch = columns.NativePacker(snap).pack(fwk, bench.make_columns(a.config, 0, a.units or W0, clusters))
+    ctx = runtime.Context(0)
+    ctx.upload_snapshot(snap)
+    ctx.upload_batch(batch)
+    variants = [v.strip() for v in a.variants.split(";") if v.strip()]
+    res = {v: [] for v in variants}
+    ref = None
+    for r in range(a.rounds):
+        for v in variants:
+            env = {} if v == "base" else dict(kv.split("=") for kv in v.split(","))
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            for _ in range(3):
+                ctx.schedule(fwk)
+            ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                ctx.schedule(fwk)
+            ctx.sync()
+            res[v].append((time.perf_counter() - t0) / a.steps * 1e3)
+            out = ctx.download()
+            if v == "base" and ref is None:
+                ref = out
+            elif ref is not None and not v.startswith("EXP"):
+                assert out.equal_rows(ref).all(), f"variant {v} changed the results"
+            for k, x in old.items():
+                if x is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = x
+    print(json.dumps({"config": a.config, "units": batch.W, "ms": {v: [round(x, 4) for x in xs] for v, xs in res.items()},
+                      "mean": {v: round(float(np.mean(xs)), 4) for v, xs in res.items()},
+                      "min": {v: round(float(np.min(xs)), 4) for v, xs in res.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
