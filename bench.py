@@ -503,7 +503,8 @@ def compact_line(out: dict, headline: bool = True) -> dict:
     line = {k: out.get(k) for k in keep}
     c = out.get("config", {})
     if "stage_ms" in c:
-        line["config"] = {k: c.get(k) for k in ("workload", "units_total", "units_per_gpu", "clusters", "parallelism")}
+        line["config"] = {k: c.get(k) for k in ("workload", "units_total", "units_per_gpu", "clusters", "parallelism",
+                                                "rccl_world_size")}
         line["config"]["stage_ms"] = {k: v for k, v in c["stage_ms"].items() if v >= 0.002}
         if headline:
             line["config"]["paths"] = c.get("paths")
@@ -536,7 +537,7 @@ def compact_line(out: dict, headline: bool = True) -> dict:
                               "blob_mb": s["blob_mb"], "pipelined_decisions_per_s": e["pipelined"]["decisions_per_s"]}
     if out.get("allgather"):
         a = out["allgather"]
-        line["allgather"] = {"ms": a["ms"], "gbs": a["gbs"], "backend": a["backend"], "verified": bool(a["verified"])}
+        line["allgather"] = {"ms": a["ms"], "gbs": a["gbs"], "backend": a["backend"], "verified": a["verified"]}
     sw = out.get("shard_sweep")
     if sw:
         line["shard_sweep"] = {n: {"max_ms": v["max_ms"], "eff": v["projected_efficiency"]}

@@ -626,11 +626,14 @@ static int refresh_derived(kad_ctx* c) {
   const int C = c->sd.C, TW = c->sd.TW;
   c->sd.res4 = nullptr;
   c->sd.res_iv = nullptr;
+  c->sd.pns4 = nullptr;
   if (c->sd.clean && C > 0) {
-    if (int r = grow(c, &c->d_rescols, &c->rescols_cap, (size_t)40 * C)) return r;
+    if (int r = grow(c, &c->d_rescols, &c->rescols_cap, res_cols_bytes(C))) return r;
     HIPCHK(c, launch_res_cols(c->sd, c->d_rescols, c->stream));
     c->sd.res4 = static_cast<const double4*>(c->d_rescols);
     c->sd.res_iv = reinterpret_cast<const float2*>(c->sd.res4 + C);
+    if (TW <= 4)
+      c->sd.pns4 = reinterpret_cast<const ulonglong4*>(static_cast<const char*>(c->d_rescols) + res_cols_pns4_offset(C));
   }
   c->sd.fold = TW >= 1 && TW <= TFOLD_MAX_TW;
   for (int t = 0; t < TFOLD_MAX_TW; t++) {

@@ -63,6 +63,9 @@ struct SnapDev {
   // alloc_mem - used_mem, alloc_cpu, alloc_mem) as f64, res_iv[c] = (float)(100 / alloc) per resource
   const double4* res4;
   const float2* res_iv;
+  // the PreferNoSchedule words of cluster c, cluster-major (words >= TW zero; TW <= 4, clean snapshots):
+  // one 32-B gather per feasible position instead of TW 8-B ones from the [TW][C] array
+  const ulonglong4* pns4;
 };
 
 struct BatchDev {
@@ -210,8 +213,10 @@ hipError_t launch_req_masks(const SnapDev& s, const BatchDev& b, hipStream_t st,
 // (SnapDev::taint_tab), rebuilt at upload / update
 hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st);
 hipError_t launch_value_rows(const SnapDev& s, uint64_t* vrows, hipStream_t st);
-// SnapDev::res4 / res_iv of a clean snapshot (buf: 40 B per cluster, res4 first)
+// SnapDev::res4 / res_iv (+ pns4 when TW <= 4) of a clean snapshot (buf: 72 B per cluster: res4, res_iv, pns4)
 hipError_t launch_res_cols(const SnapDev& s, void* buf, hipStream_t st);
+inline size_t res_cols_pns4_offset(int C) { return ((size_t)40 * C + 255) & ~(size_t)255; }
+inline size_t res_cols_bytes(int C) { return res_cols_pns4_offset(C) + (size_t)32 * C; }
 // true if the batch runs on schedule_lean_kernel (+ schedule_kernel over its
 // defer list); then launch_prep must run between launch_req_masks and launch_schedule.
 bool fast_path(int C);

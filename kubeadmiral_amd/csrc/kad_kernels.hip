@@ -34,6 +34,11 @@ __device__ unsigned long long g_wavetime[8192 * 2];
 // wide kernel: per wave (units taken, the longest unit's s_memtime cycles, realtime of the last dequeue, units
 // that straddled a tie, HW_ID, XCC_ID)
 __device__ unsigned long long g_wavex[8192 * 6];
+// wide kernel, per unit of the last launch (units < 2^20): realtime start; (duration in realtime ticks,
+// feasible count n << 32, straddle << 47, global wave << 48) — scripts/unit_trace.py
+constexpr int KAD_UTRACE_MAX = 1 << 20;
+__device__ unsigned long long g_ustart[KAD_UTRACE_MAX];
+__device__ unsigned long long g_uinfo[KAD_UTRACE_MAX];
 #define KAD_PT(v) const unsigned long long v = __builtin_readcyclecounter()
 #define KAD_PACC uint32_t pacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
@@ -268,12 +273,17 @@ __global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b, int
 }
 
 // SnapDev::res4 / res_iv (clean snapshots): the same expressions as the wide kernel's block cache
-__global__ __launch_bounds__(256) void res_cols_kernel(SnapDev s, double4* r4, float2* iv) {
+__global__ __launch_bounds__(256) void res_cols_kernel(SnapDev s, double4* r4, float2* iv, ulonglong4* p4) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= s.C) return;
   const int64_t ac = s.alloc_cpu[c], uc = s.used_cpu[c], am = s.alloc_mem[c], um = s.used_mem[c];
   r4[c] = make_double4((double)(ac - uc), (double)(am - um), (double)ac, (double)am);
   iv[c] = make_float2((float)(100.0 / (double)ac), (float)(100.0 / (double)am));
+  if (p4) {
+    const int TW = s.TW;
+    p4[c] = make_ulonglong4(TW > 0 ? s.pns[c] : 0ull, TW > 1 ? s.pns[(size_t)s.C + c] : 0ull,
+                            TW > 2 ? s.pns[2 * (size_t)s.C + c] : 0ull, TW > 3 ? s.pns[3 * (size_t)s.C + c] : 0ull);
+  }
 }
 
 // SnapDev::vrows: one wave per (key, chunk), lane = cluster; lane s < VR_SLOTS collects value s's word
@@ -2152,6 +2162,11 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     }
     const uint32_t nxt = fetch(wn);
     KAD_PT(t0);
+#ifdef KAD_PHASE_PROF
+    const unsigned long long ut0 = __builtin_amdgcn_s_memrealtime();
+    int ut_n = 0;
+    uint32_t ut_fl = 0;
+#endif
 
     auto fld = [&](int d) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)cur, d); };
     auto fld64 = [&](int d) -> int64_t { return (int64_t)(((uint64_t)fld(d + 1) << 32) | fld(d)); };
@@ -2253,6 +2268,9 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         filter_chunks(std::integral_constant<int, 0>{});
       KAD_PT(t1);
       KAD_PADD(0, t1 - t0);
+#ifdef KAD_PHASE_PROF
+      ut_n = n;
+#endif
       if (n == 0) {  // generic_scheduler.go:112-114
         wide_status(w, KAD_ST_NO_FEASIBLE);
         break;
@@ -2481,6 +2499,9 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         KAD_PADD(4, 1);
         KAD_PADD(5, t3 - t2);
       }
+#ifdef KAD_PHASE_PROF
+      ut_fl = rflags ? 1u : 0u;
+#endif
       // ---------------- output, ascending cluster id (= ascending position)
       {
         WArgs ae = wargs();
@@ -2541,6 +2562,13 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       KAD_PT(tz);
       wx_units++;
       wx_max = (tz - t0) > wx_max ? (tz - t0) : wx_max;
+      const unsigned long long ut1 = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0 && w < KAD_UTRACE_MAX) {
+        const unsigned long long gw = (unsigned long long)(blockIdx.x * nwaves + wv) & 0xFFFFull;
+        g_ustart[w] = ut0;
+        g_uinfo[w] = (ut1 - ut0) | ((unsigned long long)(ut_n & 0x7FFF) << 32) | ((unsigned long long)ut_fl << 47) |
+                     (gw << 48);
+      }
     }
 #endif
     cur = nxt;
@@ -2909,9 +2937,16 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
           r4[u] = as->s.res4[cs[u]];
           iv[u] = as->s.res_iv[cs[u]];
         }
+        if (s_tt) {  // one 32-B gather (SnapDev::pns4: the row kernel runs on clean snapshots, TW <= 4)
+          const ulonglong4 q = as->s.pns4[cs[u]];
+          pn[u][0] = q.x;
+          pn[u][1] = q.y;
+          pn[u][2] = q.z;
+          pn[u][3] = q.w;
+        } else {
 #pragma unroll
-        for (int tw = 0; tw < TFOLD_MAX_TW; ++tw)
-          pn[u][tw] = (s_tt && tw < TW) ? ldg(as->s.pns, (uint32_t)(tw * C) + cs[u]) : 0ull;
+          for (int tw = 0; tw < TFOLD_MAX_TW; ++tw) pn[u][tw] = 0ull;
+        }
       }
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
@@ -3624,6 +3659,11 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
 // ================================================================ launchers
 int debug_phase_counters(uint64_t* out, int reset) {
 #ifdef KAD_PHASE_PROF
+  if (reset == -3 || reset == -4) {  // the wide kernel's per-unit trace: out holds 2^20 entries
+    const hipError_t e = reset == -3 ? hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ustart), sizeof(unsigned long long) * KAD_UTRACE_MAX)
+                                     : hipMemcpyFromSymbol(out, HIP_SYMBOL(g_uinfo), sizeof(unsigned long long) * KAD_UTRACE_MAX);
+    return e == hipSuccess ? KAD_UTRACE_MAX : -1;
+  }
   if (reset == -2) {  // the wide kernel's per-wave extras: out holds 8192 * 6 entries
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavex), sizeof(unsigned long long) * 8192 * 6) != hipSuccess) return -1;
     return 8192;
@@ -3677,8 +3717,9 @@ hipError_t launch_res_cols(const SnapDev& s, void* buf, hipStream_t st) {
   (void)hipGetLastError();
   if (s.C <= 0) return hipSuccess;
   double4* r4 = static_cast<double4*>(buf);
+  ulonglong4* p4 = s.TW <= 4 ? reinterpret_cast<ulonglong4*>(static_cast<char*>(buf) + res_cols_pns4_offset(s.C)) : nullptr;
   hipLaunchKernelGGL(res_cols_kernel, dim3((unsigned)((s.C + 255) / 256)), dim3(256), 0, st, s, r4,
-                     reinterpret_cast<float2*>(r4 + s.C));
+                     reinterpret_cast<float2*>(r4 + s.C), p4);
   return hipGetLastError();
 }
 
