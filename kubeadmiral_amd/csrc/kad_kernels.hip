@@ -2047,11 +2047,15 @@ __device__ __forceinline__ void wide_row_or_defer(int w) {
   }
 }
 
-template <int NCH>
+// XN > 0: the kernel is specialised for exactly XN chunks; SM >= 0: for the score-plugin mask SM (the
+// profile's plugins as compile-time constants: every runtime plugin test of the hot loops folds away, and
+// with it the 64-bit condition masks the compiler otherwise keeps live — and spills — across the loop)
+template <int NCH, int XN, int SM>
 __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs args) {
   (void)args;  // read through wargs()
   constexpr int Q = WIDE_Q;
   constexpr int P = WIDE_P;
+  static_assert(XN <= NCH, "exact chunk count within the template bound");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2063,9 +2067,9 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     TWs = a->s.TW;
     W = a->b.W;
     fm = a->p.filter_mask;
-    sm = a->p.score_mask;
+    sm = SM >= 0 ? (uint32_t)SM : a->p.score_mask;
   }
-  const int nch = (C + 63) >> 6;
+  const int nch = XN > 0 ? XN : (C + 63) >> 6;
   const int Cp = nch * 64;
   const WideLayout L = wide_layout();
   const int nwaves = blockDim.x >> 6;
@@ -3832,11 +3836,23 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     wpb = wpb > WIDE_THREADS / 64 ? WIDE_THREADS / 64 : wpb;
     if (wpb < 1) return hipErrorInvalidValue;
     const size_t lds = cache + (size_t)wpb * per_wave;
+    // the instantiation: exact chunk count and score set for the bench profiles (C3: 16 chunks, LeastAllocated
+    // alone; C4: 8 chunks, the default set), the generic kernel otherwise
+    const int nch = (s.C + 63) >> 6;
+    constexpr int SM_LEAST = 1 << KAD_PL_LEAST_ALLOCATED;
+    constexpr int SM_DEFAULT = (1 << KAD_PL_TAINT_TOLERATION) | (1 << KAD_PL_BALANCED_ALLOCATION) |
+                               (1 << KAD_PL_LEAST_ALLOCATED) | (1 << KAD_PL_CLUSTER_AFFINITY);
+    const void* fn = (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1>;
+    if (nch == 16 && p.score_mask == (uint32_t)SM_LEAST)
+      fn = (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>;
+    else if (nch == 8 && p.score_mask == (uint32_t)SM_DEFAULT)
+      fn = (const void*)schedule_wide_kernel<8, 0, SM_DEFAULT>;
     static bool attr = false;
     if (!attr) {
-      if (hipError_t e = hipFuncSetAttribute((const void*)schedule_wide_kernel<WIDE_MAX_NCH>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max))
-        return e;
+      for (const void* f : {(const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1>,
+                            (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>,
+                            (const void*)schedule_wide_kernel<8, 0, SM_DEFAULT>})
+        if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max)) return e;
       attr = true;
     }
     long grid = n_cus();
@@ -3851,7 +3867,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
       if (hipError_t e = launch_rows(s, b, o, p, side)) return e;
       if (hipError_t e = hipEventRecord(join, side)) return e;
     }
-    hipLaunchKernelGGL(schedule_wide_kernel<WIDE_MAX_NCH>, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
+    hipLaunchKernelGGL((void (*)(WideArgs))fn, dim3((unsigned)grid), dim3(64 * wpb), lds, st, A);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = rec(after_main);
     if (beside) {
