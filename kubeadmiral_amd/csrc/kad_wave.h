@@ -10,7 +10,13 @@ constexpr int64_t I64_MAX = INT64_MAX;
 constexpr int64_t I64_MIN = INT64_MIN;
 constexpr int64_t NEG_INF = INT64_MIN;  // "no floor" in the clamp monoid
 
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
+// opaque at every call: a comparison with the lane index is computed where it is used, not hoisted out of
+// the loops around it and kept live as a 64-bit mask (which the long kernels then spill to VGPR lanes)
+__device__ __forceinline__ int lane_id() {
+  int l = __lane_id();
+  asm volatile("" : "+v"(l));
+  return l;
+}
 
 // Load through the constant address space: for a wave-uniform address this
 // becomes a scalar (s_load) access served by the scalar cache. Only for data
