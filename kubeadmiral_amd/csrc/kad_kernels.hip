@@ -1281,7 +1281,8 @@ __device__ __forceinline__ TT tadd(TT a, int64_t b) {
   else
     return a + (TT)b;
 }
-template <int NCH, bool CL>
+// SM >= 0: specialised for that score-plugin mask (as schedule_wide_kernel)
+template <int NCH, bool CL, int SM = -1>
 __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
   using TT = typename std::conditional<CL, int, int64_t>::type;
   (void)args;  // read through largs()
@@ -1299,7 +1300,7 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     TWs = a->s.TW;
     W = a->b.W;
     fm = a->p.filter_mask;
-    sm = a->p.score_mask;
+    sm = SM >= 0 ? (uint32_t)SM : a->p.score_mask;
   }
   const int nch = (C + 63) >> 6;
   const LeanLayout L = lean_layout(C, Q);
@@ -2708,6 +2709,8 @@ __device__ __forceinline__ void row_exclusive_scan(int* cnt, int m, int by = 0) 
   if (lane == 0) cnt[m] = carry;
 }
 
+// SM >= 0: specialised for that score-plugin mask (as schedule_wide_kernel)
+template <int SM = -1>
 __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel(RowArgs args) {
   (void)args;  // read through rargs()
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2720,7 +2723,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     C = a->s.C;
     TW = a->s.TW;
     fm = a->p.filter_mask;
-    sm = a->p.score_mask;
+    sm = SM >= 0 ? (uint32_t)SM : a->p.score_mask;
   }
   (void)fm;
   const int nch = (C + 63) >> 6;
@@ -3261,7 +3264,7 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
                                                                  int n_rows, int kmax, char* gscratch, int wave_bytes,
                                                                  int r_stride, int tbl_cp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   const int gw = blockIdx.x;
   // LDS: the row workspace of rows with K > 64 (kmax > 64 only), then the lookup tables
   char* region = GSCR ? gscratch + (size_t)gw * wave_bytes : smem;
@@ -3748,9 +3751,9 @@ hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bo
   return hipGetLastError();
 }
 
-template <int NCH, bool CL>
+template <int NCH, bool CL, int SM = -1>
 static void launch_lean(const LeanArgs& A, int grid, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((schedule_lean_kernel<NCH, CL>), dim3(grid), dim3(64 * A.waves_per_block), lds, st, A);
+  hipLaunchKernelGGL((schedule_lean_kernel<NCH, CL, SM>), dim3(grid), dim3(64 * A.waves_per_block), lds, st, A);
 }
 
 static int n_cus() {
@@ -3798,16 +3801,18 @@ static hipError_t launch_defer_pass(const SnapDev& s, const BatchDev& b, const O
 static hipError_t launch_rows(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, hipStream_t st) {
   if (!b.use_rows) return hipSuccess;
   const size_t lds = row_kernel_lds(s.C);
+  constexpr int SM_DEFAULT = (1 << KAD_PL_TAINT_TOLERATION) | (1 << KAD_PL_BALANCED_ALLOCATION) |
+                             (1 << KAD_PL_LEAST_ALLOCATED) | (1 << KAD_PL_CLUSTER_AFFINITY);
+  // the default plugin set's scores as constants (C5), else the generic kernel
+  void (*fn)(RowArgs) = p.score_mask == (uint32_t)SM_DEFAULT ? schedule_row_kernel<SM_DEFAULT> : schedule_row_kernel<-1>;
   static bool attr = false;
   if (!attr) {
-    if (hipError_t e = hipFuncSetAttribute((const void*)schedule_row_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024))
-      return e;
+    for (const void* f : {(const void*)schedule_row_kernel<SM_DEFAULT>, (const void*)schedule_row_kernel<-1>})
+      if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) return e;
     attr = true;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_row_kernel, ROW_THREADS, lds) != hipSuccess ||
-      per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, ROW_THREADS, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
   long grid = (long)n_cus() * per_cu;
   if (grid > ROW_MAX_BLOCKS) grid = ROW_MAX_BLOCKS;
@@ -3815,7 +3820,7 @@ static hipError_t launch_rows(const SnapDev& s, const BatchDev& b, const OutDev&
   if (!b.row_slabs) return hipErrorInvalidValue;
   static const int exp = tuning_env("KAD_ROW_EXPERIMENT", 0);
   const RowArgs A{s, b, o, p, b.row_slabs, exp};
-  hipLaunchKernelGGL(schedule_row_kernel, dim3((unsigned)grid), dim3(ROW_THREADS), lds, st, A);
+  hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(ROW_THREADS), lds, st, A);
   return hipGetLastError();
 }
 
@@ -3836,8 +3841,8 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     wpb = wpb > WIDE_THREADS / 64 ? WIDE_THREADS / 64 : wpb;
     if (wpb < 1) return hipErrorInvalidValue;
     const size_t lds = cache + (size_t)wpb * per_wave;
-    // the instantiation: exact chunk count and score set for the bench profiles (C3: 16 chunks, LeastAllocated
-    // alone; C4: 8 chunks, the default set), the generic kernel otherwise
+    // the instantiation: the score set of the bench profiles (C2/C3: LeastAllocated alone; C4: the default set,
+    // also at its exact 8 chunks — 16 exact chunks unroll past the 128-VGPR budget and spill), else generic
     const int nch = (s.C + 63) >> 6;
     constexpr int SM_LEAST = 1 << KAD_PL_LEAST_ALLOCATED;
     constexpr int SM_DEFAULT = (1 << KAD_PL_TAINT_TOLERATION) | (1 << KAD_PL_BALANCED_ALLOCATION) |
@@ -3846,12 +3851,12 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     if (nch == 16 && p.score_mask == (uint32_t)SM_LEAST)
       fn = (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>;
     else if (nch == 8 && p.score_mask == (uint32_t)SM_DEFAULT)
-      fn = (const void*)schedule_wide_kernel<8, 0, SM_DEFAULT>;
+      fn = (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT>;
     static bool attr = false;
     if (!attr) {
       for (const void* f : {(const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1>,
                             (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>,
-                            (const void*)schedule_wide_kernel<8, 0, SM_DEFAULT>})
+                            (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT>})
         if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max)) return e;
       attr = true;
     }
@@ -3898,13 +3903,28 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     int per_cu = 0;
     hipError_t oe;
     const bool cl = s.clean && nch >= 1 && nch <= 4;
+    // score-set specialisations of the bench profiles: C2 (4 clean chunks, LeastAllocated alone), C5 (long
+    // lists, the default set)
+    constexpr int SM_LEAST = 1 << KAD_PL_LEAST_ALLOCATED;
+    constexpr int SM_DEFAULT = (1 << KAD_PL_TAINT_TOLERATION) | (1 << KAD_PL_BALANCED_ALLOCATION) |
+                               (1 << KAD_PL_LEAST_ALLOCATED) | (1 << KAD_PL_CLUSTER_AFFINITY);
+    const bool least4 = cl && nch == 4 && p.score_mask == (uint32_t)SM_LEAST;
+    const bool def0 = nch > 4 && p.score_mask == (uint32_t)SM_DEFAULT;
 #define KAD_OCC(N, B) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<N, B>, 64 * wpb, lds)
     switch (nch) {
       case 1: oe = cl ? KAD_OCC(1, true) : KAD_OCC(1, false); break;
       case 2: oe = cl ? KAD_OCC(2, true) : KAD_OCC(2, false); break;
       case 3: oe = cl ? KAD_OCC(3, true) : KAD_OCC(3, false); break;
-      case 4: oe = cl ? KAD_OCC(4, true) : KAD_OCC(4, false); break;
-      default: oe = KAD_OCC(0, false); break;
+      case 4:
+        oe = least4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<4, true, SM_LEAST>,
+                                                                    64 * wpb, lds)
+                    : (cl ? KAD_OCC(4, true) : KAD_OCC(4, false));
+        break;
+      default:
+        oe = def0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, schedule_lean_kernel<0, false, SM_DEFAULT>,
+                                                                  64 * wpb, lds)
+                  : KAD_OCC(0, false);
+        break;
     }
 #undef KAD_OCC
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
@@ -3922,8 +3942,13 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
       case 1: cl ? launch_lean<1, true>(A, (int)grid, lds, st) : launch_lean<1, false>(A, (int)grid, lds, st); break;
       case 2: cl ? launch_lean<2, true>(A, (int)grid, lds, st) : launch_lean<2, false>(A, (int)grid, lds, st); break;
       case 3: cl ? launch_lean<3, true>(A, (int)grid, lds, st) : launch_lean<3, false>(A, (int)grid, lds, st); break;
-      case 4: cl ? launch_lean<4, true>(A, (int)grid, lds, st) : launch_lean<4, false>(A, (int)grid, lds, st); break;
-      default: launch_lean<0, false>(A, (int)grid, lds, st); break;
+      case 4:
+        if (least4)
+          launch_lean<4, true, SM_LEAST>(A, (int)grid, lds, st);
+        else
+          cl ? launch_lean<4, true>(A, (int)grid, lds, st) : launch_lean<4, false>(A, (int)grid, lds, st);
+        break;
+      default: def0 ? launch_lean<0, false, SM_DEFAULT>(A, (int)grid, lds, st) : launch_lean<0, false>(A, (int)grid, lds, st); break;
     }
     if (hipError_t e = hipGetLastError()) return e;
     if (hipError_t e = rec(after_main)) return e;

@@ -159,7 +159,7 @@ struct PlanWs {
 // returns true if two elements tie on (weight, hash) (Go order would be map-order dependent).
 template <bool GSCR>
 __device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const int32_t* list, int m) {
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   if (m <= WAVE) {  // one element per lane: compare against the others with v_readlane, no memory
     const int e = lane < m ? list[lane] : 0;
     const int64_t we = lane < m ? wt[e] : 0;
@@ -225,7 +225,7 @@ __device__ bool sort_by_weight_hash(const PlanWs& ws, const int64_t* wt, const i
 template <bool GSCR>
 __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64_t* mxv, bool use_min, bool use_cap,
                                 int m, int64_t total, bool keep, int64_t* plan, int64_t* over, uint32_t* ofl) {
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   // ---- minimum pass
   int64_t R = total;
   for (int base = 0; base < m; base += WAVE) {
@@ -349,7 +349,7 @@ __device__ int64_t desired_plan(const PlanWs& ws, const int64_t* wt, const int64
 // Leaves the final plan in ws.plan, the overflow in ws.over/EF_HAS_OVER.
 template <bool GSCR>
 __device__ uint32_t plan_row(const PlanWs& ws, int K, int64_t total, bool avoid, bool keep) {
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   uint32_t rflags = 0;
   for (int i = lane; i < K; i += WAVE) {
     ws.act[i] = i;
@@ -449,7 +449,7 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
 // kbuf (optional): 64 u64 of the wave's LDS; the listed keys are compacted there and read back as
 // broadcasts (LDS reads instead of two v_readlane per compare)
 __device__ __forceinline__ int lane_sort_rank(bool in, int64_t we, uint32_t he, bool* tie, uint64_t* kbuf = nullptr) {
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   const uint64_t lm = ballot(in);
   const int m = popc64(lm);
   int rank = 0;
@@ -498,7 +498,7 @@ __device__ __forceinline__ int lane_sort_rank(bool in, int64_t we, uint32_t he, 
 __device__ __forceinline__ int64_t desired_plan_lanes(int m, int64_t wt, int64_t mxv, int64_t Mn, bool hc, int64_t cap,
                                                       int64_t total, bool keep, int64_t& plan, int64_t& over,
                                                       uint32_t& ofl) {
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   const bool v = lane < m;
   // ---- minimum pass
   int64_t R = total;
@@ -596,7 +596,7 @@ __device__ __forceinline__ bool desired_narrow(bool v, int64_t total, int64_t wt
 __device__ __forceinline__ int64_t desired_plan_lanes32(int m, int wt, int mxv, int Mn, bool hc, int cap, int total,
                                                         bool keep, int64_t& plan64, int64_t& over64, uint32_t& ofl) {
   constexpr int NONE = INT32_MAX;  // no maximum / capacity
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   const bool v = lane < m;
   auto scan = [](int s, int t) {  // inclusive clamp scan; lanes without a source combine with (0, NEG30)
 #define KAD_C32(CTRL, RM)                                                                  \
@@ -703,7 +703,7 @@ __device__ __forceinline__ int64_t desired_plan_lanes32(int m, int wt, int mxv, 
 __device__ __forceinline__ int64_t desired_plan_any(int m, int64_t wt, int64_t mxv, int64_t Mn, bool hc, int64_t cap,
                                                     int64_t total, bool keep, int64_t& plan, int64_t& over,
                                                     uint32_t& ofl) {
-  if (desired_narrow(lane_id() < m, total, wt, mxv, Mn, hc, cap))
+  if (desired_narrow(lane_id_h() < m, total, wt, mxv, Mn, hc, cap))
     return desired_plan_lanes32(m, (int)wt, mxv == I64_MAX ? INT32_MAX : (int)mxv, (int)Mn, hc, (int)cap, (int)total,
                                 keep, plan, over, ofl);
   return desired_plan_lanes(m, wt, mxv, Mn, hc, cap, total, keep, plan, over, ofl);
@@ -713,7 +713,7 @@ __device__ __forceinline__ int64_t desired_plan_any(int m, int64_t wt, int64_t m
 // when a sort met a (weight, hash) tie.
 __device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int64_t total, bool avoid, bool keep,
                                                    PlanOut& out, uint64_t* kbuf = nullptr) {
-  const int lane = lane_id();
+  const int lane = lane_id_h();
   const bool v = lane < K;
   uint32_t rflags = 0;
   const bool hmax = v && (e.fl & EF_HAS_MAX), hcap = v && (e.fl & EF_HAS_CAP);

@@ -17,6 +17,9 @@ __device__ __forceinline__ int lane_id() {
   asm volatile("" : "+v"(l));
   return l;
 }
+// the plain lane index (the compiler may hoist comparisons with it): the planner, whose row loop keeps
+// its lane masks in registers with room to spare, is faster with them hoisted
+__device__ __forceinline__ int lane_id_h() { return __lane_id(); }
 
 // Load through the constant address space: for a wave-uniform address this
 // becomes a scalar (s_load) access served by the scalar cache. Only for data
