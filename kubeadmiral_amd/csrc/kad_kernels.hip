@@ -2150,6 +2150,11 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
   int bend = cb.x + cb.y;
   KAD_PACC;
   while (w >= 0) {
+    // per unit, opaque copies of the loop invariants its conditions derive from: the conditions are then
+    // evaluated inside the unit (a few scalar compares) instead of hoisted out of the unit loop and kept
+    // live — and spilled — across it as 64-bit masks
+    const int nch_o = XN > 0 ? nch : opq(nch);
+#define nch nch_o
     // the next unit: within this batch, else the head of the next batch
     int wn = -1;
     if (w + 1 < bend) {
@@ -2578,6 +2583,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
 #endif
     cur = nxt;
     w = wn;
+#undef nch
   }
 #ifdef KAD_PHASE_PROF
   {

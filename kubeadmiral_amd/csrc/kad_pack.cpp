@@ -440,8 +440,17 @@ static int validate_columns(kad_packer* P, const kad_su_columns* su, int threads
   const int W = su->n_units, NS = su->str.n, R = su->n_reqs;
   if (NS < 0 || R < 0 || !su->str.off) return P->fail(KAD_EINVAL, "bad string table / requirement count");
   if (su->str.off[0] != 0) return P->fail(KAD_EINVAL, "string offsets must start at 0");
-  for (int i = 0; i < NS; i++)
-    if (su->str.off[i + 1] < su->str.off[i]) return P->fail(KAD_EINVAL, "string offsets must be non-decreasing");
+  // monotone offsets, checked in parallel pieces (each piece also checks its first step from the previous one)
+  auto monotone = [&](const auto* off, int n) -> bool {
+    std::atomic<bool> ok{true};
+    parallel_for(n, threads, [&](int lo, int hi) {
+      bool good = true;
+      for (int i = lo; i < hi; i++) good &= off[i + 1] >= off[i];
+      if (!good) ok = false;
+    }, 1 << 15);
+    return ok;
+  };
+  if (!monotone(su->str.off, NS)) return P->fail(KAD_EINVAL, "string offsets must be non-decreasing");
   std::atomic<bool> bad{false};
   auto ids_ok = [&](const int32_t* a, int64_t n) {
     parallel_for((int)n, threads, [&](int lo, int hi) {
@@ -451,8 +460,7 @@ static int validate_columns(kad_packer* P, const kad_su_columns* su, int threads
   };
   auto csr = [&](const int32_t* off, int n, int64_t* total) -> bool {
     if (!off || off[0] != 0) return false;
-    for (int i = 0; i < n; i++)
-      if (off[i + 1] < off[i]) return false;
+    if (!monotone(off, n)) return false;
     *total = off[n];
     return true;
   };
@@ -480,13 +488,19 @@ static int validate_columns(kad_packer* P, const kad_su_columns* su, int threads
   ids_ok(su->rq_key, R);
   ids_ok(su->rq_op, R);
   ids_ok(su->rq_val, nv);
-  for (int64_t t = 0; t < nrt; t++)
-    if (su->rt_req[t] < 0 || su->rt_n_expr[t] < 0 || su->rt_n_field[t] < 0 ||
-        (int64_t)su->rt_req[t] + su->rt_n_expr[t] + su->rt_n_field[t] > R)
-      return P->fail(KAD_EINVAL, "required term outside the requirement table");
-  for (int64_t t = 0; t < npt; t++)
-    if (su->pt_req[t] < 0 || su->pt_n_expr[t] < 0 || (int64_t)su->pt_req[t] + su->pt_n_expr[t] > R)
-      return P->fail(KAD_EINVAL, "preferred term outside the requirement table");
+  std::atomic<bool> tbad{false};
+  parallel_for((int)nrt, threads, [&](int lo, int hi) {
+    for (int t = lo; t < hi; t++)
+      if (su->rt_req[t] < 0 || su->rt_n_expr[t] < 0 || su->rt_n_field[t] < 0 ||
+          (int64_t)su->rt_req[t] + su->rt_n_expr[t] + su->rt_n_field[t] > R)
+        tbad = true;
+  }, 1 << 15);
+  if (tbad) return P->fail(KAD_EINVAL, "required term outside the requirement table");
+  parallel_for((int)npt, threads, [&](int lo, int hi) {
+    for (int t = lo; t < hi; t++)
+      if (su->pt_req[t] < 0 || su->pt_n_expr[t] < 0 || (int64_t)su->pt_req[t] + su->pt_n_expr[t] > R) tbad = true;
+  }, 1 << 15);
+  if (tbad) return P->fail(KAD_EINVAL, "preferred term outside the requirement table");
   if (bad) return P->fail(KAD_EINVAL, "string id out of range");
   return 0;
 }
