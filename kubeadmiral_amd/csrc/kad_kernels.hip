@@ -2270,7 +2270,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       };
       // (the wide kernel runs on clean snapshots of C <= 1024: fold implies fitf; the general mode is
       // correct for any snapshot, re-testing what the static words hold)
-      if (fold && fitf)
+      // (the LeastAllocated instantiation runs only on folded, fit-folded snapshots: the host checks; at C3
+      // dropping the other modes takes its spilled SGPRs 27 -> 1, while the C4 instantiation ran 0.7 % slower
+      // without them)
+      if (SM == (1 << KAD_PL_LEAST_ALLOCATED) || (fold && fitf))
         filter_chunks(std::integral_constant<int, 3>{});
       else if (!fold && !use_cur && TWs == 1)
         filter_chunks(std::integral_constant<int, 1>{});
@@ -3854,7 +3857,8 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     constexpr int SM_DEFAULT = (1 << KAD_PL_TAINT_TOLERATION) | (1 << KAD_PL_BALANCED_ALLOCATION) |
                                (1 << KAD_PL_LEAST_ALLOCATED) | (1 << KAD_PL_CLUSTER_AFFINITY);
     const void* fn = (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1>;
-    if (nch == 16 && p.score_mask == (uint32_t)SM_LEAST)
+    const bool folded = s.fold && s.fitfold;  // the LeastAllocated specialisation compiles the folded filter only
+    if (folded && nch == 16 && p.score_mask == (uint32_t)SM_LEAST)
       fn = (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>;
     else if (nch == 8 && p.score_mask == (uint32_t)SM_DEFAULT)
       fn = (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT>;
