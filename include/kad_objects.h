@@ -1,0 +1,82 @@
+/*
+ * kad_objects.h — native SchedulingUnit builder of libkad.so (SURVEY §8(f) row
+ * f2): a batch of federated objects and the (Cluster)PropagationPolicies they
+ * name, as JSON text, → the kad_su_columns that kad_pack_batch packs.
+ *
+ * Replaces, per object, what the reference's scheduler controller does before
+ * Schedule (pkg/controllers/scheduler/scheduler.go:349-392, 445-467):
+ *   * MatchedPolicyKey (scheduler/util.go:37-49) and the policy lookup;
+ *   * schedulingUnitForFedObject (schedulingunit.go:38-163) with every
+ *     annotation override (:224-668): scheduling mode, sticky cluster, cluster
+ *     selector, affinity, tolerations, max clusters, placements (cluster names,
+ *     min / max replicas, weights), auto-migration info, and the current
+ *     clusters from spec.placements + the global scheduler's replica overrides
+ *     (getCurrentReplicasFromObject :181-222, util/overrides.go:68-112).
+ * Decoding follows Go 1.19 encoding/json where it changes the outcome
+ * (exact-then-case-folded field names, null, integer ranges, the sorted key
+ * order of runtime.DefaultUnstructuredConverter) — the same rules as
+ * kubeadmiral_amd/gojson.py, whose restatement (kubeadmiral_amd/objects.py)
+ * the parity tests compare against field by field
+ * (tests/test_native_objects.py) together with the reference's own
+ * schedulingunit table (tests/golden/schedulingunit.json).
+ *
+ * Objects are independent: they are parsed and decoded on the library's
+ * worker threads; the string table is interned in object order, so the
+ * columns are the same for any thread count.
+ */
+#ifndef KAD_OBJECTS_H
+#define KAD_OBJECTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "kad_pack.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The FederatedTypeConfig fields the scheduler reads (types_federatedtypeconfig.go). */
+typedef struct kad_type_config {
+  const char* group;
+  const char* version;
+  const char* kind;
+  const char* plural_name;
+  int32_t namespaced;          /* Spec.Scope == Namespaced                                  */
+  const char* replicas_spec;   /* Spec.PathDefinition.ReplicasSpec: dot path under spec.template, "" none */
+} kad_type_config;
+
+/* per-object outcome */
+#define KAD_OBJ_OK 0               /* a SchedulingUnit was built (columns row unit_index[i])          */
+#define KAD_OBJ_NO_POLICY 1        /* no policy label: the reference schedules to no clusters (:454-467) */
+#define KAD_OBJ_POLICY_NOT_FOUND 2 /* the labelled policy is not in `policies` (:359-372)              */
+#define KAD_OBJ_UNIT_ERROR 3       /* schedulingUnitForFedObject returns an error                     */
+#define KAD_OBJ_UNIT_PANIC 4       /* the reference panics (a non-float64 replicas override value)    */
+#define KAD_OBJ_BAD_JSON 5         /* the object's text is not a JSON object                          */
+#define KAD_OBJ_POLICY_ERROR 6     /* the matched policy's spec does not decode (json.Unmarshal error) */
+
+typedef struct kad_units kad_units;
+
+/* Build the SchedulingUnits of `objects` (JSON texts of federated objects).
+ * `policies`: JSON texts of PropagationPolicies (metadata.namespace set) and
+ * ClusterPropagationPolicies (no namespace), keyed by (namespace, name) as the
+ * informer caches are. `policy_of` NULL: each object's policy is found through
+ * its labels (MatchedPolicyKey); else policy_of[i] is object i's policy index
+ * (-1: none — a caller that did the lookup itself). `threads` <= 0: every
+ * worker of the library's pool.
+ * Returns KAD_OK with *out set (free with kad_units_free) — per-object failures
+ * are statuses, not errors — or KAD_EINVAL / KAD_ENOMEM. */
+int kad_units_from_objects(const kad_type_config* tc, const kad_strs* objects, const kad_strs* policies,
+                           const int32_t* policy_of, int threads, kad_units** out);
+/* Views into *u (valid until kad_units_free): the columns of the OK objects in object order, per object
+ * its status and its row in the columns (-1 unless OK), and the matched policy's index (-1 none). */
+int kad_units_view(const kad_units* u, kad_su_columns* cols, const int32_t** status, const int32_t** unit_index,
+                   const int32_t** policy_index);
+/* The message of object i's failure ("" when it has none); valid until kad_units_free. */
+const char* kad_units_message(const kad_units* u, int32_t i);
+void kad_units_free(kad_units* u);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KAD_OBJECTS_H */

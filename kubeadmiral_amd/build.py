@@ -16,7 +16,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libkad.so")
-SOURCES = ["kad_kernels.hip", "kad_trigger.hip", "kad_delta.hip", "kad_diff.hip", "kad_api.hip", "kad_pack.cpp"]
+SOURCES = ["kad_kernels.hip", "kad_trigger.hip", "kad_delta.hip", "kad_diff.hip", "kad_api.hip", "kad_pack.cpp", "kad_objects.cpp"]
 HEADERS = ["kad_device.h", "kad_wave.h", "kad_select.h", "kad_plan.h", "kad_pool.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KAD_OFFLOAD_ARCH", "gfx950")
@@ -24,7 +24,7 @@ ARCH = os.environ.get("KAD_OFFLOAD_ARCH", "gfx950")
 
 def _inputs():
     return [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [
-        os.path.join(os.path.dirname(HERE), "include", h) for h in ("kad_sched.h", "kad_pack.h")]
+        os.path.join(os.path.dirname(HERE), "include", h) for h in ("kad_sched.h", "kad_pack.h", "kad_objects.h")]
 
 
 def source_hash() -> str:

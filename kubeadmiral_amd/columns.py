@@ -519,3 +519,126 @@ class NativePacker:
         if not take:
             nbatch.in_place = (self, self.gen)
         return nbatch
+
+
+# ------------------------------------------------------------------ federated objects → columns (native)
+class KadTypeConfig(ctypes.Structure):
+    _fields_ = [("group", ctypes.c_char_p), ("version", ctypes.c_char_p), ("kind", ctypes.c_char_p),
+                ("plural_name", ctypes.c_char_p), ("namespaced", ctypes.c_int32), ("replicas_spec", ctypes.c_char_p)]
+
+
+# include/kad_objects.h KAD_OBJ_*
+OBJ_OK, OBJ_NO_POLICY, OBJ_POLICY_NOT_FOUND, OBJ_UNIT_ERROR, OBJ_UNIT_PANIC, OBJ_BAD_JSON, OBJ_POLICY_ERROR = range(7)
+
+_PER_UNIT = ("group", "version", "kind", "namespace_", "name", "flags", "desired", "max_clusters", "req_cpu", "req_mem",
+             "req_eph")
+_CSR_PAYLOAD = {"scalar": ("scalar_name", "scalar_val"), "tol": ("tol_key", "tol_op", "tol_value", "tol_effect"),
+                "sel": ("sel_key", "sel_value"), "rterm": ("rt_req", "rt_n_expr", "rt_n_field"),
+                "pterm": ("pt_weight", "pt_req", "pt_n_expr"), "place": ("place_name",),
+                "cur": ("cur_name", "cur_rep", "cur_has_rep"), "wt": ("wt_name", "wt_val"),
+                "min": ("min_name", "min_val"), "max": ("max_name", "max_val"), "cap": ("cap_name", "cap_val")}
+
+
+class ObjectUnits:
+    """kad_units_from_objects: the SchedulingUnits of a batch of federated objects as columns, plus per
+    object its status (``OBJ_*``), its row in the columns (-1 unless OK) and the matched policy's index."""
+
+    def __init__(self, cols: SUColumns, status: np.ndarray, unit_index: np.ndarray, policy_index: np.ndarray,
+                 messages: List[str]):
+        self.cols, self.status, self.unit_index, self.policy_index = cols, status, unit_index, policy_index
+        self.messages = messages
+
+
+def _texts(items) -> List[bytes]:
+    import json
+
+    out = []
+    for x in items:
+        if isinstance(x, (bytes, bytearray)):
+            out.append(bytes(x))
+        elif isinstance(x, str):
+            out.append(x.encode())
+        else:
+            out.append(json.dumps(x, separators=(",", ":")).encode())
+    return out
+
+
+def units_from_objects(type_config, objects: Sequence, policies: Sequence, policy_of: Optional[Sequence[int]] = None,
+                       threads: int = 0) -> ObjectUnits:
+    """Federated objects and (Cluster)PropagationPolicies — JSON texts (str / bytes) or decoded dicts — through
+    the native builder (include/kad_objects.h): MatchedPolicyKey, the policy lookup and
+    schedulingUnitForFedObject for every object, on the library's worker threads. ``policy_of``: each object's
+    policy index (-1 none) when the caller did the lookup, else the objects' labels choose."""
+    from .runtime import load_library
+
+    L = load_library()
+    P = ctypes.c_void_p
+    L.kad_units_from_objects.argtypes = [P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
+    L.kad_units_view.argtypes = [P, P, P, P, P]
+    L.kad_units_message.argtypes = [P, ctypes.c_int32]
+    L.kad_units_message.restype = ctypes.c_char_p
+    L.kad_units_free.argtypes = [P]
+    L.kad_units_free.restype = None
+    keep: list = []
+    ot, pt = _texts(objects), _texts(policies)
+
+    def strs(parts):
+        off = np.zeros(len(parts) + 1, I64)
+        if parts:
+            off[1:] = np.cumsum([len(p) for p in parts])
+        data = np.frombuffer(b"".join(parts) or b"\0", U8).copy()
+        keep.extend([off, data])
+        return KadStrs(len(parts), off.ctypes.data, data.ctypes.data)
+
+    so, sp = strs(ot), strs(pt)
+    tc = KadTypeConfig(type_config.group.encode(), type_config.version.encode(), type_config.kind.encode(),
+                       type_config.plural_name.encode(), 1 if type_config.namespaced else 0,
+                       type_config.replicas_spec.encode())
+    h = P()
+    po = None
+    if policy_of is not None:
+        po = np.ascontiguousarray(policy_of, I32)
+        if len(po) != len(ot):
+            raise ValueError("policy_of: one entry per object")
+        keep.append(po)
+    rc = L.kad_units_from_objects(ctypes.byref(tc), ctypes.byref(so), ctypes.byref(sp),
+                                  None if po is None else po.ctypes.data, threads if threads > 0 else default_threads(),
+                                  ctypes.byref(h))
+    if rc != 0:
+        raise RuntimeError(f"kad_units_from_objects failed ({rc})")
+    try:
+        v = KadSUColumns()
+        st, ui, pi = P(), P(), P()
+        rc = L.kad_units_view(h, ctypes.byref(v), ctypes.byref(st), ctypes.byref(ui), ctypes.byref(pi))
+        if rc != 0:
+            raise RuntimeError(f"kad_units_view failed ({rc})")
+        n = len(ot)
+
+        def arr(ptr, dt, cnt):
+            if cnt == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         (cnt,)).copy()
+
+        W = int(v.n_units)
+        cols = {}
+        for k in _PER_UNIT:
+            cols[k] = arr(getattr(v, k), DTYPES[k], W)
+        for g, payload in _CSR_PAYLOAD.items():
+            off = arr(getattr(v, g + "_off"), I32, W + 1)
+            cols[g + "_off"] = off
+            for k in payload:
+                cols[k] = arr(getattr(v, k), DTYPES[k], int(off[-1]))
+        R = int(v.n_reqs)
+        cols["rq_key"], cols["rq_op"] = arr(v.rq_key, I32, R), arr(v.rq_op, I32, R)
+        cols["rq_val_off"] = arr(v.rq_val_off, I32, R + 1)
+        cols["rq_val"] = arr(v.rq_val, I32, int(cols["rq_val_off"][-1]))
+        ns = int(v.str.n)
+        soff = arr(v.str.off, I64, ns + 1)
+        sdata = arr(v.str.bytes, U8, int(soff[-1])) if soff[-1] else np.zeros(1, U8)
+        status = arr(st, I32, n)
+        out = ObjectUnits(SUColumns(W, soff, sdata, cols), status, arr(ui, I32, n), arr(pi, I32, n),
+                          [L.kad_units_message(h, i).decode(errors="replace") if status[i] else "" for i in range(n)])
+        return out
+    finally:
+        L.kad_units_free(h)

@@ -28,7 +28,8 @@ namespace kad {
 // Accumulated per wave in registers, flushed once at wave exit into one of
 // 256 stripes (a shared counter per phase would serialise the waves).
 #ifdef KAD_PHASE_PROF
-__device__ unsigned long long g_phase[256 * 32];
+constexpr int KAD_PSLOTS = 40;  // per-block phase slots (scripts/phase_prof.py NAMES)
+__device__ unsigned long long g_phase[256 * KAD_PSLOTS];
 // lean kernel: (start, end) s_memtime of every wave of the last launch, for the wave-lifetime split
 __device__ unsigned long long g_wavetime[8192 * 2];
 // wide kernel: per wave (units taken, the longest unit's s_memtime cycles, realtime of the last dequeue, units
@@ -44,24 +45,25 @@ __device__ unsigned long long g_uinfo[KAD_UTRACE_MAX];
 #define KAD_PADD(i, x) pacc[i] += (uint32_t)(x)
 #define KAD_PFLUSH                                                                       \
   if (lane_id() == 0)                                                                    \
-    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + i_], pacc[i_])
+    for (int i_ = 0; i_ < 10; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * KAD_PSLOTS + i_], pacc[i_])
 // lean / wide kernel: slots 10..15 (A, B, D, E, straddles, D on straddles), 24..29 (replay: setup,
 // partitions, pivots, insertion sorts, #partitions, feasible count of replayed units)
 #define KAD_PFLUSH_LEAN                                                                  \
   if (lane_id() == 0) {                                                                  \
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 10 + i_], pacc[i_]); \
-    for (int i_ = 6; i_ < 12; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 18 + i_], pacc[i_]); \
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * KAD_PSLOTS + 10 + i_], pacc[i_]); \
+    for (int i_ = 6; i_ < 12; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * KAD_PSLOTS + 18 + i_], pacc[i_]); \
   }
 // plan kernel: slots 16..23 (setup, dynamic weights, first plan, avoid-disruption, output, units)
 #define KAD_PFLUSH_PLAN                                                                  \
   if (lane_id() == 0)                                                                    \
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + 16 + i_], pacc[i_])
+    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * KAD_PSLOTS + 16 + i_], pacc[i_])
 // row kernel (thread 0, block-synchronous phases): slots 9 (units), 20 (compaction), 22 (scores),
-// 23 (normalise), 30 (select: radix + counts), 31 (pdqsort replay)
+// 23 (normalise), 30 (select: radix + counts), 31 (pdqsort replay); within the scores 32 (preferred-term
+// words) and 33 (thread 0's position loop)
 #define KAD_PFLUSH_ROW                                                                   \
   if (threadIdx.x == 0) {                                                                \
-    const int sl_[6] = {9, 20, 22, 23, 30, 31};                                          \
-    for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * 32 + sl_[i_]], pacc[i_]); \
+    const int sl_[8] = {9, 20, 22, 23, 30, 31, 32, 33};                                  \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_phase[(blockIdx.x & 255) * KAD_PSLOTS + sl_[i_]], pacc[i_]); \
   }
 #else
 #define KAD_PFLUSH_ROW
@@ -2925,6 +2927,8 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
       }
       __syncthreads();
     }
+    KAD_PT(t1a);
+    KAD_PADD(6, t1a - t1);
     const double rqcd = (double)rqc, rqmd = (double)rqm;
     int ttmax = 0, amax = 0;
     // the unit's tolerated PreferNoSchedule words, once (scalar)
@@ -2994,6 +2998,8 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
         }
       }
     }
+    KAD_PT(t1b);
+    KAD_PADD(7, t1b - t1a);
     if (s_tt) ttmax = row_block_max(ttmax, red);
     if (s_aff) amax = row_block_max(amax, red);
     __syncthreads();
@@ -3688,17 +3694,17 @@ int debug_phase_counters(uint64_t* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wavetime), sizeof(unsigned long long) * 8192 * 2) != hipSuccess) return -1;
     return 8192;
   }
-  static unsigned long long h[256 * 32];
+  static unsigned long long h[256 * KAD_PSLOTS];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof h) != hipSuccess) return -1;
-  for (int i = 0; i < 32; ++i) {
+  for (int i = 0; i < KAD_PSLOTS; ++i) {
     out[i] = 0;
-    for (int s = 0; s < 256; ++s) out[i] += h[s * 32 + i];
+    for (int s = 0; s < 256; ++s) out[i] += h[s * KAD_PSLOTS + i];
   }
   if (reset) {
-    static const unsigned long long z[256 * 32] = {};
+    static const unsigned long long z[256 * KAD_PSLOTS] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return -1;
   }
-  return 32;
+  return KAD_PSLOTS;
 #else
   (void)out;
   (void)reset;

@@ -1,0 +1,1508 @@
+// Native SchedulingUnit builder (include/kad_objects.h): federated objects and
+// their propagation policies as JSON text → kad_su_columns.
+//
+// Per object, on the library's worker threads:
+//   1. parse the JSON text into a flat node array (objects keep every member in order, duplicates
+//      included: Go's decoder sees them all; the unstructured map view keeps the last);
+//   2. MatchedPolicyKey (scheduler/util.go:37-49) → the policy, decoded once per batch;
+//   3. schedulingUnitForFedObject (schedulingunit.go:38-163): the template's metadata, the scheduling
+//      mode and DesiredReplicas, the current clusters (spec.placements + the global scheduler's replica
+//      overrides, :181-222 and util/overrides.go:68-112), then every policy field with its annotation
+//      override (:224-668).
+// Then, serially in object order, the strings are interned into one table and the columns laid out.
+//
+// Decoding restates the Go 1.19 encoding/json rules kubeadmiral_amd/gojson.py restates (struct fields
+// exact-then-case-folded, null, integer ranges, interface{} numbers as float64, an error anywhere fails
+// the call); typed decodes of the object itself visit its members in the sorted key order of the
+// unstructured round trip (UnstructuredToInterface). Parity: tests/test_native_objects.py compares
+// every field with kubeadmiral_amd/objects.py and the reference's schedulingunit table.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <optional>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "../../include/kad_objects.h"
+#include "kad_pool.h"
+
+namespace {
+
+using sv = std::string_view;
+
+// ------------------------------------------------------------------ constants (scheduler/constants.go,
+// common/constants.go)
+constexpr sv PREFIXED_GLOBAL_SCHEDULER = "kubeadmiral.io/global-scheduler";
+constexpr sv POLICY_LABEL = "kubeadmiral.io/propagation-policy-name";
+constexpr sv CLUSTER_POLICY_LABEL = "kubeadmiral.io/cluster-propagation-policy-name";
+constexpr sv SCHEDULING_MODE_ANN = "kubeadmiral.io/scheduling-mode";
+constexpr sv STICKY_ANN = "kubeadmiral.io/sticky-cluster";
+constexpr sv TOLERATIONS_ANN = "kubeadmiral.io/tolerations";
+constexpr sv PLACEMENTS_ANN = "kubeadmiral.io/placements";
+constexpr sv SELECTOR_ANN = "kubeadmiral.io/clusterSelector";
+constexpr sv AFFINITY_ANN = "kubeadmiral.io/affinity";
+constexpr sv MAX_CLUSTERS_ANN = "kubeadmiral.io/maxClusters";
+constexpr sv AUTO_MIGRATION_INFO_ANN = "kubeadmiral.io/auto-migration-info";
+constexpr sv DUPLICATE = "Duplicate", DIVIDE = "Divide";
+
+struct Fail {  // the reference returns an error (status) or panics
+  int status;
+  std::string msg;
+};
+[[noreturn]] void fail(int st, std::string m) { throw Fail{st, std::move(m)}; }
+
+// ------------------------------------------------------------------ JSON text → nodes
+enum JT : uint8_t { J_NULL, J_FALSE, J_TRUE, J_NUM, J_STR, J_ARR, J_OBJ };
+struct JV {
+  JT t = J_NULL;
+  bool isint = false;  // number: an integer literal (no fraction or exponent)
+  bool fits = false;   //   ... within int64
+  int64_t i = 0;
+  double d = 0;        // number: the literal as float64 (±inf beyond range)
+  uint32_t a = 0, n = 0;  // string: bytes s[a, a+n); array: kids[a, a+n); object: kids[a, a+2n) as (key, value)
+};
+struct JDoc {
+  std::vector<JV> v;
+  std::vector<uint32_t> kids;
+  std::string s;
+  sv str(uint32_t x) const { return sv(s.data() + v[x].a, v[x].n); }
+};
+
+struct Parser {
+  const char* p;
+  const char* e;
+  JDoc& d;
+  std::vector<uint32_t> stack;  // children of the open containers
+  static constexpr int MAX_DEPTH = 1000;
+
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  static void put_utf8(std::string& o, uint32_t c) {
+    if (c < 0x80) {
+      o += (char)c;
+    } else if (c < 0x800) {
+      o += (char)(0xC0 | (c >> 6));
+      o += (char)(0x80 | (c & 0x3F));
+    } else if (c < 0x10000) {
+      o += (char)(0xE0 | (c >> 12));
+      o += (char)(0x80 | ((c >> 6) & 0x3F));
+      o += (char)(0x80 | (c & 0x3F));
+    } else {
+      o += (char)(0xF0 | (c >> 18));
+      o += (char)(0x80 | ((c >> 12) & 0x3F));
+      o += (char)(0x80 | ((c >> 6) & 0x3F));
+      o += (char)(0x80 | (c & 0x3F));
+    }
+  }
+  bool hex4(uint32_t* out) {
+    if (e - p < 4) return false;
+    uint32_t x = 0;
+    for (int k = 0; k < 4; ++k) {
+      const char c = p[k];
+      x <<= 4;
+      if (c >= '0' && c <= '9') x |= (uint32_t)(c - '0');
+      else if (c >= 'a' && c <= 'f') x |= (uint32_t)(c - 'a' + 10);
+      else if (c >= 'A' && c <= 'F') x |= (uint32_t)(c - 'A' + 10);
+      else return false;
+    }
+    p += 4;
+    *out = x;
+    return true;
+  }
+  // a string (p at the opening quote) appended to d.s; unpaired surrogate escapes become U+FFFD
+  // (Go's decoder; gojson._fix_str), control characters are an error (both decoders)
+  bool str(uint32_t* a, uint32_t* n) {
+    ++p;
+    const size_t start = d.s.size();
+    for (;;) {
+      const char* q = p;
+      while (q < e && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) ++q;
+      d.s.append(p, (size_t)(q - p));
+      p = q;
+      if (p >= e || (unsigned char)*p < 0x20) return false;
+      if (*p == '"') {
+        ++p;
+        break;
+      }
+      ++p;  // backslash
+      if (p >= e) return false;
+      const char c = *p++;
+      switch (c) {
+        case '"': d.s += '"'; break;
+        case '\\': d.s += '\\'; break;
+        case '/': d.s += '/'; break;
+        case 'b': d.s += '\b'; break;
+        case 'f': d.s += '\f'; break;
+        case 'n': d.s += '\n'; break;
+        case 'r': d.s += '\r'; break;
+        case 't': d.s += '\t'; break;
+        case 'u': {
+          uint32_t c1;
+          if (!hex4(&c1)) return false;
+          if (c1 >= 0xD800 && c1 < 0xDC00 && e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            const char* save = p;
+            p += 2;
+            uint32_t c2;
+            if (hex4(&c2) && c2 >= 0xDC00 && c2 < 0xE000) {
+              put_utf8(d.s, 0x10000 + ((c1 - 0xD800) << 10) + (c2 - 0xDC00));
+              break;
+            }
+            p = save;  // not a low surrogate: c1 is unpaired, the next escape is read on its own
+          }
+          put_utf8(d.s, (c1 >= 0xD800 && c1 < 0xE000) ? 0xFFFDu : c1);
+          break;
+        }
+        default: return false;
+      }
+    }
+    *a = (uint32_t)start;
+    *n = (uint32_t)(d.s.size() - start);
+    return true;
+  }
+  bool num(JV& x) {
+    const char* s0 = p;
+    if (p < e && *p == '-') ++p;
+    if (p >= e) return false;
+    if (*p == '0') {
+      ++p;
+    } else if (*p >= '1' && *p <= '9') {
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    } else {
+      return false;
+    }
+    bool isint = true;
+    if (p < e && *p == '.') {
+      ++p;
+      if (p >= e || *p < '0' || *p > '9') return false;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+      isint = false;
+    }
+    if (p < e && (*p == 'e' || *p == 'E')) {
+      ++p;
+      if (p < e && (*p == '+' || *p == '-')) ++p;
+      if (p >= e || *p < '0' || *p > '9') return false;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+      isint = false;
+    }
+    std::string lit(s0, (size_t)(p - s0));
+    x.t = J_NUM;
+    x.isint = isint;
+    x.d = std::strtod(lit.c_str(), nullptr);
+    if (isint) {
+      const bool neg = lit[0] == '-';
+      const uint64_t lim = neg ? (uint64_t)1 << 63 : ((uint64_t)1 << 63) - 1;
+      uint64_t v = 0;
+      bool ok = true;
+      for (size_t k = neg ? 1 : 0; k < lit.size(); ++k) {
+        const uint64_t dg = (uint64_t)(lit[k] - '0');
+        if (v > (lim - dg) / 10) {
+          ok = false;
+          break;
+        }
+        v = v * 10 + dg;
+      }
+      x.fits = ok;
+      x.i = ok ? (neg ? (int64_t)(0 - v) : (int64_t)v) : 0;
+    }
+    return true;
+  }
+  bool lit(const char* w, size_t n) {
+    if ((size_t)(e - p) < n || std::memcmp(p, w, n) != 0) return false;
+    p += n;
+    return true;
+  }
+  // one value; its node index in *out
+  bool value(uint32_t* out, int depth) {
+    if (depth > MAX_DEPTH) return false;
+    ws();
+    if (p >= e) return false;
+    JV x;
+    const char c = *p;
+    if (c == '{' || c == '[') {
+      const bool obj = c == '{';
+      ++p;
+      const size_t base = stack.size();
+      ws();
+      const char close = obj ? '}' : ']';
+      if (p < e && *p == close) {
+        ++p;
+      } else {
+        for (;;) {
+          if (obj) {
+            ws();
+            if (p >= e || *p != '"') return false;
+            JV k;
+            k.t = J_STR;
+            if (!str(&k.a, &k.n)) return false;
+            d.v.push_back(k);
+            stack.push_back((uint32_t)(d.v.size() - 1));
+            ws();
+            if (p >= e || *p != ':') return false;
+            ++p;
+          }
+          uint32_t ch;
+          if (!value(&ch, depth + 1)) return false;
+          stack.push_back(ch);
+          ws();
+          if (p < e && *p == ',') {
+            ++p;
+            continue;
+          }
+          if (p < e && *p == close) {
+            ++p;
+            break;
+          }
+          return false;
+        }
+      }
+      x.t = obj ? J_OBJ : J_ARR;
+      x.a = (uint32_t)d.kids.size();
+      const size_t cnt = stack.size() - base;
+      x.n = (uint32_t)(obj ? cnt / 2 : cnt);
+      d.kids.insert(d.kids.end(), stack.begin() + (long)base, stack.end());
+      stack.resize(base);
+    } else if (c == '"') {
+      x.t = J_STR;
+      if (!str(&x.a, &x.n)) return false;
+    } else if (c == 't') {
+      if (!lit("true", 4)) return false;
+      x.t = J_TRUE;
+    } else if (c == 'f') {
+      if (!lit("false", 5)) return false;
+      x.t = J_FALSE;
+    } else if (c == 'n') {
+      if (!lit("null", 4)) return false;
+      x.t = J_NULL;
+    } else {
+      if (!num(x)) return false;
+    }
+    d.v.push_back(x);
+    *out = (uint32_t)(d.v.size() - 1);
+    return true;
+  }
+};
+
+// parse a whole text (one value, surrounding whitespace only); the root is d.v.back()
+bool parse(sv text, JDoc& d, uint32_t* root) {
+  d.v.clear();
+  d.kids.clear();
+  d.s.clear();
+  Parser ps{text.data(), text.data() + text.size(), d, {}};
+  if (!ps.value(root, 0)) return false;
+  ps.ws();
+  return ps.p == ps.e;
+}
+
+// ------------------------------------------------------------------ unstructured (map) view
+// m[key] of a decoded map: the last member with that key (a Go / Python map keeps the last)
+int64_t get(const JDoc& d, uint32_t obj, sv key) {
+  if (d.v[obj].t != J_OBJ) return -1;
+  const JV& o = d.v[obj];
+  for (int64_t k = (int64_t)o.n - 1; k >= 0; --k)
+    if (d.str(d.kids[o.a + 2 * k]) == key) return d.kids[o.a + 2 * k + 1];
+  return -1;
+}
+
+// the members a typed decode visits: in text order (json.Unmarshal of text), or — for the object
+// itself, re-read through UnstructuredToInterface — unique keys (last wins) sorted bytewise
+void members(const JDoc& d, uint32_t obj, bool sorted_unique, std::vector<std::pair<sv, uint32_t>>& out) {
+  out.clear();
+  const JV& o = d.v[obj];
+  for (uint32_t k = 0; k < o.n; ++k) out.emplace_back(d.str(d.kids[o.a + 2 * k]), d.kids[o.a + 2 * k + 1]);
+  if (!sorted_unique || out.size() < 2) return;
+  std::stable_sort(out.begin(), out.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+  size_t w = 0;
+  for (size_t r = 0; r < out.size(); ++r) {
+    if (w > 0 && out[w - 1].first == out[r].first) out[w - 1] = out[r];  // later text position wins
+    else out[w++] = out[r];
+  }
+  out.resize(w);
+}
+
+// bytes.EqualFold against an ASCII field name as gojson._fold does it: ASCII case, U+017F → s, U+212A → k
+bool fold_eq(sv key, sv lower_field) {  // lower_field: compared lower-cased
+  size_t i = 0, j = 0;
+  while (i < key.size()) {
+    const unsigned char c = (unsigned char)key[i];
+    char f;
+    if (c < 0x80) {
+      f = (char)(c >= 'A' && c <= 'Z' ? c + 32 : c);
+      i += 1;
+    } else if (c == 0xC5 && i + 1 < key.size() && (unsigned char)key[i + 1] == 0xBF) {
+      f = 's';
+      i += 2;
+    } else if (c == 0xE2 && i + 2 < key.size() && (unsigned char)key[i + 1] == 0x84 && (unsigned char)key[i + 2] == 0xAA) {
+      f = 'k';
+      i += 3;
+    } else {
+      return false;
+    }
+    const char g = lower_field[j < lower_field.size() ? j : 0];
+    if (j >= lower_field.size() || (char)(g >= 'A' && g <= 'Z' ? g + 32 : g) != f) return false;
+    ++j;
+  }
+  return j == lower_field.size();
+}
+
+// ------------------------------------------------------------------ Go typed decoding
+struct Dec {
+  const JDoc& d;
+  bool sorted;  // member order: see members()
+  // the first error (json.Unmarshal's result is discarded on any error, so decoding stops there): recorded,
+  // not thrown — the annotation overrides that fail fall back silently and are common enough for C++
+  // exceptions (serialised in the unwinder) to cost more than the decode
+  const char* err = nullptr;
+
+  void type_err(const char* want) {
+    if (!err) err = want;
+  }
+  const JV& at(uint32_t x) const { return d.v[x]; }
+  bool null(uint32_t x) const { return d.v[x].t == J_NULL; }
+
+  // struct: visit each member matched to a field (exact name first, else case-folded; the first field of
+  // that folded name); fields: their JSON names. null leaves the struct as it is
+  template <size_t N, class F>
+  void fields(uint32_t x, const sv (&names)[N], F&& on) {
+    if (null(x) || err) return;
+    if (at(x).t != J_OBJ) return type_err("struct");
+    std::vector<std::pair<sv, uint32_t>> ms;
+    members(d, x, sorted, ms);
+    for (const auto& [key, val] : ms) {
+      if (err) return;
+      int f = -1;
+      for (size_t k = 0; k < N && f < 0; ++k)
+        if (names[k] == key) f = (int)k;
+      for (size_t k = 0; k < N && f < 0; ++k)
+        if (fold_eq(key, names[k])) f = (int)k;
+      if (f >= 0) on(f, val);
+    }
+  }
+  // null leaves string / bool / integer / struct values as they are
+  void str(uint32_t x, std::string& out) {
+    if (null(x)) return;
+    if (at(x).t != J_STR) return type_err("string");
+    out.assign(d.str(x));
+  }
+  void boolean(uint32_t x, bool& out) {
+    if (null(x)) return;
+    if (at(x).t != J_TRUE && at(x).t != J_FALSE) return type_err("bool");
+    out = at(x).t == J_TRUE;
+  }
+  void int64(uint32_t x, int64_t& out) {
+    if (null(x)) return;
+    if (at(x).t != J_NUM || !at(x).isint || !at(x).fits) return type_err("int64");
+    out = at(x).i;
+  }
+  void int32(uint32_t x, int32_t& out) {
+    if (null(x)) return;
+    const JV& v = at(x);
+    if (v.t != J_NUM || !v.isint || !v.fits || v.i < INT32_MIN || v.i > INT32_MAX) return type_err("int32");
+    out = (int32_t)v.i;
+  }
+  // *int64 / *string / *struct: null → nil, else decode into the pointee (a fresh zero when nil)
+  void ptr_int64(uint32_t x, std::optional<int64_t>& out) {
+    if (null(x)) {
+      out.reset();
+      return;
+    }
+    int64_t v = out.value_or(0);
+    int64(x, v);
+    out = v;
+  }
+  void ptr_str(uint32_t x, std::optional<std::string>& out) {
+    if (null(x)) {
+      out.reset();
+      return;
+    }
+    std::string v = out.value_or(std::string());
+    str(x, v);
+    out = std::move(v);
+  }
+  // []T: null → nil, else a new slice of freshly decoded elements
+  template <class T, class F>
+  void slice(uint32_t x, std::optional<std::vector<T>>& out, F&& elem) {
+    if (null(x)) {
+      out.reset();
+      return;
+    }
+    if (err) return;
+    if (at(x).t != J_ARR) return type_err("slice");
+    std::vector<T> v(at(x).n);
+    for (uint32_t k = 0; k < at(x).n && !err; ++k) elem(d.kids[at(x).a + k], v[k]);
+    out = std::move(v);
+  }
+  // map[string]T: null → nil, else the current map (or a new one) with every member set to a freshly
+  // decoded value (insertion order kept; a repeated key keeps its first position)
+  template <class T, class F>
+  void map(uint32_t x, std::optional<std::vector<std::pair<std::string, T>>>& out, F&& elem) {
+    if (null(x)) {
+      out.reset();
+      return;
+    }
+    if (err) return;
+    if (at(x).t != J_OBJ) return type_err("map");
+    std::vector<std::pair<std::string, T>> m = out ? std::move(*out) : std::vector<std::pair<std::string, T>>();
+    std::unordered_map<std::string, size_t> pos;
+    if (m.size() > 8)
+      for (size_t k = 0; k < m.size(); ++k) pos.emplace(m[k].first, k);
+    const JV& o = at(x);
+    for (uint32_t k = 0; k < o.n && !err; ++k) {
+      std::string key(d.str(d.kids[o.a + 2 * k]));
+      T v{};
+      elem(d.kids[o.a + 2 * k + 1], v);
+      size_t at_ = SIZE_MAX;
+      if (m.size() > 8 || !pos.empty()) {
+        if (pos.empty())
+          for (size_t q = 0; q < m.size(); ++q) pos.emplace(m[q].first, q);
+        auto it = pos.find(key);
+        if (it != pos.end()) at_ = it->second;
+      } else {
+        for (size_t q = 0; q < m.size(); ++q)
+          if (m[q].first == key) at_ = q;
+      }
+      if (at_ != SIZE_MAX) {
+        m[at_].second = std::move(v);
+      } else {
+        if (!pos.empty()) pos.emplace(key, m.size());
+        m.emplace_back(std::move(key), std::move(v));
+      }
+    }
+    out = std::move(m);
+  }
+  // interface{}: validated (numbers must be finite float64s); kind and float value kept
+  struct Any {
+    JT t = J_NULL;
+    double f = 0;
+  };
+  void any(uint32_t x, Any& out) {
+    const JV& v = at(x);
+    out.t = v.t;
+    if (v.t == J_NUM) {
+      if (!std::isfinite(v.d) && !err) err = "number out of range";
+      out.f = v.d;
+    } else if (v.t == J_ARR) {
+      Any sub;
+      for (uint32_t k = 0; k < v.n; ++k) any(d.kids[v.a + k], sub);
+    } else if (v.t == J_OBJ) {
+      Any sub;
+      for (uint32_t k = 0; k < v.n; ++k) any(d.kids[v.a + 2 * k + 1], sub);
+    }
+  }
+};
+
+template <class T>
+using OMap = std::vector<std::pair<std::string, T>>;
+
+// ------------------------------------------------------------------ the Go types (objects.py decoders)
+struct Req {  // ClusterSelectorRequirement
+  std::string key, op;
+  std::optional<std::vector<std::string>> values;
+};
+struct Term {  // ClusterSelectorTerm
+  std::optional<std::vector<Req>> exprs, fields;
+};
+struct Selector {
+  std::optional<std::vector<Term>> terms;
+};
+struct PrefTerm {
+  int32_t weight = 0;
+  Term pref;
+};
+struct ClusterAffinity {
+  std::optional<Selector> required;
+  std::optional<std::vector<PrefTerm>> preferred;
+};
+struct Affinity {
+  std::optional<ClusterAffinity> ca;
+};
+struct Toleration {
+  std::string key, op, value, effect;
+  std::optional<int64_t> secs;
+};
+struct Preferences {
+  int64_t min = 0;
+  std::optional<int64_t> max, weight;
+};
+struct Placement {
+  std::string cluster;
+  Preferences prefs;
+};
+struct AutoMigration {
+  std::optional<std::string> pod_unschedulable_for;
+  bool keep = false;
+};
+struct PolicySpec {
+  std::string profile, mode;
+  bool sticky = false;
+  std::optional<OMap<std::string>> selector;
+  std::optional<std::vector<Term>> affinity;
+  std::optional<std::vector<Toleration>> tolerations;
+  std::optional<int64_t> max_clusters;
+  std::optional<std::vector<Placement>> placements;
+  bool disable_follower = false;
+  std::optional<AutoMigration> am;
+  std::optional<bool> avoid_disruption;  // ReplicaRescheduling != nil: its AvoidDisruption
+};
+
+void dec_strings(Dec& D, uint32_t x, std::optional<std::vector<std::string>>& out) {
+  D.slice(x, out, [&](uint32_t e, std::string& s) { D.str(e, s); });
+}
+void dec_req(Dec& D, uint32_t x, Req& r) {
+  static const sv N[] = {"key", "operator", "values"};
+  if (D.null(x)) return;
+  D.fields(x, N, [&](int f, uint32_t v) {
+    if (f == 0) D.str(v, r.key);
+    else if (f == 1) D.str(v, r.op);
+    else dec_strings(D, v, r.values);
+  });
+}
+void dec_term(Dec& D, uint32_t x, Term& t) {
+  static const sv N[] = {"matchExpressions", "matchFields"};
+  if (D.null(x)) return;
+  D.fields(x, N, [&](int f, uint32_t v) {
+    D.slice(v, f == 0 ? t.exprs : t.fields, [&](uint32_t e, Req& r) { dec_req(D, e, r); });
+  });
+}
+void dec_terms(Dec& D, uint32_t x, std::optional<std::vector<Term>>& out) {
+  D.slice(x, out, [&](uint32_t e, Term& t) { dec_term(D, e, t); });
+}
+void dec_selector(Dec& D, uint32_t x, Selector& s) {
+  static const sv N[] = {"clusterSelectorTerms"};
+  if (D.null(x)) return;
+  D.fields(x, N, [&](int, uint32_t v) { dec_terms(D, v, s.terms); });
+}
+void dec_affinity(Dec& D, uint32_t x, Affinity& a) {
+  static const sv NA[] = {"clusterAffinity"};
+  static const sv NC[] = {"requiredDuringSchedulingIgnoredDuringExecution", "preferredDuringSchedulingIgnoredDuringExecution"};
+  static const sv NP[] = {"weight", "preference"};
+  if (D.null(x)) return;
+  D.fields(x, NA, [&](int, uint32_t v) {
+    if (D.null(v)) {
+      a.ca.reset();
+      return;
+    }
+    if (!a.ca) a.ca.emplace();
+    ClusterAffinity& ca = *a.ca;
+    D.fields(v, NC, [&](int f, uint32_t w) {
+      if (f == 0) {
+        if (D.null(w)) {
+          ca.required.reset();
+          return;
+        }
+        if (!ca.required) ca.required.emplace();
+        dec_selector(D, w, *ca.required);
+      } else {
+        D.slice(w, ca.preferred, [&](uint32_t e, PrefTerm& p) {
+          if (D.null(e)) return;
+          D.fields(e, NP, [&](int g, uint32_t y) {
+            if (g == 0) D.int32(y, p.weight);
+            else dec_term(D, y, p.pref);
+          });
+        });
+      }
+    });
+  });
+}
+void dec_tolerations(Dec& D, uint32_t x, std::optional<std::vector<Toleration>>& out) {
+  static const sv N[] = {"key", "operator", "value", "effect", "tolerationSeconds"};
+  D.slice(x, out, [&](uint32_t e, Toleration& t) {
+    if (D.null(e)) return;
+    D.fields(e, N, [&](int f, uint32_t v) {
+      if (f == 0) D.str(v, t.key);
+      else if (f == 1) D.str(v, t.op);
+      else if (f == 2) D.str(v, t.value);
+      else if (f == 3) D.str(v, t.effect);
+      else D.ptr_int64(v, t.secs);
+    });
+  });
+}
+void dec_placements(Dec& D, uint32_t x, std::optional<std::vector<Placement>>& out) {
+  static const sv N[] = {"cluster", "preferences"};
+  static const sv NP[] = {"minReplicas", "maxReplicas", "weight"};
+  D.slice(x, out, [&](uint32_t e, Placement& p) {
+    if (D.null(e)) return;
+    D.fields(e, N, [&](int f, uint32_t v) {
+      if (f == 0) {
+        D.str(v, p.cluster);
+      } else if (!D.null(v)) {
+        D.fields(v, NP, [&](int g, uint32_t w) {
+          if (g == 0) D.int64(w, p.prefs.min);
+          else if (g == 1) D.ptr_int64(w, p.prefs.max);
+          else D.ptr_int64(w, p.prefs.weight);
+        });
+      }
+    });
+  });
+}
+void dec_string_map(Dec& D, uint32_t x, std::optional<OMap<std::string>>& out) {
+  D.map(x, out, [&](uint32_t e, std::string& s) { D.str(e, s); });
+}
+// POLICY_SPEC (types_propagationpolicy.go:62-110)
+void dec_policy_spec(Dec& D, uint32_t x, PolicySpec& s) {
+  static const sv N[] = {"schedulingProfile", "schedulingMode", "stickyCluster", "clusterSelector", "clusterAffinity",
+                         "tolerations", "maxClusters", "placement", "disableFollowerScheduling", "autoMigration",
+                         "replicaRescheduling"};
+  static const sv NAM[] = {"when", "keepUnschedulableReplicas"};
+  static const sv NW[] = {"podUnschedulableFor"};
+  static const sv NRR[] = {"avoidDisruption"};
+  if (D.null(x)) return;
+  D.fields(x, N, [&](int f, uint32_t v) {
+    switch (f) {
+      case 0: D.str(v, s.profile); break;
+      case 1: D.str(v, s.mode); break;
+      case 2: D.boolean(v, s.sticky); break;
+      case 3: dec_string_map(D, v, s.selector); break;
+      case 4: dec_terms(D, v, s.affinity); break;
+      case 5: dec_tolerations(D, v, s.tolerations); break;
+      case 6: D.ptr_int64(v, s.max_clusters); break;
+      case 7: dec_placements(D, v, s.placements); break;
+      case 8: D.boolean(v, s.disable_follower); break;
+      case 9:
+        if (D.null(v)) {
+          s.am.reset();
+          break;
+        }
+        if (!s.am) s.am.emplace();
+        D.fields(v, NAM, [&](int g, uint32_t w) {
+          if (g == 1) {
+            D.boolean(w, s.am->keep);
+          } else if (!D.null(w)) {
+            D.fields(w, NW, [&](int, uint32_t y) { D.ptr_str(y, s.am->pod_unschedulable_for); });
+          }
+        });
+        break;
+      default:
+        if (D.null(v)) {
+          s.avoid_disruption.reset();
+          break;
+        }
+        if (!s.avoid_disruption) s.avoid_disruption = false;
+        D.fields(v, NRR, [&](int, uint32_t w) {
+          bool b = *s.avoid_disruption;
+          D.boolean(w, b);
+          s.avoid_disruption = b;
+        });
+    }
+  });
+}
+
+// ------------------------------------------------------------------ the policy table
+struct Policy {
+  std::string ns, name;
+  bool ok = false;
+  std::string err;
+  PolicySpec spec;
+};
+// PropagationPolicy.from_json: metadata name / namespace, spec decoded (a missing or null spec = {})
+void load_policy(sv text, Policy& P) {
+  JDoc d;
+  uint32_t root;
+  if (!parse(text, d, &root) || d.v[root].t != J_OBJ) {
+    P.err = "policy: not a JSON object";
+    return;
+  }
+  const int64_t meta = get(d, root, "metadata");
+  if (meta >= 0 && d.v[meta].t == J_OBJ) {
+    const int64_t nm = get(d, (uint32_t)meta, "name"), ns = get(d, (uint32_t)meta, "namespace");
+    if (nm >= 0 && d.v[nm].t == J_STR) P.name.assign(d.str((uint32_t)nm));
+    if (ns >= 0 && d.v[ns].t == J_STR) P.ns.assign(d.str((uint32_t)ns));
+  }
+  const int64_t spec = get(d, root, "spec");
+  // `d.get("spec") or {}`: null, {}, "" , 0, false and [] all decode as the empty spec
+  bool empty = spec < 0;
+  if (!empty) {
+    const JV& v = d.v[spec];
+    empty = v.t == J_NULL || v.t == J_FALSE || (v.t == J_OBJ && v.n == 0) || (v.t == J_ARR && v.n == 0) ||
+            (v.t == J_STR && v.n == 0) || (v.t == J_NUM && v.d == 0.0);
+  }
+  if (empty) {
+    P.ok = true;
+    return;
+  }
+  Dec D{d, true};
+  dec_policy_spec(D, (uint32_t)spec, P.spec);
+  if (D.err) P.err = std::string("policy spec: json: cannot unmarshal into ") + D.err;
+  else P.ok = true;
+}
+
+// ------------------------------------------------------------------ one object → one SchedulingUnit
+struct Unit {  // strings by value; interned in the serial merge
+  int status = KAD_OBJ_OK;
+  std::string msg;
+  int32_t policy = -1;
+  std::string ns, name;
+  uint32_t flags = 0;
+  int64_t desired = 0, max_clusters = 0;
+  std::vector<std::pair<std::string, std::string>> sel;
+  std::vector<Toleration> tols;
+  std::vector<Term> rterms;
+  std::vector<PrefTerm> pterms;
+  std::vector<std::string> place;  // sorted, unique
+  std::vector<std::pair<std::string, std::optional<int64_t>>> cur;
+  OMap<int64_t> wt, mn, mx, cap;
+};
+
+int64_t f64_to_i64(double x) {  // Go int64(f) on amd64: truncation, NaN / out of range → MinInt64
+  if (x != x || !(x >= -9.223372036854776e18 && x < 9.223372036854776e18)) return INT64_MIN;
+  return (int64_t)x;
+}
+// strconv.Atoi on a 64-bit platform
+bool atoi64(sv s, int64_t* out) {
+  size_t i = 0;
+  bool neg = false;
+  if (!s.empty() && (s[0] == '+' || s[0] == '-')) {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i >= s.size()) return false;
+  const uint64_t lim = neg ? (uint64_t)1 << 63 : ((uint64_t)1 << 63) - 1;
+  uint64_t v = 0;
+  for (; i < s.size(); ++i) {
+    const char c = s[i];
+    if (c < '0' || c > '9') return false;
+    const uint64_t dg = (uint64_t)(c - '0');
+    if (v > (lim - dg) / 10) return false;
+    v = v * 10 + dg;
+  }
+  *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+  return true;
+}
+
+struct Builder {
+  const kad_type_config& tc;
+  const std::vector<Policy>& pols;
+  const std::unordered_map<std::string, int32_t>& pol_index;  // namespace + '\0' + name
+  std::vector<std::string> replicas_fields;                   // spec.template + the dot path
+  std::string replicas_slash;                                 // ToSlashPath(ReplicasSpec)
+  bool replicas_empty;                                        // ReplicasSpec == ""
+
+  // metadata.annotations / .labels as GetAnnotations reads them: a string map, else none
+  static int64_t string_map(const JDoc& d, uint32_t root, sv field) {
+    const int64_t meta = get(d, root, "metadata");
+    if (meta < 0 || d.v[meta].t != J_OBJ) return -1;
+    const int64_t m = get(d, (uint32_t)meta, field);
+    if (m < 0 || d.v[m].t != J_OBJ) return -1;
+    const JV& o = d.v[m];
+    for (uint32_t k = 0; k < o.n; ++k)
+      if (d.v[d.kids[o.a + 2 * k + 1]].t != J_STR) return -1;
+    return m;
+  }
+
+  // forced >= -1: the caller's policy index (-1 none); -2: MatchedPolicyKey through the labels
+  void build(sv text, Unit& u, JDoc& d, JDoc& ad, int32_t forced) {
+    uint32_t root;
+    if (!parse(text, d, &root) || d.v[root].t != J_OBJ) fail(KAD_OBJ_BAD_JSON, "object: not a JSON object");
+    const int64_t labels = string_map(d, root, "labels");
+    const int64_t anns = string_map(d, root, "annotations");
+    auto ann = [&](sv key) -> std::optional<sv> {
+      if (anns < 0) return std::nullopt;
+      const int64_t v = get(d, (uint32_t)anns, key);
+      if (v < 0) return std::nullopt;
+      return d.str((uint32_t)v);
+    };
+    // MatchedPolicyKey (scheduler/util.go:37-49) and the informer lookup (scheduler.go:359-372)
+    if (forced >= -1) {
+      if (forced < 0 || forced >= (int32_t)pols.size()) {
+        u.status = KAD_OBJ_NO_POLICY;
+        return;
+      }
+      u.policy = forced;
+    } else {
+      std::optional<std::string> key;
+      const int64_t pl = labels >= 0 ? get(d, (uint32_t)labels, POLICY_LABEL) : -1;
+      const int64_t cl = labels >= 0 ? get(d, (uint32_t)labels, CLUSTER_POLICY_LABEL) : -1;
+      if (pl >= 0 && tc.namespaced) {
+        std::string ns;
+        const int64_t meta = get(d, root, "metadata");
+        const int64_t nsv = meta >= 0 && d.v[meta].t == J_OBJ ? get(d, (uint32_t)meta, "namespace") : -1;
+        if (nsv >= 0 && d.v[nsv].t == J_STR) ns.assign(d.str((uint32_t)nsv));
+        key = ns + '\0' + std::string(d.str((uint32_t)pl));
+      } else if (cl >= 0) {
+        key = std::string(1, '\0') + std::string(d.str((uint32_t)cl));
+      }
+      if (!key) {
+        u.status = KAD_OBJ_NO_POLICY;
+        return;
+      }
+      auto it = pol_index.find(*key);
+      if (it == pol_index.end()) {
+        u.status = KAD_OBJ_POLICY_NOT_FOUND;
+        return;
+      }
+      u.policy = it->second;
+    }
+    const Policy& P = pols[(size_t)u.policy];
+    if (!P.ok) fail(KAD_OBJ_POLICY_ERROR, P.err);
+    const PolicySpec& spec = P.spec;
+
+    // getTemplate (schedulingunit.go:165-179)
+    {
+      const int64_t sp = get(d, root, "spec");
+      if (sp < 0) fail(KAD_OBJ_UNIT_ERROR, "template not found");
+      if (d.v[sp].t != J_OBJ) fail(KAD_OBJ_UNIT_ERROR, "error retrieving template: .spec accessor error");
+      const int64_t t = get(d, (uint32_t)sp, "template");
+      if (t < 0) fail(KAD_OBJ_UNIT_ERROR, "template not found");
+      if (d.v[t].t != J_OBJ) fail(KAD_OBJ_UNIT_ERROR, "error retrieving template: .spec.template accessor error: not a map");
+      const uint32_t tm = (uint32_t)t;
+      for (sv k : {sv("apiVersion"), sv("kind")}) {
+        const int64_t x = get(d, tm, k);
+        if (x >= 0 && d.v[x].t != J_NULL && d.v[x].t != J_STR) fail(KAD_OBJ_UNIT_ERROR, "template cannot be converted from unstructured");
+      }
+      const int64_t meta = get(d, tm, "metadata");
+      if (meta >= 0 && d.v[meta].t != J_NULL) {
+        if (d.v[meta].t != J_OBJ) fail(KAD_OBJ_UNIT_ERROR, "template cannot be converted from unstructured");
+        const uint32_t m = (uint32_t)meta;
+        for (sv k : {sv("name"), sv("namespace"), sv("generateName")}) {
+          const int64_t x = get(d, m, k);
+          if (x >= 0 && d.v[x].t != J_NULL && d.v[x].t != J_STR) fail(KAD_OBJ_UNIT_ERROR, "template cannot be converted from unstructured");
+          if (x >= 0 && d.v[x].t == J_STR) {
+            if (k == "name") u.name.assign(d.str((uint32_t)x));
+            else if (k == "namespace") u.ns.assign(d.str((uint32_t)x));
+          }
+        }
+        for (sv k : {sv("labels"), sv("annotations")}) {
+          const int64_t x = get(d, m, k);
+          if (x < 0 || d.v[x].t == J_NULL) continue;
+          if (d.v[x].t != J_OBJ) fail(KAD_OBJ_UNIT_ERROR, "template cannot be converted from unstructured");
+          const JV& o = d.v[x];
+          for (uint32_t q = 0; q < o.n; ++q)
+            if (d.v[d.kids[o.a + 2 * q + 1]].t != J_STR) fail(KAD_OBJ_UNIT_ERROR, "template cannot be converted from unstructured");
+        }
+      }
+    }
+
+    // scheduling mode (:224-259) and DesiredReplicas (:48-58, GetInt64FromPath)
+    sv mode = (spec.mode == DUPLICATE || spec.mode == DIVIDE) ? sv(spec.mode) : DUPLICATE;
+    if (auto m = ann(SCHEDULING_MODE_ANN); m && (*m == DUPLICATE || *m == DIVIDE)) mode = *m;
+    if (mode == DIVIDE && replicas_empty) mode = DUPLICATE;  // ReplicasSpec == ""
+    if (mode == DIVIDE) {
+      uint32_t x = root;
+      bool found = true;
+      for (const std::string& f : replicas_fields) {
+        if (d.v[x].t != J_OBJ) fail(KAD_OBJ_UNIT_ERROR, "cannot access [spec template]: accessor error: not a map");
+        const int64_t y = get(d, x, f);
+        if (y < 0) {
+          found = false;
+          break;
+        }
+        x = (uint32_t)y;
+      }
+      if (found) {
+        const JV& v = d.v[x];
+        if (v.t != J_NUM || !v.isint || !v.fits) fail(KAD_OBJ_UNIT_ERROR, "cannot access [spec template]: expected int64");
+        u.flags |= KAD_SU_HAS_DESIRED;
+        u.desired = v.i;
+      }
+    }
+
+    current_replicas(d, root, u);
+
+    u.flags |= KAD_SU_AVOID_DISRUPTION;
+    if (spec.am) {  // :91-100, getAutoMigrationInfo :261-272
+      u.flags |= KAD_SU_HAS_AUTO_MIGRATION;
+      if (spec.am->keep) u.flags |= KAD_SU_KEEP_UNSCHED;
+      if (auto v = ann(AUTO_MIGRATION_INFO_ANN)) {
+        JDoc& a = ad;
+        uint32_t r;
+        if (!parse(*v, a, &r)) fail(KAD_OBJ_UNIT_ERROR, "auto-migration-info: invalid JSON");
+        Dec D{a, false};
+        std::optional<OMap<int64_t>> ec;
+        static const sv N[] = {"estimatedCapacity"};
+        if (!D.null(r))
+          D.fields(r, N, [&](int, uint32_t x) { D.map(x, ec, [&](uint32_t e, int64_t& i) { D.int64(e, i); }); });
+        if (D.err) fail(KAD_OBJ_UNIT_ERROR, std::string("auto-migration-info: json: cannot unmarshal into ") + D.err);
+        if (ec) u.cap = std::move(*ec);
+      }
+    }
+    if (spec.avoid_disruption && !*spec.avoid_disruption) u.flags &= ~KAD_SU_AVOID_DISRUPTION;
+    if (mode == DUPLICATE) u.flags |= KAD_SU_DUPLICATE;
+
+    bool sticky = spec.sticky;  // :278-304
+    if (auto v = ann(STICKY_ANN)) {
+      if (*v == "true") sticky = true;
+      else if (*v == "false") sticky = false;
+    }
+    if (sticky) u.flags |= KAD_SU_STICKY;
+
+    // ClusterSelector (:306-334): the annotation replaces the policy's when it decodes
+    const std::optional<OMap<std::string>>* selp = &spec.selector;
+    std::optional<OMap<std::string>> sel_ann;
+    if (auto v = ann(SELECTOR_ANN)) {
+      JDoc& a = ad;
+      uint32_t r;
+      if (parse(*v, a, &r)) {
+        Dec D{a, false};
+        dec_string_map(D, r, sel_ann);
+        if (!D.err) selp = &sel_ann;
+      }
+    }
+    if (*selp) u.sel = **selp;
+
+    // placements (:450-668): the annotation's list, else the policy's
+    std::optional<std::vector<Placement>> ann_pl;
+    bool have_ann_pl = false;
+    if (auto v = ann(PLACEMENTS_ANN)) {
+      JDoc& a = ad;
+      uint32_t r;
+      if (parse(*v, a, &r)) {
+        Dec D{a, false};
+        dec_placements(D, r, ann_pl);
+        if (!D.err) {
+          have_ann_pl = true;
+          if (!ann_pl) ann_pl.emplace();  // "null": an empty list
+        }
+      }
+    }
+    const std::vector<Placement>* pols_pl = spec.placements ? &*spec.placements : nullptr;
+    const std::vector<Placement>* names_from = have_ann_pl ? &*ann_pl : pols_pl;
+    if (names_from) {
+      for (const Placement& p : *names_from) u.place.push_back(p.cluster);
+      std::sort(u.place.begin(), u.place.end());
+      u.place.erase(std::unique(u.place.begin(), u.place.end()), u.place.end());
+    }
+    auto pref_map = [&](const std::vector<Placement>& pl, int which, OMap<int64_t>& out) {
+      out.clear();
+      std::unordered_map<std::string, size_t> pos;  // (long lists only)
+      for (const Placement& p : pl) {
+        int64_t v;
+        if (which == 0) v = p.prefs.min;
+        else if (which == 1) {
+          if (!p.prefs.max) continue;
+          v = *p.prefs.max;
+        } else {
+          if (!p.prefs.weight) continue;
+          v = *p.prefs.weight;
+        }
+        size_t at = SIZE_MAX;
+        if (pl.size() <= 16) {
+          for (size_t q = 0; q < out.size() && at == SIZE_MAX; ++q)
+            if (out[q].first == p.cluster) at = q;
+        } else if (auto it = pos.find(p.cluster); it != pos.end()) {
+          at = it->second;
+        }
+        if (at != SIZE_MAX) {
+          out[at].second = v;
+        } else {
+          if (pl.size() > 16) pos.emplace(p.cluster, out.size());
+          out.emplace_back(p.cluster, v);
+        }
+      }
+    };
+    for (int which = 0; which < 3; ++which) {
+      OMap<int64_t>& dst = which == 0 ? u.mn : (which == 1 ? u.mx : u.wt);
+      if (pols_pl) pref_map(*pols_pl, which, dst);
+      if (have_ann_pl) {
+        OMap<int64_t> m;
+        pref_map(*ann_pl, which, m);
+        bool ok = true;
+        for (const auto& kv : m) ok = ok && kv.second >= 0;
+        if (ok) dst = std::move(m);  // negative values invalidate the override (:510-624)
+      }
+    }
+
+    // Affinity (:336-377)
+    std::optional<Affinity> aff;
+    if (spec.affinity && !spec.affinity->empty()) {
+      aff.emplace();
+      aff->ca.emplace();
+      aff->ca->required.emplace();
+      aff->ca->required->terms = *spec.affinity;
+    }
+    if (auto v = ann(AFFINITY_ANN)) {
+      JDoc& a = ad;
+      uint32_t r;
+      if (parse(*v, a, &r)) {
+        Dec D{a, false};
+        std::optional<Affinity> x;
+        if (!D.null(r)) {
+          x.emplace();
+          dec_affinity(D, r, *x);
+        }
+        if (!D.err) aff = std::move(x);
+      }
+    }
+    if (aff && aff->ca) {
+      u.flags |= KAD_SU_HAS_CLUSTER_AFFINITY;
+      const ClusterAffinity& ca = *aff->ca;
+      if (ca.required) {
+        u.flags |= KAD_SU_HAS_REQUIRED;
+        if (ca.required->terms) u.rterms = *ca.required->terms;
+      }
+      if (ca.preferred) u.pterms = *ca.preferred;
+    }
+
+    // Tolerations (:379-407): "null" decodes to none
+    const std::optional<std::vector<Toleration>>* tolp = &spec.tolerations;
+    std::optional<std::vector<Toleration>> tol_ann;
+    if (auto v = ann(TOLERATIONS_ANN)) {
+      JDoc& a = ad;
+      uint32_t r;
+      if (parse(*v, a, &r)) {
+        Dec D{a, false};
+        dec_tolerations(D, r, tol_ann);
+        if (!D.err) tolp = &tol_ann;
+      }
+    }
+    if (*tolp) u.tols = **tolp;
+
+    // MaxClusters (:409-448)
+    std::optional<int64_t> mc = spec.max_clusters;
+    if (auto v = ann(MAX_CLUSTERS_ANN)) {
+      int64_t n;
+      if (atoi64(*v, &n) && n >= 0) mc = n;
+    }
+    if (mc) {
+      u.flags |= KAD_SU_HAS_MAX_CLUSTERS;
+      u.max_clusters = *mc;
+    }
+  }
+
+  // getCurrentReplicasFromObject (schedulingunit.go:181-222): the global scheduler's placement and its
+  // replica overrides (util.GetOverrides, util/overrides.go:68-112)
+  void current_replicas(const JDoc& d, uint32_t root, Unit& u) {
+    Dec D{d, true};
+    // the placements view (_OBJ_PLACEMENTS): type-checks apiVersion, kind, metadata and spec.placements
+    std::optional<std::vector<std::string>> names;
+    bool seen_ctrl = false;
+    {
+      static const sv N[] = {"apiVersion", "kind", "metadata", "spec"};
+      static const sv NM[] = {"name", "namespace", "generateName", "uid", "resourceVersion", "generation", "labels", "annotations"};
+      static const sv NS[] = {"placements"};
+      static const sv NPC[] = {"controller", "placement"};
+      static const sv NPL[] = {"clusters"};
+      static const sv NCR[] = {"name"};
+      struct PC {
+        std::string controller;
+        std::optional<std::vector<std::string>> clusters;
+      };
+      std::optional<std::vector<PC>> pls;
+      std::string scratch;
+      D.fields(root, N, [&](int f, uint32_t v) {
+        if (f <= 1) {
+          D.str(v, scratch);
+        } else if (f == 2) {
+          if (D.null(v)) return;
+          D.fields(v, NM, [&](int g, uint32_t w) {
+            if (g <= 4) {
+              D.str(w, scratch);
+            } else if (g == 5) {
+              int64_t i = 0;
+              D.int64(w, i);
+            } else {
+              std::optional<OMap<std::string>> m;
+              dec_string_map(D, w, m);
+            }
+          });
+        } else {
+          if (D.null(v)) return;
+          D.fields(v, NS, [&](int, uint32_t w) {
+            D.slice(w, pls, [&](uint32_t e, PC& pc) {
+              if (D.null(e)) return;
+              D.fields(e, NPC, [&](int g, uint32_t y) {
+                if (g == 0) {
+                  D.str(y, pc.controller);
+                } else if (!D.null(y)) {
+                  D.fields(y, NPL, [&](int, uint32_t z) {
+                    D.slice(z, pc.clusters, [&](uint32_t q, std::string& s) {
+                      if (D.null(q)) return;
+                      D.fields(q, NCR, [&](int, uint32_t r) { D.str(r, s); });
+                    });
+                  });
+                }
+              });
+            });
+          });
+        }
+      });
+      if (D.err) fail(KAD_OBJ_UNIT_ERROR, std::string("placements: json: cannot unmarshal into ") + D.err);
+      if (pls)
+        for (const PC& pc : *pls)
+          if (pc.controller == PREFIXED_GLOBAL_SCHEDULER) {
+            seen_ctrl = true;
+            if (pc.clusters) names = pc.clusters;
+            break;
+          }
+    }
+    (void)seen_ctrl;
+    // the overrides view (_OBJ_OVERRIDES)
+    struct Patch {
+      std::string op, path;
+      Dec::Any value;
+    };
+    struct CO {
+      std::string cluster;
+      std::optional<std::vector<Patch>> patches;
+    };
+    struct CtrlO {
+      std::string controller;
+      std::optional<std::vector<CO>> clusters;
+    };
+    std::optional<std::vector<CtrlO>> ovs;
+    {
+      static const sv N[] = {"spec"};
+      static const sv NS[] = {"overrides"};
+      static const sv NC[] = {"controller", "clusters"};
+      static const sv NCO[] = {"clusterName", "paths"};
+      static const sv NP[] = {"op", "path", "value"};
+      D.fields(root, N, [&](int, uint32_t v) {
+        if (D.null(v)) {
+          ovs.reset();
+          return;
+        }
+        D.fields(v, NS, [&](int, uint32_t w) {
+          D.slice(w, ovs, [&](uint32_t e, CtrlO& c) {
+            if (D.null(e)) return;
+            D.fields(e, NC, [&](int g, uint32_t y) {
+              if (g == 0) {
+                D.str(y, c.controller);
+              } else {
+                D.slice(y, c.clusters, [&](uint32_t q, CO& co) {
+                  if (D.null(q)) return;
+                  D.fields(q, NCO, [&](int h, uint32_t r) {
+                    if (h == 0) {
+                      D.str(r, co.cluster);
+                    } else {
+                      D.slice(r, co.patches, [&](uint32_t s, Patch& p) {
+                        if (D.null(s)) return;
+                        D.fields(s, NP, [&](int k, uint32_t t) {
+                          if (k == 0) D.str(t, p.op);
+                          else if (k == 1) D.str(t, p.path);
+                          else D.any(t, p.value);
+                        });
+                      });
+                    }
+                  });
+                });
+              }
+            });
+          });
+        });
+      });
+    }
+    if (D.err) fail(KAD_OBJ_UNIT_ERROR, std::string("overrides: json: cannot unmarshal into ") + D.err);
+    const std::vector<CO>* clusters = nullptr;
+    if (ovs)
+      for (const CtrlO& c : *ovs)
+        if (c.controller == PREFIXED_GLOBAL_SCHEDULER) {
+          if (c.clusters) clusters = &*c.clusters;
+          break;
+        }
+    std::unordered_map<std::string, const std::vector<Patch>*> by_cluster;
+    if (clusters) {
+      for (const CO& co : *clusters) {
+        if (by_cluster.count(co.cluster)) fail(KAD_OBJ_UNIT_ERROR, "cluster \"" + co.cluster + "\" appears more than once");
+        if (co.patches)
+          for (const Patch& p : *co.patches)
+            if (p.path == "/metadata/namespace" || p.path == "/metadata/name" || p.path == "/metadata/generateName" ||
+                p.path == "/kind")
+              fail(KAD_OBJ_UNIT_ERROR, "override for cluster \"" + co.cluster + "\" has an invalid path: " + p.path);
+        by_cluster.emplace(co.cluster, co.patches ? &*co.patches : nullptr);
+      }
+    }
+    if (!names) return;
+    std::vector<std::string> uniq;
+    {
+      std::unordered_map<std::string, int> seen;
+      for (const std::string& n : *names)
+        if (seen.emplace(n, 1).second) uniq.push_back(n);
+    }
+    for (const std::string& n : uniq) {
+      std::optional<int64_t> rep;
+      auto it = by_cluster.find(n);
+      if (it != by_cluster.end() && it->second)
+        for (const Patch& p : *it->second)
+          if (p.path == replicas_slash && (p.op == "replace" || p.op.empty())) {
+            if (p.value.t != J_NUM) fail(KAD_OBJ_UNIT_PANIC, "interface conversion: interface {} is not float64");
+            rep = f64_to_i64(p.value.f);
+            break;
+          }
+      u.cur.emplace_back(n, rep);
+    }
+  }
+};
+
+template <class F>
+void parallel_for(int n, int threads, F f, int grain) {
+  if (n <= 0) return;
+  if (threads <= 1 || n < 2 * grain) {
+    f(0, n);
+    return;
+  }
+  const int T = std::min(threads, (n + grain - 1) / grain);
+  kadpool::pool().run(T, [&](int t) { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
+}
+
+struct Interner {
+  std::unordered_map<std::string, int32_t> ids;
+  std::vector<int64_t> off{0};
+  std::vector<uint8_t> bytes;
+  int32_t id(const std::string& s) {
+    auto it = ids.find(s);
+    if (it != ids.end()) return it->second;
+    const int32_t i = (int32_t)ids.size();
+    ids.emplace(s, i);
+    bytes.insert(bytes.end(), s.begin(), s.end());
+    off.push_back((int64_t)bytes.size());
+    return i;
+  }
+};
+
+}  // namespace
+
+struct kad_units {
+  std::vector<int32_t> status, unit_index, policy_index;
+  std::vector<std::string> msg;
+  Interner st;
+  int32_t n_units = 0;
+  std::vector<int32_t> group, version, kind, ns, name;
+  std::vector<uint32_t> flags;
+  std::vector<int64_t> desired, max_clusters, req_cpu, req_mem, req_eph;
+  std::vector<int32_t> scalar_off{0}, scalar_name;
+  std::vector<int64_t> scalar_val;
+  std::vector<int32_t> tol_off{0}, tol_key, tol_op, tol_value, tol_effect;
+  std::vector<int32_t> sel_off{0}, sel_key, sel_value;
+  std::vector<int32_t> rq_key, rq_op, rq_val_off{0}, rq_val;
+  std::vector<int32_t> rterm_off{0}, rt_req, rt_n_expr, rt_n_field;
+  std::vector<int32_t> pterm_off{0}, pt_weight, pt_req, pt_n_expr;
+  std::vector<int32_t> place_off{0}, place_name;
+  std::vector<int32_t> cur_off{0}, cur_name;
+  std::vector<int64_t> cur_rep;
+  std::vector<uint8_t> cur_has_rep;
+  std::vector<int32_t> wt_off{0}, wt_name, min_off{0}, min_name, max_off{0}, max_name, cap_off{0}, cap_name;
+  std::vector<int64_t> wt_val, min_val, max_val, cap_val;
+};
+
+namespace {
+
+void merge(kad_units& R, const kad_type_config& tc, std::vector<Unit>& units) {
+  Interner& S = R.st;
+  const int32_t g = S.id(tc.group ? tc.group : ""), v = S.id(tc.version ? tc.version : ""),
+                k = S.id(tc.kind ? tc.kind : "");
+  auto add_req = [&](const Req& r) {
+    R.rq_key.push_back(S.id(r.key));
+    R.rq_op.push_back(S.id(r.op));
+    if (r.values)
+      for (const std::string& x : *r.values) R.rq_val.push_back(S.id(x));
+    R.rq_val_off.push_back((int32_t)R.rq_val.size());
+  };
+  for (size_t i = 0; i < units.size(); ++i) {
+    Unit& u = units[i];
+    R.status[i] = u.status;
+    R.policy_index[i] = u.policy;
+    R.msg[i] = std::move(u.msg);
+    if (u.status != KAD_OBJ_OK) continue;
+    R.unit_index[i] = R.n_units++;
+    R.group.push_back(g);
+    R.version.push_back(v);
+    R.kind.push_back(k);
+    R.ns.push_back(S.id(u.ns));
+    R.name.push_back(S.id(u.name));
+    R.flags.push_back(u.flags);
+    R.desired.push_back(u.desired);
+    R.max_clusters.push_back(u.max_clusters);
+    R.req_cpu.push_back(0);  // schedulingUnitForFedObject leaves ResourceRequest zero
+    R.req_mem.push_back(0);
+    R.req_eph.push_back(0);
+    R.scalar_off.push_back((int32_t)R.scalar_name.size());
+    for (const Toleration& t : u.tols) {
+      R.tol_key.push_back(S.id(t.key));
+      R.tol_op.push_back(S.id(t.op));
+      R.tol_value.push_back(S.id(t.value));
+      R.tol_effect.push_back(S.id(t.effect));
+    }
+    R.tol_off.push_back((int32_t)R.tol_key.size());
+    for (const auto& kv : u.sel) {
+      R.sel_key.push_back(S.id(kv.first));
+      R.sel_value.push_back(S.id(kv.second));
+    }
+    R.sel_off.push_back((int32_t)R.sel_key.size());
+    for (const Term& t : u.rterms) {
+      R.rt_req.push_back((int32_t)R.rq_key.size());
+      R.rt_n_expr.push_back(t.exprs ? (int32_t)t.exprs->size() : 0);
+      R.rt_n_field.push_back(t.fields ? (int32_t)t.fields->size() : 0);
+      if (t.exprs)
+        for (const Req& r : *t.exprs) add_req(r);
+      if (t.fields)
+        for (const Req& r : *t.fields) add_req(r);
+    }
+    R.rterm_off.push_back((int32_t)R.rt_req.size());
+    for (const PrefTerm& p : u.pterms) {
+      R.pt_weight.push_back(p.weight);
+      R.pt_req.push_back((int32_t)R.rq_key.size());
+      R.pt_n_expr.push_back(p.pref.exprs ? (int32_t)p.pref.exprs->size() : 0);
+      if (p.pref.exprs)
+        for (const Req& r : *p.pref.exprs) add_req(r);
+    }
+    R.pterm_off.push_back((int32_t)R.pt_weight.size());
+    for (const std::string& n : u.place) R.place_name.push_back(S.id(n));
+    R.place_off.push_back((int32_t)R.place_name.size());
+    for (const auto& c : u.cur) {
+      R.cur_name.push_back(S.id(c.first));
+      R.cur_rep.push_back(c.second ? *c.second : 0);
+      R.cur_has_rep.push_back(c.second ? 1 : 0);
+    }
+    R.cur_off.push_back((int32_t)R.cur_name.size());
+    auto put = [&](const OMap<int64_t>& m, std::vector<int32_t>& off, std::vector<int32_t>& nm, std::vector<int64_t>& val) {
+      for (const auto& kv : m) {
+        nm.push_back(S.id(kv.first));
+        val.push_back(kv.second);
+      }
+      off.push_back((int32_t)nm.size());
+    };
+    put(u.wt, R.wt_off, R.wt_name, R.wt_val);
+    put(u.mn, R.min_off, R.min_name, R.min_val);
+    put(u.mx, R.max_off, R.max_name, R.max_val);
+    put(u.cap, R.cap_off, R.cap_name, R.cap_val);
+    u = Unit();
+  }
+}
+
+}  // namespace
+
+extern "C" int kad_units_from_objects(const kad_type_config* tc, const kad_strs* objects, const kad_strs* policies,
+                                      const int32_t* policy_of, int threads, kad_units** out) {
+  if (!tc || !objects || !out || objects->n < 0 || (objects->n > 0 && (!objects->off || !objects->bytes)) ||
+      (policies && policies->n > 0 && (!policies->off || !policies->bytes)))
+    return KAD_EINVAL;
+  *out = nullptr;
+  try {
+    auto R = std::make_unique<kad_units>();
+    const int n = objects->n;
+    const int np = policies ? policies->n : 0;
+    if (threads <= 0) threads = 1 << 20;
+    auto text = [](const kad_strs* s, int i) {
+      return sv(reinterpret_cast<const char*>(s->bytes) + s->off[i], (size_t)(s->off[i + 1] - s->off[i]));
+    };
+    std::vector<Policy> pols((size_t)np);
+    parallel_for(np, threads, [&](int lo, int hi) {
+      for (int i = lo; i < hi; ++i) load_policy(text(policies, i), pols[(size_t)i]);
+    }, 64);
+    std::unordered_map<std::string, int32_t> pol_index;
+    for (int i = 0; i < np; ++i) pol_index[pols[(size_t)i].ns + '\0' + pols[(size_t)i].name] = i;  // the last wins
+    Builder B{*tc, pols, pol_index, {"spec", "template"}, "/", !tc->replicas_spec || !*tc->replicas_spec};
+    {
+      const std::string path = tc->replicas_spec ? tc->replicas_spec : "";
+      std::vector<std::string> parts;
+      size_t a = 0;
+      for (size_t i = 0; i <= path.size(); ++i)
+        if (i == path.size() || path[i] == '.') {
+          if (i > a) parts.push_back(path.substr(a, i - a));
+          a = i + 1;
+        }
+      for (size_t i = 0; i < parts.size(); ++i) {
+        B.replicas_fields.push_back(parts[i]);
+        B.replicas_slash += (i ? "/" : "") + parts[i];
+      }
+    }
+    std::vector<Unit> units((size_t)n);
+    parallel_for(n, threads, [&](int lo, int hi) {
+      JDoc d, ad;  // the object's nodes, an annotation's nodes (capacity kept across objects)
+      for (int i = lo; i < hi; ++i) {
+        Unit& u = units[(size_t)i];
+        try {
+          B.build(text(objects, i), u, d, ad, policy_of ? policy_of[i] : -2);
+        } catch (const Fail& f) {
+          const int32_t pol = u.policy;
+          u = Unit();
+          u.status = f.status;
+          u.msg = f.msg;
+          u.policy = pol;
+        }
+      }
+    }, 256);
+    R->status.assign((size_t)n, 0);
+    R->unit_index.assign((size_t)n, -1);
+    R->policy_index.assign((size_t)n, -1);
+    R->msg.assign((size_t)n, std::string());
+    merge(*R, *tc, units);
+    *out = R.release();
+    return KAD_OK;
+  } catch (const std::bad_alloc&) {
+    return KAD_ENOMEM;
+  } catch (...) {
+    return KAD_EINVAL;
+  }
+}
+
+extern "C" int kad_units_view(const kad_units* u, kad_su_columns* c, const int32_t** status, const int32_t** unit_index,
+                              const int32_t** policy_index) {
+  if (!u) return KAD_EINVAL;
+  if (status) *status = u->status.data();
+  if (unit_index) *unit_index = u->unit_index.data();
+  if (policy_index) *policy_index = u->policy_index.data();
+  if (!c) return KAD_OK;
+  std::memset(c, 0, sizeof *c);
+  c->n_units = u->n_units;
+  c->str.n = (int32_t)(u->st.off.size() - 1);
+  c->str.off = u->st.off.data();
+  c->str.bytes = u->st.bytes.data();
+  c->group = u->group.data();
+  c->version = u->version.data();
+  c->kind = u->kind.data();
+  c->namespace_ = u->ns.data();
+  c->name = u->name.data();
+  c->flags = u->flags.data();
+  c->desired = u->desired.data();
+  c->max_clusters = u->max_clusters.data();
+  c->req_cpu = u->req_cpu.data();
+  c->req_mem = u->req_mem.data();
+  c->req_eph = u->req_eph.data();
+  c->scalar_off = u->scalar_off.data();
+  c->scalar_name = u->scalar_name.data();
+  c->scalar_val = u->scalar_val.data();
+  c->tol_off = u->tol_off.data();
+  c->tol_key = u->tol_key.data();
+  c->tol_op = u->tol_op.data();
+  c->tol_value = u->tol_value.data();
+  c->tol_effect = u->tol_effect.data();
+  c->sel_off = u->sel_off.data();
+  c->sel_key = u->sel_key.data();
+  c->sel_value = u->sel_value.data();
+  c->n_reqs = (int32_t)u->rq_key.size();
+  c->rq_key = u->rq_key.data();
+  c->rq_op = u->rq_op.data();
+  c->rq_val_off = u->rq_val_off.data();
+  c->rq_val = u->rq_val.data();
+  c->rterm_off = u->rterm_off.data();
+  c->rt_req = u->rt_req.data();
+  c->rt_n_expr = u->rt_n_expr.data();
+  c->rt_n_field = u->rt_n_field.data();
+  c->pterm_off = u->pterm_off.data();
+  c->pt_weight = u->pt_weight.data();
+  c->pt_req = u->pt_req.data();
+  c->pt_n_expr = u->pt_n_expr.data();
+  c->place_off = u->place_off.data();
+  c->place_name = u->place_name.data();
+  c->cur_off = u->cur_off.data();
+  c->cur_name = u->cur_name.data();
+  c->cur_rep = u->cur_rep.data();
+  c->cur_has_rep = u->cur_has_rep.data();
+  c->wt_off = u->wt_off.data();
+  c->wt_name = u->wt_name.data();
+  c->wt_val = u->wt_val.data();
+  c->min_off = u->min_off.data();
+  c->min_name = u->min_name.data();
+  c->min_val = u->min_val.data();
+  c->max_off = u->max_off.data();
+  c->max_name = u->max_name.data();
+  c->max_val = u->max_val.data();
+  c->cap_off = u->cap_off.data();
+  c->cap_name = u->cap_name.data();
+  c->cap_val = u->cap_val.data();
+  return KAD_OK;
+}
+
+extern "C" const char* kad_units_message(const kad_units* u, int32_t i) {
+  if (!u || i < 0 || (size_t)i >= u->msg.size()) return "";
+  return u->msg[(size_t)i].c_str();
+}
+
+extern "C" void kad_units_free(kad_units* u) { delete u; }

@@ -50,13 +50,13 @@ _lib = None
 
 
 def declared_functions() -> List[str]:
-    """Names of the functions include/*.h declare (kad_sched.h, kad_pack.h)."""
+    """Names of the functions include/*.h declare (kad_sched.h, kad_pack.h, kad_objects.h)."""
     import glob
 
     names = set()
     for h in sorted(glob.glob(os.path.join(os.path.dirname(HEADER), "*.h"))):
         with open(h) as f:
-            names |= set(re.findall(r"^\s*(?:int|const char\*)\s+(kad_\w+)\s*\(", f.read(), re.M))
+            names |= set(re.findall(r"^\s*(?:int|void|const char\*)\s+(kad_\w+)\s*\(", f.read(), re.M))
     return sorted(names)
 
 

@@ -29,7 +29,7 @@ NAMES = ["A_filter", "B_score", "C_normalize", "D_select", "E_output", "n_stradd
          "lean_n_straddle", "lean_D_select_straddle", "plan_P0_setup", "plan_P1_weights", "plan_P2_plan",
          "plan_P3_output", "row_compact", "plan_rows", "row_score", "row_normalize",
          "replay_setup", "replay_partition", "replay_pivot", "replay_insertion", "replay_n_partitions",
-         "replay_sum_n", "row_select", "row_replay"]
+         "replay_sum_n", "row_select", "row_replay", "row_terms", "row_positions"]
 
 
 def main():
@@ -59,7 +59,7 @@ def main():
     ctx = runtime.Context(0)
     ctx.upload_snapshot(snap)
     ctx.upload_batch(batch)
-    cnt = np.zeros(32, dtype=np.uint64)
+    cnt = np.zeros(40, dtype=np.uint64)
     ctx.schedule(fwk)
     ctx.sync()
     L.kad_debug_phase_counters(cnt.ctypes.data, 1)
