@@ -1,7 +1,11 @@
 /*
- * kad_objects.h — native SchedulingUnit builder of libkad.so (SURVEY §8(f) row
- * f2): a batch of federated objects and the (Cluster)PropagationPolicies they
- * name, as JSON text, → the kad_su_columns that kad_pack_batch packs.
+ * kad_objects.h — the host side of the batch scheduler's object formats in
+ * libkad.so, for a batch of federated objects as
+ * JSON text:
+ *   f2  kad_units_from_objects — objects + the (Cluster)PropagationPolicies they
+ *       name → the kad_su_columns that kad_pack_batch packs;
+ *   f3  kad_apply_results — kad_schedule's results written back into the
+ *       objects (placements, replica overrides, annotations).
  *
  * Replaces, per object, what the reference's scheduler controller does before
  * Schedule (pkg/controllers/scheduler/scheduler.go:349-392, 445-467):
@@ -75,6 +79,35 @@ int kad_units_view(const kad_units* u, kad_su_columns* cols, const int32_t** sta
 /* The message of object i's failure ("" when it has none); valid until kad_units_free. */
 const char* kad_units_message(const kad_units* u, int32_t i);
 void kad_units_free(kad_units* u);
+
+/* ------------------------------------------------------------ row f3
+ * applySchedulingResult (scheduler.go:632-695) for a batch: each object's
+ * placement for the global scheduler (util.SetPlacementClusterNames,
+ * util/placement.go:44-59), its replica overrides (UpdateReplicasOverride /
+ * OverrideUpdateNeeded / updateOverridesMap, scheduler/util.go:71-185;
+ * util.SetOverrides, util/overrides.go:114-169) and the follower-scheduling /
+ * pod-unschedulable-threshold annotations. Results in kad_results_download's
+ * form: object i's clusters are res_cluster[res_off[i] .. res_off[i+1]) (ids
+ * into `cluster_names`, the snapshot order) with res_replicas (-1: nil,
+ * Duplicate mode); follower[i]: !DisableFollowerScheduling; threshold_ns[i]:
+ * the policy's AutoMigration.When.PodUnschedulableFor (INT64_MIN: no
+ * auto-migration; NULL: none for every object). A modified object comes back
+ * as json.Marshal of its unstructured map (keys sorted, Go string escaping
+ * and float64 formatting); an unchanged or failed one as its input text. */
+#define KAD_APPLY_OK 0       /* applied; modified[i] says whether the object changed                  */
+#define KAD_APPLY_ERROR 1    /* applySchedulingResult returns an error (the object is returned as it was) */
+#define KAD_APPLY_PANIC 2    /* the reference panics (SetOverrides on an object whose spec is nil)     */
+#define KAD_APPLY_BAD_JSON 3 /* the object's text is not a JSON object                                 */
+
+typedef struct kad_applied kad_applied;
+
+int kad_apply_results(const kad_type_config* tc, const kad_strs* objects, const kad_strs* cluster_names,
+                      const int32_t* res_off, const int32_t* res_cluster, const int64_t* res_replicas,
+                      const uint8_t* follower, const int64_t* threshold_ns, int threads, kad_applied** out);
+/* Views into *a (valid until kad_applied_free): per object its status, whether it changed, and its text. */
+int kad_applied_view(const kad_applied* a, const int32_t** status, const uint8_t** modified, kad_strs* texts);
+const char* kad_applied_message(const kad_applied* a, int32_t i);
+void kad_applied_free(kad_applied* a);
 
 #ifdef __cplusplus
 }

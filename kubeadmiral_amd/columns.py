@@ -642,3 +642,74 @@ def units_from_objects(type_config, objects: Sequence, policies: Sequence, polic
         return out
     finally:
         L.kad_units_free(h)
+
+
+# include/kad_objects.h KAD_APPLY_*
+APPLY_OK, APPLY_ERROR, APPLY_PANIC, APPLY_BAD_JSON = range(4)
+
+
+def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], res_off, res_cluster, res_replicas,
+                  follower=None, threshold_ns=None, threads: int = 0):
+    """kad_apply_results: applySchedulingResult for a batch of objects (JSON texts or dicts) with results in
+    kad_results_download's form (CSR of snapshot cluster ids, replicas -1 = nil). ``follower``: per object
+    !DisableFollowerScheduling (default all True); ``threshold_ns``: per object the pod-unschedulable threshold
+    or None. Returns (status, modified, texts, messages): texts are the objects' new JSON (bytes)."""
+    from .runtime import load_library
+
+    L = load_library()
+    P = ctypes.c_void_p
+    L.kad_apply_results.argtypes = [P, P, P, P, P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
+    L.kad_applied_view.argtypes = [P, P, P, P]
+    L.kad_applied_message.argtypes = [P, ctypes.c_int32]
+    L.kad_applied_message.restype = ctypes.c_char_p
+    L.kad_applied_free.argtypes = [P]
+    L.kad_applied_free.restype = None
+    ot = _texts(objects)
+    n = len(ot)
+    keep: list = []
+
+    def strs(parts):
+        off = np.zeros(len(parts) + 1, I64)
+        if parts:
+            off[1:] = np.cumsum([len(p) for p in parts])
+        data = np.frombuffer(b"".join(parts) or b"\0", U8).copy()
+        keep.extend([off, data])
+        return KadStrs(len(parts), off.ctypes.data, data.ctypes.data)
+
+    so, sc = strs(ot), strs([c.encode() for c in cluster_names])
+    ro = np.ascontiguousarray(res_off, I32)
+    rc_ = np.ascontiguousarray(res_cluster, I32) if len(res_cluster) else np.zeros(1, I32)
+    rr = np.ascontiguousarray(res_replicas, I64) if len(res_replicas) else np.zeros(1, I64)
+    fo = np.ascontiguousarray(np.ones(n, U8) if follower is None else np.asarray(follower, U8))
+    th = np.full(max(1, n), np.iinfo(np.int64).min, I64)
+    if threshold_ns is not None:
+        for i, t in enumerate(threshold_ns):
+            if t is not None:
+                th[i] = t
+    if len(ro) != n + 1:
+        raise ValueError("res_off: n_objects + 1 entries")
+    h = P()
+    rc = L.kad_apply_results(ctypes.byref(KadTypeConfig(
+        type_config.group.encode(), type_config.version.encode(), type_config.kind.encode(),
+        type_config.plural_name.encode(), 1 if type_config.namespaced else 0, type_config.replicas_spec.encode())),
+        ctypes.byref(so), ctypes.byref(sc), ro.ctypes.data, rc_.ctypes.data, rr.ctypes.data, fo.ctypes.data,
+        th.ctypes.data, threads if threads > 0 else default_threads(), ctypes.byref(h))
+    if rc != 0:
+        raise RuntimeError(f"kad_apply_results failed ({rc})")
+    try:
+        st, md = P(), P()
+        tx = KadStrs()
+        L.kad_applied_view(h, ctypes.byref(st), ctypes.byref(md), ctypes.byref(tx))
+        status = np.ctypeslib.as_array(ctypes.cast(st, ctypes.POINTER(ctypes.c_int32)), (n,)).copy() if n else \
+            np.zeros(0, I32)
+        modified = np.ctypeslib.as_array(ctypes.cast(md, ctypes.POINTER(ctypes.c_uint8)), (n,)).astype(bool) if n \
+            else np.zeros(0, bool)
+        texts = []
+        if n:
+            off = np.ctypeslib.as_array(ctypes.cast(tx.off, ctypes.POINTER(ctypes.c_int64)), (n + 1,))
+            data = ctypes.string_at(tx.bytes, int(off[-1])) if off[-1] else b""
+            texts = [data[int(off[i]):int(off[i + 1])] for i in range(n)]
+        msgs = [L.kad_applied_message(h, i).decode(errors="replace") if status[i] else "" for i in range(n)]
+        return status, modified, texts, msgs
+    finally:
+        L.kad_applied_free(h)

@@ -17,6 +17,7 @@
 // unstructured round trip (UnstructuredToInterface). Parity: tests/test_native_objects.py compares
 // every field with kubeadmiral_amd/objects.py and the reference's schedulingunit table.
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -51,6 +52,8 @@ constexpr sv AFFINITY_ANN = "kubeadmiral.io/affinity";
 constexpr sv MAX_CLUSTERS_ANN = "kubeadmiral.io/maxClusters";
 constexpr sv AUTO_MIGRATION_INFO_ANN = "kubeadmiral.io/auto-migration-info";
 constexpr sv DUPLICATE = "Duplicate", DIVIDE = "Divide";
+constexpr sv ENABLE_FOLLOWER_ANN = "internal.kubeadmiral.io/enable-follower-scheduling";
+constexpr sv POD_UNSCHEDULABLE_THRESHOLD_ANN = "internal.kubeadmiral.io/pod-unschedulable-threshold";
 
 struct Fail {  // the reference returns an error (status) or panics
   int status;
@@ -733,6 +736,121 @@ void load_policy(sv text, Policy& P) {
   else P.ok = true;
 }
 
+// ------------------------------------------------------------------ typed views of the object itself
+// (decoded through the unstructured round trip: sorted unique keys)
+struct PC {  // PlacementWithController
+  std::string controller;
+  std::optional<std::vector<std::string>> clusters;
+};
+// _OBJ_PLACEMENTS: type-checks apiVersion, kind, metadata and spec.placements; the error or null
+const char* decode_placements_view(const JDoc& d, uint32_t root, std::optional<std::vector<PC>>& pls) {
+  static const sv N[] = {"apiVersion", "kind", "metadata", "spec"};
+  static const sv NM[] = {"name", "namespace", "generateName", "uid", "resourceVersion", "generation", "labels", "annotations"};
+  static const sv NS[] = {"placements"};
+  static const sv NPC[] = {"controller", "placement"};
+  static const sv NPL[] = {"clusters"};
+  static const sv NCR[] = {"name"};
+  Dec D{d, true};
+  std::string scratch;
+  D.fields(root, N, [&](int f, uint32_t v) {
+    if (f <= 1) {
+      D.str(v, scratch);
+    } else if (f == 2) {
+      D.fields(v, NM, [&](int g, uint32_t w) {
+        if (g <= 4) {
+          D.str(w, scratch);
+        } else if (g == 5) {
+          int64_t i = 0;
+          D.int64(w, i);
+        } else {
+          std::optional<OMap<std::string>> m;
+          dec_string_map(D, w, m);
+        }
+      });
+    } else {
+      D.fields(v, NS, [&](int, uint32_t w) {
+        D.slice(w, pls, [&](uint32_t e, PC& pc) {
+          D.fields(e, NPC, [&](int g, uint32_t y) {
+            if (g == 0) {
+              D.str(y, pc.controller);
+            } else {
+              D.fields(y, NPL, [&](int, uint32_t z) {
+                D.slice(z, pc.clusters, [&](uint32_t q, std::string& s) {
+                  D.fields(q, NCR, [&](int, uint32_t r) { D.str(r, s); });
+                });
+              });
+            }
+          });
+        });
+      });
+    }
+  });
+  return D.err;
+}
+struct Patch {  // OverridePatch; value: interface{} (a node of the object), or a replica count set here
+  std::string op, path;
+  Dec::Any value;
+  uint32_t node = 0;
+  bool set = false;  // value = n (written by updateOverridesMap)
+  int64_t n = 0;
+};
+struct CO {
+  std::string cluster;
+  std::optional<std::vector<Patch>> patches;
+};
+struct CtrlO {
+  std::string controller;
+  std::optional<std::vector<CO>> clusters;
+};
+// _OBJ_OVERRIDES; spec_set: spec decoded to a non-nil pointer
+const char* decode_overrides_view(const JDoc& d, uint32_t root, std::optional<std::vector<CtrlO>>& ovs, bool& spec_set) {
+  static const sv N[] = {"spec"};
+  static const sv NS[] = {"overrides"};
+  static const sv NC[] = {"controller", "clusters"};
+  static const sv NCO[] = {"clusterName", "paths"};
+  static const sv NP[] = {"op", "path", "value"};
+  Dec D{d, true};
+  D.fields(root, N, [&](int, uint32_t v) {
+    if (D.null(v)) {  // *spec = nil (a later case-folded "spec" member may set it again)
+      ovs.reset();
+      spec_set = false;
+      return;
+    }
+    if (D.at(v).t == J_OBJ) spec_set = true;
+    D.fields(v, NS, [&](int, uint32_t w) {
+      D.slice(w, ovs, [&](uint32_t e, CtrlO& c) {
+        D.fields(e, NC, [&](int g, uint32_t y) {
+          if (g == 0) {
+            D.str(y, c.controller);
+          } else {
+            D.slice(y, c.clusters, [&](uint32_t q, CO& co) {
+              D.fields(q, NCO, [&](int h, uint32_t r) {
+                if (h == 0) {
+                  D.str(r, co.cluster);
+                } else {
+                  D.slice(r, co.patches, [&](uint32_t s, Patch& p) {
+                    D.fields(s, NP, [&](int k, uint32_t t) {
+                      if (k == 0) {
+                        D.str(t, p.op);
+                      } else if (k == 1) {
+                        D.str(t, p.path);
+                      } else {
+                        D.any(t, p.value);
+                        p.node = t;
+                      }
+                    });
+                  });
+                }
+              });
+            });
+          }
+        });
+      });
+    });
+  });
+  return D.err;
+}
+
 // ------------------------------------------------------------------ one object → one SchedulingUnit
 struct Unit {  // strings by value; interned in the serial merge
   int status = KAD_OBJ_OK;
@@ -1068,126 +1186,22 @@ struct Builder {
   // getCurrentReplicasFromObject (schedulingunit.go:181-222): the global scheduler's placement and its
   // replica overrides (util.GetOverrides, util/overrides.go:68-112)
   void current_replicas(const JDoc& d, uint32_t root, Unit& u) {
-    Dec D{d, true};
-    // the placements view (_OBJ_PLACEMENTS): type-checks apiVersion, kind, metadata and spec.placements
     std::optional<std::vector<std::string>> names;
-    bool seen_ctrl = false;
     {
-      static const sv N[] = {"apiVersion", "kind", "metadata", "spec"};
-      static const sv NM[] = {"name", "namespace", "generateName", "uid", "resourceVersion", "generation", "labels", "annotations"};
-      static const sv NS[] = {"placements"};
-      static const sv NPC[] = {"controller", "placement"};
-      static const sv NPL[] = {"clusters"};
-      static const sv NCR[] = {"name"};
-      struct PC {
-        std::string controller;
-        std::optional<std::vector<std::string>> clusters;
-      };
       std::optional<std::vector<PC>> pls;
-      std::string scratch;
-      D.fields(root, N, [&](int f, uint32_t v) {
-        if (f <= 1) {
-          D.str(v, scratch);
-        } else if (f == 2) {
-          if (D.null(v)) return;
-          D.fields(v, NM, [&](int g, uint32_t w) {
-            if (g <= 4) {
-              D.str(w, scratch);
-            } else if (g == 5) {
-              int64_t i = 0;
-              D.int64(w, i);
-            } else {
-              std::optional<OMap<std::string>> m;
-              dec_string_map(D, w, m);
-            }
-          });
-        } else {
-          if (D.null(v)) return;
-          D.fields(v, NS, [&](int, uint32_t w) {
-            D.slice(w, pls, [&](uint32_t e, PC& pc) {
-              if (D.null(e)) return;
-              D.fields(e, NPC, [&](int g, uint32_t y) {
-                if (g == 0) {
-                  D.str(y, pc.controller);
-                } else if (!D.null(y)) {
-                  D.fields(y, NPL, [&](int, uint32_t z) {
-                    D.slice(z, pc.clusters, [&](uint32_t q, std::string& s) {
-                      if (D.null(q)) return;
-                      D.fields(q, NCR, [&](int, uint32_t r) { D.str(r, s); });
-                    });
-                  });
-                }
-              });
-            });
-          });
-        }
-      });
-      if (D.err) fail(KAD_OBJ_UNIT_ERROR, std::string("placements: json: cannot unmarshal into ") + D.err);
+      if (const char* e = decode_placements_view(d, root, pls))
+        fail(KAD_OBJ_UNIT_ERROR, std::string("placements: json: cannot unmarshal into ") + e);
       if (pls)
         for (const PC& pc : *pls)
           if (pc.controller == PREFIXED_GLOBAL_SCHEDULER) {
-            seen_ctrl = true;
             if (pc.clusters) names = pc.clusters;
             break;
           }
     }
-    (void)seen_ctrl;
-    // the overrides view (_OBJ_OVERRIDES)
-    struct Patch {
-      std::string op, path;
-      Dec::Any value;
-    };
-    struct CO {
-      std::string cluster;
-      std::optional<std::vector<Patch>> patches;
-    };
-    struct CtrlO {
-      std::string controller;
-      std::optional<std::vector<CO>> clusters;
-    };
     std::optional<std::vector<CtrlO>> ovs;
-    {
-      static const sv N[] = {"spec"};
-      static const sv NS[] = {"overrides"};
-      static const sv NC[] = {"controller", "clusters"};
-      static const sv NCO[] = {"clusterName", "paths"};
-      static const sv NP[] = {"op", "path", "value"};
-      D.fields(root, N, [&](int, uint32_t v) {
-        if (D.null(v)) {
-          ovs.reset();
-          return;
-        }
-        D.fields(v, NS, [&](int, uint32_t w) {
-          D.slice(w, ovs, [&](uint32_t e, CtrlO& c) {
-            if (D.null(e)) return;
-            D.fields(e, NC, [&](int g, uint32_t y) {
-              if (g == 0) {
-                D.str(y, c.controller);
-              } else {
-                D.slice(y, c.clusters, [&](uint32_t q, CO& co) {
-                  if (D.null(q)) return;
-                  D.fields(q, NCO, [&](int h, uint32_t r) {
-                    if (h == 0) {
-                      D.str(r, co.cluster);
-                    } else {
-                      D.slice(r, co.patches, [&](uint32_t s, Patch& p) {
-                        if (D.null(s)) return;
-                        D.fields(s, NP, [&](int k, uint32_t t) {
-                          if (k == 0) D.str(t, p.op);
-                          else if (k == 1) D.str(t, p.path);
-                          else D.any(t, p.value);
-                        });
-                      });
-                    }
-                  });
-                });
-              }
-            });
-          });
-        });
-      });
-    }
-    if (D.err) fail(KAD_OBJ_UNIT_ERROR, std::string("overrides: json: cannot unmarshal into ") + D.err);
+    bool spec_set = false;
+    const char* oerr = decode_overrides_view(d, root, ovs, spec_set);
+    if (oerr) fail(KAD_OBJ_UNIT_ERROR, std::string("overrides: json: cannot unmarshal into ") + oerr);
     const std::vector<CO>* clusters = nullptr;
     if (ovs)
       for (const CtrlO& c : *ovs)
@@ -1226,6 +1240,483 @@ struct Builder {
           }
       u.cur.emplace_back(n, rep);
     }
+  }
+};
+
+
+// ------------------------------------------------------------------ f3: applySchedulingResult
+// A mutable copy of the object (the unstructured map: unique keys, the last member wins) that the result is
+// written into, then re-marshalled the way the reference's Update sends it (json.Marshal of the map: keys
+// sorted, Go's string escaping and float64 formatting).
+struct MV {
+  JT t = J_NULL;
+  bool isint = false, fits = false;  // number: an integer literal within int64 (an unstructured int64)
+  int64_t i = 0;
+  double d = 0;
+  std::string s;
+  std::vector<std::pair<std::string, MV>> o;
+  std::vector<MV> a;
+
+  MV* get(sv key) {
+    for (auto& kv : o)
+      if (kv.first == key) return &kv.second;
+    return nullptr;
+  }
+  void set(sv key, MV v) {
+    if (MV* x = get(key)) *x = std::move(v);
+    else o.emplace_back(std::string(key), std::move(v));
+  }
+  void erase(sv key) {
+    for (size_t k = 0; k < o.size(); ++k)
+      if (o[k].first == key) {
+        o.erase(o.begin() + (long)k);
+        return;
+      }
+  }
+  static MV str(sv x) {
+    MV m;
+    m.t = J_STR;
+    m.s.assign(x);
+    return m;
+  }
+  static MV obj() {
+    MV m;
+    m.t = J_OBJ;
+    return m;
+  }
+  static MV arr() {
+    MV m;
+    m.t = J_ARR;
+    return m;
+  }
+  static MV f64(double x) {
+    MV m;
+    m.t = J_NUM;
+    m.d = x;
+    return m;
+  }
+};
+// the node as Go holds it: floats_only — an interface{} value decoded by json.Unmarshal (every number a float64)
+MV mv_of(const JDoc& d, uint32_t x, bool floats_only) {
+  const JV& v = d.v[x];
+  MV m;
+  m.t = v.t;
+  if (v.t == J_NUM) {
+    m.isint = v.isint && !floats_only;
+    m.fits = v.fits;
+    m.i = v.i;
+    m.d = v.d;
+  } else if (v.t == J_STR) {
+    m.s.assign(d.str(x));
+  } else if (v.t == J_ARR) {
+    m.a.reserve(v.n);
+    for (uint32_t k = 0; k < v.n; ++k) m.a.push_back(mv_of(d, d.kids[v.a + k], floats_only));
+  } else if (v.t == J_OBJ) {
+    for (uint32_t k = 0; k < v.n; ++k) m.set(d.str(d.kids[v.a + 2 * k]), mv_of(d, d.kids[v.a + 2 * k + 1], floats_only));
+  }
+  return m;
+}
+
+// encodeState.string (Go 1.19, HTML escaping on); gojson._enc_str
+void emit_str(sv s, std::string& out) {
+  static const char* hex = "0123456789abcdef";
+  out += '"';
+  for (size_t i = 0; i < s.size();) {
+    const unsigned char c = (unsigned char)s[i];
+    if (c < 0x80) {
+      if (c == '"') out += "\\\"";
+      else if (c == '\\') out += "\\\\";
+      else if (c >= 0x20 && c != '<' && c != '>' && c != '&') out += (char)c;
+      else if (c == '\n') out += "\\n";
+      else if (c == '\r') out += "\\r";
+      else if (c == '\t') out += "\\t";
+      else {
+        out += "\\u00";
+        out += hex[c >> 4];
+        out += hex[c & 0xF];
+      }
+      ++i;
+      continue;
+    }
+    // one UTF-8 sequence (the parser only produces valid ones); U+2028 / U+2029 escaped
+    const size_t n = c >= 0xF0 ? 4 : (c >= 0xE0 ? 3 : 2);
+    if (n == 3 && c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 &&
+        ((unsigned char)s[i + 2] == 0xA8 || (unsigned char)s[i + 2] == 0xA9)) {
+      out += (unsigned char)s[i + 2] == 0xA8 ? "\\u2028" : "\\u2029";
+    } else {
+      out.append(s.data() + i, std::min(n, s.size() - i));
+    }
+    i += n;
+  }
+  out += '"';
+}
+// floatEncoder (encoding/json/encode.go): 'f' unless the magnitude is < 1e-6 or >= 1e21, shortest digits
+void emit_f64(double f, std::string& out) {
+  char buf[64];
+  const double ab = std::fabs(f);
+  const bool e = ab != 0 && (ab < 1e-6 || ab >= 1e21);
+  auto r = std::to_chars(buf, buf + sizeof buf, f, e ? std::chars_format::scientific : std::chars_format::fixed);
+  std::string t(buf, r.ptr);
+  if (e) {  // e-07 → e-7
+    const size_t n = t.size();
+    if (n >= 4 && t[n - 4] == 'e' && t[n - 3] == '-' && t[n - 2] == '0') t.erase(n - 2, 1);
+  }
+  out += t;
+}
+void emit(const MV& m, std::string& out) {
+  switch (m.t) {
+    case J_NULL: out += "null"; break;
+    case J_TRUE: out += "true"; break;
+    case J_FALSE: out += "false"; break;
+    case J_STR: emit_str(m.s, out); break;
+    case J_NUM:
+      if (m.isint && m.fits) out += std::to_string(m.i);
+      else emit_f64(m.d, out);
+      break;
+    case J_ARR:
+      out += '[';
+      for (size_t k = 0; k < m.a.size(); ++k) {
+        if (k) out += ',';
+        emit(m.a[k], out);
+      }
+      out += ']';
+      break;
+    case J_OBJ: {
+      std::vector<const std::pair<std::string, MV>*> ks;
+      ks.reserve(m.o.size());
+      for (const auto& kv : m.o) ks.push_back(&kv);
+      std::sort(ks.begin(), ks.end(), [](auto* x, auto* y) { return x->first < y->first; });
+      out += '{';
+      for (size_t k = 0; k < ks.size(); ++k) {
+        if (k) out += ',';
+        emit_str(ks[k]->first, out);
+        out += ':';
+        emit(ks[k]->second, out);
+      }
+      out += '}';
+    }
+  }
+}
+
+// unstructured.SetNestedField(obj, value, a, b): a created when missing, an error when it is not a map
+void set_nested(MV& root, sv a, sv b, MV value) {
+  MV* x = root.get(a);
+  if (!x) {
+    root.set(a, MV::obj());
+    x = root.get(a);
+  } else if (x->t != J_OBJ) {
+    fail(KAD_APPLY_ERROR, std::string("value cannot be set because ") + std::string(a) + " is not a map[string]interface{}");
+  }
+  x->set(b, std::move(value));
+}
+
+// time.Duration.String
+std::string duration_string(int64_t d) {
+  if (d == 0) return "0s";
+  const bool neg = d < 0;
+  uint64_t u = neg ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+  auto frac = [](uint64_t v, int prec, std::string& fs) {
+    std::string digits;
+    bool printed = false;
+    for (int k = 0; k < prec; ++k) {
+      const int dg = (int)(v % 10);
+      printed = printed || dg != 0;
+      if (printed) digits += (char)('0' + dg);
+      v /= 10;
+    }
+    std::reverse(digits.begin(), digits.end());
+    fs = printed ? "." + digits : "";
+    return v;
+  };
+  std::string s, fs;
+  if (u < 1000000000ull) {
+    if (u < 1000) {
+      s = std::to_string(u) + "ns";
+    } else if (u < 1000000) {
+      const uint64_t w = frac(u, 3, fs);
+      s = std::to_string(w) + fs + "\xC2\xB5s";
+    } else {
+      const uint64_t w = frac(u, 6, fs);
+      s = std::to_string(w) + fs + "ms";
+    }
+  } else {
+    uint64_t w = frac(u, 9, fs);
+    s = std::to_string(w % 60) + fs + "s";
+    w /= 60;
+    if (w > 0) {
+      s = std::to_string(w % 60) + "m" + s;
+      w /= 60;
+      if (w > 0) s = std::to_string(w) + "h" + s;
+    }
+  }
+  return neg ? "-" + s : s;
+}
+
+struct Applier {
+  const kad_type_config& tc;
+  std::string replicas_slash;  // ToSlashPath(ReplicasSpec)
+
+  MV patch_json(const JDoc& d, const Patch& p) {  // the typed patch, marshalled (value: float64 after the round trip)
+    MV m = MV::obj();
+    if (!p.op.empty()) m.set("op", MV::str(p.op));
+    m.set("path", MV::str(p.path));
+    if (p.set) m.set("value", MV::f64((double)p.n));
+    else if (p.value.t != J_NULL) m.set("value", mv_of(d, p.node, true));
+    return m;
+  }
+
+  // applySchedulingResult (scheduler.go:632-695) on the parsed object; true if anything changed
+  bool apply(const JDoc& d, uint32_t root, MV& obj, const std::vector<std::string>& clusters,
+             const OMap<int64_t>& desired, bool follower, std::optional<int64_t> threshold) {
+    bool modified = false;
+    bool spec_created = false;
+    // util.SetPlacementClusterNames (util/placement.go:44-59)
+    {
+      std::optional<std::vector<PC>> po;
+      if (const char* e = decode_placements_view(d, root, po)) fail(KAD_APPLY_ERROR, std::string("placements: ") + e);
+      std::vector<PC> pls = po ? *po : std::vector<PC>();
+      int idx = -1;
+      for (size_t k = 0; k < pls.size() && idx < 0; ++k)
+        if (pls[k].controller == PREFIXED_GLOBAL_SCHEDULER) idx = (int)k;
+      bool write = false;
+      if (clusters.empty()) {
+        if (idx >= 0) {
+          pls.erase(pls.begin() + idx);
+          write = true;
+        }
+      } else {
+        if (idx < 0) {
+          pls.push_back(PC{std::string(PREFIXED_GLOBAL_SCHEDULER), std::nullopt});
+          idx = (int)pls.size() - 1;
+        }
+        std::vector<std::string> old = pls[(size_t)idx].clusters ? *pls[(size_t)idx].clusters : std::vector<std::string>();
+        std::sort(old.begin(), old.end());
+        old.erase(std::unique(old.begin(), old.end()), old.end());
+        if (old != clusters) {  // clusters: sorted, unique
+          pls[(size_t)idx].clusters = clusters;
+          write = true;
+        }
+      }
+      if (write) {
+        MV value;
+        if (po || !pls.empty()) {
+          value = MV::arr();
+          for (const PC& pc : pls) {
+            MV e = MV::obj();
+            e.set("controller", MV::str(pc.controller));
+            MV pl = MV::obj();
+            if (pc.clusters && !pc.clusters->empty()) {
+              MV cs = MV::arr();
+              for (const std::string& n : *pc.clusters) {
+                MV c = MV::obj();
+                c.set("name", MV::str(n));
+                cs.a.push_back(std::move(c));
+              }
+              pl.set("clusters", std::move(cs));
+            }
+            e.set("placement", std::move(pl));
+            value.a.push_back(std::move(e));
+          }
+        }
+        spec_created = obj.get("spec") == nullptr;
+        set_nested(obj, "spec", "placements", std::move(value));
+        modified = true;
+      }
+    }
+    // UpdateReplicasOverride (scheduler/util.go:71-94)
+    {
+      std::optional<std::vector<CtrlO>> ovs;
+      bool spec_set = false;
+      if (const char* e = decode_overrides_view(d, root, ovs, spec_set))
+        fail(KAD_APPLY_ERROR, std::string("Error reading cluster overrides: ") + e);
+      // util.GetOverrides: the controller's clusters, by name, in list order
+      OMap<std::optional<std::vector<Patch>>> ov;
+      if (ovs)
+        for (const CtrlO& c : *ovs)
+          if (c.controller == PREFIXED_GLOBAL_SCHEDULER) {
+            if (c.clusters)
+              for (const CO& co : *c.clusters) {
+                for (const auto& kv : ov)
+                  if (kv.first == co.cluster) fail(KAD_APPLY_ERROR, "Error reading cluster overrides: cluster \"" + co.cluster + "\" appears more than once");
+                if (co.patches)
+                  for (const Patch& p : *co.patches)
+                    if (p.path == "/metadata/namespace" || p.path == "/metadata/name" ||
+                        p.path == "/metadata/generateName" || p.path == "/kind")
+                      fail(KAD_APPLY_ERROR, "Error reading cluster overrides: invalid path " + p.path);
+                ov.emplace_back(co.cluster, co.patches);
+              }
+            break;
+          }
+      auto desired_of = [&](const std::string& c) -> const int64_t* {
+        for (const auto& kv : desired)
+          if (kv.first == c) return &kv.second;
+        return nullptr;
+      };
+      // OverrideUpdateNeeded (:154-185)
+      bool needed = false;
+      size_t checked = 0;
+      for (const auto& [cluster, patches] : ov) {
+        if (!patches || needed) continue;
+        for (const Patch& p : *patches) {
+          if (p.path != replicas_slash) continue;
+          const int64_t* want = desired_of(cluster);
+          if (p.value.t != J_NUM || !want || f64_to_i64(p.value.f) != *want) {
+            needed = true;
+            break;
+          }
+          ++checked;
+        }
+      }
+      if (!needed) needed = checked != desired.size();
+      if (needed) {
+        // updateOverridesMap (:109-152)
+        for (size_t k = 0; k < ov.size();) {
+          auto& [cluster, patches] = ov[k];
+          if (desired_of(cluster) || !patches) {
+            ++k;
+            continue;
+          }
+          bool erased = false;
+          for (size_t q = 0; q < patches->size(); ++q)
+            if ((*patches)[q].path == replicas_slash) {
+              patches->erase(patches->begin() + (long)q);
+              if (patches->empty()) {
+                ov.erase(ov.begin() + (long)k);
+                erased = true;
+              }
+              break;
+            }
+          if (!erased) ++k;
+        }
+        for (const auto& [cluster, n] : desired) {
+          auto* slot = (std::optional<std::vector<Patch>>*)nullptr;
+          for (auto& kv : ov)
+            if (kv.first == cluster) slot = &kv.second;
+          bool found = false;
+          if (slot && *slot)
+            for (Patch& p : **slot)
+              if (p.path == replicas_slash) {
+                p.set = true;
+                p.n = n;
+                found = true;
+                break;
+              }
+          if (!found) {
+            Patch np;
+            np.path = replicas_slash;
+            np.set = true;
+            np.n = n;
+            if (slot) {
+              if (!*slot) slot->emplace();
+              (*slot)->push_back(std::move(np));
+            } else {
+              ov.emplace_back(cluster, std::vector<Patch>{std::move(np)});
+            }
+          }
+        }
+        // util.SetOverrides (util/overrides.go:114-169)
+        OMap<std::vector<Patch>> keep;
+        for (auto& kv : ov)
+          if (kv.second && !kv.second->empty()) keep.emplace_back(kv.first, std::move(*kv.second));
+        if (!spec_set && !spec_created) fail(KAD_APPLY_PANIC, "invalid memory address or nil pointer dereference");
+        std::optional<std::vector<CtrlO>> cos = ovs;  // the object's overrides (SetOverrides re-reads them)
+        int idx = -1;
+        if (cos)
+          for (size_t k = 0; k < cos->size() && idx < 0; ++k)
+            if ((*cos)[k].controller == PREFIXED_GLOBAL_SCHEDULER) idx = (int)k;
+        if (keep.empty()) {
+          if (idx >= 0) cos->erase(cos->begin() + idx);
+        } else {
+          if (idx < 0) {
+            if (!cos) cos.emplace();
+            cos->push_back(CtrlO{std::string(PREFIXED_GLOBAL_SCHEDULER), std::nullopt});
+            idx = (int)cos->size() - 1;
+          }
+          std::sort(keep.begin(), keep.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+          std::vector<CO> cl;
+          for (auto& kv : keep) cl.push_back(CO{kv.first, std::move(kv.second)});
+          (*cos)[(size_t)idx].clusters = std::move(cl);
+        }
+        MV value;
+        if (cos) {
+          value = MV::arr();
+          for (const CtrlO& co : *cos) {
+            MV e = MV::obj();
+            e.set("controller", MV::str(co.controller));
+            MV cs;
+            if (co.clusters) {
+              cs = MV::arr();
+              for (const CO& c : *co.clusters) {
+                MV x = MV::obj();
+                x.set("clusterName", MV::str(c.cluster));
+                if (c.patches && !c.patches->empty()) {
+                  MV ps = MV::arr();
+                  for (const Patch& p : *c.patches) ps.a.push_back(patch_json(d, p));
+                  x.set("paths", std::move(ps));
+                }
+                cs.a.push_back(std::move(x));
+              }
+            }
+            e.set("clusters", std::move(cs));
+            value.a.push_back(std::move(e));
+          }
+        }
+        set_nested(obj, "spec", "overrides", std::move(value));
+        modified = true;
+      }
+    }
+    // the follower-scheduling and pod-unschedulable-threshold annotations (:660-690)
+    {
+      OMap<std::string> ann;
+      const int64_t am = Builder::string_map(d, root, "annotations");
+      if (am >= 0) {
+        const JV& o = d.v[am];
+        for (uint32_t k = 0; k < o.n; ++k) {
+          const sv key = d.str(d.kids[o.a + 2 * k]), val = d.str(d.kids[o.a + 2 * k + 1]);
+          bool found = false;
+          for (auto& kv : ann)
+            if (kv.first == key) {
+              kv.second.assign(val);
+              found = true;
+            }
+          if (!found) ann.emplace_back(std::string(key), std::string(val));
+        }
+      }
+      auto find = [&](sv key) -> std::string* {
+        for (auto& kv : ann)
+          if (kv.first == key) return &kv.second;
+        return nullptr;
+      };
+      bool changed = false;
+      const std::string fv = follower ? "true" : "false";
+      if (std::string* x = find(ENABLE_FOLLOWER_ANN); !x || *x != fv) {
+        if (x) *x = fv;
+        else ann.emplace_back(std::string(ENABLE_FOLLOWER_ANN), fv);
+        changed = true;
+      }
+      if (!threshold) {
+        for (size_t k = 0; k < ann.size(); ++k)
+          if (ann[k].first == POD_UNSCHEDULABLE_THRESHOLD_ANN) {
+            ann.erase(ann.begin() + (long)k);
+            changed = true;
+            break;
+          }
+      } else {
+        const std::string ds = duration_string(*threshold);
+        if (std::string* x = find(POD_UNSCHEDULABLE_THRESHOLD_ANN); !x || *x != ds) {
+          if (x) *x = ds;
+          else ann.emplace_back(std::string(POD_UNSCHEDULABLE_THRESHOLD_ANN), ds);
+          changed = true;
+        }
+      }
+      if (changed) {
+        MV m = MV::obj();
+        for (const auto& kv : ann) m.set(kv.first, MV::str(kv.second));
+        set_nested(obj, "metadata", "annotations", std::move(m));
+        modified = true;
+      }
+    }
+    return modified;
   }
 };
 
@@ -1506,3 +1997,111 @@ extern "C" const char* kad_units_message(const kad_units* u, int32_t i) {
 }
 
 extern "C" void kad_units_free(kad_units* u) { delete u; }
+
+struct kad_applied {
+  std::vector<int32_t> status;
+  std::vector<uint8_t> modified;
+  std::vector<int64_t> off{0};
+  std::vector<uint8_t> bytes;
+  std::vector<std::string> msg;
+};
+
+extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* objects, const kad_strs* cluster_names,
+                                 const int32_t* res_off, const int32_t* res_cluster, const int64_t* res_replicas,
+                                 const uint8_t* follower, const int64_t* threshold_ns, int threads, kad_applied** out) {
+  if (!tc || !objects || !cluster_names || !res_off || !out || objects->n < 0 ||
+      (objects->n > 0 && (!objects->off || !objects->bytes)) || cluster_names->n < 0 ||
+      (cluster_names->n > 0 && (!cluster_names->off || !cluster_names->bytes)))
+    return KAD_EINVAL;
+  *out = nullptr;
+  const int n = objects->n;
+  if (n > 0 && res_off[n] > 0 && (!res_cluster || !res_replicas)) return KAD_EINVAL;
+  for (int i = 0; i < n; ++i)
+    if (res_off[i] < 0 || res_off[i + 1] < res_off[i]) return KAD_EINVAL;
+  for (int32_t k = 0; n > 0 && k < res_off[n]; ++k)
+    if (res_cluster[k] < 0 || res_cluster[k] >= cluster_names->n) return KAD_EINVAL;
+  try {
+    auto R = std::make_unique<kad_applied>();
+    if (threads <= 0) threads = 1 << 20;
+    auto text = [](const kad_strs* s, int i) {
+      return sv(reinterpret_cast<const char*>(s->bytes) + s->off[i], (size_t)(s->off[i + 1] - s->off[i]));
+    };
+    Applier A{*tc, "/"};
+    {
+      const std::string path = tc->replicas_spec ? tc->replicas_spec : "";
+      std::string slash;
+      size_t a = 0;
+      for (size_t i = 0; i <= path.size(); ++i)
+        if (i == path.size() || path[i] == '.') {
+          if (i > a) slash += (slash.empty() ? "" : "/") + path.substr(a, i - a);
+          a = i + 1;
+        }
+      A.replicas_slash = "/" + slash;
+    }
+    R->status.assign((size_t)n, KAD_APPLY_OK);
+    R->modified.assign((size_t)n, 0);
+    R->msg.assign((size_t)n, std::string());
+    std::vector<std::string> texts((size_t)n);
+    parallel_for(n, threads, [&](int lo, int hi) {
+      JDoc d;
+      for (int i = lo; i < hi; ++i) {
+        const sv t = text(objects, i);
+        try {
+          uint32_t root;
+          if (!parse(t, d, &root) || d.v[root].t != J_OBJ) fail(KAD_APPLY_BAD_JSON, "object: not a JSON object");
+          std::vector<std::string> clusters;
+          OMap<int64_t> desired;
+          for (int32_t k = res_off[i]; k < res_off[i + 1]; ++k) {
+            std::string name(text(cluster_names, res_cluster[k]));
+            if (res_replicas[k] >= 0) desired.emplace_back(name, res_replicas[k]);
+            clusters.push_back(std::move(name));
+          }
+          std::sort(clusters.begin(), clusters.end());
+          clusters.erase(std::unique(clusters.begin(), clusters.end()), clusters.end());
+          MV obj = mv_of(d, root, false);
+          std::optional<int64_t> th;
+          if (threshold_ns && threshold_ns[i] != INT64_MIN) th = threshold_ns[i];
+          const bool mod = A.apply(d, root, obj, clusters, desired, follower && follower[i], th);
+          R->modified[(size_t)i] = mod ? 1 : 0;
+          if (mod) emit(obj, texts[(size_t)i]);
+        } catch (const Fail& f) {
+          R->status[(size_t)i] = f.status;
+          R->msg[(size_t)i] = f.msg;
+        }
+      }
+    }, 64);
+    for (int i = 0; i < n; ++i) {
+      if (R->modified[(size_t)i]) R->bytes.insert(R->bytes.end(), texts[(size_t)i].begin(), texts[(size_t)i].end());
+      else {
+        const sv t = text(objects, i);  // unchanged (or failed): the object as it was
+        R->bytes.insert(R->bytes.end(), t.begin(), t.end());
+      }
+      R->off.push_back((int64_t)R->bytes.size());
+    }
+    *out = R.release();
+    return KAD_OK;
+  } catch (const std::bad_alloc&) {
+    return KAD_ENOMEM;
+  } catch (...) {
+    return KAD_EINVAL;
+  }
+}
+
+extern "C" int kad_applied_view(const kad_applied* a, const int32_t** status, const uint8_t** modified, kad_strs* texts) {
+  if (!a) return KAD_EINVAL;
+  if (status) *status = a->status.data();
+  if (modified) *modified = a->modified.data();
+  if (texts) {
+    texts->n = (int32_t)a->status.size();
+    texts->off = a->off.data();
+    texts->bytes = a->bytes.data();
+  }
+  return KAD_OK;
+}
+
+extern "C" const char* kad_applied_message(const kad_applied* a, int32_t i) {
+  if (!a || i < 0 || (size_t)i >= a->msg.size()) return "";
+  return a->msg[(size_t)i].c_str();
+}
+
+extern "C" void kad_applied_free(kad_applied* a) { delete a; }

@@ -380,3 +380,117 @@ def test_columns_pack_like_python_units():
     nb = K.NativePacker(snap).pack(fwk, got.cols)
     pb = Batch(snap, fwk, units)
     assert nb.blob.tobytes() == pb.blob.tobytes()
+
+
+# ------------------------------------------------------------------ f3: kad_apply_results
+NAMES = ["a", "b", "c", "d", "e", "ü", "cluster-1", "z"]
+
+
+def python_apply(ftc, objs, res_off, res_cluster, res_rep, follower, thresholds):
+    out = []
+    for i, obj in enumerate(objs):
+        o = json.loads(obj) if isinstance(obj, (str, bytes)) else json.loads(json.dumps(obj))
+        sc = {NAMES[res_cluster[k]]: (None if res_rep[k] < 0 else int(res_rep[k]))
+              for k in range(res_off[i], res_off[i + 1])}
+        try:
+            mod = O.apply_scheduling_result(ftc, o, T.ScheduleResult(sc), bool(follower[i]), thresholds[i])
+            out.append((K.APPLY_OK, mod, o))
+        except O.ObjectError:
+            out.append((K.APPLY_ERROR, False, None))
+        except O.GoPanic:
+            out.append((K.APPLY_PANIC, False, None))
+    return out
+
+
+def _results(rng, n, dup_share=0.4):
+    off, cl, rep = [0], [], []
+    for _ in range(n):
+        k = rng.choice([0, 0, 1, 2, 3, 4])
+        ids = rng.sample(range(len(NAMES)), k)
+        dup = rng.random() < dup_share
+        for c in ids:
+            cl.append(c)
+            rep.append(-1 if dup else rng.randint(0, 9))
+        off.append(len(cl))
+    return off, cl, rep
+
+
+def assert_apply_same(ftc, objs, off, cl, rep, follower, thresholds, threads=0):
+    st, mod, texts, msgs = K.apply_results(ftc, objs, NAMES, off, cl, rep, follower, thresholds, threads=threads)
+    want = python_apply(ftc, objs, off, cl, rep, follower, thresholds)
+    for i, (s, m, o) in enumerate(want):
+        assert st[i] == s, (i, st[i], s, msgs[i], objs[i])
+        if s != K.APPLY_OK:
+            continue
+        assert mod[i] == m, (i, objs[i])
+        if m:
+            assert json.loads(texts[i]) == o, (i, objs[i], texts[i])
+        else:
+            assert texts[i] == (objs[i] if isinstance(objs[i], bytes)
+                                else json.dumps(objs[i], separators=(",", ":")).encode())
+    return st, mod, texts
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_apply_results_match_python(seed):
+    rng = random.Random(100 + seed)
+    policies = [_policy(rng, f"p{i}", False) for i in range(4)]
+    objs = [_object(rng, policies) for _ in range(500)]
+    for o in objs[::7]:  # the result already applied: nothing to change on the second pass
+        o["metadata"]["annotations"][O.ENABLE_FOLLOWER_SCHEDULING_ANNOTATION] = "true"
+    for o in objs[::11]:
+        o["spec"].pop("template", None)
+        if rng.random() < 0.5:
+            o.pop("spec")
+    for o in objs[::13]:
+        o["spec"] = None  # SetOverrides on a nil spec panics; SetPlacementClusterNames fails
+    off, cl, rep = _results(rng, len(objs))
+    follower = [rng.random() < 0.7 for _ in objs]
+    thresholds = [rng.choice([None, None, 90 * 10**9, 1500, 10**9 + 1]) for _ in objs]
+    st, mod, texts = assert_apply_same(DEPLOY, objs, off, cl, rep, follower, thresholds)
+    assert {K.APPLY_OK, K.APPLY_ERROR} <= set(st.tolist())
+    assert mod.any() and not mod.all()
+    # a second pass over the applied objects (mostly no change; the reference is not idempotent where a
+    # non-number replicas override of a cluster outside the result survives the first pass) — still equal
+    ok = [i for i in range(len(objs)) if st[i] == K.APPLY_OK]
+    again = [texts[i] for i in ok]
+    off2, cl2, rep2 = [0], [], []
+    for i in ok:
+        cl2 += cl[off[i]:off[i + 1]]
+        rep2 += rep[off[i]:off[i + 1]]
+        off2.append(len(cl2))
+    st2, mod2, _ = assert_apply_same(DEPLOY, again, off2, cl2, rep2, [follower[i] for i in ok],
+                                     [thresholds[i] for i in ok])
+    assert (st2 == K.APPLY_OK).all() and mod2.mean() < 0.1
+
+
+def test_applied_objects_schedule_as_current_clusters():
+    """The unit the next reconcile builds from an applied object sees the result as its current clusters."""
+    rng = random.Random(9)
+    pol = {"metadata": {"name": "p"}, "spec": {"schedulingMode": "Divide"}}
+    lab = {O.CLUSTER_PROPAGATION_POLICY_NAME_LABEL: "p"}
+    objs = [{"metadata": {"name": f"o{i}", "labels": lab}, "spec": {"template": {"spec": {"replicas": 5}}}}
+            for i in range(50)]
+    off, cl, rep = _results(rng, len(objs), dup_share=0.3)
+    st, mod, texts, _ = K.apply_results(DEPLOY, objs, NAMES, off, cl, rep)
+    assert (st == K.APPLY_OK).all()
+    got = K.units_from_objects(DEPLOY, texts, [pol])
+    units = K.to_units(got.cols)
+    for i in range(len(objs)):
+        want = {NAMES[cl[k]]: (None if rep[k] < 0 else rep[k]) for k in range(off[i], off[i + 1])}
+        assert (units[got.unit_index[i]].current_clusters or {}) == want
+
+
+def test_marshal_matches_go_encoding():
+    """Keys sorted bytewise, HTML-escaped strings, U+2028/2029 escaped, float64 as Go formats it."""
+    obj = {"metadata": {"name": "x<y>&z  \x01é"}, "b": 1, "a": [0.1, 1e21, 1e-7, 3.0, 123456789.0, -0.0],
+           "spec": {"template": {}, "overrides": [{"controller": GS, "clusters": [
+               {"clusterName": "a", "paths": [{"path": "/spec/replicas", "value": 2}]},
+               {"clusterName": "b", "paths": [{"path": "/x", "value": {"k": 1e300, "j": [1, 2.5]}}]}]}]}}
+    st, mod, texts, _ = K.apply_results(DEPLOY, [obj], NAMES, [0, 1], [0], [4])
+    assert st[0] == K.APPLY_OK and mod[0]
+    t = texts[0].decode()
+    assert t.startswith('{"a":[0.1,1e+21,1e-7,3,123456789,-0],"b":1,"metadata":{"annotations":')
+    assert '"name":"x\\u003cy\\u003e\\u0026z\\u2028\\u2029\\u0001é"' in t
+    assert '{"clusterName":"b","paths":[{"path":"/x","value":{"j":[1,2.5],"k":1e+300}}]}' in t
+    assert '{"clusterName":"a","paths":[{"path":"/spec/replicas","value":4}]}' in t
