@@ -48,8 +48,12 @@ class ReconcileOutcome:
 class BatchReconciler:
     """Scheduler.reconcile for a batch of federated objects of one FederatedTypeConfig."""
 
-    def __init__(self, type_config: O.FederatedTypeConfig, ctx: Optional[Context] = None, device: int = 0):
+    def __init__(self, type_config: O.FederatedTypeConfig, ctx: Optional[Context] = None, device: int = 0,
+                 native_objects: bool = True):
+        """``native_objects``: SchedulingUnits built and results applied by the library (kad_units_from_objects /
+        kad_apply_results, include/kad_objects.h) over the objects' JSON, instead of objects.py per object."""
         self.type_config = type_config
+        self.native_objects = native_objects
         self.ctx = ctx if ctx is not None else Context(device)
         self.hasher = TriggerHasher(self.ctx)
         self.scheduler = BatchScheduler(self.ctx)
@@ -120,6 +124,10 @@ class BatchReconciler:
             else:
                 to_schedule.append(i)
 
+        if self.native_objects:
+            self._schedule_and_apply_native(objs, to_schedule, ctx_pol, ctx_prof, profiles, clusters, out)
+            return out  # type: ignore[return-value]
+
         # schedule :445-521 — units grouped by framework, one GPU batch per framework
         results: Dict[int, T.ScheduleResult] = {}
         groups: Dict[Optional[str], List[Tuple[int, T.SchedulingUnit]]] = {}
@@ -166,3 +174,103 @@ class BatchReconciler:
                 continue
             out[i] = ReconcileOutcome(STATUS_ALL_OK, "scheduled", True, modified, r)
         return out  # type: ignore[return-value]
+
+    # ------------------------------------------------------------------ the native object path
+    @staticmethod
+    def _apply_params(pol):
+        """(follower, threshold ns) of reconcile :291-308; raises like the reference."""
+        if pol is None:
+            return False, None
+        threshold = None
+        am = pol.spec.auto_migration
+        if am is not None:
+            if am.when.pod_unschedulable_for is None:
+                raise O.GoPanic("invalid memory address or nil pointer dereference")  # :302
+            threshold = O.parse_duration(am.when.pod_unschedulable_for)
+        return not pol.spec.disable_follower_scheduling, threshold
+
+    def _schedule_and_apply_native(self, objs, to_schedule, ctx_pol, ctx_prof, profiles, clusters, out):
+        """The schedule and apply stages over the objects' JSON: per framework one kad_units_from_objects, one
+        packed GPU batch, then one kad_apply_results for every object with a result."""
+        import json
+
+        from . import columns as K
+        from .results import to_schedule_result_cols
+
+        results: Dict[int, T.ScheduleResult] = {}
+        groups: Dict[Optional[str], List[int]] = {}
+        for i in to_schedule:
+            if ctx_pol[i] is None:
+                results[i] = T.ScheduleResult({})  # :454-467 no policy: schedule to no clusters
+                continue
+            groups.setdefault(ctx_prof[i], []).append(i)
+        pol_index: Dict[int, int] = {}
+        pol_json: List[dict] = []
+        for i in to_schedule:
+            if ctx_pol[i] is not None and id(ctx_pol[i]) not in pol_index:
+                pol_index[id(ctx_pol[i])] = len(pol_json)
+                pol_json.append(O.policy_to_json(ctx_pol[i]))
+        pol_text = [json.dumps(p) for p in pol_json]
+        names: List[str] = []
+        for prof_name, members in groups.items():
+            try:
+                fwk = self._framework(profiles.get(prof_name) if prof_name else None)
+            except F.FrameworkError as e:
+                for i in members:
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "framework-error", error=str(e))
+                continue
+            built = K.units_from_objects(self.type_config, [json.dumps(objs[i]) for i in members], pol_text,
+                                         [pol_index[id(ctx_pol[i])] for i in members])
+            ok = []
+            for k, i in enumerate(members):
+                if built.status[k] == K.OBJ_OK:
+                    ok.append((i, int(built.unit_index[k])))
+                else:
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "unit-error", error=built.messages[k])
+            if not ok:
+                continue
+            res, snap = self.scheduler.schedule_columns(fwk, built.cols, clusters)
+            names = snap.names
+            for i, w in ok:
+                r = to_schedule_result_cols(res, w, built.cols, names)
+                if isinstance(r, T.ScheduleError):
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "schedule-error", error=str(r))
+                else:
+                    results[i] = r
+
+        # reconcile :291-308 + persistSchedulingResult → applySchedulingResult, one native pass
+        todo, follower, threshold = [], [], []
+        for i, r in sorted(results.items()):
+            try:
+                f, t = self._apply_params(ctx_pol[i])
+            except (O.ObjectError, O.GoPanic) as e:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=r, error=str(e))
+                continue
+            todo.append(i)
+            follower.append(f)
+            threshold.append(t)
+        if not todo:
+            return
+        table = list(names)
+        at = {n: k for k, n in enumerate(table)}
+        off, cl, rep = [0], [], []
+        for i in todo:
+            for n, v in (results[i].suggested_clusters or {}).items():
+                if n not in at:  # a sticky result's cluster that left the snapshot
+                    at[n] = len(table)
+                    table.append(n)
+                cl.append(at[n])
+                rep.append(-1 if v is None else v)
+            off.append(len(cl))
+        st, modified, texts, msgs = K.apply_results(self.type_config, [json.dumps(objs[i]) for i in todo], table,
+                                                    off, cl, rep, follower, threshold)
+        for k, i in enumerate(todo):
+            r = results[i]
+            if st[k] != K.APPLY_OK:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=r, error=msgs[k])
+                continue
+            if modified[k]:  # the object is updated in place, as the reference mutates its deep copy
+                new = json.loads(texts[k])
+                objs[i].clear()
+                objs[i].update(new)
+            out[i] = ReconcileOutcome(STATUS_ALL_OK, "scheduled", True, bool(modified[k]), r)

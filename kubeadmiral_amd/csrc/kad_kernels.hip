@@ -2908,6 +2908,10 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
         }
       }
     }
+    int wabs = 0;  // sum of |weight|: bounds |raw affinity score|
+#pragma unroll
+    for (int t = 0; t < ROW_MAX_TERMS; ++t) wabs += t < n_terms ? (wt[t] < 0 ? -wt[t] : wt[t]) : 0;
+    const bool apack = s_aff && wabs <= 4095;
     auto raw_aff = [&](uint32_t c) {
       int af = 0;
 #pragma unroll
@@ -2990,12 +2994,15 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
 #pragma unroll
           for (int tw = 0; tw < TFOLD_MAX_TW; ++tw)
             if (tw < TW) tc += popc64(pn[u][tw] & ~tpn[tw]);
-        key[j] = (uint32_t)x | ((uint32_t)tc << 16);
-        ttmax = tc > ttmax ? tc : ttmax;
+        int af = 0;
         if (s_aff) {  // |raw| <= 2^20 (wider units were deferred above)
-          const int af = raw_aff(c);
+          af = raw_aff(c);
           amax = af > amax ? af : amax;
         }
+        // x <= 300 (three resource scores), tc <= 256 (TW <= 4); the raw affinity score rides along when the
+        // unit's weights keep it within 13 signed bits, so the normalisation does not recompute it
+        key[j] = (uint32_t)x | ((uint32_t)tc << 10) | (apack ? ((uint32_t)af & 0x1FFFu) << 19 : 0u);
+        ttmax = tc > ttmax ? tc : ttmax;
       }
     }
     KAD_PT(t1b);
@@ -3010,10 +3017,10 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     int mn = INT32_MAX, mx = INT32_MIN;
     for (int j = tid; j < n; j += ROW_THREADS) {
       const uint32_t x = key[j];
-      int t = (int)(x & 0xFFFFu);
-      if (s_tt) t += ttmax == 0 ? 100 : 100 - (int)small_quot(100 * (int)(x >> 16), ttmax);
+      int t = (int)(x & 0x3FFu);
+      if (s_tt) t += ttmax == 0 ? 100 : 100 - (int)small_quot(100 * (int)((x >> 10) & 0x1FFu), ttmax);
       if (s_aff) {
-        const int af = raw_aff(idx[j]);
+        const int af = apack ? ((int32_t)x >> 19) : raw_aff(idx[j]);
         const int num = 100 * af;
         t += amax == 0 ? af : (num >= 0 && num < (1 << 24) ? (int)small_quot(num, amax) : num / amax);
       }

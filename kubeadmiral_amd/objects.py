@@ -135,6 +135,52 @@ class PropagationPolicy:
         return PropagationPolicy(meta.get("name", ""), meta.get("namespace", ""), int(meta.get("generation", 0)), spec)
 
 
+def policy_to_json(pol: "PropagationPolicy") -> dict:
+    """The (Cluster)PropagationPolicy as the API object the informer holds (metadata + spec JSON): the inverse of
+    :meth:`PropagationPolicy.from_json` (``from_json(policy_to_json(p)) == p``), for the native object path
+    (include/kad_objects.h), which reads policies as JSON."""
+    sp = pol.spec
+    spec: dict = {}
+    if sp.scheduling_profile:
+        spec["schedulingProfile"] = sp.scheduling_profile
+    if sp.scheduling_mode:
+        spec["schedulingMode"] = sp.scheduling_mode
+    if sp.sticky_cluster:
+        spec["stickyCluster"] = True
+    if sp.cluster_selector is not None:
+        spec["clusterSelector"] = dict(sp.cluster_selector)
+    if sp.cluster_affinity is not None:
+        spec["clusterAffinity"] = [t.to_json() for t in sp.cluster_affinity]
+    if sp.tolerations is not None:
+        spec["tolerations"] = [t.to_json() for t in sp.tolerations]
+    if sp.max_clusters is not None:
+        spec["maxClusters"] = sp.max_clusters
+    if sp.placements is not None:
+        pls = []
+        for p in sp.placements:
+            pr = {"minReplicas": p.preferences.min_replicas}
+            if p.preferences.max_replicas is not None:
+                pr["maxReplicas"] = p.preferences.max_replicas
+            if p.preferences.weight is not None:
+                pr["weight"] = p.preferences.weight
+            pls.append({"cluster": p.cluster, "preferences": pr})
+        spec["placement"] = pls
+    if sp.disable_follower_scheduling:
+        spec["disableFollowerScheduling"] = True
+    if sp.auto_migration is not None:
+        when = {}
+        if sp.auto_migration.when.pod_unschedulable_for is not None:
+            when["podUnschedulableFor"] = sp.auto_migration.when.pod_unschedulable_for
+        spec["autoMigration"] = {"when": when,
+                                 "keepUnschedulableReplicas": sp.auto_migration.keep_unschedulable_replicas}
+    if sp.replica_rescheduling is not None:
+        spec["replicaRescheduling"] = {"avoidDisruption": sp.replica_rescheduling.avoid_disruption}
+    meta = {"name": pol.name, "generation": pol.generation}
+    if pol.namespace:
+        meta["namespace"] = pol.namespace
+    return {"metadata": meta, "spec": spec}
+
+
 @dataclass
 class FederatedTypeConfig:
     """The FederatedTypeConfig fields the scheduler reads (types_federatedtypeconfig.go)."""

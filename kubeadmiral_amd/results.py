@@ -73,3 +73,16 @@ def to_schedule_result(res: BatchResult, w: int, unit: T.SchedulingUnit, names: 
     if st != ST_OK:
         raise RuntimeError(f"unit {w}: invalid status {st}")
     return T.ScheduleResult({names[c]: (None if r < 0 else int(r)) for c, r in pairs})
+
+
+def to_schedule_result_cols(res: BatchResult, w: int, cols, names: List[str]
+                            ) -> Union[T.ScheduleResult, T.ScheduleError]:
+    """:func:`to_schedule_result` for unit w of a columnar batch (``columns.SUColumns``): a sticky unit keeps its
+    CurrentClusters, read from the columns."""
+    if int(res.status[w]) == ST_STICKY:
+        C = cols.cols
+        S = cols.strings()
+        a, b = int(C["cur_off"][w]), int(C["cur_off"][w + 1])
+        cur = {S[C["cur_name"][i]]: (int(C["cur_rep"][i]) if C["cur_has_rep"][i] else None) for i in range(a, b)}
+        return T.ScheduleResult(cur)  # sticky: CurrentClusters is non-empty (generic_scheduler.go:98-104)
+    return to_schedule_result(res, w, None, names)

@@ -447,3 +447,16 @@ class BatchScheduler:
         batch = Batch(snap, fwk, units)
         res = self.ctx.run(fwk, batch)
         return [to_schedule_result(res, w, su, snap.names) for w, su in enumerate(units)]
+
+    def schedule_columns(self, fwk: Framework, cols, clusters: List[T.FederatedCluster]):
+        """The same for units already in columns (``columns.SUColumns``, e.g. from ``columns.units_from_objects``):
+        the native packer, one GPU batch. Returns (BatchResult, snapshot)."""
+        from .columns import NativePacker
+
+        snap = self.set_clusters(clusters)
+        pk = getattr(self, "_packer", None)
+        if pk is None or pk.snap is not snap or getattr(self, "_packer_fp", None) != snap.fingerprint:
+            pk = self._packer = NativePacker(snap)  # the packer interns against the snapshot's vocabulary
+            self._packer_fp = snap.fingerprint
+        batch = pk.pack(fwk, cols)
+        return self.ctx.run(fwk, batch), snap

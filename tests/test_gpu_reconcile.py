@@ -57,7 +57,8 @@ def _expected(ftc, objs, pols_by_key, clusters):
     return objs, outs
 
 
-def test_batch_reconcile_matches_per_object_path():
+@pytest.mark.parametrize("native", [True, False], ids=["native-objects", "python-objects"])
+def test_batch_reconcile_matches_per_object_path(native):
     from kubeadmiral_amd.controller import BatchReconciler
 
     ftc, clusters, objs, pols = synth.gen_trigger_workload(np.random.default_rng(5), 400, 16, n_policies=8)
@@ -72,7 +73,7 @@ def test_batch_reconcile_matches_per_object_path():
     objs[5]["metadata"]["labels"][O.PROPAGATION_POLICY_NAME_LABEL] = "missing"
     want_objs, want = _expected(ftc, objs, by_key, clusters)
 
-    rec = BatchReconciler(ftc)
+    rec = BatchReconciler(ftc, native_objects=native)
     got = rec.reconcile(objs, by_key, clusters)
     for i, (g, (stage, r)) in enumerate(zip(got, want)):
         assert g.stage == stage, i
@@ -91,7 +92,8 @@ def test_batch_reconcile_matches_per_object_path():
     assert all(g.stage in ("scheduled", "policy-not-found") for g in third)
 
 
-def test_same_length_list_with_changed_label_reschedules():
+@pytest.mark.parametrize("native", [True, False], ids=["native-objects", "python-objects"])
+def test_same_length_list_with_changed_label_reschedules(native):
     """A NEW list object of the same length whose only change is a cluster label: the trigger hash must
     change (schedulingtriggers.go:132-134 hashes cluster labels), so every object is rescheduled."""
     from kubeadmiral_amd.controller import BatchReconciler
@@ -102,7 +104,7 @@ def test_same_length_list_with_changed_label_reschedules():
         if p.spec.auto_migration is not None:
             p.spec.auto_migration.when.pod_unschedulable_for = "2m"
         by_key[(p.namespace, p.name)] = p
-    rec = BatchReconciler(ftc)
+    rec = BatchReconciler(ftc, native_objects=native)
     rec.reconcile(objs, by_key, clusters)
     same = [copy.deepcopy(c) for c in clusters]  # equal content, new objects
     assert all(g.stage == "unchanged" for g in rec.reconcile(objs, by_key, same))
