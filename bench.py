@@ -569,10 +569,20 @@ def emit(out: dict, cfg: str):
     out["detail"] = write_full(out, cfg)
     lines = []
     for k, v in (out.get("extra") or {}).items():
-        s = json.dumps(compact_line(v, headline=False))
+        c = compact_line(v, headline=False)
+        s = json.dumps(c)
+        # over the budget: shed the least useful fields first, keeping roofline and cpu_baseline
+        for path in (("end_to_end",), ("data",), ("config", "stage_ms"), ("roofline", "stages"),
+                     ("roofline", "algorithmic_bytes_per_launch")):
+            if len(s) <= EXTRA_MAX:
+                break
+            tgt = c
+            for key in path[:-1]:
+                tgt = tgt.get(key) if isinstance(tgt.get(key), dict) else {}
+            tgt.pop(path[-1], None)
+            s = json.dumps(c)
         if len(s) > EXTRA_MAX:
-            s = json.dumps({f: compact_line(v, headline=False)[f] for f in ("metric", "value", "unit", "ms_per_step",
-                                                                            "config", "parity")})
+            s = json.dumps({f: c[f] for f in ("metric", "value", "unit", "ms_per_step", "config", "parity") if f in c})
         lines.append(s)
     head = json.dumps(compact_line(out))
     if len(head) > HEADLINE_MAX:  # never let the headline outgrow the driver's capture
