@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define KAD_ABI_VERSION 1
+#define KAD_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- errors */
 #define KAD_OK 0
@@ -207,10 +207,10 @@ enum kad_batch_array {
   KAD_B_CUR_REP,       /* i64[]    replicas (nil resolved to DesiredReplicas, rsp.go:119-126) */
   KAD_B_PREF_OFF,      /* i32[W+1] per-cluster Weights/MinReplicas/MaxReplicas/EstimatedCapacity */
   KAD_B_PREF_ID,       /* i32[]    snapshot cluster id (sorted)                           */
-  KAD_B_PREF_W,        /* i64[]    Weights[cluster]                                       */
-  KAD_B_PREF_MIN,      /* i64[]    MinReplicas[cluster]                                   */
-  KAD_B_PREF_MAX,      /* i64[]    MaxReplicas[cluster]                                   */
-  KAD_B_PREF_CAP,      /* i64[]    EstimatedCapacity[cluster] (only entries >= 0)         */
+  KAD_B_PREF_W,        /* i64[]    Weights[cluster]           (i32[]: KAD_BATCH_NARROW_PREFS) */
+  KAD_B_PREF_MIN,      /* i64[]    MinReplicas[cluster]       (i32[]: KAD_BATCH_NARROW_PREFS) */
+  KAD_B_PREF_MAX,      /* i64[]    MaxReplicas[cluster]       (i32[]: KAD_BATCH_NARROW_PREFS) */
+  KAD_B_PREF_CAP,      /* i64[]    EstimatedCapacity[cluster] (only entries >= 0; i32[] narrow) */
   KAD_B_PREF_FLAGS,    /* u32[]    bit0 has weight, bit1 has max, bit2 has cap            */
   KAD_B_KEY_OFF,       /* i32[W+1] su.Key() bytes (types.go:123-128)                      */
   KAD_B_KEY,           /* u8[]                                                            */
@@ -224,6 +224,12 @@ enum kad_batch_array {
 #define KAD_PREF_HAS_MAX 2u
 #define KAD_PREF_HAS_CAP 4u
 
+/* kad_batch_header.flags */
+#define KAD_BATCH_NARROW_PREFS 1u /* every value of every unit's Weights, MinReplicas, MaxReplicas and
+                                     (AutoMigration units) EstimatedCapacity map fits int32: the four
+                                     KAD_B_PREF_{W,MIN,MAX,CAP} columns are i32[] (the packers decide it
+                                     from the input maps, so both produce the same bytes)             */
+
 typedef struct kad_batch_header {
   uint32_t magic;
   uint32_t abi_version;
@@ -236,6 +242,8 @@ typedef struct kad_batch_header {
   uint32_t packed_filter_mask;  /* profile the output bounds were sized for:  */
   int32_t packed_select_plugin; /* kad_schedule rejects any other profile     */
   int32_t n_reqs;       /* NR: distinct requirements in KAD_B_REQ                         */
+  uint32_t flags;       /* KAD_BATCH_*                                                    */
+  uint32_t reserved;    /* 0                                                              */
   uint64_t total_bytes;
   uint64_t snapshot_fingerprint;
   uint64_t off[KAD_B_NARRAYS];

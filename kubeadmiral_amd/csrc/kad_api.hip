@@ -258,6 +258,9 @@ static int validate_batch(kad_ctx* c, const void* blob, size_t nbytes, const kad
       !k.extent(KAD_B_TOLSET, Wu, 4, "tolset") || !k.extent(KAD_B_TOL_ALL, (uint64_t)NT * TW, 8, "tol_all") ||
       !k.extent(KAD_B_TOL_PNS, (uint64_t)NT * TW, 8, "tol_pns") || !k.extent(KAD_B_OUT_OFF, Wu + 1, 8, "out_off"))
     return KAD_EINVAL;
+  if ((h.flags & ~KAD_BATCH_NARROW_PREFS) != 0 || h.reserved != 0)
+    return fail(c, KAD_EINVAL, "batch: unknown header flags");
+  const uint32_t pvb = (h.flags & KAD_BATCH_NARROW_PREFS) ? 4u : 8u;  // bytes per preference value
   int64_t n_s, n_f, n_sp, n_pl, n_cur, n_pref, n_key, n_req;
   if (!k.csr(KAD_B_SREQ_OFF, W, KAD_B_SREQ_ID, 4, "sreq", &n_s) || !k.extent(KAD_B_SREQ_VAL, n_s, 8, "sreq_val") ||
       !k.csr(KAD_B_FPROG_OFF, W, KAD_B_FPROG, 4, "fprog", &n_f) ||
@@ -265,8 +268,8 @@ static int validate_batch(kad_ctx* c, const void* blob, size_t nbytes, const kad
       !k.csr(KAD_B_PLACE_OFF, W, KAD_B_PLACE, 4, "place", &n_pl) ||
       !k.csr(KAD_B_CUR_OFF, W, KAD_B_CUR_ID, 4, "cur", &n_cur) || !k.extent(KAD_B_CUR_REP, n_cur, 8, "cur_rep") ||
       !k.csr(KAD_B_PREF_OFF, W, KAD_B_PREF_ID, 4, "pref", &n_pref) ||
-      !k.extent(KAD_B_PREF_W, n_pref, 8, "pref_w") || !k.extent(KAD_B_PREF_MIN, n_pref, 8, "pref_min") ||
-      !k.extent(KAD_B_PREF_MAX, n_pref, 8, "pref_max") || !k.extent(KAD_B_PREF_CAP, n_pref, 8, "pref_cap") ||
+      !k.extent(KAD_B_PREF_W, n_pref, pvb, "pref_w") || !k.extent(KAD_B_PREF_MIN, n_pref, pvb, "pref_min") ||
+      !k.extent(KAD_B_PREF_MAX, n_pref, pvb, "pref_max") || !k.extent(KAD_B_PREF_CAP, n_pref, pvb, "pref_cap") ||
       !k.extent(KAD_B_PREF_FLAGS, n_pref, 4, "pref_flags") || !k.csr(KAD_B_KEY_OFF, W, KAD_B_KEY, 1, "key", &n_key) ||
       !k.csr(KAD_B_REQ_OFF, NR, KAD_B_REQ, 4, "req", &n_req))
     return KAD_EINVAL;
@@ -1041,10 +1044,15 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   b.cur_rep = at<int64_t>(base, h.off, KAD_B_CUR_REP);
   b.pref_off = at<int32_t>(base, h.off, KAD_B_PREF_OFF);
   b.pref_id = at<int32_t>(base, h.off, KAD_B_PREF_ID);
-  b.pref_w = at<int64_t>(base, h.off, KAD_B_PREF_W);
-  b.pref_min = at<int64_t>(base, h.off, KAD_B_PREF_MIN);
-  b.pref_max = at<int64_t>(base, h.off, KAD_B_PREF_MAX);
-  b.pref_cap = at<int64_t>(base, h.off, KAD_B_PREF_CAP);
+  b.pref_narrow = (h.flags & KAD_BATCH_NARROW_PREFS) ? 1 : 0;
+  b.pref_w = b.pref_narrow ? nullptr : at<int64_t>(base, h.off, KAD_B_PREF_W);
+  b.pref_min = b.pref_narrow ? nullptr : at<int64_t>(base, h.off, KAD_B_PREF_MIN);
+  b.pref_max = b.pref_narrow ? nullptr : at<int64_t>(base, h.off, KAD_B_PREF_MAX);
+  b.pref_cap = b.pref_narrow ? nullptr : at<int64_t>(base, h.off, KAD_B_PREF_CAP);
+  b.pref_w32 = b.pref_narrow ? at<int32_t>(base, h.off, KAD_B_PREF_W) : nullptr;
+  b.pref_min32 = b.pref_narrow ? at<int32_t>(base, h.off, KAD_B_PREF_MIN) : nullptr;
+  b.pref_max32 = b.pref_narrow ? at<int32_t>(base, h.off, KAD_B_PREF_MAX) : nullptr;
+  b.pref_cap32 = b.pref_narrow ? at<int32_t>(base, h.off, KAD_B_PREF_CAP) : nullptr;
   b.pref_fl = at<uint32_t>(base, h.off, KAD_B_PREF_FLAGS);
   b.key_off = at<int32_t>(base, h.off, KAD_B_KEY_OFF);
   b.key = at<uint8_t>(base, h.off, KAD_B_KEY);

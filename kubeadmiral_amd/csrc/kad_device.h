@@ -81,7 +81,9 @@ struct BatchDev {
   const int32_t *fprog_off, *fprog, *sprog_off, *sprog, *place_off, *place, *cur_off, *cur_id;
   const int64_t* cur_rep;
   const int32_t *pref_off, *pref_id;
-  const int64_t *pref_w, *pref_min, *pref_max, *pref_cap;
+  const int64_t *pref_w, *pref_min, *pref_max, *pref_cap;          // wide batches (null when narrow)
+  const int32_t *pref_w32, *pref_min32, *pref_max32, *pref_cap32;  // KAD_BATCH_NARROW_PREFS batches
+  int pref_narrow;
   const uint32_t* pref_fl;
   const int32_t* key_off;
   const uint8_t* key;

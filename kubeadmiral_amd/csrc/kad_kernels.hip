@@ -3387,8 +3387,18 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
       if (pi >= 0) {
         // all five columns in one round trip (pi is in bounds), flags select after
         const uint32_t pf = b.pref_fl[pi];
-        const int64_t pw = b.pref_w[pi], pmx = b.pref_max[pi], pcp = b.pref_cap[pi];
-        e.mn = b.pref_min[pi];
+        int64_t pw, pmx, pcp;
+        if (b.pref_narrow) {  // i32 columns (KAD_BATCH_NARROW_PREFS)
+          pw = b.pref_w32[pi];
+          pmx = b.pref_max32[pi];
+          pcp = b.pref_cap32[pi];
+          e.mn = b.pref_min32[pi];
+        } else {
+          pw = b.pref_w[pi];
+          pmx = b.pref_max[pi];
+          pcp = b.pref_cap[pi];
+          e.mn = b.pref_min[pi];
+        }
         if (pf & KAD_PREF_HAS_WEIGHT) e.w = pw;
         if (pf & KAD_PREF_HAS_MAX) {
           e.fl |= EF_HAS_MAX;

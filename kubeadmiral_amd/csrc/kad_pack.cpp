@@ -1240,30 +1240,58 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   auto& o_cur = X.o_cur;
   auto& o_pref = X.o_pref;
   auto& o_key = X.o_key;
-  if (!csr_off(n_sreq, o_sreq) || !csr_off(n_fp, o_fp) || !csr_off(n_sp, o_sp) || !csr_off(n_place, o_place) ||
-      !csr_off(n_cur, o_cur) || !csr_off(n_pref, o_pref) || !csr_off(n_key, o_key))
-    return P->fail(KAD_EINVAL, "CSR array exceeds 2^31 entries; split the batch");
   auto& o_out = X.o_out;
   o_out.resize((size_t)W + 1);
-  o_out[0] = 0;
   int64_t max_row = 0;
-  for (int w = 0; w < W; w++) {
-    o_out[w + 1] = o_out[w] + out_len[w];
-    max_row = std::max(max_row, out_len[w]);
+  // the eight prefix sums are independent: one worker each
+  bool csr_ok[7] = {true, true, true, true, true, true, true};
+  {
+    const std::vector<int32_t>* lens[7] = {&n_sreq, &n_fp, &n_sp, &n_place, &n_cur, &n_pref, &n_key};
+    std::vector<int32_t>* offs[7] = {&o_sreq, &o_fp, &o_sp, &o_place, &o_cur, &o_pref, &o_key};
+    parallel_for(8, threads, [&](int a, int b) {
+      for (int q = a; q < b; q++) {
+        if (q < 7) {
+          csr_ok[q] = csr_off(*lens[q], *offs[q]);
+          continue;
+        }
+        o_out[0] = 0;
+        for (int w = 0; w < W; w++) {
+          o_out[w + 1] = o_out[w] + out_len[w];
+          max_row = std::max(max_row, out_len[w]);
+        }
+      }
+    }, 1);
   }
+  for (bool ok : csr_ok)
+    if (!ok) return P->fail(KAD_EINVAL, "CSR array exceeds 2^31 entries; split the batch");
   auto& req_off = X.req_off;
   req_off.resize((size_t)NR + 1);
   req_off[0] = 0;
   for (int r = 0; r < NR; r++) req_off[r + 1] = req_off[r] + (int32_t)(reqs[r].size() / 4);
   const size_t nS = (size_t)o_sreq[W], nF = (size_t)o_fp[W], nSP = (size_t)o_sp[W], nPL = (size_t)o_place[W],
                nC = (size_t)o_cur[W], nP = (size_t)o_pref[W], nK = (size_t)o_key[W], nRQ = (size_t)req_off[NR];
+  // KAD_BATCH_NARROW_PREFS: every value of the input preference maps fits int32 (pack.py applies the same
+  // rule to the same maps, so both packers choose the same layout)
+  bool narrow = true;
+  {
+    auto fits = [](const int64_t* v, int64_t n) {
+      for (int64_t i = 0; i < n; i++)
+        if (v[i] < INT32_MIN || v[i] > INT32_MAX) return false;
+      return true;
+    };
+    narrow = fits(su->wt_val, su->wt_off[W]) && fits(su->min_val, su->min_off[W]) && fits(su->max_val, su->max_off[W]);
+    for (int w = 0; w < W && narrow; w++)
+      if (su->flags[w] & KAD_SU_HAS_AUTO_MIGRATION)
+        narrow = fits(su->cap_val + su->cap_off[w], su->cap_off[w + 1] - su->cap_off[w]);
+  }
+  const size_t pv = narrow ? 4 : 8;  // bytes per preference value
   const size_t sizes[KAD_B_NARRAYS] = {
       4 * (size_t)W, 4 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 4 * (size_t)W,
       8 * (size_t)NT * TW, 8 * (size_t)NT * TW,
       4 * ((size_t)W + 1), 4 * nS, 8 * nS,
       4 * ((size_t)W + 1), 4 * nF, 4 * ((size_t)W + 1), 4 * nSP,
       4 * ((size_t)W + 1), 4 * nPL, 4 * ((size_t)W + 1), 4 * nC, 8 * nC,
-      4 * ((size_t)W + 1), 4 * nP, 8 * nP, 8 * nP, 8 * nP, 8 * nP, 4 * nP,
+      4 * ((size_t)W + 1), 4 * nP, pv * nP, pv * nP, pv * nP, pv * nP, 4 * nP,
       4 * ((size_t)W + 1), nK, 8 * ((size_t)W + 1), 4 * ((size_t)NR + 1), 4 * nRQ};
   kad_batch_header h;
   std::memset(&h, 0, sizeof(h));
@@ -1284,6 +1312,7 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   h.packed_filter_mask = prof->filter_mask;
   h.packed_select_plugin = prof->select_plugin;
   h.n_reqs = NR;
+  h.flags = narrow ? KAD_BATCH_NARROW_PREFS : 0u;
   h.total_bytes = total;
   h.snapshot_fingerprint = P->fingerprint;
   uint8_t* base = P->reserve(total);
@@ -1343,10 +1372,15 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   int32_t* cur_id = reinterpret_cast<int32_t*>(A(KAD_B_CUR_ID));
   int64_t* cur_rep = reinterpret_cast<int64_t*>(A(KAD_B_CUR_REP));
   int32_t* pref_id = reinterpret_cast<int32_t*>(A(KAD_B_PREF_ID));
-  int64_t* pref_w = reinterpret_cast<int64_t*>(A(KAD_B_PREF_W));
-  int64_t* pref_min = reinterpret_cast<int64_t*>(A(KAD_B_PREF_MIN));
-  int64_t* pref_max = reinterpret_cast<int64_t*>(A(KAD_B_PREF_MAX));
-  int64_t* pref_cap = reinterpret_cast<int64_t*>(A(KAD_B_PREF_CAP));
+  uint8_t* const pref_col[4] = {A(KAD_B_PREF_W), A(KAD_B_PREF_MIN), A(KAD_B_PREF_MAX), A(KAD_B_PREF_CAP)};
+  // entry j's weight, min, max, capacity, in the batch's width
+  auto put_pref = [&](int64_t j, int64_t wv, int64_t mn, int64_t mx, int64_t cp) {
+    const int64_t v[4] = {wv, mn, mx, cp};
+    for (int q = 0; q < 4; q++) {
+      if (narrow) reinterpret_cast<int32_t*>(pref_col[q])[j] = (int32_t)v[q];
+      else reinterpret_cast<int64_t*>(pref_col[q])[j] = v[q];
+    }
+  };
   uint32_t* pref_fl = reinterpret_cast<uint32_t*>(A(KAD_B_PREF_FLAGS));
   uint8_t* keyb = A(KAD_B_KEY);
   struct PrefEntry {
@@ -1452,10 +1486,8 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
           const uint8_t m = dm[c];
           dm[c] = 0;
           pref_id[j] = c;
-          pref_w[j] = (m & 1) ? dv[c] : 0;
-          pref_min[j] = (m & 2) ? dv[(size_t)C + c] : 0;
-          pref_max[j] = (m & 4) ? dv[2 * (size_t)C + c] : 0;
-          pref_cap[j] = (m & 8) ? dv[3 * (size_t)C + c] : 0;
+          put_pref(j, (m & 1) ? dv[c] : 0, (m & 2) ? dv[(size_t)C + c] : 0, (m & 4) ? dv[2 * (size_t)C + c] : 0,
+                   (m & 8) ? dv[3 * (size_t)C + c] : 0);
           pref_fl[j] = ((m & 1) ? KAD_PREF_HAS_WEIGHT : 0u) | ((m & 4) ? KAD_PREF_HAS_MAX : 0u) |
                        ((m & 8) ? KAD_PREF_HAS_CAP : 0u);
           j++;
@@ -1489,10 +1521,7 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
           }
         }
         pref_id[j] = c;
-        pref_w[j] = wv;
-        pref_min[j] = mn;
-        pref_max[j] = mx;
-        pref_cap[j] = cp;
+        put_pref(j, wv, mn, mx, cp);
         pref_fl[j] = fl;
         j++;
       }

@@ -25,6 +25,7 @@ from fractions import Fraction
 
 INT64_MIN = -(1 << 63)
 INT64_MAX = (1 << 63) - 1
+INT32_MIN, INT32_MAX = -(1 << 31), (1 << 31) - 1
 
 _BIN = {"Ki": 1 << 10, "Mi": 1 << 20, "Gi": 1 << 30, "Ti": 1 << 40, "Pi": 1 << 50, "Ei": 1 << 60}
 _DEC = {"n": Fraction(1, 10 ** 9), "u": Fraction(1, 10 ** 6), "m": Fraction(1, 10 ** 3), "": Fraction(1),

@@ -25,7 +25,7 @@ from . import k8s
 from . import types as T
 from .framework import ClusterAffinity, ClusterResourcesFit, Framework, PlacementFilter
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 ALIGN = 256
 
 # ---------------------------------------------------------------- header mirrors
@@ -40,6 +40,7 @@ S_ALLOC_CPU, S_ALLOC_MEM, S_USED_CPU, S_USED_MEM, S_ALLOC_SCALAR, S_USED_SCALAR,
 
 SNAPSHOT_MAGIC = 0x5344414B
 BATCH_MAGIC = 0x4241444B
+BATCH_NARROW_PREFS = 1  # kad_batch_header.flags KAD_BATCH_NARROW_PREFS
 
 W_DUPLICATE = 1 << 0
 W_STICKY = 1 << 1
@@ -76,7 +77,8 @@ class BatchHeader(ctypes.Structure):
                 ("n_clusters", ctypes.c_int32), ("n_taint_words", ctypes.c_int32), ("n_tolsets", ctypes.c_int32),
                 ("n_out_slots", ctypes.c_int64), ("max_row_slots", ctypes.c_int32),
                 ("packed_filter_mask", ctypes.c_uint32), ("packed_select_plugin", ctypes.c_int32),
-                ("n_reqs", ctypes.c_int32), ("total_bytes", ctypes.c_uint64),
+                ("n_reqs", ctypes.c_int32), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("total_bytes", ctypes.c_uint64),
                 ("snapshot_fingerprint", ctypes.c_uint64), ("off", ctypes.c_uint64 * B_NARRAYS)]
 
 
@@ -588,6 +590,7 @@ class Batch:
         sreq, fprog, sprog, place, cur_id, cur_rep, keys = [], [], [], [], [], [], []
         pref_id, pref_w, pref_min, pref_max, pref_cap, pref_fl = [], [], [], [], [], []
         out_len = np.zeros(W, np.int64)
+        narrow = True  # KAD_BATCH_NARROW_PREFS: every preference map value fits int32
         n_reqs = np.zeros(W, np.int64)
         n_tols = np.zeros(W, np.int64)
         select_max = fwk.select_plugin == 8
@@ -651,6 +654,8 @@ class Batch:
             ec = {}
             if am is not None:
                 ec = {n: v for n, v in (am.estimated_capacity or {}).items() if v >= 0}
+            for m in (su.weights, su.min_replicas, su.max_replicas, am.estimated_capacity if am is not None else None):
+                narrow = narrow and all(k8s.INT32_MIN <= v <= k8s.INT32_MAX for v in (m or {}).values())
             pn = set(su.weights or {}) | set(su.min_replicas or {}) | set(su.max_replicas or {}) | set(ec)
             prefs = sorted((snap.name_id[n], n) for n in pn if n in snap.name_id)
             pid, pw, pmin, pmax, pcap, pfl = [], [], [], [], [], []
@@ -709,10 +714,11 @@ class Batch:
         cur_off, cur_id_a = _csr(cur_id, np.int32)
         _, cur_rep_a = _csr(cur_rep, np.int64)
         pref_off, pref_id_a = _csr(pref_id, np.int32)
-        _, pref_w_a = _csr(pref_w, np.int64)
-        _, pref_min_a = _csr(pref_min, np.int64)
-        _, pref_max_a = _csr(pref_max, np.int64)
-        _, pref_cap_a = _csr(pref_cap, np.int64)
+        pdt = np.int32 if narrow else np.int64
+        _, pref_w_a = _csr(pref_w, pdt)
+        _, pref_min_a = _csr(pref_min, pdt)
+        _, pref_max_a = _csr(pref_max, pdt)
+        _, pref_cap_a = _csr(pref_cap, pdt)
         _, pref_fl_a = _csr(pref_fl, np.uint32)
         key_off, key_a = _csr(keys, np.uint8)
         req_off, req_a = _csr(comp.reqs, np.int32)
@@ -731,6 +737,7 @@ class Batch:
         hdr.packed_filter_mask = fwk.filter_mask
         hdr.packed_select_plugin = fwk.select_plugin
         hdr.n_reqs = len(comp.reqs)
+        hdr.flags = BATCH_NARROW_PREFS if narrow else 0
         hdr.snapshot_fingerprint = snap.fingerprint
         self.blob = _assemble(hdr, arrays)
         self.n_reqs = n_reqs

@@ -232,6 +232,23 @@ def make_config(config: str, scale: float = 1.0, seed: Optional[int] = None, W: 
 
 
 # ------------------------------------------------------------------- fuzz
+def widen_prefs(units, seed: int, share: float = 0.3):
+    """Push some preference-map values of ``units`` (in place) past int32 — weights, min / max replicas,
+    estimated capacities of 2^31 … 2^40 — so the packers choose the wide (i64) preference columns
+    (KAD_BATCH_NARROW_PREFS off). Returns the units."""
+    rng = np.random.default_rng(seed)
+    for su in units:
+        if rng.random() >= share:
+            continue
+        maps = [m for m in (su.weights, su.min_replicas, su.max_replicas,
+                            su.auto_migration.estimated_capacity if su.auto_migration is not None else None) if m]
+        for m in maps:
+            for k in list(m):
+                if rng.random() < 0.5 and m[k] is not None and m[k] >= 0:
+                    m[k] = int(m[k]) + int(rng.integers(1 << 31, 1 << 40))
+    return units
+
+
 def gen_fuzz(seed: int, W: int = 60, C: Optional[int] = None, n_taints: int = 9):
     """Small batch hitting every branch: all operators, invalid requirements, nil/empty terms, fields,
     sticky, current clusters, scalars, NoExecute on scheduled clusters, ties, weights/min/max/caps.

@@ -50,7 +50,8 @@ typedef struct {
   const int32_t *fprog_off, *fprog, *sprog_off, *sprog, *place_off, *place, *cur_off, *cur_id;
   const int64_t* cur_rep;
   const int32_t *pref_off, *pref_id;
-  const int64_t *pref_w, *pref_min, *pref_max, *pref_cap;
+  const void *pref_w, *pref_min, *pref_max, *pref_cap; /* i64[], or i32[] with KAD_BATCH_NARROW_PREFS */
+  int pref_narrow;
   const uint32_t* pref_fl;
   const int32_t* key_off;
   const uint8_t* key;
@@ -74,6 +75,11 @@ static int parse_snap(const void* blob, snap_t* s) {
   return 0;
 }
 
+/* preference column q's entry k in the batch's width */
+static inline int64_t pref_val(const batch_t* b, const void* col, int k) {
+  return b->pref_narrow ? (int64_t)((const int32_t*)col)[k] : ((const int64_t*)col)[k];
+}
+
 static int parse_batch(const void* blob, batch_t* b) {
   const kad_batch_header* h = (const kad_batch_header*)blob;
   if (h->magic != KAD_BATCH_MAGIC) return -1;
@@ -91,6 +97,7 @@ static int parse_batch(const void* blob, batch_t* b) {
   b->pref_w = PTR(blob, h, KAD_B_PREF_W); b->pref_min = PTR(blob, h, KAD_B_PREF_MIN);
   b->pref_max = PTR(blob, h, KAD_B_PREF_MAX); b->pref_cap = PTR(blob, h, KAD_B_PREF_CAP);
   b->pref_fl = PTR(blob, h, KAD_B_PREF_FLAGS);
+  b->pref_narrow = (h->flags & KAD_BATCH_NARROW_PREFS) != 0;
   b->key_off = PTR(blob, h, KAD_B_KEY_OFF); b->key = PTR(blob, h, KAD_B_KEY); b->out_off = PTR(blob, h, KAD_B_OUT_OFF);
   b->req_off = PTR(blob, h, KAD_B_REQ_OFF); b->req = PTR(blob, h, KAD_B_REQ);
   return 0;
@@ -563,10 +570,10 @@ static int replica_scheduling(const snap_t* s, const batch_t* b, int w, const in
     for (int k = b->pref_off[w]; k < b->pref_off[w + 1]; k++) {
       if (b->pref_id[k] != c) continue;
       uint32_t pf = b->pref_fl[k];
-      weight[i] = (pf & KAD_PREF_HAS_WEIGHT) ? b->pref_w[k] : 0;
-      minr[i] = b->pref_min[k];
-      if (pf & KAD_PREF_HAS_MAX) { has_max[i] = 1; maxr[i] = b->pref_max[k]; }
-      if (pf & KAD_PREF_HAS_CAP) { has_cap[i] = 1; capv[i] = b->pref_cap[k]; }
+      weight[i] = (pf & KAD_PREF_HAS_WEIGHT) ? pref_val(b, b->pref_w, k) : 0;
+      minr[i] = pref_val(b, b->pref_min, k);
+      if (pf & KAD_PREF_HAS_MAX) { has_max[i] = 1; maxr[i] = pref_val(b, b->pref_max, k); }
+      if (pf & KAD_PREF_HAS_CAP) { has_cap[i] = 1; capv[i] = pref_val(b, b->pref_cap, k); }
     }
     cur[i] = 0;
     for (int k = b->cur_off[w]; k < b->cur_off[w + 1]; k++) if (b->cur_id[k] == c) cur[i] = b->cur_rep[k];

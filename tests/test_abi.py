@@ -19,7 +19,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     lib = runtime.load_library()
-    assert lib.kad_abi_version() == 1
+    assert lib.kad_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -33,5 +33,6 @@ def test_header_layout_matches_packer():
     from kubeadmiral_amd import pack
     assert ctypes.sizeof(pack.SnapshotHeader) == 48 + 8 * pack.S_NARRAYS
     assert pack.BatchHeader.n_out_slots.offset == 24
-    assert pack.BatchHeader.total_bytes.offset == 48
-    assert pack.BatchHeader.off.offset == 64
+    assert pack.BatchHeader.flags.offset == 48
+    assert pack.BatchHeader.total_bytes.offset == 56
+    assert pack.BatchHeader.off.offset == 72

@@ -99,3 +99,16 @@ def test_c_select_rows_match_python_sort():
         go_sort_slice(items, lambda a, b: a[1] > b[1])
         want = [i for i, _ in items[:min(k, n)]]
         assert ref.select_row(scores, k) == want
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_c_oracle_matches_python_oracle_wide_prefs(seed):
+    """The C oracle reads the i64 preference columns of a wide batch (values past int32) as the object oracle
+    computes them."""
+    from kubeadmiral_amd import pack
+    clusters, units = synth.gen_fuzz(700 + seed, W=50)
+    synth.widen_prefs(units, seed, share=0.5)
+    fwk = synth.fuzz_framework(seed)
+    assert pack.header_of(pack.Batch(pack.Snapshot(clusters), fwk, units).blob, pack.BatchHeader).flags == 0
+    bad = compare(clusters, units, fwk)
+    assert not bad, bad[:3]

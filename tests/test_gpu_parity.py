@@ -173,6 +173,17 @@ def test_fuzz_gpu_equals_c_oracle(ctx, seed):
     assert_same(res, c_oracle(snap, batch, fwk), f"fuzz seed {seed}")
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_wide_prefs_gpu_equals_c_oracle(ctx, seed):
+    """Preference values past int32: the planner reads the i64 columns (KAD_BATCH_NARROW_PREFS off)."""
+    clusters, units = synth.gen_fuzz(2000 + seed, W=80)
+    synth.widen_prefs(units, seed, share=0.5)
+    fwk = synth.fuzz_framework(seed)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert pack.header_of(batch.blob, pack.BatchHeader).flags == 0
+    assert_same(res, c_oracle(snap, batch, fwk), f"wide fuzz seed {seed}")
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_fuzz_gpu_equals_python_oracle(ctx, seed):
     from test_c_oracle import py_results, same

@@ -375,3 +375,17 @@ def test_columns_slice_packs_like_its_units(cfg, W, C):
         got = CO.NativePacker(snap).pack(fwk, part)
         want = pack.Batch(snap, fwk, units[lo:hi])
         assert np.array_equal(got.blob, want.blob), (lo, hi)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_wide_preference_values_blob_identical(seed):
+    """Preference values past int32 keep the i64 columns (KAD_BATCH_NARROW_PREFS off); both packers agree on the
+    layout and the bytes, and batches within int32 get the narrow columns."""
+    clusters, units = synth.gen_fuzz(300 + seed, W=80)
+    snap, fwk = pack.Snapshot(clusters), synth.fuzz_framework(seed)
+    narrow = _same(snap, fwk, units)
+    assert pack.header_of(narrow.blob, pack.BatchHeader).flags == pack.BATCH_NARROW_PREFS
+    synth.widen_prefs(units, seed, share=0.5)
+    wide = _same(snap, fwk, units)
+    assert pack.header_of(wide.blob, pack.BatchHeader).flags == 0
+    assert wide.blob.nbytes > narrow.blob.nbytes
