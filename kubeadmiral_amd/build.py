@@ -27,13 +27,21 @@ def _inputs():
         os.path.join(os.path.dirname(HERE), "include", h) for h in ("kad_sched.h", "kad_pack.h", "kad_objects.h")]
 
 
+# host code that no kernel launch depends on (the object formats either side of the batch): left out of the
+# profile hash, so that editing it does not invalidate the kernels' PMC profiles
+HOST_ONLY = ("kad_objects.cpp", "kad_objects.h")
+
+
 def source_hash() -> str:
-    """16 hex digits of SHA-256 over libkad.so's sources and headers: profiles/pmc_<cfg>.json records the
-    hash of the code it was collected on, and bench.py uses its counters only when they match."""
+    """16 hex digits of SHA-256 over the sources and headers the measured kernels depend on (libkad.so's,
+    except ``HOST_ONLY``): profiles/pmc_<cfg>.json records the hash of the code it was collected on, and
+    bench.py uses its counters only when they match."""
     import hashlib
 
     h = hashlib.sha256()
     for p in _inputs():
+        if os.path.basename(p) in HOST_ONLY:
+            continue
         with open(p, "rb") as f:
             h.update(os.path.basename(p).encode() + b"\0" + f.read())
     return h.hexdigest()[:16]

@@ -1371,6 +1371,7 @@ void emit(const MV& m, std::string& out) {
     case J_STR: emit_str(m.s, out); break;
     case J_NUM:
       if (m.isint && m.fits) out += std::to_string(m.i);
+      else if (!std::isfinite(m.d)) fail(KAD_APPLY_BAD_JSON, "object: a number out of float64 range");  // Go rejects it
       else emit_f64(m.d, out);
       break;
     case J_ARR:

@@ -494,3 +494,11 @@ def test_marshal_matches_go_encoding():
     assert '"name":"x\\u003cy\\u003e\\u0026z\\u2028\\u2029\\u0001é"' in t
     assert '{"clusterName":"b","paths":[{"path":"/x","value":{"j":[1,2.5],"k":1e+300}}]}' in t
     assert '{"clusterName":"a","paths":[{"path":"/spec/replicas","value":4}]}' in t
+
+
+def test_apply_refuses_numbers_outside_float64():
+    """A number past float64 (1e400) cannot be in an object Go decoded (json.Unmarshal fails on it); the native
+    edit refuses to marshal one rather than write invalid JSON."""
+    text = b'{"metadata": {"name": "o"}, "spec": {"template": {}, "x": 1e400}}'
+    st, mod, texts, _ = K.apply_results(DEPLOY, [text], NAMES, [0, 1], [0], [3])
+    assert st[0] == K.APPLY_BAD_JSON and texts[0] == text
