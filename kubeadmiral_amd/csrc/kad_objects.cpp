@@ -2065,9 +2065,11 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
           const bool mod = A.apply(d, root, obj, clusters, desired, follower && follower[i], th);
           R->modified[(size_t)i] = mod ? 1 : 0;
           if (mod) emit(obj, texts[(size_t)i]);
-        } catch (const Fail& f) {
+        } catch (const Fail& f) {  // the object comes back as it was
           R->status[(size_t)i] = f.status;
           R->msg[(size_t)i] = f.msg;
+          R->modified[(size_t)i] = 0;
+          texts[(size_t)i].clear();
         }
       }
     }, 64);
