@@ -27,6 +27,8 @@ string cannot hold, are written as the U+FFFD Go's decoder puts there) — what
 from __future__ import annotations
 
 import json
+import json.encoder
+import re
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 INT64_MIN, INT64_MAX = -(1 << 63), (1 << 63) - 1
@@ -215,7 +217,31 @@ def unmarshal(text: str, t: T, cur=None):
 _HEX = "0123456789abcdef"
 
 
+def _escape_table():
+    t = {c: "\\u00" + _HEX[c >> 4] + _HEX[c & 0xF] for c in range(0x20)}  # control characters
+    t.update({ord("\n"): "\\n", ord("\r"): "\\r", ord("\t"): "\\t", ord('"'): '\\"', ord("\\"): "\\\\"})
+    t.update({ord(ch): "\\u00" + _HEX[ord(ch) >> 4] + _HEX[ord(ch) & 0xF] for ch in "<>&"})
+    t.update({0x2028: "\\u2028", 0x2029: "\\u2029"})
+    t.update({c: "\ufffd" for c in range(0xD800, 0xE000)})  # a Go string holds U+FFFD there
+    return t
+
+
+_ESCAPES = _escape_table()
+
+
+# where Python's C string encoder (json.encoder.encode_basestring) and Go's differ: HTML characters, U+2028/9,
+# surrogates, and \b / \f (Go 1.19 writes \u0008 / \u000c)
+_GO_DIFF = re.compile("[<>&\u2028\u2029\ud800-\udfff\x08\x0c]")
+_c_encode = json.encoder.encode_basestring
+
+
 def _enc_str(s: str, out: List[str]) -> None:
+    """encodeState.string with HTML escaping (_enc_str_ref: the per-character restatement it equals,
+    tests/test_objects.py): Python's C encoder where the two agree, one str.translate elsewhere."""
+    out.append(_c_encode(s) if _GO_DIFF.search(s) is None else '"' + s.translate(_ESCAPES) + '"')
+
+
+def _enc_str_ref(s: str, out: List[str]) -> None:
     out.append('"')
     for ch in s:
         c = ord(ch)

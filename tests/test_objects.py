@@ -318,3 +318,18 @@ def test_trigger_hash_format():
                  b'"ephemeralStorage":0,"scalarResources":null},"policyName":"","policyGeneration":0,'
                  b'"clusterLabels":[],"clusterTaints":[],"clusterAPIResourceTypes":[]}')
     assert O.format_trigger_hash(fnv1_32(b)) == OT.trigger_hash({}, 0, None, [])
+
+
+def test_go_string_encoder_equals_its_restatement():
+    """gojson._enc_str (the C encoder where Go agrees, a translate table elsewhere) == the per-character
+    restatement of encodeState.string, on strings over every class of character."""
+    rng = random.Random(17)
+    pool = [chr(c) for c in range(0x80)] + [" ", " ", "\ud800", "\udfff", "\ud83d", "é", "😀", "�"]
+    for i in range(20000):
+        s = "".join(rng.choice(pool) for _ in range(rng.randint(0, 24)))
+        if i % 2:  # the fast path: nothing Go and Python encode differently
+            s = "".join(ch for ch in s if ch not in "<>&\x08\x0c  " and not 0xD800 <= ord(ch) <= 0xDFFF)
+        a, b = [], []
+        J._enc_str(s, a)
+        J._enc_str_ref(s, b)
+        assert a == ["".join(b)], repr(s)
