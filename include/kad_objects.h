@@ -106,6 +106,10 @@ int kad_apply_results(const kad_type_config* tc, const kad_strs* objects, const 
                       const uint8_t* follower, const int64_t* threshold_ns, int threads, kad_applied** out);
 /* Views into *a (valid until kad_applied_free): per object its status, whether it changed, and its text. */
 int kad_applied_view(const kad_applied* a, const int32_t** status, const uint8_t** modified, kad_strs* texts);
+/* The written fields alone, 3 strings per object (3i: spec.placements, 3i+1: spec.overrides, 3i+2:
+ * metadata.annotations): the field's new JSON value, "" where it was not written — what a caller holding the
+ * object decoded (or sending a patch) needs instead of re-reading the whole text. */
+int kad_applied_fields(const kad_applied* a, kad_strs* fields);
 const char* kad_applied_message(const kad_applied* a, int32_t i);
 void kad_applied_free(kad_applied* a);
 

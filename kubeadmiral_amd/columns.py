@@ -648,18 +648,23 @@ def units_from_objects(type_config, objects: Sequence, policies: Sequence, polic
 APPLY_OK, APPLY_ERROR, APPLY_PANIC, APPLY_BAD_JSON = range(4)
 
 
+APPLY_FIELDS = (("spec", "placements"), ("spec", "overrides"), ("metadata", "annotations"))
+
+
 def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], res_off, res_cluster, res_replicas,
-                  follower=None, threshold_ns=None, threads: int = 0):
+                  follower=None, threshold_ns=None, threads: int = 0, with_fields: bool = False):
     """kad_apply_results: applySchedulingResult for a batch of objects (JSON texts or dicts) with results in
     kad_results_download's form (CSR of snapshot cluster ids, replicas -1 = nil). ``follower``: per object
     !DisableFollowerScheduling (default all True); ``threshold_ns``: per object the pod-unschedulable threshold
-    or None. Returns (status, modified, texts, messages): texts are the objects' new JSON (bytes)."""
+    or None. Returns (status, modified, texts, messages): texts are the objects' new JSON (bytes); with
+    ``with_fields`` also, per object, the new JSON of each of ``APPLY_FIELDS`` it wrote (None where not written)."""
     from .runtime import load_library
 
     L = load_library()
     P = ctypes.c_void_p
     L.kad_apply_results.argtypes = [P, P, P, P, P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
     L.kad_applied_view.argtypes = [P, P, P, P]
+    L.kad_applied_fields.argtypes = [P, P]
     L.kad_applied_message.argtypes = [P, ctypes.c_int32]
     L.kad_applied_message.restype = ctypes.c_char_p
     L.kad_applied_free.argtypes = [P]
@@ -710,6 +715,17 @@ def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], 
             data = ctypes.string_at(tx.bytes, int(off[-1])) if off[-1] else b""
             texts = [data[int(off[i]):int(off[i + 1])] for i in range(n)]
         msgs = [L.kad_applied_message(h, i).decode(errors="replace") if status[i] else "" for i in range(n)]
-        return status, modified, texts, msgs
+        if not with_fields:
+            return status, modified, texts, msgs
+        fs = KadStrs()
+        L.kad_applied_fields(h, ctypes.byref(fs))
+        fields = []
+        if n:
+            m = len(APPLY_FIELDS)
+            foff = np.ctypeslib.as_array(ctypes.cast(fs.off, ctypes.POINTER(ctypes.c_int64)), (m * n + 1,))
+            fdata = ctypes.string_at(fs.bytes, int(foff[-1])) if foff[-1] else b""
+            for i in range(n):
+                fields.append(tuple(fdata[int(foff[m * i + q]):int(foff[m * i + q + 1])] or None for q in range(m)))
+        return status, modified, texts, msgs, fields
     finally:
         L.kad_applied_free(h)

@@ -262,15 +262,15 @@ class BatchReconciler:
                 cl.append(at[n])
                 rep.append(-1 if v is None else v)
             off.append(len(cl))
-        st, modified, texts, msgs = K.apply_results(self.type_config, [json.dumps(objs[i]) for i in todo], table,
-                                                    off, cl, rep, follower, threshold)
+        st, modified, texts, msgs, fields = K.apply_results(self.type_config, [json.dumps(objs[i]) for i in todo],
+                                                            table, off, cl, rep, follower, threshold, with_fields=True)
         for k, i in enumerate(todo):
             r = results[i]
             if st[k] != K.APPLY_OK:
                 out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=r, error=msgs[k])
                 continue
-            if modified[k]:  # the object is updated in place, as the reference mutates its deep copy
-                new = json.loads(texts[k])
-                objs[i].clear()
-                objs[i].update(new)
+            if modified[k]:  # the written fields are set in place, as the reference mutates its deep copy
+                for (a, b), v in zip(K.APPLY_FIELDS, fields[k]):
+                    if v is not None:
+                        objs[i].setdefault(a, {})[b] = json.loads(v)
             out[i] = ReconcileOutcome(STATUS_ALL_OK, "scheduled", True, bool(modified[k]), r)

@@ -1467,7 +1467,9 @@ struct Applier {
   }
 
   // applySchedulingResult (scheduler.go:632-695) on the parsed object; true if anything changed
-  bool apply(const JDoc& d, uint32_t root, MV& obj, const std::vector<std::string>& clusters,
+  // the fields apply() wrote (bit 0 spec.placements, 1 spec.overrides, 2 metadata.annotations)
+  static constexpr int N_DELTA = 3;
+  bool apply(const JDoc& d, uint32_t root, MV& obj, uint32_t& wrote, const std::vector<std::string>& clusters,
              const OMap<int64_t>& desired, bool follower, std::optional<int64_t> threshold) {
     bool modified = false;
     bool spec_created = false;
@@ -1521,6 +1523,7 @@ struct Applier {
         }
         spec_created = obj.get("spec") == nullptr;
         set_nested(obj, "spec", "placements", std::move(value));
+        wrote |= 1u;
         modified = true;
       }
     }
@@ -1663,6 +1666,7 @@ struct Applier {
           }
         }
         set_nested(obj, "spec", "overrides", std::move(value));
+        wrote |= 2u;
         modified = true;
       }
     }
@@ -1714,6 +1718,7 @@ struct Applier {
         MV m = MV::obj();
         for (const auto& kv : ann) m.set(kv.first, MV::str(kv.second));
         set_nested(obj, "metadata", "annotations", std::move(m));
+        wrote |= 4u;
         modified = true;
       }
     }
@@ -2004,6 +2009,8 @@ struct kad_applied {
   std::vector<uint8_t> modified;
   std::vector<int64_t> off{0};
   std::vector<uint8_t> bytes;
+  std::vector<int64_t> doff{0};  // the written fields' new values, 3 per object
+  std::vector<uint8_t> dbytes;
   std::vector<std::string> msg;
 };
 
@@ -2043,6 +2050,7 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
     R->modified.assign((size_t)n, 0);
     R->msg.assign((size_t)n, std::string());
     std::vector<std::string> texts((size_t)n);
+    std::vector<std::string> deltas((size_t)n * Applier::N_DELTA);
     parallel_for(n, threads, [&](int lo, int hi) {
       JDoc d;
       for (int i = lo; i < hi; ++i) {
@@ -2062,14 +2070,22 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
           MV obj = mv_of(d, root, false);
           std::optional<int64_t> th;
           if (threshold_ns && threshold_ns[i] != INT64_MIN) th = threshold_ns[i];
-          const bool mod = A.apply(d, root, obj, clusters, desired, follower && follower[i], th);
+          uint32_t wrote = 0;
+          const bool mod = A.apply(d, root, obj, wrote, clusters, desired, follower && follower[i], th);
           R->modified[(size_t)i] = mod ? 1 : 0;
-          if (mod) emit(obj, texts[(size_t)i]);
+          if (mod) {
+            emit(obj, texts[(size_t)i]);
+            static const sv where[Applier::N_DELTA][2] = {{"spec", "placements"}, {"spec", "overrides"},
+                                                          {"metadata", "annotations"}};
+            for (int q = 0; q < Applier::N_DELTA; ++q)
+              if (wrote & (1u << q)) emit(*obj.get(where[q][0])->get(where[q][1]), deltas[(size_t)i * Applier::N_DELTA + q]);
+          }
         } catch (const Fail& f) {  // the object comes back as it was
           R->status[(size_t)i] = f.status;
           R->msg[(size_t)i] = f.msg;
           R->modified[(size_t)i] = 0;
           texts[(size_t)i].clear();
+          for (int q = 0; q < Applier::N_DELTA; ++q) deltas[(size_t)i * Applier::N_DELTA + q].clear();
         }
       }
     }, 64);
@@ -2080,6 +2096,11 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
         R->bytes.insert(R->bytes.end(), t.begin(), t.end());
       }
       R->off.push_back((int64_t)R->bytes.size());
+      for (int q = 0; q < Applier::N_DELTA; ++q) {
+        const std::string& x = deltas[(size_t)i * Applier::N_DELTA + q];
+        R->dbytes.insert(R->dbytes.end(), x.begin(), x.end());
+        R->doff.push_back((int64_t)R->dbytes.size());
+      }
     }
     *out = R.release();
     return KAD_OK;
@@ -2099,6 +2120,14 @@ extern "C" int kad_applied_view(const kad_applied* a, const int32_t** status, co
     texts->off = a->off.data();
     texts->bytes = a->bytes.data();
   }
+  return KAD_OK;
+}
+
+extern "C" int kad_applied_fields(const kad_applied* a, kad_strs* fields) {
+  if (!a || !fields) return KAD_EINVAL;
+  fields->n = (int32_t)(a->doff.size() - 1);
+  fields->off = a->doff.data();
+  fields->bytes = a->dbytes.data();
   return KAD_OK;
 }
 

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--objects", type=int, default=20000)
     ap.add_argument("--clusters", type=int, default=64)
     ap.add_argument("--out", default="")
+    ap.add_argument("--profile", default="", help="cProfile the native first pass into this file (top functions)")
     a = ap.parse_args()
     import numpy as np
 
@@ -40,8 +41,17 @@ def main():
         rec = BatchReconciler(ftc, native_objects=native)
         objs = copy.deepcopy(objs0)
         t0 = time.perf_counter()
+        if a.profile and native:
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
         got = rec.reconcile(objs, by_key, clusters)  # first pass: every object is scheduled and applied
         t1 = time.perf_counter()
+        if a.profile and native:
+            pr.disable()
+            with open(a.profile, "w") as f:
+                pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(25)
         again = rec.reconcile(objs, by_key, clusters)  # second pass: every trigger hash unchanged
         t2 = time.perf_counter()
         name = "native" if native else "python"

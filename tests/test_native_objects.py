@@ -502,3 +502,22 @@ def test_apply_refuses_numbers_outside_float64():
     text = b'{"metadata": {"name": "o"}, "spec": {"template": {}, "x": 1e400}}'
     st, mod, texts, _ = K.apply_results(DEPLOY, [text], NAMES, [0, 1], [0], [3])
     assert st[0] == K.APPLY_BAD_JSON and texts[0] == text
+
+
+def test_apply_fields_rebuild_the_object():
+    """The written fields alone (kad_applied_fields) set into the input object give the returned text's object."""
+    rng = random.Random(23)
+    policies = [_policy(rng, f"p{i}", False) for i in range(4)]
+    objs = [_object(rng, policies) for _ in range(300)]
+    off, cl, rep = _results(rng, len(objs))
+    st, mod, texts, _, fields = K.apply_results(DEPLOY, objs, NAMES, off, cl, rep, with_fields=True)
+    assert mod.any()
+    for i, o in enumerate(objs):
+        if st[i] != K.APPLY_OK or not mod[i]:
+            assert fields[i] == (None, None, None)
+            continue
+        o = json.loads(json.dumps(o))
+        for (a, b), v in zip(K.APPLY_FIELDS, fields[i]):
+            if v is not None:
+                o.setdefault(a, {})[b] = json.loads(v)
+        assert o == json.loads(texts[i]), i
