@@ -1,5 +1,5 @@
 #!/bin/bash
-# Host-code sanitizer run of the object formats (csrc/kad_objects.cpp: JSON parser, Go decoders, object edit):
+# Host-code sanitizer runs. First the object formats (csrc/kad_objects.cpp: JSON parser, Go decoders, object edit):
 # an ASan + UBSan build of that file alone (no HIP in it), driven by tests/test_native_objects.py's seeded
 # parity batches and malformed inputs through the same Python bindings. CPU only.
 set -e
@@ -27,3 +27,15 @@ print("sanitizers: clean")
 PY
 LD_PRELOAD="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)" ASAN_OPTIONS=detect_leaks=0 \
     UBSAN_OPTIONS=halt_on_error=1 python /tmp/kad_asan_run.py
+
+# and the whole library's host code (packer, upload checks, object formats) in an ASan build of libkad.so
+# (device code unchanged: -Xarch_host), under the CPU tests of the packer and the object formats
+python -c "from kubeadmiral_amd import build; build.build(force=True, out='/tmp/libkad_asan.so', extra=['-Xarch_host', '-fsanitize=address', '-Xarch_host', '-fno-omit-frame-pointer', '-shared-libasan'])"
+cat > /tmp/kad_asanplug.py <<'PY'
+from kubeadmiral_amd import runtime
+runtime._lib = None
+runtime.load_library("/tmp/libkad_asan.so")  # every later load_library() returns it
+PY
+PYTHONPATH=/tmp:. LD_PRELOAD="$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so)" \
+    ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0 \
+    python -m pytest -p kad_asanplug tests/test_native_pack.py tests/test_native_objects.py -x -q -p no:cacheprovider
