@@ -103,15 +103,39 @@ typedef struct kad_applied kad_applied;
 
 int kad_apply_results(const kad_type_config* tc, const kad_strs* objects, const kad_strs* cluster_names,
                       const int32_t* res_off, const int32_t* res_cluster, const int64_t* res_replicas,
-                      const uint8_t* follower, const int64_t* threshold_ns, int threads, kad_applied** out);
-/* Views into *a (valid until kad_applied_free): per object its status, whether it changed, and its text. */
-int kad_applied_view(const kad_applied* a, const int32_t** status, const uint8_t** modified, kad_strs* texts);
+                      const uint8_t* follower, const int64_t* threshold_ns, const kad_strs* trigger,
+                      const uint8_t* ann_only, int threads, kad_applied** out);
+/* `trigger` (may be NULL): per object the scheduling-trigger-hash annotation value the reconcile adds first
+ * (annotation.AddAnnotation, scheduler.go:407-417; "" none); `ann_only` (may be NULL): per object 1 = only that
+ * annotation, no result to apply (the reconcile's no-scheduling / error stages).
+ * Views into *a (valid until kad_applied_free): per object its status, applySchedulingResult's "modified",
+ * whether the text changed at all (modified, or the trigger annotation), and its text. */
+int kad_applied_view(const kad_applied* a, const int32_t** status, const uint8_t** modified, const uint8_t** changed,
+                     kad_strs* texts);
 /* The written fields alone, 3 strings per object (3i: spec.placements, 3i+1: spec.overrides, 3i+2:
  * metadata.annotations): the field's new JSON value, "" where it was not written — what a caller holding the
  * object decoded (or sending a patch) needs instead of re-reading the whole text. */
 int kad_applied_fields(const kad_applied* a, kad_strs* fields);
 const char* kad_applied_message(const kad_applied* a, int32_t i);
 void kad_applied_free(kad_applied* a);
+
+/* ------------------------------------------------------------ row f4 (host side)
+ * The object part of computeSchedulingTriggerHash (schedulingtriggers.go:106-134) for a batch of object texts —
+ * the bytes kad_trigger_prefixes_upload (kad_sched.h) takes — with MatchedPolicyKey + the policy lookup (or
+ * `policy_of`, as in kad_units_from_objects), per object its status (KAD_OBJ_OK, _POLICY_NOT_FOUND,
+ * _POLICY_ERROR, _BAD_JSON, _UNIT_ERROR = getReplicaCount's error), the matched policy (-1 none), the current
+ * value of the kubeadmiral.io/scheduling-trigger-hash annotation and the flags below. */
+#define KAD_TRIG_HAS_HASH 1u      /* the annotations (a string map) hold a trigger hash     */
+#define KAD_TRIG_NO_SCHEDULING 2u /* kubeadmiral.io/no-scheduling is set (non-empty)         */
+
+typedef struct kad_trigger_objs kad_trigger_objs;
+
+int kad_trigger_prefixes(const kad_type_config* tc, const kad_strs* objects, const kad_strs* policies,
+                         const int32_t* policy_of, int threads, kad_trigger_objs** out);
+int kad_trigger_objs_view(const kad_trigger_objs* t, const int32_t** status, const int32_t** policy_index,
+                          const uint8_t** flags, kad_strs* prefixes, kad_strs* current_hash);
+const char* kad_trigger_objs_message(const kad_trigger_objs* t, int32_t i);
+void kad_trigger_objs_free(kad_trigger_objs* t);
 
 #ifdef __cplusplus
 }

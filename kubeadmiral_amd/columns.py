@@ -651,19 +651,30 @@ APPLY_OK, APPLY_ERROR, APPLY_PANIC, APPLY_BAD_JSON = range(4)
 APPLY_FIELDS = (("spec", "placements"), ("spec", "overrides"), ("metadata", "annotations"))
 
 
-def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], res_off, res_cluster, res_replicas,
-                  follower=None, threshold_ns=None, threads: int = 0, with_fields: bool = False):
+class Applied:
+    """kad_apply_results' outputs: per object the status (``APPLY_*``), applySchedulingResult's "modified",
+    whether the text changed at all (modified, or the added trigger annotation), the new texts (bytes), the
+    failure messages and, per object, the new JSON of each of ``APPLY_FIELDS`` it wrote (None where not)."""
+
+    def __init__(self, status, modified, changed, texts, messages, fields):
+        self.status, self.modified, self.changed = status, modified, changed
+        self.texts, self.messages, self.fields = texts, messages, fields
+
+
+def apply_results_ex(type_config, objects: Sequence, cluster_names: Sequence[str], res_off, res_cluster, res_replicas,
+                     follower=None, threshold_ns=None, trigger: Optional[Sequence[Optional[str]]] = None,
+                     ann_only=None, threads: int = 0) -> Applied:
     """kad_apply_results: applySchedulingResult for a batch of objects (JSON texts or dicts) with results in
     kad_results_download's form (CSR of snapshot cluster ids, replicas -1 = nil). ``follower``: per object
     !DisableFollowerScheduling (default all True); ``threshold_ns``: per object the pod-unschedulable threshold
-    or None. Returns (status, modified, texts, messages): texts are the objects' new JSON (bytes); with
-    ``with_fields`` also, per object, the new JSON of each of ``APPLY_FIELDS`` it wrote (None where not written)."""
+    or None; ``trigger``: per object the scheduling-trigger-hash annotation to add first (None: none);
+    ``ann_only``: per object True = only that annotation (no result)."""
     from .runtime import load_library
 
     L = load_library()
     P = ctypes.c_void_p
-    L.kad_apply_results.argtypes = [P, P, P, P, P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
-    L.kad_applied_view.argtypes = [P, P, P, P]
+    L.kad_apply_results.argtypes = [P, P, P, P, P, P, P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
+    L.kad_applied_view.argtypes = [P, P, P, P, P]
     L.kad_applied_fields.argtypes = [P, P]
     L.kad_applied_message.argtypes = [P, ctypes.c_int32]
     L.kad_applied_message.restype = ctypes.c_char_p
@@ -682,6 +693,8 @@ def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], 
         return KadStrs(len(parts), off.ctypes.data, data.ctypes.data)
 
     so, sc = strs(ot), strs([c.encode() for c in cluster_names])
+    st_trig = strs([(t or "").encode() for t in trigger]) if trigger is not None else None
+    ao = np.ascontiguousarray(np.asarray(ann_only, U8)) if ann_only is not None else None
     ro = np.ascontiguousarray(res_off, I32)
     rc_ = np.ascontiguousarray(res_cluster, I32) if len(res_cluster) else np.zeros(1, I32)
     rr = np.ascontiguousarray(res_replicas, I64) if len(res_replicas) else np.zeros(1, I64)
@@ -698,25 +711,27 @@ def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], 
         type_config.group.encode(), type_config.version.encode(), type_config.kind.encode(),
         type_config.plural_name.encode(), 1 if type_config.namespaced else 0, type_config.replicas_spec.encode())),
         ctypes.byref(so), ctypes.byref(sc), ro.ctypes.data, rc_.ctypes.data, rr.ctypes.data, fo.ctypes.data,
-        th.ctypes.data, threads if threads > 0 else default_threads(), ctypes.byref(h))
+        th.ctypes.data, None if st_trig is None else ctypes.byref(st_trig), None if ao is None else ao.ctypes.data,
+        threads if threads > 0 else default_threads(), ctypes.byref(h))
     if rc != 0:
         raise RuntimeError(f"kad_apply_results failed ({rc})")
     try:
-        st, md = P(), P()
+        st, md, ch = P(), P(), P()
         tx = KadStrs()
-        L.kad_applied_view(h, ctypes.byref(st), ctypes.byref(md), ctypes.byref(tx))
-        status = np.ctypeslib.as_array(ctypes.cast(st, ctypes.POINTER(ctypes.c_int32)), (n,)).copy() if n else \
-            np.zeros(0, I32)
-        modified = np.ctypeslib.as_array(ctypes.cast(md, ctypes.POINTER(ctypes.c_uint8)), (n,)).astype(bool) if n \
-            else np.zeros(0, bool)
+        L.kad_applied_view(h, ctypes.byref(st), ctypes.byref(md), ctypes.byref(ch), ctypes.byref(tx))
+
+        def arr(ptr, ct, dt):
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), (n,)).astype(dt) if n else np.zeros(0, dt)
+
+        status = arr(st, ctypes.c_int32, I32)
+        modified = arr(md, ctypes.c_uint8, bool)
+        changed = arr(ch, ctypes.c_uint8, bool)
         texts = []
         if n:
             off = np.ctypeslib.as_array(ctypes.cast(tx.off, ctypes.POINTER(ctypes.c_int64)), (n + 1,))
             data = ctypes.string_at(tx.bytes, int(off[-1])) if off[-1] else b""
             texts = [data[int(off[i]):int(off[i + 1])] for i in range(n)]
         msgs = [L.kad_applied_message(h, i).decode(errors="replace") if status[i] else "" for i in range(n)]
-        if not with_fields:
-            return status, modified, texts, msgs
         fs = KadStrs()
         L.kad_applied_fields(h, ctypes.byref(fs))
         fields = []
@@ -726,6 +741,92 @@ def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], 
             fdata = ctypes.string_at(fs.bytes, int(foff[-1])) if foff[-1] else b""
             for i in range(n):
                 fields.append(tuple(fdata[int(foff[m * i + q]):int(foff[m * i + q + 1])] or None for q in range(m)))
-        return status, modified, texts, msgs, fields
+        return Applied(status, modified, changed, texts, msgs, fields)
     finally:
         L.kad_applied_free(h)
+
+
+def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], res_off, res_cluster, res_replicas,
+                  follower=None, threshold_ns=None, threads: int = 0, with_fields: bool = False):
+    """:func:`apply_results_ex` as (status, modified, texts, messages[, fields])."""
+    a = apply_results_ex(type_config, objects, cluster_names, res_off, res_cluster, res_replicas, follower,
+                         threshold_ns, threads=threads)
+    if with_fields:
+        return a.status, a.modified, a.texts, a.messages, a.fields
+    return a.status, a.modified, a.texts, a.messages
+
+
+# include/kad_objects.h KAD_TRIG_*
+TRIG_HAS_HASH, TRIG_NO_SCHEDULING = 1, 2
+
+
+class TriggerObjects:
+    """kad_trigger_prefixes: per object the status (``OBJ_*``), the matched policy index (-1 none), the flags
+    (``TRIG_*``), the trigger JSON's object part (bytes), the current trigger-hash annotation and messages."""
+
+    def __init__(self, status, policy_index, flags, prefixes, current_hash, messages):
+        self.status, self.policy_index, self.flags = status, policy_index, flags
+        self.prefixes, self.current_hash, self.messages = prefixes, current_hash, messages
+
+
+def trigger_prefixes(type_config, objects: Sequence, policies: Sequence, policy_of: Optional[Sequence[int]] = None,
+                     threads: int = 0) -> TriggerObjects:
+    """The object part of every object's scheduling-trigger JSON (objects.trigger_prefix) from the objects' texts,
+    natively, with the policy lookup of kad_units_from_objects."""
+    from .runtime import load_library
+
+    L = load_library()
+    P = ctypes.c_void_p
+    L.kad_trigger_prefixes.argtypes = [P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
+    L.kad_trigger_objs_view.argtypes = [P, P, P, P, P, P]
+    L.kad_trigger_objs_message.argtypes = [P, ctypes.c_int32]
+    L.kad_trigger_objs_message.restype = ctypes.c_char_p
+    L.kad_trigger_objs_free.argtypes = [P]
+    L.kad_trigger_objs_free.restype = None
+    keep: list = []
+    ot, pt = _texts(objects), _texts(policies)
+    n = len(ot)
+
+    def strs(parts):
+        off = np.zeros(len(parts) + 1, I64)
+        if parts:
+            off[1:] = np.cumsum([len(p) for p in parts])
+        data = np.frombuffer(b"".join(parts) or b"\0", U8).copy()
+        keep.extend([off, data])
+        return KadStrs(len(parts), off.ctypes.data, data.ctypes.data)
+
+    so, sp = strs(ot), strs(pt)
+    po = None
+    if policy_of is not None:
+        po = np.ascontiguousarray(policy_of, I32)
+        keep.append(po)
+    h = P()
+    rc = L.kad_trigger_prefixes(ctypes.byref(KadTypeConfig(
+        type_config.group.encode(), type_config.version.encode(), type_config.kind.encode(),
+        type_config.plural_name.encode(), 1 if type_config.namespaced else 0, type_config.replicas_spec.encode())),
+        ctypes.byref(so), ctypes.byref(sp), None if po is None else po.ctypes.data,
+        threads if threads > 0 else default_threads(), ctypes.byref(h))
+    if rc != 0:
+        raise RuntimeError(f"kad_trigger_prefixes failed ({rc})")
+    try:
+        st, pi, fl = P(), P(), P()
+        pf, ch = KadStrs(), KadStrs()
+        L.kad_trigger_objs_view(h, ctypes.byref(st), ctypes.byref(pi), ctypes.byref(fl), ctypes.byref(pf),
+                                ctypes.byref(ch))
+
+        def arr(ptr, ct, dt):
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), (n,)).astype(dt) if n else np.zeros(0, dt)
+
+        def split(s):
+            if not n:
+                return []
+            off = np.ctypeslib.as_array(ctypes.cast(s.off, ctypes.POINTER(ctypes.c_int64)), (n + 1,))
+            data = ctypes.string_at(s.bytes, int(off[-1])) if off[-1] else b""
+            return [data[int(off[i]):int(off[i + 1])] for i in range(n)]
+
+        status = arr(st, ctypes.c_int32, I32)
+        msgs = [L.kad_trigger_objs_message(h, i).decode(errors="replace") if status[i] else "" for i in range(n)]
+        return TriggerObjects(status, arr(pi, ctypes.c_int32, I32), arr(fl, ctypes.c_uint8, U8), split(pf),
+                              [x.decode(errors="surrogateescape") for x in split(ch)], msgs)
+    finally:
+        L.kad_trigger_objs_free(h)

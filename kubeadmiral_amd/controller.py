@@ -274,3 +274,158 @@ class BatchReconciler:
                     if v is not None:
                         objs[i].setdefault(a, {})[b] = json.loads(v)
             out[i] = ReconcileOutcome(STATUS_ALL_OK, "scheduled", True, bool(modified[k]), r)
+
+    # ------------------------------------------------------------------ the reconcile over JSON texts
+    def reconcile_texts(self, texts: Sequence, policies: Sequence, clusters: List[T.FederatedCluster],
+                        profiles: Optional[Dict[str, Optional[dict]]] = None
+                        ) -> Tuple[List[ReconcileOutcome], List[Optional[bytes]]]:
+        """:meth:`reconcile` over the federated objects' JSON texts (what an informer or a watch hands over),
+        with every per-object step native: the trigger JSON's object part (kad_trigger_prefixes), the trigger
+        hashes (kad_trigger_run), the SchedulingUnits (kad_units_from_objects), the schedule (kad_schedule) and
+        the write-back with the trigger annotation (kad_apply_results). ``policies``: the
+        (Cluster)PropagationPolicies' JSON; each object's policy is found through its labels as
+        MatchedPolicyKey does. Returns the outcomes (stages as :meth:`reconcile`, plus ``bad-json`` and
+        ``policy-error`` for texts that do not decode) and per object its new text — the deep copy the
+        reference goes on to Update (``scheduled``) or holds when it skips scheduling (``no-scheduling``) —
+        or None where the reconcile left the object as it was or dropped its copy on an error."""
+        import json
+
+        from . import columns as K
+        from .results import to_schedule_result_cols
+
+        profiles = profiles or {}
+        ot, pt = K._texts(texts), K._texts(policies)
+        n = len(ot)
+        out: List[Optional[ReconcileOutcome]] = [None] * n
+        new_text: List[Optional[bytes]] = [None] * n
+        pols: List[Optional[O.PropagationPolicy]] = []
+        for t in pt:  # a handful: decoded once for the profile name and the apply parameters
+            try:
+                pols.append(O.PropagationPolicy.from_json(json.loads(t)))
+            except Exception:  # noqa: BLE001 — the native lookup reports it as KAD_OBJ_POLICY_ERROR
+                pols.append(None)
+        tr = K.trigger_prefixes(self.type_config, ot, pt)
+
+        # prepareToSchedule :349-392 — policy and profile lookup, then the trigger JSON (:394-399)
+        hashed: List[int] = []
+        pol_of = tr.policy_index
+        for i in range(n):
+            st = int(tr.status[i])
+            if st == K.OBJ_POLICY_NOT_FOUND:
+                out[i] = ReconcileOutcome(STATUS_ALL_OK, "policy-not-found")
+                continue
+            if st == K.OBJ_BAD_JSON:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "bad-json", error=tr.messages[i])
+                continue
+            if st == K.OBJ_POLICY_ERROR:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "policy-error", error=tr.messages[i])
+                continue
+            p = pols[pol_of[i]] if pol_of[i] >= 0 else None
+            if p is not None and p.spec.scheduling_profile and p.spec.scheduling_profile not in profiles:
+                out[i] = ReconcileOutcome(STATUS_ALL_OK, "profile-not-found")
+                continue
+            if st != K.OBJ_OK:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "trigger-error", error=tr.messages[i])
+                continue
+            hashed.append(i)
+
+        # :394-421 — the hashes in one GPU pass; AddAnnotation's "changed" against the current annotation
+        key = T.clusters_fingerprint(clusters)
+        if key != self._clusters_key:
+            self.hasher.set_clusters(clusters)
+            self._clusters_key = key
+        self.ctx.trigger_prefixes_upload([tr.prefixes[i] for i in hashed])
+        self.ctx.trigger_run()
+        hashes = self.ctx.trigger_download()
+        trig: List[Optional[str]] = [None] * n
+        ann_only = [False] * n
+        to_schedule: List[int] = []
+        for i, h in zip(hashed, hashes.tolist()):
+            hv = O.format_trigger_hash(h)
+            if tr.flags[i] & K.TRIG_HAS_HASH and tr.current_hash[i] == hv:
+                out[i] = ReconcileOutcome(STATUS_ALL_OK, "unchanged")
+                continue
+            trig[i] = hv
+            if tr.flags[i] & K.TRIG_NO_SCHEDULING:
+                out[i] = ReconcileOutcome(STATUS_ALL_OK, "no-scheduling")
+                ann_only[i] = True
+            else:
+                to_schedule.append(i)
+
+        # schedule :445-521 — per framework one native unit build and one GPU batch
+        results: Dict[int, T.ScheduleResult] = {}
+        groups: Dict[Optional[str], List[int]] = {}
+        for i in to_schedule:
+            p = pols[pol_of[i]] if pol_of[i] >= 0 else None
+            if p is None:
+                results[i] = T.ScheduleResult({})  # :454-467 no policy: schedule to no clusters
+                continue
+            groups.setdefault(p.spec.scheduling_profile or None, []).append(i)
+        names: List[str] = []
+        for prof_name, members in groups.items():
+            try:
+                fwk = self._framework(profiles.get(prof_name) if prof_name else None)
+            except F.FrameworkError as e:
+                for i in members:
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "framework-error", error=str(e))
+                continue
+            built = K.units_from_objects(self.type_config, [ot[i] for i in members], pt,
+                                         [int(pol_of[i]) for i in members])
+            ok = []
+            for k, i in enumerate(members):
+                if built.status[k] == K.OBJ_OK:
+                    ok.append((i, int(built.unit_index[k])))
+                else:
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "unit-error", error=built.messages[k])
+            if not ok:
+                continue
+            res, snap = self.scheduler.schedule_columns(fwk, built.cols, clusters)
+            names = snap.names
+            for i, w in ok:
+                r = to_schedule_result_cols(res, w, built.cols, names)
+                if isinstance(r, T.ScheduleError):
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "schedule-error", error=str(r))
+                else:
+                    results[i] = r
+
+        # reconcile :291-308 + applySchedulingResult, and the no-scheduling objects' annotation, in one pass
+        todo, follower, threshold = [], [], []
+        for i in range(n):
+            if ann_only[i]:
+                todo.append(i)
+                follower.append(False)
+                threshold.append(None)
+            elif i in results:
+                try:
+                    f, t = self._apply_params(pols[pol_of[i]] if pol_of[i] >= 0 else None)
+                except (O.ObjectError, O.GoPanic) as e:
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=results[i], error=str(e))
+                    continue
+                todo.append(i)
+                follower.append(f)
+                threshold.append(t)
+        if not todo:
+            return out, new_text  # type: ignore[return-value]
+        table = list(names)
+        at = {c: k for k, c in enumerate(table)}
+        off, cl, rep = [0], [], []
+        for i in todo:
+            if not ann_only[i]:
+                for c, v in (results[i].suggested_clusters or {}).items():
+                    if c not in at:  # a sticky result's cluster that left the snapshot
+                        at[c] = len(table)
+                        table.append(c)
+                    cl.append(at[c])
+                    rep.append(-1 if v is None else v)
+            off.append(len(cl))
+        a = K.apply_results_ex(self.type_config, [ot[i] for i in todo], table, off, cl, rep, follower, threshold,
+                               trigger=[trig[i] for i in todo], ann_only=[ann_only[i] for i in todo])
+        for k, i in enumerate(todo):
+            if a.status[k] != K.APPLY_OK:
+                out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=results.get(i), error=a.messages[k])
+                continue
+            if a.changed[k]:
+                new_text[i] = a.texts[k]
+            if not ann_only[i]:
+                out[i] = ReconcileOutcome(STATUS_ALL_OK, "scheduled", True, bool(a.modified[k]), results[i])
+        return out, new_text  # type: ignore[return-value]

@@ -53,6 +53,9 @@ constexpr sv MAX_CLUSTERS_ANN = "kubeadmiral.io/maxClusters";
 constexpr sv AUTO_MIGRATION_INFO_ANN = "kubeadmiral.io/auto-migration-info";
 constexpr sv DUPLICATE = "Duplicate", DIVIDE = "Divide";
 constexpr sv ENABLE_FOLLOWER_ANN = "internal.kubeadmiral.io/enable-follower-scheduling";
+constexpr sv TRIGGER_HASH_ANN = "kubeadmiral.io/scheduling-trigger-hash";
+constexpr sv NO_SCHEDULING_ANN = "kubeadmiral.io/no-scheduling";
+constexpr sv FOLLOWS_OBJECT_ANN = "kubeadmiral.io/follows-object";
 constexpr sv POD_UNSCHEDULABLE_THRESHOLD_ANN = "internal.kubeadmiral.io/pod-unschedulable-threshold";
 
 struct Fail {  // the reference returns an error (status) or panics
@@ -700,6 +703,7 @@ void dec_policy_spec(Dec& D, uint32_t x, PolicySpec& s) {
 // ------------------------------------------------------------------ the policy table
 struct Policy {
   std::string ns, name;
+  int64_t generation = 0;  // metadata.generation (the trigger hash's policyGeneration)
   bool ok = false;
   std::string err;
   PolicySpec spec;
@@ -717,6 +721,8 @@ void load_policy(sv text, Policy& P) {
     const int64_t nm = get(d, (uint32_t)meta, "name"), ns = get(d, (uint32_t)meta, "namespace");
     if (nm >= 0 && d.v[nm].t == J_STR) P.name.assign(d.str((uint32_t)nm));
     if (ns >= 0 && d.v[ns].t == J_STR) P.ns.assign(d.str((uint32_t)ns));
+    const int64_t g = get(d, (uint32_t)meta, "generation");
+    if (g >= 0 && d.v[g].t == J_NUM && d.v[g].isint && d.v[g].fits) P.generation = d.v[g].i;
   }
   const int64_t spec = get(d, root, "spec");
   // `d.get("spec") or {}`: null, {}, "" , 0, false and [] all decode as the empty spec
@@ -742,8 +748,11 @@ struct PC {  // PlacementWithController
   std::string controller;
   std::optional<std::vector<std::string>> clusters;
 };
-// _OBJ_PLACEMENTS: type-checks apiVersion, kind, metadata and spec.placements; the error or null
-const char* decode_placements_view(const JDoc& d, uint32_t root, std::optional<std::vector<PC>>& pls) {
+// _OBJ_PLACEMENTS: type-checks apiVersion, kind, metadata and spec.placements; the error or null.
+// replaced_ann: the metadata.annotations node a trigger annotation replaced (AddAnnotation over annotations
+// that are not a string map writes a fresh one), not type-checked
+const char* decode_placements_view(const JDoc& d, uint32_t root, std::optional<std::vector<PC>>& pls,
+                                   uint32_t replaced_ann = UINT32_MAX) {
   static const sv N[] = {"apiVersion", "kind", "metadata", "spec"};
   static const sv NM[] = {"name", "namespace", "generateName", "uid", "resourceVersion", "generation", "labels", "annotations"};
   static const sv NS[] = {"placements"};
@@ -762,7 +771,7 @@ const char* decode_placements_view(const JDoc& d, uint32_t root, std::optional<s
         } else if (g == 5) {
           int64_t i = 0;
           D.int64(w, i);
-        } else {
+        } else if (g == 6 || w != replaced_ann) {
           std::optional<OMap<std::string>> m;
           dec_string_map(D, w, m);
         }
@@ -1469,14 +1478,27 @@ struct Applier {
   // applySchedulingResult (scheduler.go:632-695) on the parsed object; true if anything changed
   // the fields apply() wrote (bit 0 spec.placements, 1 spec.overrides, 2 metadata.annotations)
   static constexpr int N_DELTA = 3;
+  // trigger: the scheduling-trigger-hash annotation to add first (annotation.AddAnnotation, util/annotation/
+  // annotation.go:70-97), as the reconcile does before it schedules; trig_changed: it changed the object (not
+  // part of the returned applySchedulingResult flag); ann_only: only that (no result to apply)
   bool apply(const JDoc& d, uint32_t root, MV& obj, uint32_t& wrote, const std::vector<std::string>& clusters,
-             const OMap<int64_t>& desired, bool follower, std::optional<int64_t> threshold) {
+             const OMap<int64_t>& desired, bool follower, std::optional<int64_t> threshold,
+             std::optional<sv> trigger, bool ann_only, bool& trig_changed) {
+    trig_changed = false;
     bool modified = false;
     bool spec_created = false;
+    if (ann_only) goto annotations;
     // util.SetPlacementClusterNames (util/placement.go:44-59)
     {
       std::optional<std::vector<PC>> po;
-      if (const char* e = decode_placements_view(d, root, po)) fail(KAD_APPLY_ERROR, std::string("placements: ") + e);
+      uint32_t replaced = UINT32_MAX;
+      if (trigger) {
+        const int64_t meta = get(d, root, "metadata");
+        const int64_t an = meta >= 0 && d.v[meta].t == J_OBJ ? get(d, (uint32_t)meta, "annotations") : -1;
+        if (an >= 0) replaced = (uint32_t)an;
+      }
+      if (const char* e = decode_placements_view(d, root, po, replaced))
+        fail(KAD_APPLY_ERROR, std::string("placements: ") + e);
       std::vector<PC> pls = po ? *po : std::vector<PC>();
       int idx = -1;
       for (size_t k = 0; k < pls.size() && idx < 0; ++k)
@@ -1671,7 +1693,7 @@ struct Applier {
       }
     }
     // the follower-scheduling and pod-unschedulable-threshold annotations (:660-690)
-    {
+  annotations: {
       OMap<std::string> ann;
       const int64_t am = Builder::string_map(d, root, "annotations");
       if (am >= 0) {
@@ -1693,6 +1715,24 @@ struct Applier {
         return nullptr;
       };
       bool changed = false;
+      if (trigger) {  // AddAnnotation: changed unless the string-map view already holds the value
+        std::string* x = find(TRIGGER_HASH_ANN);
+        if (am < 0 || !x || *x != *trigger) {
+          if ((x = find(TRIGGER_HASH_ANN))) x->assign(*trigger);
+          else ann.emplace_back(std::string(TRIGGER_HASH_ANN), std::string(*trigger));
+          trig_changed = true;
+        }
+      }
+      if (ann_only) {
+        if (trig_changed) {
+          MV m = MV::obj();
+          for (const auto& kv : ann) m.set(kv.first, MV::str(kv.second));
+          set_nested(obj, "metadata", "annotations", std::move(m));
+          wrote |= 4u;
+          modified = true;
+        }
+        return false;
+      }
       const std::string fv = follower ? "true" : "false";
       if (std::string* x = find(ENABLE_FOLLOWER_ANN); !x || *x != fv) {
         if (x) *x = fv;
@@ -1714,12 +1754,12 @@ struct Applier {
           changed = true;
         }
       }
-      if (changed) {
+      if (changed || trig_changed) {
         MV m = MV::obj();
         for (const auto& kv : ann) m.set(kv.first, MV::str(kv.second));
         set_nested(obj, "metadata", "annotations", std::move(m));
         wrote |= 4u;
-        modified = true;
+        modified = modified || changed;
       }
     }
     return modified;
@@ -2006,7 +2046,8 @@ extern "C" void kad_units_free(kad_units* u) { delete u; }
 
 struct kad_applied {
   std::vector<int32_t> status;
-  std::vector<uint8_t> modified;
+  std::vector<uint8_t> modified;  // applySchedulingResult's result
+  std::vector<uint8_t> changed;   // the text changed (that, or the added trigger annotation)
   std::vector<int64_t> off{0};
   std::vector<uint8_t> bytes;
   std::vector<int64_t> doff{0};  // the written fields' new values, 3 per object
@@ -2016,13 +2057,15 @@ struct kad_applied {
 
 extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* objects, const kad_strs* cluster_names,
                                  const int32_t* res_off, const int32_t* res_cluster, const int64_t* res_replicas,
-                                 const uint8_t* follower, const int64_t* threshold_ns, int threads, kad_applied** out) {
+                                 const uint8_t* follower, const int64_t* threshold_ns, const kad_strs* trigger,
+                                 const uint8_t* ann_only, int threads, kad_applied** out) {
   if (!tc || !objects || !cluster_names || !res_off || !out || objects->n < 0 ||
       (objects->n > 0 && (!objects->off || !objects->bytes)) || cluster_names->n < 0 ||
       (cluster_names->n > 0 && (!cluster_names->off || !cluster_names->bytes)))
     return KAD_EINVAL;
   *out = nullptr;
   const int n = objects->n;
+  if (trigger && (trigger->n != n || (n > 0 && (!trigger->off || !trigger->bytes)))) return KAD_EINVAL;
   if (n > 0 && res_off[n] > 0 && (!res_cluster || !res_replicas)) return KAD_EINVAL;
   for (int i = 0; i < n; ++i)
     if (res_off[i] < 0 || res_off[i + 1] < res_off[i]) return KAD_EINVAL;
@@ -2048,6 +2091,7 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
     }
     R->status.assign((size_t)n, KAD_APPLY_OK);
     R->modified.assign((size_t)n, 0);
+    R->changed.assign((size_t)n, 0);
     R->msg.assign((size_t)n, std::string());
     std::vector<std::string> texts((size_t)n);
     std::vector<std::string> deltas((size_t)n * Applier::N_DELTA);
@@ -2071,9 +2115,14 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
           std::optional<int64_t> th;
           if (threshold_ns && threshold_ns[i] != INT64_MIN) th = threshold_ns[i];
           uint32_t wrote = 0;
-          const bool mod = A.apply(d, root, obj, wrote, clusters, desired, follower && follower[i], th);
+          std::optional<sv> trig;
+          if (trigger && trigger->off[i + 1] > trigger->off[i]) trig = text(trigger, i);
+          bool trig_changed = false;
+          const bool mod = A.apply(d, root, obj, wrote, clusters, desired, follower && follower[i], th, trig,
+                                   ann_only && ann_only[i], trig_changed);
           R->modified[(size_t)i] = mod ? 1 : 0;
-          if (mod) {
+          R->changed[(size_t)i] = (mod || trig_changed) ? 1 : 0;
+          if (mod || trig_changed) {
             emit(obj, texts[(size_t)i]);
             static const sv where[Applier::N_DELTA][2] = {{"spec", "placements"}, {"spec", "overrides"},
                                                           {"metadata", "annotations"}};
@@ -2084,13 +2133,14 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
           R->status[(size_t)i] = f.status;
           R->msg[(size_t)i] = f.msg;
           R->modified[(size_t)i] = 0;
+          R->changed[(size_t)i] = 0;
           texts[(size_t)i].clear();
           for (int q = 0; q < Applier::N_DELTA; ++q) deltas[(size_t)i * Applier::N_DELTA + q].clear();
         }
       }
     }, 64);
     for (int i = 0; i < n; ++i) {
-      if (R->modified[(size_t)i]) R->bytes.insert(R->bytes.end(), texts[(size_t)i].begin(), texts[(size_t)i].end());
+      if (R->changed[(size_t)i]) R->bytes.insert(R->bytes.end(), texts[(size_t)i].begin(), texts[(size_t)i].end());
       else {
         const sv t = text(objects, i);  // unchanged (or failed): the object as it was
         R->bytes.insert(R->bytes.end(), t.begin(), t.end());
@@ -2111,10 +2161,12 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
   }
 }
 
-extern "C" int kad_applied_view(const kad_applied* a, const int32_t** status, const uint8_t** modified, kad_strs* texts) {
+extern "C" int kad_applied_view(const kad_applied* a, const int32_t** status, const uint8_t** modified,
+                                const uint8_t** changed, kad_strs* texts) {
   if (!a) return KAD_EINVAL;
   if (status) *status = a->status.data();
   if (modified) *modified = a->modified.data();
+  if (changed) *changed = a->changed.data();
   if (texts) {
     texts->n = (int32_t)a->status.size();
     texts->off = a->off.data();
@@ -2137,3 +2189,210 @@ extern "C" const char* kad_applied_message(const kad_applied* a, int32_t i) {
 }
 
 extern "C" void kad_applied_free(kad_applied* a) { delete a; }
+
+// ------------------------------------------------------------------ f4 host side: the trigger hash's object part
+// computeSchedulingTriggerHash (schedulingtriggers.go:106-134) up to and including "clusterLabels": — the bytes
+// objects.trigger_prefix builds — for a batch of object texts, with the policy lookup and the two annotation facts
+// the reconcile needs next (the current hash annotation, the no-scheduling annotation).
+struct kad_trigger_objs {
+  std::vector<int32_t> status, policy_index;
+  std::vector<uint8_t> flags;         // KAD_TRIG_HAS_HASH, KAD_TRIG_NO_SCHEDULING
+  std::vector<int64_t> off{0}, hoff{0};
+  std::vector<uint8_t> bytes, hbytes;  // prefixes; current hash annotation values
+  std::vector<std::string> msg;
+};
+
+namespace {
+
+constexpr sv KNOWN_SCHED_ANNS[] = {SCHEDULING_MODE_ANN, STICKY_ANN, TOLERATIONS_ANN, PLACEMENTS_ANN,
+                                   SELECTOR_ANN, AFFINITY_ANN, MAX_CLUSTERS_ANN, FOLLOWS_OBJECT_ANN};
+
+struct TrigOut {
+  int status = KAD_OBJ_OK;
+  int32_t policy = -1;
+  uint8_t flags = 0;
+  std::string prefix, hash, msg;
+};
+
+void trigger_one(const kad_type_config& tc, const std::vector<Policy>& pols,
+                 const std::unordered_map<std::string, int32_t>& pol_index, const std::vector<std::string>& rfields,
+                 bool replicas_empty, int32_t forced, sv text, JDoc& d, TrigOut& o) {
+  uint32_t root;
+  if (!parse(text, d, &root) || d.v[root].t != J_OBJ) fail(KAD_OBJ_BAD_JSON, "object: not a JSON object");
+  const int64_t anns = Builder::string_map(d, root, "annotations");
+  const int64_t labels = Builder::string_map(d, root, "labels");
+  auto ann = [&](sv key) -> std::optional<sv> {
+    if (anns < 0) return std::nullopt;
+    const int64_t v = get(d, (uint32_t)anns, key);
+    if (v < 0) return std::nullopt;
+    return d.str((uint32_t)v);
+  };
+  // MatchedPolicyKey + lookup (scheduler.go:359-372), as Builder::build
+  if (forced >= -1) {
+    o.policy = forced >= 0 && forced < (int32_t)pols.size() ? forced : -1;
+  } else {
+    std::optional<std::string> key;
+    const int64_t pl = labels >= 0 ? get(d, (uint32_t)labels, POLICY_LABEL) : -1;
+    const int64_t cl = labels >= 0 ? get(d, (uint32_t)labels, CLUSTER_POLICY_LABEL) : -1;
+    if (pl >= 0 && tc.namespaced) {
+      std::string ns;
+      const int64_t meta = get(d, root, "metadata");
+      const int64_t nsv = meta >= 0 && d.v[meta].t == J_OBJ ? get(d, (uint32_t)meta, "namespace") : -1;
+      if (nsv >= 0 && d.v[nsv].t == J_STR) ns.assign(d.str((uint32_t)nsv));
+      key = ns + '\0' + std::string(d.str((uint32_t)pl));
+    } else if (cl >= 0) {
+      key = std::string(1, '\0') + std::string(d.str((uint32_t)cl));
+    }
+    if (key) {
+      auto it = pol_index.find(*key);
+      if (it == pol_index.end()) {
+        o.status = KAD_OBJ_POLICY_NOT_FOUND;
+        return;
+      }
+      o.policy = it->second;
+    }
+  }
+  const Policy* P = o.policy >= 0 ? &pols[(size_t)o.policy] : nullptr;
+  if (P && !P->ok) fail(KAD_OBJ_POLICY_ERROR, P->err);
+  // getReplicaCount (schedulingtriggers.go:171-186)
+  int64_t replicas = 0;
+  if (!replicas_empty) {
+    uint32_t x = root;
+    bool found = true;
+    for (const std::string& f : rfields) {
+      if (d.v[x].t != J_OBJ) fail(KAD_OBJ_UNIT_ERROR, "cannot access [spec template]: accessor error: not a map");
+      const int64_t y = get(d, x, f);
+      if (y < 0) {
+        found = false;
+        break;
+      }
+      x = (uint32_t)y;
+    }
+    if (found) {
+      const JV& v = d.v[x];
+      if (v.t != J_NUM || !v.isint || !v.fits) fail(KAD_OBJ_UNIT_ERROR, "cannot access [spec template]: expected int64");
+      replicas = v.i;
+    }
+  }
+  std::string& s = o.prefix;
+  s += "{\"schedulingAnnotations\":[";
+  {  // sortMap of the scheduling annotations: keys unique, bytewise order
+    std::vector<std::pair<sv, sv>> kv;
+    for (sv k : KNOWN_SCHED_ANNS)
+      if (auto v = ann(k)) kv.emplace_back(k, *v);
+    std::sort(kv.begin(), kv.end());
+    for (size_t i = 0; i < kv.size(); ++i) {
+      s += i ? ",{\"key\":" : "{\"key\":";
+      emit_str(kv[i].first, s);
+      s += ",\"value\":";
+      emit_str(kv[i].second, s);
+      s += '}';
+    }
+  }
+  s += "],\"replicaCount\":" + std::to_string(replicas) +
+       ",\"resourceRequest\":{\"millicpu\":0,\"memory\":0,\"ephemeralStorage\":0,\"scalarResources\":null}";
+  if (P && P->spec.am) {
+    if (auto v = ann(AUTO_MIGRATION_INFO_ANN)) {
+      s += ",\"autoMigrationInfo\":";
+      emit_str(*v, s);
+    }
+  }
+  s += ",\"policyName\":";
+  emit_str(P ? sv(P->name) : sv(), s);
+  s += ",\"policyGeneration\":" + std::to_string(P ? P->generation : 0) + ",\"clusterLabels\":";
+  if (auto h = ann(TRIGGER_HASH_ANN)) {
+    o.flags |= KAD_TRIG_HAS_HASH;
+    o.hash.assign(*h);
+  }
+  if (auto ns = ann(NO_SCHEDULING_ANN); ns && !ns->empty()) o.flags |= KAD_TRIG_NO_SCHEDULING;
+}
+
+}  // namespace
+
+extern "C" int kad_trigger_prefixes(const kad_type_config* tc, const kad_strs* objects, const kad_strs* policies,
+                                    const int32_t* policy_of, int threads, kad_trigger_objs** out) {
+  if (!tc || !objects || !out || objects->n < 0 || (objects->n > 0 && (!objects->off || !objects->bytes)) ||
+      (policies && policies->n > 0 && (!policies->off || !policies->bytes)))
+    return KAD_EINVAL;
+  *out = nullptr;
+  try {
+    auto R = std::make_unique<kad_trigger_objs>();
+    const int n = objects->n, np = policies ? policies->n : 0;
+    if (threads <= 0) threads = 1 << 20;
+    auto text = [](const kad_strs* s, int i) {
+      return sv(reinterpret_cast<const char*>(s->bytes) + s->off[i], (size_t)(s->off[i + 1] - s->off[i]));
+    };
+    std::vector<Policy> pols((size_t)np);
+    parallel_for(np, threads, [&](int lo, int hi) {
+      for (int i = lo; i < hi; ++i) load_policy(text(policies, i), pols[(size_t)i]);
+    }, 64);
+    std::unordered_map<std::string, int32_t> pol_index;
+    for (int i = 0; i < np; ++i) pol_index[pols[(size_t)i].ns + '\0' + pols[(size_t)i].name] = i;
+    std::vector<std::string> rfields{"spec", "template"};
+    {
+      const std::string path = tc->replicas_spec ? tc->replicas_spec : "";
+      size_t a = 0;
+      for (size_t i = 0; i <= path.size(); ++i)
+        if (i == path.size() || path[i] == '.') {
+          if (i > a) rfields.push_back(path.substr(a, i - a));
+          a = i + 1;
+        }
+    }
+    const bool replicas_empty = !tc->replicas_spec || !*tc->replicas_spec;
+    std::vector<TrigOut> outs((size_t)n);
+    parallel_for(n, threads, [&](int lo, int hi) {
+      JDoc d;
+      for (int i = lo; i < hi; ++i) {
+        TrigOut& o = outs[(size_t)i];
+        try {
+          trigger_one(*tc, pols, pol_index, rfields, replicas_empty, policy_of ? policy_of[i] : -2, text(objects, i), d, o);
+        } catch (const Fail& f) {
+          const int32_t pol = o.policy;
+          o = TrigOut();
+          o.status = f.status;
+          o.msg = f.msg;
+          o.policy = pol;
+        }
+      }
+    }, 256);
+    R->status.resize((size_t)n);
+    R->policy_index.resize((size_t)n);
+    R->flags.resize((size_t)n);
+    R->msg.resize((size_t)n);
+    for (int i = 0; i < n; ++i) {
+      TrigOut& o = outs[(size_t)i];
+      R->status[(size_t)i] = o.status;
+      R->policy_index[(size_t)i] = o.policy;
+      R->flags[(size_t)i] = o.flags;
+      R->msg[(size_t)i] = std::move(o.msg);
+      R->bytes.insert(R->bytes.end(), o.prefix.begin(), o.prefix.end());
+      R->off.push_back((int64_t)R->bytes.size());
+      R->hbytes.insert(R->hbytes.end(), o.hash.begin(), o.hash.end());
+      R->hoff.push_back((int64_t)R->hbytes.size());
+    }
+    *out = R.release();
+    return KAD_OK;
+  } catch (const std::bad_alloc&) {
+    return KAD_ENOMEM;
+  } catch (...) {
+    return KAD_EINVAL;
+  }
+}
+
+extern "C" int kad_trigger_objs_view(const kad_trigger_objs* t, const int32_t** status, const int32_t** policy_index,
+                                     const uint8_t** flags, kad_strs* prefixes, kad_strs* current_hash) {
+  if (!t) return KAD_EINVAL;
+  if (status) *status = t->status.data();
+  if (policy_index) *policy_index = t->policy_index.data();
+  if (flags) *flags = t->flags.data();
+  if (prefixes) *prefixes = kad_strs{(int32_t)t->status.size(), t->off.data(), t->bytes.data()};
+  if (current_hash) *current_hash = kad_strs{(int32_t)t->status.size(), t->hoff.data(), t->hbytes.data()};
+  return KAD_OK;
+}
+
+extern "C" const char* kad_trigger_objs_message(const kad_trigger_objs* t, int32_t i) {
+  if (!t || i < 0 || (size_t)i >= t->msg.size()) return "";
+  return t->msg[(size_t)i].c_str();
+}
+
+extern "C" void kad_trigger_objs_free(kad_trigger_objs* t) { delete t; }

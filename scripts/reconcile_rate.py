@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Objects per second through BatchReconciler.reconcile (f1: policy lookup, trigger hashes on the GPU, units,
+"""Objects per second through BatchReconciler.reconcile and reconcile_texts (f1: policy lookup, trigger hashes on the GPU, units,
 one packed batch per framework, schedule, result application), with the native object path
 (include/kad_objects.h) and with objects.py, on synth.gen_trigger_workload objects. GPU required.
 
@@ -64,6 +64,27 @@ def main():
         results[name] = (objs, [(g.stage, g.result) for g in got])
         print(json.dumps({name: out[name]}), flush=True)
     out["same_outcome"] = results["native"][1] == results["python"][1] and results["native"][0] == results["python"][0]
+
+    # the reconcile over the objects' JSON texts (reconcile_texts: every per-object step native)
+    from kubeadmiral_amd import objects as O
+
+    texts = [json.dumps(o).encode() for o in objs0]
+    ptexts = [json.dumps(O.policy_to_json(p)) for p in pols]
+    rec = BatchReconciler(ftc)
+    t0 = time.perf_counter()
+    got, new = rec.reconcile_texts(texts, ptexts, clusters)
+    t1 = time.perf_counter()
+    again, _ = rec.reconcile_texts([n if n is not None else t for n, t in zip(new, texts)], ptexts, clusters)
+    t2 = time.perf_counter()
+    stages = {}
+    for g in got:
+        stages[g.stage] = stages.get(g.stage, 0) + 1
+    out["texts"] = {"first_pass_objects_per_s": round(a.objects / (t1 - t0)),
+                    "unchanged_pass_objects_per_s": round(a.objects / (t2 - t1)), "stages": stages,
+                    "unchanged": sum(g.stage == "unchanged" for g in again)}
+    out["texts_same_outcome"] = ([(g.stage, g.result) for g in got] == results["python"][1] and
+                                 all(json.loads(n) == o for n, o in zip(new, results["python"][0]) if n is not None))
+    print(json.dumps({"texts": out["texts"]}), flush=True)
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as f:

@@ -115,3 +115,51 @@ def test_same_length_list_with_changed_label_reschedules(native):
     # and in place on the very same list object
     relabeled[6].taints = relabeled[6].taints + [T.Taint("new", "t", T.TAINT_PREFER_NO_SCHEDULE)]
     assert all(g.stage != "unchanged" for g in rec.reconcile(objs, by_key, relabeled))
+
+
+def test_text_reconcile_matches_dict_reconcile():
+    """BatchReconciler.reconcile_texts (every step native, over the objects' JSON) == reconcile on the decoded
+    objects (objects.py per object): outcomes, results, and the new texts == the mutated objects; a second pass
+    over the new texts finds every trigger hash unchanged."""
+    import json
+
+    from kubeadmiral_amd.controller import BatchReconciler
+
+    ftc, clusters, objs, pols = synth.gen_trigger_workload(np.random.default_rng(8), 400, 16, n_policies=8)
+    by_key = {}
+    for p in pols:
+        if p.spec.auto_migration is not None:
+            p.spec.auto_migration.when.pod_unschedulable_for = "2m"
+        by_key[(p.namespace, p.name)] = p
+    for o in objs[:5]:
+        del o["metadata"]["labels"][O.PROPAGATION_POLICY_NAME_LABEL]
+    objs[5]["metadata"]["labels"][O.PROPAGATION_POLICY_NAME_LABEL] = "missing"
+    for o in objs[6:16]:
+        o["metadata"].setdefault("annotations", {})[O.NO_SCHEDULING_ANNOTATION] = "true"
+    objs[16]["spec"]["template"]["spec"]["replicas"] = "5"       # getReplicaCount fails: trigger-error
+    objs[17]["metadata"]["annotations"] = {"x": 1}               # not a string map: AddAnnotation replaces it
+    objs[18]["metadata"].pop("annotations", None)
+    texts = [json.dumps(o) for o in objs]
+    ptexts = [json.dumps(O.policy_to_json(p)) for p in pols]
+
+    want_objs = copy.deepcopy(objs)
+    want = BatchReconciler(ftc, native_objects=False).reconcile(want_objs, by_key, clusters)
+    rec = BatchReconciler(ftc)
+    got, new = rec.reconcile_texts(texts, ptexts, clusters)
+    stages = set()
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert (g.stage, g.status) == (w.stage, w.status), (i, g.error, w.error)
+        stages.add(g.stage)
+        if g.stage == "scheduled":
+            assert g.result == w.result and g.modified == w.modified, i
+        if g.stage in ("scheduled", "no-scheduling"):
+            assert json.loads(new[i]) == want_objs[i], i
+        else:
+            assert new[i] is None, i
+    assert {"scheduled", "no-scheduling", "policy-not-found", "trigger-error"} <= stages
+
+    texts2 = [n if n is not None else t for n, t in zip(new, texts)]
+    again, new2 = rec.reconcile_texts(texts2, ptexts, clusters)
+    for i, g in enumerate(again):
+        if got[i].stage in ("scheduled", "no-scheduling"):
+            assert g.stage == "unchanged" and new2[i] is None, i

@@ -521,3 +521,95 @@ def test_apply_fields_rebuild_the_object():
             if v is not None:
                 o.setdefault(a, {})[b] = json.loads(v)
         assert o == json.loads(texts[i]), i
+
+
+# ------------------------------------------------------------------ f4 host side: kad_trigger_prefixes
+def test_trigger_prefixes_match_python():
+    """The trigger JSON's object part, the policy lookup, the current hash and the no-scheduling flag from the
+    objects' texts == objects.trigger_prefix / matched_policy_key / get_annotations on the decoded objects."""
+    rng = random.Random(31)
+    policies = [_policy(rng, f"p{i}", i % 2 == 0) for i in range(6)]
+    for p in policies:
+        p["metadata"]["generation"] = rng.randint(0, 9)
+    objs = [_object(rng, policies) for _ in range(800)]
+    for o in objs[::5]:
+        if isinstance(o["metadata"]["annotations"], dict) and "x" not in o["metadata"]["annotations"]:
+            o["metadata"]["annotations"][O.SCHEDULING_TRIGGER_HASH_ANNOTATION] = str(rng.randint(0, 2 ** 32 - 1))
+    for o in objs[::7]:
+        if isinstance(o["metadata"]["annotations"], dict) and "x" not in o["metadata"]["annotations"]:
+            o["metadata"]["annotations"][O.NO_SCHEDULING_ANNOTATION] = rng.choice(["", "true"])
+    by_key = {}
+    for p in policies:
+        try:
+            by_key[(p["metadata"].get("namespace", ""), p["metadata"]["name"])] = O.PropagationPolicy.from_json(p)
+        except Exception:  # noqa: BLE001 — a policy that does not decode
+            by_key[(p["metadata"].get("namespace", ""), p["metadata"]["name"])] = None
+    for ftc in (DEPLOY, O.FederatedTypeConfig("", "v1", "ConfigMap", "configmaps", "Cluster", "")):
+        got = K.trigger_prefixes(ftc, objs, policies)
+        seen = set()
+        for i, o in enumerate(objs):
+            key = O.matched_policy_key(o, ftc.namespaced)
+            st = int(got.status[i])
+            seen.add(st)
+            if key is not None and key not in by_key:
+                assert st == K.OBJ_POLICY_NOT_FOUND, i
+                continue
+            pol = by_key[key] if key is not None else None
+            if key is not None and pol is None:
+                assert st == K.OBJ_POLICY_ERROR, i
+                continue
+            try:
+                want = O.trigger_prefix(ftc, o, pol)
+            except O.ObjectError:
+                assert st == K.OBJ_UNIT_ERROR, (i, got.messages[i])
+                continue
+            assert st == K.OBJ_OK, (i, got.messages[i])
+            assert got.prefixes[i] == want, i
+            ann = O.get_annotations(o) or {}
+            h = ann.get(O.SCHEDULING_TRIGGER_HASH_ANNOTATION)
+            assert bool(got.flags[i] & K.TRIG_HAS_HASH) == (h is not None), i
+            assert got.current_hash[i] == (h or "")
+            assert bool(got.flags[i] & K.TRIG_NO_SCHEDULING) == bool(ann.get(O.NO_SCHEDULING_ANNOTATION)), i
+        assert {K.OBJ_OK, K.OBJ_POLICY_NOT_FOUND} | ({K.OBJ_UNIT_ERROR} if ftc.replicas_spec else set()) <= seen
+    assert K.trigger_prefixes(DEPLOY, ["nope"], policies).status[0] == K.OBJ_BAD_JSON
+
+
+def test_apply_with_trigger_annotation_matches_python():
+    """kad_apply_results with the trigger annotation first (AddAnnotation, scheduler.go:407-417) and the
+    annotation-only objects == add_annotation (+ apply_scheduling_result) on the decoded objects."""
+    rng = random.Random(37)
+    policies = [_policy(rng, f"p{i}", False) for i in range(4)]
+    objs = [_object(rng, policies) for _ in range(500)]
+    for o in objs[::3]:
+        if isinstance(o["metadata"]["annotations"], dict):
+            o["metadata"]["annotations"][O.SCHEDULING_TRIGGER_HASH_ANNOTATION] = "17"
+    for o in objs[::9]:
+        o["metadata"].pop("annotations")
+    off, cl, rep = _results(rng, len(objs))
+    follower = [rng.random() < 0.7 for _ in objs]
+    thresholds = [rng.choice([None, 90 * 10**9]) for _ in objs]
+    trig = [rng.choice(["17", "18", "4294967295"]) for _ in objs]
+    ann_only = [rng.random() < 0.3 for _ in objs]
+    a = K.apply_results_ex(DEPLOY, objs, NAMES, off, cl, rep, follower, thresholds, trigger=trig, ann_only=ann_only)
+    kinds = set()
+    for i, obj in enumerate(objs):
+        o = json.loads(json.dumps(obj))
+        tch = O.add_annotation(o, O.SCHEDULING_TRIGGER_HASH_ANNOTATION, trig[i])
+        if ann_only[i]:
+            assert a.status[i] == K.APPLY_OK and not a.modified[i] and a.changed[i] == tch, i
+            mod = False
+        else:
+            sc = {NAMES[cl[k]]: (None if rep[k] < 0 else int(rep[k])) for k in range(off[i], off[i + 1])}
+            try:
+                mod = O.apply_scheduling_result(DEPLOY, o, T.ScheduleResult(sc), follower[i], thresholds[i])
+            except (O.ObjectError, O.GoPanic):
+                assert a.status[i] != K.APPLY_OK, i
+                continue
+            assert a.status[i] == K.APPLY_OK, (i, a.messages[i])
+            assert a.modified[i] == mod and a.changed[i] == (mod or tch), i
+        kinds.add((bool(tch), bool(mod)))
+        if a.changed[i]:
+            assert json.loads(a.texts[i]) == o, i
+        else:
+            assert a.texts[i] == json.dumps(obj, separators=(",", ":")).encode(), i
+    assert kinds == {(False, False), (False, True), (True, False), (True, True)}
