@@ -127,6 +127,8 @@ void kad_applied_free(kad_applied* a);
  * value of the kubeadmiral.io/scheduling-trigger-hash annotation and the flags below. */
 #define KAD_TRIG_HAS_HASH 1u      /* the annotations (a string map) hold a trigger hash     */
 #define KAD_TRIG_NO_SCHEDULING 2u /* kubeadmiral.io/no-scheduling is set (non-empty)         */
+#define KAD_TRIG_ANN_NOT_MAP 4u   /* metadata.annotations is set but not a string map: the trigger annotation
+                                   * replaces it, so the SchedulingUnit is built from the annotated text */
 
 typedef struct kad_trigger_objs kad_trigger_objs;
 

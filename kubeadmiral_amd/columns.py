@@ -757,7 +757,7 @@ def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], 
 
 
 # include/kad_objects.h KAD_TRIG_*
-TRIG_HAS_HASH, TRIG_NO_SCHEDULING = 1, 2
+TRIG_HAS_HASH, TRIG_NO_SCHEDULING, TRIG_ANN_NOT_MAP = 1, 2, 4
 
 
 class TriggerObjects:

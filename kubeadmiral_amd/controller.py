@@ -361,6 +361,14 @@ class BatchReconciler:
                 results[i] = T.ScheduleResult({})  # :454-467 no policy: schedule to no clusters
                 continue
             groups.setdefault(p.spec.scheduling_profile or None, []).append(i)
+        # the unit is built from the object after AddAnnotation (:407); that only differs where the annotation
+        # replaced annotations that were not a string map (the typed view would reject the old ones)
+        unit_text = {}
+        fix = [i for i in to_schedule if tr.flags[i] & K.TRIG_ANN_NOT_MAP]
+        if fix:
+            a = K.apply_results_ex(self.type_config, [ot[i] for i in fix], [], [0] * (len(fix) + 1), [], [],
+                                   trigger=[trig[i] for i in fix], ann_only=[True] * len(fix))
+            unit_text = {i: a.texts[k] for k, i in enumerate(fix) if a.status[k] == K.APPLY_OK}
         names: List[str] = []
         for prof_name, members in groups.items():
             try:
@@ -369,7 +377,7 @@ class BatchReconciler:
                 for i in members:
                     out[i] = ReconcileOutcome(STATUS_ERROR, "framework-error", error=str(e))
                 continue
-            built = K.units_from_objects(self.type_config, [ot[i] for i in members], pt,
+            built = K.units_from_objects(self.type_config, [unit_text.get(i, ot[i]) for i in members], pt,
                                          [int(pol_of[i]) for i in members])
             ok = []
             for k, i in enumerate(members):

@@ -2305,6 +2305,11 @@ void trigger_one(const kad_type_config& tc, const std::vector<Policy>& pols,
     o.hash.assign(*h);
   }
   if (auto ns = ann(NO_SCHEDULING_ANN); ns && !ns->empty()) o.flags |= KAD_TRIG_NO_SCHEDULING;
+  if (anns < 0) {
+    const int64_t meta = get(d, root, "metadata");
+    const int64_t an = meta >= 0 && d.v[meta].t == J_OBJ ? get(d, (uint32_t)meta, "annotations") : -1;
+    if (an >= 0 && d.v[an].t != J_NULL) o.flags |= KAD_TRIG_ANN_NOT_MAP;
+  }
 }
 
 }  // namespace

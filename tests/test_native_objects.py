@@ -570,6 +570,9 @@ def test_trigger_prefixes_match_python():
             assert bool(got.flags[i] & K.TRIG_HAS_HASH) == (h is not None), i
             assert got.current_hash[i] == (h or "")
             assert bool(got.flags[i] & K.TRIG_NO_SCHEDULING) == bool(ann.get(O.NO_SCHEDULING_ANNOTATION)), i
+            raw = o["metadata"].get("annotations")
+            not_map = raw is not None and not (isinstance(raw, dict) and all(isinstance(v, str) for v in raw.values()))
+            assert bool(got.flags[i] & K.TRIG_ANN_NOT_MAP) == not_map, i
         assert {K.OBJ_OK, K.OBJ_POLICY_NOT_FOUND} | ({K.OBJ_UNIT_ERROR} if ftc.replicas_spec else set()) <= seen
     assert K.trigger_prefixes(DEPLOY, ["nope"], policies).status[0] == K.OBJ_BAD_JSON
 
