@@ -663,7 +663,7 @@ class Applied:
 
 def apply_results_ex(type_config, objects: Sequence, cluster_names: Sequence[str], res_off, res_cluster, res_replicas,
                      follower=None, threshold_ns=None, trigger: Optional[Sequence[Optional[str]]] = None,
-                     ann_only=None, threads: int = 0) -> Applied:
+                     ann_only=None, threads: int = 0, with_fields: bool = True) -> Applied:
     """kad_apply_results: applySchedulingResult for a batch of objects (JSON texts or dicts) with results in
     kad_results_download's form (CSR of snapshot cluster ids, replicas -1 = nil). ``follower``: per object
     !DisableFollowerScheduling (default all True); ``threshold_ns``: per object the pod-unschedulable threshold
@@ -735,7 +735,7 @@ def apply_results_ex(type_config, objects: Sequence, cluster_names: Sequence[str
         fs = KadStrs()
         L.kad_applied_fields(h, ctypes.byref(fs))
         fields = []
-        if n:
+        if n and with_fields:
             m = len(APPLY_FIELDS)
             foff = np.ctypeslib.as_array(ctypes.cast(fs.off, ctypes.POINTER(ctypes.c_int64)), (m * n + 1,))
             fdata = ctypes.string_at(fs.bytes, int(foff[-1])) if foff[-1] else b""
@@ -750,7 +750,7 @@ def apply_results(type_config, objects: Sequence, cluster_names: Sequence[str], 
                   follower=None, threshold_ns=None, threads: int = 0, with_fields: bool = False):
     """:func:`apply_results_ex` as (status, modified, texts, messages[, fields])."""
     a = apply_results_ex(type_config, objects, cluster_names, res_off, res_cluster, res_replicas, follower,
-                         threshold_ns, threads=threads)
+                         threshold_ns, threads=threads, with_fields=with_fields)
     if with_fields:
         return a.status, a.modified, a.texts, a.messages, a.fields
     return a.status, a.modified, a.texts, a.messages

@@ -398,17 +398,24 @@ class BatchReconciler:
 
         # reconcile :291-308 + applySchedulingResult, and the no-scheduling objects' annotation, in one pass
         todo, follower, threshold = [], [], []
+        params: Dict[int, object] = {}  # per policy: (follower, threshold) or the error
         for i in range(n):
             if ann_only[i]:
                 todo.append(i)
                 follower.append(False)
                 threshold.append(None)
             elif i in results:
-                try:
-                    f, t = self._apply_params(pols[pol_of[i]] if pol_of[i] >= 0 else None)
-                except (O.ObjectError, O.GoPanic) as e:
-                    out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=results[i], error=str(e))
+                pi = int(pol_of[i])
+                if pi not in params:
+                    try:
+                        params[pi] = self._apply_params(pols[pi] if pi >= 0 else None)
+                    except (O.ObjectError, O.GoPanic) as e:
+                        params[pi] = e
+                ft = params[pi]
+                if isinstance(ft, Exception):
+                    out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=results[i], error=str(ft))
                     continue
+                f, t = ft
                 todo.append(i)
                 follower.append(f)
                 threshold.append(t)
@@ -427,7 +434,8 @@ class BatchReconciler:
                     rep.append(-1 if v is None else v)
             off.append(len(cl))
         a = K.apply_results_ex(self.type_config, [ot[i] for i in todo], table, off, cl, rep, follower, threshold,
-                               trigger=[trig[i] for i in todo], ann_only=[ann_only[i] for i in todo])
+                               trigger=[trig[i] for i in todo], ann_only=[ann_only[i] for i in todo],
+                               with_fields=False)
         for k, i in enumerate(todo):
             if a.status[k] != K.APPLY_OK:
                 out[i] = ReconcileOutcome(STATUS_ERROR, "apply-error", result=results.get(i), error=a.messages[k])

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--clusters", type=int, default=64)
     ap.add_argument("--out", default="")
     ap.add_argument("--profile", default="", help="cProfile the native first pass into this file (top functions)")
+    ap.add_argument("--profile-texts", default="", help="cProfile the texts first pass into this file")
     a = ap.parse_args()
     import numpy as np
 
@@ -69,11 +70,20 @@ def main():
     from kubeadmiral_amd import objects as O
 
     texts = [json.dumps(o).encode() for o in objs0]
-    ptexts = [json.dumps(O.policy_to_json(p)) for p in pols]
+    ptexts = [json.dumps(O.policy_to_json(p)) for p in by_key.values()]  # the informer's policies, once each
     rec = BatchReconciler(ftc)
+    if a.profile_texts:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
     t0 = time.perf_counter()
     got, new = rec.reconcile_texts(texts, ptexts, clusters)
     t1 = time.perf_counter()
+    if a.profile_texts:
+        pr.disable()
+        with open(a.profile_texts, "w") as f:
+            pstats.Stats(pr, stream=f).sort_stats("tottime").print_stats(30)
     again, _ = rec.reconcile_texts([n if n is not None else t for n, t in zip(new, texts)], ptexts, clusters)
     t2 = time.perf_counter()
     stages = {}

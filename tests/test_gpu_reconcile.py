@@ -140,7 +140,7 @@ def test_text_reconcile_matches_dict_reconcile():
     objs[17]["metadata"]["annotations"] = {"x": 1}               # not a string map: AddAnnotation replaces it
     objs[18]["metadata"].pop("annotations", None)
     texts = [json.dumps(o) for o in objs]
-    ptexts = [json.dumps(O.policy_to_json(p)) for p in pols]
+    ptexts = [json.dumps(O.policy_to_json(p)) for p in by_key.values()]
 
     want_objs = copy.deepcopy(objs)
     want = BatchReconciler(ftc, native_objects=False).reconcile(want_objs, by_key, clusters)
