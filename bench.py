@@ -647,12 +647,15 @@ def shard_sweep(args, cfg, local, t1_ms, ns=(2, 4, 8)):
     return out
 
 
-def end_to_end(ctx, snap, fwk, cols, res, C, packer_for, chunks=4):
+def end_to_end(ctx, snap, fwk, cols, res, C, packer_for, chunks=4, packs=2):
     """The hot path as a caller sees it, from columnar units to downloaded placements, one rank, warm:
     * sequential: native pack (in place, page-locked) → kad_batch_upload (one DMA) → schedule → D2H;
-    * pipelined: the batch in ``chunks`` unit ranges, two packers and two contexts alternating, so chunk i+1
-      is packed on the host (a worker thread: ctypes releases the GIL) while chunk i is uploaded, scheduled
-      and downloaded — what a batching caller (batcher.CoalescingScheduler) does with a stream of units.
+    * pipelined: the batch in ``chunks`` unit ranges, two contexts alternating and ``packs`` chunk packs in
+      flight on worker threads (ctypes releases the GIL; one packer each, plus the one being uploaded), so
+      chunks i+1.. are packed on the host while chunk i is uploaded, scheduled and downloaded — what a
+      batching caller (batcher.CoalescingScheduler) does with a stream of units. Two packs in flight overlap
+      one pack's narrow phases with the other's parallel ones; the upload checks then run on the library's
+      side pool instead of waiting behind a pack (kad_pool.h run_checks).
     Both must reproduce the timed run's rows exactly."""
     from concurrent.futures import ThreadPoolExecutor
 
@@ -686,28 +689,30 @@ def end_to_end(ctx, snap, fwk, cols, res, C, packer_for, chunks=4):
     ctx2 = Context(ctx.device)
     ctx2.upload_snapshot(packer_for)
     ctxs = (ctx, ctx2)
-    packers = (packer, CO.NativePacker(packer_for))
+    packers = [packer] + [CO.NativePacker(packer_for) for _ in range(packs)]
     bounds = [W * i // chunks for i in range(chunks + 1)]
     parts = [cols.slice(bounds[i], bounds[i + 1]) for i in range(chunks)]
     bufs = None
     pipe = None
-    with ThreadPoolExecutor(max_workers=1) as pool:
-        for rep in range(2):  # first pass warms both packers / contexts and sizes the result buffers
+    with ThreadPoolExecutor(max_workers=packs) as pool:
+        for rep in range(2):  # first pass warms the packers / contexts and sizes the result buffers
             outs = []
             t0 = time.perf_counter()
-            fut = pool.submit(packers[0].pack, fwk, parts[0], 0, False)
+            futs = {i: pool.submit(packers[i % len(packers)].pack, fwk, parts[i], 0, False)
+                    for i in range(min(packs, chunks))}
             for i in range(chunks):
-                nbi = fut.result()
-                if i + 1 < chunks:
-                    fut = pool.submit(packers[(i + 1) % 2].pack, fwk, parts[i + 1], 0, False)
+                nbi = futs.pop(i).result()
+                if i + packs < chunks:
+                    j = i + packs
+                    futs[j] = pool.submit(packers[j % len(packers)].pack, fwk, parts[j], 0, False)
                 c = ctxs[i % 2]
                 c.upload_batch(nbi)
                 c.schedule(fwk)
                 r = c.download(out=bufs[i] if bufs else None)
-                r.out_off = np.array(r.out_off)  # a view into the packer's buffer, which chunk i + 2 reuses
+                r.out_off = np.array(r.out_off)  # a view into the packer's buffer, which chunk i + packs + 1 reuses
                 outs.append(r)
             tot = time.perf_counter() - t0
-            pipe = {"chunks": chunks, "total_ms": tot * 1e3, "decisions_per_s": W * C / tot}
+            pipe = {"chunks": chunks, "packs_in_flight": packs, "total_ms": tot * 1e3, "decisions_per_s": W * C / tot}
             if bufs is None:
                 bufs = [BatchResult.pinned(len(r.status), len(r.cluster)) for r in outs]
     ctx2.close()

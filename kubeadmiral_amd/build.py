@@ -27,9 +27,10 @@ def _inputs():
         os.path.join(os.path.dirname(HERE), "include", h) for h in ("kad_sched.h", "kad_pack.h", "kad_objects.h")]
 
 
-# host code that no kernel launch depends on (the object formats either side of the batch): left out of the
-# profile hash, so that editing it does not invalidate the kernels' PMC profiles
-HOST_ONLY = ("kad_objects.cpp", "kad_objects.h")
+# host code that no kernel launch depends on (the object formats either side of the batch; the native packer,
+# whose blob the tests pin byte for byte to pack.py's; the host worker pool): left out of the profile hash,
+# so that editing it does not invalidate the kernels' PMC profiles
+HOST_ONLY = ("kad_objects.cpp", "kad_objects.h", "kad_pack.cpp", "kad_pool.h")
 
 
 def source_hash() -> str:

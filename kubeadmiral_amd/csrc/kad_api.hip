@@ -168,7 +168,7 @@ static void host_parallel(int n, F f, int serial_below = 4096) {
     f(0, n);
     return;
   }
-  kadpool::pool().run(T, [&](int t) { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
+  kadpool::run_checks(T, [&](int t) { f((int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T)); });
 }
 // the smallest i in [0, n) with bad(i), or -1: pieces checked on up to 16 host threads, each
 // stopping at its first failure or once an earlier one is known — the same index, so the same
@@ -182,7 +182,7 @@ static int64_t first_bad(int64_t n, F bad) {
   }
   std::atomic<int64_t> best{INT64_MAX};
   const int T = kadpool::pool().threads();
-  kadpool::pool().run(T, [&](int t) {
+  kadpool::run_checks(T, [&](int t) {
     const int64_t lo = n * t / T, hi = n * (t + 1) / T;
     for (int64_t i = lo; i < hi; i++) {
       if ((i & 1023) == 0 && i > best.load(std::memory_order_relaxed)) return;

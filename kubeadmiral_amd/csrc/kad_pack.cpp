@@ -1264,6 +1264,7 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   }
   for (bool ok : csr_ok)
     if (!ok) return P->fail(KAD_EINVAL, "CSR array exceeds 2^31 entries; split the batch");
+  lap("offsets");
   auto& req_off = X.req_off;
   req_off.resize((size_t)NR + 1);
   req_off[0] = 0;
@@ -1272,18 +1273,12 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
                nC = (size_t)o_cur[W], nP = (size_t)o_pref[W], nK = (size_t)o_key[W], nRQ = (size_t)req_off[NR];
   // KAD_BATCH_NARROW_PREFS: every value of the input preference maps fits int32 (pack.py applies the same
   // rule to the same maps, so both packers choose the same layout)
+  // The rule is checked where the values are read anyway: the rows pass below tests every input value (those
+  // of entries it skips too) and, when one does not fit, the layout and rows are redone wide (a second pass
+  // only for batches with out-of-range preference values).
   bool narrow = true;
-  {
-    auto fits = [](const int64_t* v, int64_t n) {
-      for (int64_t i = 0; i < n; i++)
-        if (v[i] < INT32_MIN || v[i] > INT32_MAX) return false;
-      return true;
-    };
-    narrow = fits(su->wt_val, su->wt_off[W]) && fits(su->min_val, su->min_off[W]) && fits(su->max_val, su->max_off[W]);
-    for (int w = 0; w < W && narrow; w++)
-      if (su->flags[w] & KAD_SU_HAS_AUTO_MIGRATION)
-        narrow = fits(su->cap_val + su->cap_off[w], su->cap_off[w + 1] - su->cap_off[w]);
-  }
+  std::atomic<bool> wide_seen{false};
+relayout:
   const size_t pv = narrow ? 4 : 8;  // bytes per preference value
   const size_t sizes[KAD_B_NARRAYS] = {
       4 * (size_t)W, 4 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 8 * (size_t)W, 4 * (size_t)W,
@@ -1386,7 +1381,9 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   struct PrefEntry {
     int32_t c, m, i;
   };
+  auto fits32 = [](int64_t v) { return v >= INT32_MIN && v <= INT32_MAX; };
   parallel_for(W, threads, [&](int a, int b) {
+    bool wide = false;  // an input value of this range outside int32 (the narrow rule)
     std::vector<int32_t> ids;
     std::vector<std::pair<int32_t, int64_t>> cl;
     std::vector<PrefEntry> pe;
@@ -1472,15 +1469,23 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
           dm[c] |= (uint8_t)(1u << m);
           set.add(c);
         };
-        for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++)
+        for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++) {
+          wide |= !fits32(su->wt_val[i]);
           if (wt_c[i] >= 0) put(wt_c[i], 0, su->wt_val[i]);
-        for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++)
+        }
+        for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++) {
+          wide |= !fits32(su->min_val[i]);
           if (min_c[i] >= 0) put(min_c[i], 1, su->min_val[i]);
-        for (int i = su->max_off[w]; i < su->max_off[w + 1]; i++)
+        }
+        for (int i = su->max_off[w]; i < su->max_off[w + 1]; i++) {
+          wide |= !fits32(su->max_val[i]);
           if (max_c[i] >= 0) put(max_c[i], 2, su->max_val[i]);
+        }
         if (am)
-          for (int i = su->cap_off[w]; i < su->cap_off[w + 1]; i++)
+          for (int i = su->cap_off[w]; i < su->cap_off[w + 1]; i++) {
+            wide |= !fits32(su->cap_val[i]);
             if (cap_c[i] >= 0 && su->cap_val[i] >= 0) put(cap_c[i], 3, su->cap_val[i]);
+          }
         int j = o_pref[w];
         set.drain([&](int c) {
           const uint8_t m = dm[c];
@@ -1494,6 +1499,11 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
         });
       } else {
       pe.clear();
+      for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++) wide |= !fits32(su->wt_val[i]);
+      for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++) wide |= !fits32(su->min_val[i]);
+      for (int i = su->max_off[w]; i < su->max_off[w + 1]; i++) wide |= !fits32(su->max_val[i]);
+      if (am)
+        for (int i = su->cap_off[w]; i < su->cap_off[w + 1]; i++) wide |= !fits32(su->cap_val[i]);
       for (int i = su->wt_off[w]; i < su->wt_off[w + 1]; i++)
         if (wt_c[i] >= 0) pe.push_back({wt_c[i], 0, i});
       for (int i = su->min_off[w]; i < su->min_off[w + 1]; i++)
@@ -1536,9 +1546,14 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
       }
       if (!nm.empty()) std::memcpy(kb, nm.data(), nm.size());
     }
+    if (wide) wide_seen.store(true, std::memory_order_relaxed);
   });
 
   lap("rows");
+  if (narrow && wide_seen.load()) {
+    narrow = false;
+    goto relayout;
+  }
   // tolerated-taint masks per toleration set (framework/util.go:406-450 via Toleration.ToleratesTaint)
   uint64_t* tol_all = reinterpret_cast<uint64_t*>(A(KAD_B_TOL_ALL));
   uint64_t* tol_pns = reinterpret_cast<uint64_t*>(A(KAD_B_TOL_PNS));

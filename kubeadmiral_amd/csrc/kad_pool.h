@@ -53,6 +53,23 @@ class Pool {
       return;
     }
     std::lock_guard<std::mutex> rg(run_mu_);  // one job at a time
+    run_locked(n, f);
+  }
+  // run() if no other thread's job holds the pool; false (nothing run) if one does
+  bool try_run(int n, const std::function<void(int)>& f) {
+    if (n <= 0) return true;
+    if (n == 1 || in_task() || th_.empty()) {
+      for (int t = 0; t < n; t++) f(t);
+      return true;
+    }
+    std::unique_lock<std::mutex> rg(run_mu_, std::try_to_lock);
+    if (!rg.owns_lock()) return false;
+    run_locked(n, f);
+    return true;
+  }
+
+ private:
+  void run_locked(int n, const std::function<void(int)>& f) {
     const int P = std::min(n, threads());
     err_ = nullptr;
     pending_.store(P - 1, std::memory_order_relaxed);
@@ -78,8 +95,6 @@ class Pool {
       std::rethrow_exception(e);
     }
   }
-
- private:
   static bool& in_task() {
     static thread_local bool flag = false;
     return flag;
@@ -145,21 +160,37 @@ inline Holder& holder() {
   return h;
 }
 
-// fork() child: only the forking thread exists; forget the parent's pool and reset the creation lock
+// the second pool (side_pool): 8 threads for the upload / download checks while another thread's job (a
+// packer's, in a pipelined caller) holds the main one
+inline Holder& side_holder() {
+  static Holder h;
+  return h;
+}
+
+// fork() child: only the forking thread exists; forget the parent's pools and reset the creation locks
 inline void on_fork_child() {
-  Holder& h = holder();
-  new (&h.mu) std::mutex();
-  h.p = nullptr;
+  for (Holder* h : {&holder(), &side_holder()}) {
+    new (&h->mu) std::mutex();
+    h->p = nullptr;
+  }
+}
+
+inline Pool& make(Holder& h, unsigned max_threads) {
+  static std::once_flag once;
+  std::call_once(once, [] { pthread_atfork(nullptr, nullptr, &on_fork_child); });
+  std::lock_guard<std::mutex> g(h.mu);
+  if (!h.p) h.p = new Pool((int)std::min<unsigned>(max_threads, std::max(1u, std::thread::hardware_concurrency())) - 1);
+  return *h.p;
 }
 
 // up to 16 threads (the GPU box's CPU share), created on first use (per process)
-inline Pool& pool() {
-  static std::once_flag once;
-  std::call_once(once, [] { pthread_atfork(nullptr, nullptr, &on_fork_child); });
-  Holder& h = holder();
-  std::lock_guard<std::mutex> g(h.mu);
-  if (!h.p) h.p = new Pool((int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())) - 1);
-  return *h.p;
+inline Pool& pool() { return make(holder(), 16u); }
+inline Pool& side_pool() { return make(side_holder(), 8u); }
+
+// a checks job: on the main pool when it is free, else on the side pool (created on first need) rather than
+// waiting behind the other thread's job
+inline void run_checks(int n, const std::function<void(int)>& f) {
+  if (!pool().try_run(n, f)) side_pool().run(n, f);
 }
 
 }  // namespace kadpool
