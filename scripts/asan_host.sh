@@ -10,7 +10,7 @@ cat > /tmp/kad_asan_run.py <<'PY'
 import ctypes, random, sys
 sys.path[:0] = [".", "tests"]
 from kubeadmiral_amd import runtime
-runtime._lib = ctypes.CDLL("/tmp/libkad_objects_asan.so")  # the bindings below only call kad_units_* / kad_applied_*
+runtime._lib = ctypes.CDLL("/tmp/libkad_objects_asan.so")  # the bindings below only call kad_units_* / kad_applied_* / kad_trigger_*
 import test_native_objects as t
 from kubeadmiral_amd import columns as K
 for seed in range(1, 6):
@@ -20,9 +20,17 @@ for seed in range(1, 6):
     t.assert_same(t.DEPLOY, objs, policies, threads=4)
     off, cl, rep = t._results(rng, len(objs))
     t.assert_apply_same(t.DEPLOY, objs, off, cl, rep, [True] * len(objs), [None] * len(objs), threads=4)
+    K.trigger_prefixes(t.DEPLOY, objs, policies, threads=4)
+    K.apply_results_ex(t.DEPLOY, objs, t.NAMES, off, cl, rep, trigger=[str(i) for i in range(len(objs))],
+                       ann_only=[i % 3 == 0 for i in range(len(objs))], threads=4)
+t.test_trigger_prefixes_match_python()
+t.test_apply_with_trigger_annotation_matches_python()
 bad = [b"", b"{", b"[", b'{"a":', b'"\\ud800', b"1e400", b'{"x": ' + b"[" * 2000 + b"]" * 2000 + b"}", b"\xff\xfe"]
 K.units_from_objects(t.DEPLOY, bad, [{"metadata": {"name": "p"}, "spec": {}}], threads=2)
 K.apply_results(t.DEPLOY, bad, t.NAMES, list(range(len(bad) + 1)), [0] * len(bad), [1] * len(bad))
+K.trigger_prefixes(t.DEPLOY, bad, [{"metadata": {"name": "p"}, "spec": {}}], threads=2)
+K.apply_results_ex(t.DEPLOY, bad, t.NAMES, list(range(len(bad) + 1)), [0] * len(bad), [1] * len(bad),
+                   trigger=["1"] * len(bad), ann_only=[i % 2 == 0 for i in range(len(bad))])
 print("sanitizers: clean")
 PY
 LD_PRELOAD="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)" ASAN_OPTIONS=detect_leaks=0 \

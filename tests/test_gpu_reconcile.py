@@ -139,13 +139,21 @@ def test_text_reconcile_matches_dict_reconcile():
     objs[16]["spec"]["template"]["spec"]["replicas"] = "5"       # getReplicaCount fails: trigger-error
     objs[17]["metadata"]["annotations"] = {"x": 1}               # not a string map: AddAnnotation replaces it
     objs[18]["metadata"].pop("annotations", None)
+    # a profile that exists, one that does not, and an auto-migration policy without its duration (:302 panics)
+    uniq = list(by_key.values())
+    uniq[0].spec.scheduling_profile = "p1"
+    uniq[1].spec.scheduling_profile = "gone"
+    am = [p for p in uniq[2:] if p.spec.auto_migration is not None]
+    if am:
+        am[0].spec.auto_migration.when.pod_unschedulable_for = None
+    profiles = {"p1": None}
     texts = [json.dumps(o) for o in objs]
-    ptexts = [json.dumps(O.policy_to_json(p)) for p in by_key.values()]
+    ptexts = [json.dumps(O.policy_to_json(p)) for p in uniq]
 
     want_objs = copy.deepcopy(objs)
-    want = BatchReconciler(ftc, native_objects=False).reconcile(want_objs, by_key, clusters)
+    want = BatchReconciler(ftc, native_objects=False).reconcile(want_objs, by_key, clusters, profiles)
     rec = BatchReconciler(ftc)
-    got, new = rec.reconcile_texts(texts, ptexts, clusters)
+    got, new = rec.reconcile_texts(texts, ptexts, clusters, profiles)
     stages = set()
     for i, (g, w) in enumerate(zip(got, want)):
         assert (g.stage, g.status) == (w.stage, w.status), (i, g.error, w.error)
@@ -156,10 +164,11 @@ def test_text_reconcile_matches_dict_reconcile():
             assert json.loads(new[i]) == want_objs[i], i
         else:
             assert new[i] is None, i
-    assert {"scheduled", "no-scheduling", "policy-not-found", "trigger-error"} <= stages
+    assert {"scheduled", "no-scheduling", "policy-not-found", "trigger-error", "profile-not-found"} <= stages
+    assert not am or "apply-error" in stages
 
     texts2 = [n if n is not None else t for n, t in zip(new, texts)]
-    again, new2 = rec.reconcile_texts(texts2, ptexts, clusters)
+    again, new2 = rec.reconcile_texts(texts2, ptexts, clusters, profiles)
     for i, g in enumerate(again):
         if got[i].stage in ("scheduled", "no-scheduling"):
             assert g.stage == "unchanged" and new2[i] is None, i
