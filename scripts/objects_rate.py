@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Host rates of the f2 / f3 object paths (no GPU): native kad_units_from_objects / kad_apply_results vs the
-Python restatement (objects.py), on seeded federated objects of tests/test_native_objects.py's generator.
+"""Host rates of the f2 / f3 / f4 object paths (no GPU): native kad_units_from_objects / kad_apply_results /
+kad_trigger_prefixes vs the Python restatement (objects.py), on seeded federated objects of tests/test_native_objects.py's generator.
 
     python scripts/objects_rate.py [--objects 100000] [--threads 16] [--out file.json]
 """
@@ -36,7 +36,8 @@ def main():
     K.units_from_objects(t.DEPLOY, texts[:1000], policies, threads=a.threads)  # pool warm-up
     for name, fn in (("units", lambda: K.units_from_objects(t.DEPLOY, texts, policies, threads=a.threads)),
                      ("apply", lambda: K.apply_results(t.DEPLOY, texts, t.NAMES, off, cl, rep, fol, th,
-                                                        threads=a.threads))):
+                                                        threads=a.threads)),
+                     ("trigger_prefixes", lambda: K.trigger_prefixes(t.DEPLOY, texts, policies, threads=a.threads))):
         best = 1e9
         for _ in range(3):
             t0 = time.perf_counter()
@@ -50,6 +51,24 @@ def main():
     t0 = time.perf_counter()
     t.python_apply(t.DEPLOY, texts[:n], off[:n + 1], cl, rep, fol, th)
     out["python_apply_objects_per_s"] = round(n / (time.perf_counter() - t0))
+    # objects.py's trigger prefix from the decoded objects (policy lookup as the reconcile does it)
+    from kubeadmiral_amd import objects as O
+
+    pols = {}
+    for p in policies:
+        try:
+            pols[(p["metadata"].get("namespace", ""), p["metadata"]["name"])] = O.PropagationPolicy.from_json(p)
+        except Exception:  # noqa: BLE001
+            pass
+    t0 = time.perf_counter()
+    for x in texts[:n]:
+        o = json.loads(x)
+        key = O.matched_policy_key(o, t.DEPLOY.namespaced)
+        try:
+            O.trigger_prefix(t.DEPLOY, o, pols.get(key) if key else None)
+        except O.ObjectError:
+            pass
+    out["python_trigger_prefixes_objects_per_s"] = round(n / (time.perf_counter() - t0))
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as f:
