@@ -1,7 +1,7 @@
 """BatchReconciler.reconcile_texts' host logic on the CPU: the device steps replaced by their checkers.
 
-The reconciler's context (trigger hashing, snapshot, schedule) is a stand-in that hashes with
-``oracle.triggers.fnv1_32`` and schedules with the C oracle (``oracle/ref.py``) on the same packed blobs, so the
+The reconciler's context (trigger hashing, snapshot, schedule) is a stand-in that hashes with the C restatement
+(``oracle/kad_trigger_ref.c``) and schedules with the C oracle (``oracle/ref.py``) on the same packed blobs, so the
 CPU suite covers what the text reconcile does around the device — the native trigger prefixes and policy lookup,
 the skip decisions, the per-profile unit builds and the annotated write-back — against the dict reconcile on
 ``objects.py`` (the same stand-in under it). The GPU test (tests/test_gpu_reconcile.py) runs both on the device.
@@ -16,7 +16,6 @@ from kubeadmiral_amd import objects as O
 from kubeadmiral_amd import synth
 from kubeadmiral_amd.controller import BatchReconciler
 from oracle import ref
-from oracle.triggers import fnv1_32
 
 
 class OracleContext:
@@ -46,7 +45,7 @@ class OracleContext:
         pass
 
     def trigger_download(self):
-        return np.array([fnv1_32(p + self.suffix) for p in self.prefixes], np.uint32)
+        return np.asarray(ref.trigger_hashes(self.prefixes, self.suffix), np.uint32)
 
 
 def _workload(seed, n=300):
