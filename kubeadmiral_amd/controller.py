@@ -321,6 +321,9 @@ class BatchReconciler:
                 out[i] = ReconcileOutcome(STATUS_ERROR, "policy-error", error=tr.messages[i])
                 continue
             p = pols[pol_of[i]] if pol_of[i] >= 0 else None
+            if p is None and pol_of[i] >= 0:  # the library decoded it but objects.py did not: not scheduled on
+                out[i] = ReconcileOutcome(STATUS_ERROR, "policy-error", error="policy does not decode")
+                continue
             if p is not None and p.spec.scheduling_profile and p.spec.scheduling_profile not in profiles:
                 out[i] = ReconcileOutcome(STATUS_ALL_OK, "profile-not-found")
                 continue
