@@ -224,26 +224,26 @@ def cpu_baseline(snap, batch, fwk, C, target_s):
 
 def verify_rows(snap, batch, fwk, res, want=None, n_want=0, max_units=200_000):
     """Parity of the timed run's rows against the C oracle (oracle/kad_ref.c), outside every timed region:
-    units [0, n_want) from the CPU baseline's own oracle pass when there was one, else 16 equal windows
-    spread over the batch holding ~max_units units. Rows compare status, count, (cluster, replicas) pairs
-    and result flags."""
+    units [0, n_want) from the CPU baseline's own oracle pass when there was one (and the rest of a batch of
+    at most max_units units by a pass of its own), else 16 equal windows spread over the batch holding
+    ~max_units units. Rows compare status, count, (cluster, replicas) pairs and result flags."""
     from oracle import ref
 
     W = batch.W
     threads = min(16, os.cpu_count() or 1)
     if want is not None and n_want > 0:
-        wins = [(0, n_want)]
+        wins = [(0, n_want, want)]
+        if n_want < W <= max_units:  # a time-bounded CPU pass stopped short: the remaining units too
+            wins.append((n_want, W, None))
+    elif W <= max_units:
+        wins = [(0, W, None)]
     else:
-        want = None
-        if W <= max_units:
-            wins = [(0, W)]
-        else:
-            span = max_units // 16
-            wins = [(W * i // 16, W * i // 16 + span) for i in range(16)]
+        span = max_units // 16
+        wins = [(W * i // 16, W * i // 16 + span, None) for i in range(16)]
     bad = 0
     first = None
-    for lo, hi in wins:
-        w = want if want is not None else ref.schedule(snap, batch, fwk, lo, hi, threads)
+    for lo, hi, have in wins:
+        w = have if have is not None else ref.schedule(snap, batch, fwk, lo, hi, threads)
         sl = slice(lo, hi)
         eq = np.ones(hi - lo, bool)
         eq &= (res.status[sl] == w.status[sl]) & (res.count[sl] == w.count[sl]) & (res.flags[sl] == w.flags[sl])
@@ -258,7 +258,7 @@ def verify_rows(snap, batch, fwk, res, want=None, n_want=0, max_units=200_000):
         if nb and first is None:
             first = lo + int(np.nonzero(~eq)[0][0])
         bad += nb
-    checked = sum(hi - lo for lo, hi in wins)
+    checked = sum(hi - lo for lo, hi, _ in wins)
     return {"units_checked": checked, "of": W, "mismatches": bad, "first_mismatch": first,
             "oracle": "oracle/kad_ref.c", "windows": len(wins)}
 
