@@ -56,6 +56,8 @@ WORKLOAD_DESC = {
     "c2": "100k SchedulingUnits x 256 FederatedClusters: Fit+Taint+Affinity(+APIResources) filters, "
           "LeastAllocated score, MaxCluster select, Duplicate",
     "c3": "1M SchedulingUnits x 1k FederatedClusters (c2 generator), sharded over the GPUs",
+    "c3r": "c3 with production-shaped snapshots: ~150 Kind-sorted discovery API resources per cluster "
+           "(clusterstatus.go:221-266) and units over 8 workload kinds",
     "c4": "1M Divide SchedulingUnits x 512 clusters: weights, min/max replicas, capacity caps",
     "c5": "100k SchedulingUnits x 10k clusters: dense label affinity, many taints, API-resource gaps",
     "t1": "scheduling-trigger hashes: 1k federated Deployments x 16 joined clusters",
@@ -94,7 +96,11 @@ def make_clusters(cfg: str, C: int):
     if cfg == "c5":
         return synth.gen_clusters(rng, C, n_keys=64, n_vals=16, n_int_keys=4, n_taints=256, taints_per=(4, 16),
                                   p_gvk=0.9, gvks=synth.GVKS)
-    return synth.gen_clusters(rng, C)
+    cl = synth.gen_clusters(rng, C)
+    if cfg == "c3r":  # C3's clusters with discovery-shaped API-resource lists (their own random stream)
+        for c, api in zip(cl, synth.discovery_api_resources(np.random.default_rng([synth.SEEDS[cfg], 0xA91]), C)):
+            c.api_resource_types = api
+    return cl
 
 
 def make_columns(cfg: str, lo: int, hi: int, clusters):
@@ -105,6 +111,8 @@ def make_columns(cfg: str, lo: int, hi: int, clusters):
     rng = np.random.default_rng([synth.SEEDS[cfg], lo])
     if cfg in ("c2", "c3"):
         return synth.gen_units_c2_columns(rng, hi - lo, prefix=f"su{lo}")
+    if cfg == "c3r":  # C3's units (same stream) over 8 workload kinds
+        return synth.gen_units_c2_columns(rng, hi - lo, prefix=f"su{lo}", workloads=synth.C3R_WORKLOADS)
     if cfg == "c4":  # vectorised generators: 1M C4 units in seconds (the object generator takes minutes)
         return synth.gen_units_c4_columns(rng, hi - lo, [c.name for c in clusters], prefix=f"c4-{lo}")
     if cfg == "c5":
@@ -896,7 +904,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the embedded C2/C4/C5 lines of the default run")
-    ap.add_argument("--extras", default="c2,c4,c5", help="configs embedded under `extra` in the default C3 run")
+    ap.add_argument("--extras", default="c3r,c2,c4,c5", help="configs embedded under `extra` in the default C3 run")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 shard-size sweep of the default run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pack -> upload -> schedule -> download timing")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),

@@ -29,8 +29,9 @@ struct SnapDev {
   int C, GW, TW, K, S;
   int clean;  // host: every cluster's cpu/mem fit the lean kernel's exact-f64 path (kad_api.hip res_clean)
   // TW <= TFOLD_MAX_TW: prep_kernel folds TaintToleration's and APIResources' filters into each unit's
-  // static filter words from per-id cluster bitmask slices ([128*TW + 64][nch]: rows t < 64*TW the
-  // NoSchedule|NoExecute taint id t, rows 64*TW + t the NoExecute taint id t, rows 128*TW + g GVK id g),
+  // static filter words from per-id cluster bitmask slices ([128*TW + 64*GW][nch]: rows t < 64*TW the
+  // NoSchedule|NoExecute taint id t, rows 64*TW + t the NoExecute taint id t, rows 128*TW + g GVK id g of
+  // any GVK word — a discovery list of ~150 API resources per cluster is 3 words, clusterstatus.go:221-266),
   // so the schedule kernels only test resource fit per lane (or nothing, with SnapDev::fitfold)
   int fold;
   uint64_t present_taints[TFOLD_MAX_TW];  // per taint word: OR of every cluster's NoSchedule|NoExecute word

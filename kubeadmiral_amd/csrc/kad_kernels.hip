@@ -865,13 +865,13 @@ __device__ __forceinline__ void id_list_words(const int32_t* ids, int lo, int hi
 }
 
 // SnapDev::slices row r (r < 64*TW: NoSchedule|NoExecute taint id r; r < 128*TW: NoExecute taint id
-// r - 64*TW; else GVK id r - 128*TW of word 0), chunk ch: one wave per (row, ch), lane = cluster
+// r - 64*TW; else GVK id r - 128*TW, any of the GW words), chunk ch: one wave per (row, ch), lane = cluster
 __global__ __launch_bounds__(256) void slice_kernel(SnapDev s, uint64_t* out) {
   const int lane = lane_id();
   const int nch = (s.C + 63) >> 6;
   const int TW = s.TW;
   const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gw >= (128L * TW + 64) * nch) return;
+  if (gw >= (128L * TW + 64L * s.GW) * nch) return;
   const int ch = (int)(gw % nch), r = (int)(gw / nch);
   const int c = ch * WAVE + lane;
   const uint32_t cl = c < s.C ? (uint32_t)c : 0u;
@@ -883,8 +883,9 @@ __global__ __launch_bounds__(256) void slice_kernel(SnapDev s, uint64_t* out) {
     word = r < 64 * TW ? ldg(s.nsne, at) : ldg(s.ne, at);
     bit = t & 63;
   } else {
-    word = ldg(s.gvk, cl);
-    bit = r - 128 * TW;
+    const int g = r - 128 * TW;
+    word = ldg(s.gvk, (uint32_t)(g >> 6) * (uint32_t)s.C + cl);
+    bit = g & 63;
   }
   const uint64_t m = ballot(c < s.C && ((word >> bit) & 1));
   if (lane == 0) out[(size_t)r * nch + ch] = m;
@@ -945,10 +946,11 @@ __device__ __forceinline__ void folded_words(const SnapDev& s, uint32_t fm, uint
 #pragma unroll
     for (int k = 0; k < CPL; k++) out[k] = cur ? ((cw[k] & ~bad_ne[k]) | (~cw[k] & ~bad_ns[k])) : ~bad_ns[k];
   }
-  if (fm & (1u << KAD_PL_API_RESOURCES)) {
-    const uint64_t* rg = s.slices + ((size_t)128 * s.TW + (gvk >= 0 && gvk < 64 ? gvk : 0)) * nch;
+  if (fm & (1u << KAD_PL_API_RESOURCES)) {  // any GVK id of the snapshot's GW words (-1: no cluster has it)
+    const bool has = gvk >= 0 && gvk < 64 * s.GW;
+    const uint64_t* rg = s.slices + ((size_t)128 * s.TW + (has ? gvk : 0)) * nch;
 #pragma unroll
-    for (int k = 0; k < CPL; k++) out[k] &= (gvk >= 0 && gvk < 64) ? rg[cc[k]] : 0ull;
+    for (int k = 0; k < CPL; k++) out[k] &= has ? rg[cc[k]] : 0ull;
   }
 }
 
@@ -1021,7 +1023,8 @@ __global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDe
   const int32_t so0 = b.sreq_off[w], so1 = b.sreq_off[w + 1];
   const uint64_t tol0 = b.tol_all[(size_t)tolset * b.TW], tolp0 = b.tol_pns[(size_t)tolset * b.TW];
   bool full = force_full != 0;
-  if ((fm & (1u << KAD_PL_API_RESOURCES)) && gvk >= 64) full = true;
+  // the unfolded schedule kernels cache GVK word 0 only; folded snapshots take every GVK id from the slices
+  if ((fm & (1u << KAD_PL_API_RESOURCES)) && gvk >= 64 && !s.fold) full = true;
   if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && so0 < so1) full = true;
   const uint32_t rflags = f | (((f & KAD_W_HAS_DESIRED) && desired > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
   const bool act = ch0 < nch && !(f & KAD_W_STICKY);
@@ -3765,12 +3768,12 @@ hipError_t launch_res_cols(const SnapDev& s, void* buf, hipStream_t st) {
 hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
-  const long waves = (128L * s.TW + 64) * nch;
+  const long waves = (128L * s.TW + 64L * s.GW) * nch;
   if (waves == 0) return hipSuccess;
   hipLaunchKernelGGL(slice_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, s, slices);
   const long lanes = 2L * 8 * s.TW * 256 * nch;
   hipLaunchKernelGGL(taint_table_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, s,
-                     slices + (128L * s.TW + 64) * nch);
+                     slices + (128L * s.TW + 64L * s.GW) * nch);
   return hipGetLastError();
 }
 

@@ -33,14 +33,107 @@ GVKS = [("apps", "v1", "Deployment"), ("apps", "v1", "StatefulSet"), ("apps", "v
         ("batch", "v1", "Job"), ("", "v1", "ConfigMap"), ("", "v1", "Service"), ("batch", "v1", "CronJob"),
         ("networking.k8s.io", "v1", "Ingress")]
 
-SEEDS = {"c1": 0xC1, "c2": 0xC2, "c3": 0xC3, "c4": 0xC4, "c5": 0xC5}
+SEEDS = {"c1": 0xC1, "c2": 0xC2, "c3": 0xC3, "c4": 0xC4, "c5": 0xC5, "c3r": 0xC3}
 SIZES = {"c1": (1000, 16), "c2": (100_000, 256), "c3": (1_000_000, 1000), "c4": (1_000_000, 512),
-         "c5": (100_000, 10_000)}
+         "c5": (100_000, 10_000), "c3r": (1_000_000, 1000)}
+
+# ------------------------------------------------------- production-shaped API-resource lists
+# What a member cluster's discovery returns (kube 1.26 built-ins and commonly installed operators' CRDs), as
+# FederatedCluster.Status.APIResourceTypes holds it: updateClusterAPIResources
+# (pkg/controllers/federatedcluster/clusterstatus.go:204-268) keeps every resource of every group version
+# whose name has no "/" (subresources skipped, :239-241) and sorts the list by Kind (:262-264). The same Kind
+# appears under several group versions (autoscaling/v1 and v2 HorizontalPodAutoscaler, core and events.k8s.io
+# Event, ...). Go's sort.Slice is unstable, so the order among equal Kinds is pdqsort's; here it is discovery
+# order (a stable sort) — the order only decides the snapshot's GVK ids, never a scheduling result.
+_BUILTIN_API = [
+    ("", "v1", ["Binding", "ComponentStatus", "ConfigMap", "Endpoints", "Event", "LimitRange", "Namespace", "Node",
+                "PersistentVolumeClaim", "PersistentVolume", "Pod", "PodTemplate", "ReplicationController",
+                "ResourceQuota", "Secret", "ServiceAccount", "Service"]),
+    ("admissionregistration.k8s.io", "v1", ["MutatingWebhookConfiguration", "ValidatingWebhookConfiguration"]),
+    ("apiextensions.k8s.io", "v1", ["CustomResourceDefinition"]),
+    ("apiregistration.k8s.io", "v1", ["APIService"]),
+    ("apps", "v1", ["ControllerRevision", "DaemonSet", "Deployment", "ReplicaSet", "StatefulSet"]),
+    ("authentication.k8s.io", "v1", ["TokenReview"]),
+    ("authorization.k8s.io", "v1", ["LocalSubjectAccessReview", "SelfSubjectAccessReview", "SelfSubjectRulesReview",
+                                    "SubjectAccessReview"]),
+    ("autoscaling", "v1", ["HorizontalPodAutoscaler"]),
+    ("autoscaling", "v2", ["HorizontalPodAutoscaler"]),
+    ("batch", "v1", ["CronJob", "Job"]),
+    ("certificates.k8s.io", "v1", ["CertificateSigningRequest"]),
+    ("coordination.k8s.io", "v1", ["Lease"]),
+    ("discovery.k8s.io", "v1", ["EndpointSlice"]),
+    ("events.k8s.io", "v1", ["Event"]),
+    ("flowcontrol.apiserver.k8s.io", "v1beta2", ["FlowSchema", "PriorityLevelConfiguration"]),
+    ("flowcontrol.apiserver.k8s.io", "v1beta3", ["FlowSchema", "PriorityLevelConfiguration"]),
+    ("networking.k8s.io", "v1", ["IngressClass", "Ingress", "NetworkPolicy"]),
+    ("node.k8s.io", "v1", ["RuntimeClass"]),
+    ("policy", "v1", ["PodDisruptionBudget"]),
+    ("rbac.authorization.k8s.io", "v1", ["ClusterRoleBinding", "ClusterRole", "RoleBinding", "Role"]),
+    ("scheduling.k8s.io", "v1", ["PriorityClass"]),
+    ("storage.k8s.io", "v1", ["CSIDriver", "CSINode", "CSIStorageCapacity", "StorageClass", "VolumeAttachment"]),
+    ("metrics.k8s.io", "v1beta1", ["NodeMetrics", "PodMetrics"]),
+]
+# operators: a cluster has each one's whole group (p = 0.9), so some clusters lack a kind (API-resource gaps)
+_OPERATOR_API = [
+    ("cert-manager.io", "v1", ["Certificate", "CertificateRequest", "ClusterIssuer", "Issuer"]),
+    ("acme.cert-manager.io", "v1", ["Challenge", "Order"]),
+    ("monitoring.coreos.com", "v1", ["Alertmanager", "PodMonitor", "Probe", "Prometheus", "PrometheusRule",
+                                     "ServiceMonitor", "ThanosRuler"]),
+    ("monitoring.coreos.com", "v1alpha1", ["AlertmanagerConfig"]),
+    ("argoproj.io", "v1alpha1", ["AnalysisRun", "AnalysisTemplate", "ClusterAnalysisTemplate", "Experiment",
+                                 "Rollout"]),
+    ("apps.kruise.io", "v1alpha1", ["AdvancedCronJob", "BroadcastJob", "CloneSet", "DaemonSet", "ImagePullJob",
+                                    "NodeImage", "ResourceDistribution", "SidecarSet", "UnitedDeployment",
+                                    "WorkloadSpread"]),
+    ("apps.kruise.io", "v1beta1", ["StatefulSet"]),
+    ("snapshot.storage.k8s.io", "v1", ["VolumeSnapshotClass", "VolumeSnapshotContent", "VolumeSnapshot"]),
+    ("networking.istio.io", "v1beta1", ["DestinationRule", "Gateway", "ServiceEntry", "Sidecar", "VirtualService",
+                                        "WorkloadEntry", "WorkloadGroup"]),
+    ("security.istio.io", "v1beta1", ["AuthorizationPolicy", "PeerAuthentication", "RequestAuthentication"]),
+    ("keda.sh", "v1alpha1", ["ClusterTriggerAuthentication", "ScaledJob", "ScaledObject", "TriggerAuthentication"]),
+    ("velero.io", "v1", ["Backup", "BackupStorageLocation", "DeleteBackupRequest", "DownloadRequest",
+                         "PodVolumeBackup", "PodVolumeRestore", "Restore", "Schedule", "ServerStatusRequest",
+                         "VolumeSnapshotLocation"]),
+]
+# workload kinds a federation schedules (FederatedTypeConfig targets): the c3r units' GVKs and their shares
+C3R_WORKLOADS = [(("apps", "v1", "Deployment"), 0.40), (("apps", "v1", "StatefulSet"), 0.15),
+                 (("apps", "v1", "DaemonSet"), 0.10), (("batch", "v1", "Job"), 0.10),
+                 (("batch", "v1", "CronJob"), 0.05), (("", "v1", "Service"), 0.10),
+                 (("argoproj.io", "v1alpha1", "Rollout"), 0.05), (("apps.kruise.io", "v1alpha1", "CloneSet"), 0.05)]
+
+
+def discovery_api_resources(rng: np.random.Generator, C: int, n_extra_crds: int = 40, p_operator: float = 0.9,
+                            p_builtin: float = 1.0):
+    """C clusters' ``APIResourceTypes`` shaped like updateClusterAPIResources' output (module comment above):
+    the ~60 built-in resources (each with probability ``p_builtin``: 1 on real clusters), each operator's
+    group with probability ``p_operator``, and ``n_extra_crds`` single-kind CRDs with probability
+    ``p_operator`` each; Kind-sorted. About 150 entries per cluster (3 GVK words)."""
+    def res(groups):
+        out = []
+        for g, v, kinds in groups:
+            for k in kinds:
+                out.append(T.APIResource(g, v, k, k.lower() + "s", "Namespaced"))
+        return out
+
+    builtin = res(_BUILTIN_API)
+    ops = [res([grp]) for grp in _OPERATOR_API]
+    extra = [T.APIResource(f"crd{i // 4}.example.com", "v1", f"Custom{i:02d}", f"custom{i:02d}s", "Namespaced")
+             for i in range(n_extra_crds)]
+    lists = []
+    for _ in range(C):
+        lst = list(builtin) if p_builtin >= 1.0 else [r for r, k in zip(builtin, rng.random(len(builtin)) < p_builtin) if k]
+        for grp, keep in zip(ops, rng.random(len(ops)) < p_operator):
+            if keep:
+                lst.extend(grp)
+        lst.extend(r for r, keep in zip(extra, rng.random(len(extra)) < p_operator) if keep)
+        lst.sort(key=lambda r: r.kind)  # clusterstatus.go:262-264 (stable here, see module comment)
+        lists.append(lst)
+    return lists
 
 
 def profile_for(config: str) -> F.Framework:
     """The plugin set each config is quoted on (BASELINE.json configs)."""
-    if config in ("c2", "c3"):
+    if config in ("c2", "c3", "c3r"):
         return F.Framework(F.EnabledPlugins(
             [F.APIResources, F.TaintToleration, F.ClusterResourcesFit, F.ClusterAffinity],
             [F.ClusterResourcesLeastAllocated], [F.MaxCluster], [F.ClusterCapacityWeight]))
@@ -221,6 +314,17 @@ def make_config(config: str, scale: float = 1.0, seed: Optional[int] = None, W: 
     if config in ("c2", "c3"):
         cl = gen_clusters(rng, C)
         return cl, gen_units_c2(rng, W), profile_for(config)
+    if config == "c3r":
+        cl = gen_clusters(rng, C)
+        for c, api in zip(cl, discovery_api_resources(np.random.default_rng([SEEDS[config], 0xA91]), C)):
+            c.api_resource_types = api
+        units = gen_units_c2(rng, W)
+        r2 = np.random.default_rng([SEEDS[config], 0x6E7])
+        gv = [g for g, _ in C3R_WORKLOADS]
+        share = np.array([p for _, p in C3R_WORKLOADS])
+        for su, i in zip(units, r2.choice(len(gv), size=W, p=share / share.sum())):
+            su.group, su.version, su.kind = gv[i]
+        return cl, units, profile_for(config)
     if config == "c4":
         cl = gen_clusters(rng, C)
         return cl, gen_units_c4(rng, W, cl), profile_for(config)
@@ -334,6 +438,20 @@ def gen_fuzz(seed: int, W: int = 60, C: Optional[int] = None, n_taints: int = 9)
             max_clusters=(int(rng.integers(-1, 8)) if r() < 0.8 else None), min_replicas=mins, max_replicas=maxs,
             weights=weights))
     return cl, units
+
+
+def with_discovery(clusters, units, seed: int, p_operator: float = 0.7, p_builtin: float = 0.9):
+    """``clusters`` (in place) with discovery-shaped API-resource lists (:func:`discovery_api_resources`, with
+    gaps in the built-ins too) and ``units`` (in place) over :data:`C3R_WORKLOADS`' kinds plus one kind no
+    cluster serves: GVK ids past the first 64 (the snapshot interns ~150). Returns (clusters, units)."""
+    rng = np.random.default_rng([seed, 0xD15C])
+    for c, api in zip(clusters, discovery_api_resources(rng, len(clusters), p_operator=p_operator,
+                                                        p_builtin=p_builtin)):
+        c.api_resource_types = api
+    kinds = [g for g, _ in C3R_WORKLOADS] + [("example.com", "v1", "NowhereServed")]
+    for su, i in zip(units, rng.integers(0, len(kinds), len(units))):
+        su.group, su.version, su.kind = kinds[int(i)]
+    return clusters, units
 
 
 FUZZ_PROFILES = [
@@ -461,10 +579,14 @@ def mutate_clusters(rng: np.random.Generator, clusters: List[T.FederatedCluster]
 
 # ------------------------------------------------------------ columnar generator (native packer input)
 def gen_units_c2_columns(rng: np.random.Generator, W: int, n_keys=8, n_vals=8, n_taints=16,
-                         mode=T.SCHEDULING_MODE_DUPLICATE, prefix="su"):
+                         mode=T.SCHEDULING_MODE_DUPLICATE, prefix="su", workloads=None):
     """The C2/C3 workload of :func:`gen_units_c2` (same distributions, its own random stream) generated
     directly as ``columns.SUColumns`` with numpy — the packer input a Go shim would hand over — so 1M-unit
-    batches (C3) are generated in about a second instead of minutes of Python objects."""
+    batches (C3) are generated in about a second instead of minutes of Python objects.
+
+    ``workloads``: [((group, version, kind), share), ...] — each unit's GVK drawn with these shares (c3r:
+    :data:`C3R_WORKLOADS`) after every other column, so the rest of the batch equals the one without it;
+    default: every unit an apps/v1 Deployment."""
     from . import columns as CO
 
     st = CO.StringTable()
@@ -539,6 +661,14 @@ def gen_units_c2_columns(rng: np.random.Generator, W: int, n_keys=8, n_vals=8, n
     for kname, dt in CO.FIELDS:
         if kname not in cols:
             cols[kname] = np.zeros(0, dt)
+    if workloads:
+        gvks = [wk for wk, _ in workloads]
+        share = np.array([p for _, p in workloads], np.float64)
+        pick = rng.choice(len(gvks), size=W, p=share / share.sum())
+        # the string table already holds every unit name: new strings go after them
+        ids = np.array([[st.id(x) for x in g] for g in gvks], np.int32)
+        str_off, str_data = st.arrays()
+        cols["group"], cols["version"], cols["kind"] = ids[pick, 0], ids[pick, 1], ids[pick, 2]
     return CO.SUColumns(W, str_off, str_data, cols)
 
 

@@ -67,6 +67,26 @@ def test_c_oracle_matches_python_oracle_many_taint_words(seed, n_taints):
         assert not bad, (i, bad[:3])
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_c_oracle_matches_python_oracle_discovery_lists(seed):
+    """Production-shaped API-resource lists (~150 Kind-sorted discovery entries per cluster, 3 GVK words;
+    clusterstatus.go:221-266) with units over 8 workload kinds and one no cluster serves: APIResources.Filter
+    (apiresources.go:25-43) on GVK ids past the first word, under every fuzz profile."""
+    clusters, units = synth.with_discovery(*synth.gen_fuzz(700 + seed, W=40), seed)
+    snap = pack.Snapshot(clusters)
+    assert snap.GW >= 3 and max(snap.gvk_id.values()) >= 128
+    bad = compare(clusters, units, synth.fuzz_framework(seed))
+    assert not bad, bad[:3]
+
+
+def test_c_oracle_matches_python_oracle_c3r_small():
+    clusters, units, fwk = synth.make_config("c3r", W=150, C=64)
+    snap = pack.Snapshot(clusters)
+    assert snap.GW >= 3
+    assert sum(snap.gvk_id[(su.group, su.version, su.kind)] >= 64 for su in units) > 50
+    assert not compare(clusters, units, fwk)
+
+
 def test_c_oracle_matches_python_oracle_c1():
     clusters, units, fwk = synth.make_config("c1", W=200)
     assert not compare(clusters, units, fwk, n_threads=4)

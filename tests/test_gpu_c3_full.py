@@ -23,25 +23,43 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 W, C = 1_000_000, 1000
 
 
-@pytest.fixture(scope="module")
-def full_c3():
+def _full(cfg):
     import torch  # noqa: F401  (the HIP runtime is torch's: initialise it before libkad.so)
     sys.path.insert(0, ROOT)
     import bench
     from kubeadmiral_amd import build, runtime
     build.build()
-    clusters = bench.make_clusters("c3", C)
-    cols = bench.make_columns("c3", 0, W, clusters)
+    clusters = bench.make_clusters(cfg, C)
+    cols = bench.make_columns(cfg, 0, W, clusters)
     snap = pack.Snapshot(clusters)
-    fwk = synth.profile_for("c3")
+    fwk = synth.profile_for(cfg)
     nb = CO.NativePacker(snap).pack(fwk, cols)
     ctx = runtime.Context(0)
     ctx.upload_snapshot(snap)
     ctx.upload_batch(nb)
     ctx.schedule(fwk)
     res = ctx.download()
-    yield ctx, snap, nb, cols, fwk, res
-    ctx.close()
+    return ctx, snap, nb, cols, fwk, res
+
+
+@pytest.fixture(scope="module")
+def full_c3():
+    out = _full("c3")
+    yield out
+    out[0].close()
+
+
+def test_c3r_full_equals_c_oracle():
+    """c3r at full size: C3 with ~150 Kind-sorted discovery API resources per cluster (3 GVK words) and units
+    over 8 workload kinds — the APIResources filter on GVK ids past word 0 stays on the folded fast path (no
+    unit on the full kernel) and every row equals the C oracle's."""
+    ctx, snap, nb, cols, fwk, res = _full("c3r")
+    try:
+        assert snap.GW == 3
+        assert ctx.path_counts()["full_kernel"] == 0
+        assert_same(res, c_oracle(snap, nb, fwk), "c3r 1M x 1000")
+    finally:
+        ctx.close()
 
 
 def test_c3_full_equals_c_oracle(full_c3):

@@ -278,6 +278,34 @@ def test_c3_long_lists_routed_beside_the_wide_kernel(ctx, seed):
     assert_same(res, c_oracle(snap, batch, fwk), f"c3 long lists seed {seed}")
 
 
+@pytest.mark.parametrize("seed,C,n_taints", [(7301, 30, 9), (7302, 300, 9), (7303, 1000, 9), (7304, 3000, 9),
+                                             (7305, 800, 160), (7306, 500, 300)])
+def test_fuzz_discovery_lists(ctx, seed, C, n_taints):
+    """Production-shaped API-resource lists (~150 Kind-sorted discovery entries per cluster, GVK ids in 3
+    words; clusterstatus.go:221-266) with units over 8 workload kinds and one no cluster serves, under every
+    fuzz profile against the C oracle: APIResources.Filter (apiresources.go:25-43) from any GVK word's slice
+    on folded snapshots (TW <= 4), from the full kernel on unfolded ones (the last case, TW = 5)."""
+    clusters, units = synth.with_discovery(*synth.gen_fuzz(seed, W=120, C=C, n_taints=n_taints), seed)
+    for i in range(len(synth.FUZZ_PROFILES)):
+        fwk = synth.fuzz_framework(i)
+        snap, batch, res = run(ctx, clusters, units, fwk)
+        assert snap.GW >= 3
+        assert_same(res, c_oracle(snap, batch, fwk), f"discovery fuzz seed {seed} profile {i}")
+
+
+def test_c3r_clusters_1000(ctx):
+    """c3r on 20k units: C3's generator with discovery-shaped API-resource lists and 8 workload kinds (most
+    GVK ids >= 64). No unit may fall to the one-wave-per-unit full kernel (GVK ids past word 0
+    routed there), and every row equals the C oracle's."""
+    clusters, units, fwk = synth.make_config("c3r", W=20_000)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    gv = [snap.gvk_id.get((su.group, su.version, su.kind), -1) for su in units]
+    assert sum(g >= 64 for g in gv) > 0.5 * len(units)
+    assert ctx.path_counts()["full_kernel"] == 0
+    assert (res.status == pack.ST_OK).mean() > 0.5
+    assert_same(res, c_oracle(snap, batch, fwk), "c3r 20k x 1000")
+
+
 def test_c3_default_set_divide_subrun(ctx):
     """'a parity sub-run with the full default plugin set in Divide mode' (C = 1000)."""
     rng = np.random.default_rng(synth.SEEDS["c3"] + 1)
