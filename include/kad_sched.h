@@ -59,6 +59,7 @@ extern "C" {
 #define KAD_ENOMEM -3       /* device allocation failed                     */
 #define KAD_ESTATE -4       /* e.g. schedule before snapshot/batch upload   */
 #define KAD_EUNSUPPORTED -5 /* plugin not in the in-tree set (webhook)      */
+#define KAD_EHOST -6        /* other host-side failure (e.g. a pool thread could not start) */
 
 /* ------------------------------------------------------------- plugins
  * In-tree plugin ids = bit positions in kad_profile masks.
@@ -363,6 +364,52 @@ int kad_results_copy_device(kad_ctx* ctx, const kad_result_view* dev_out);
 /* All in one: upload batch, schedule, download (blocking). */
 int kad_schedule_batch(kad_ctx* ctx, const kad_profile* profile, const void* batch_blob, size_t nbytes,
                        const kad_result_view* out);
+
+/* ---------------------------------------------------- multi-GPU group
+ * One process driving N GPUs of a node: the reference runs one scheduler process whose --worker-count
+ * goroutines call Schedule (worker.go:132-134, scheduler.go:507), and units are independent given the
+ * read-only cluster list (scheduler.go:246-309), so a batch splits into N contiguous unit ranges with no
+ * exchange while scheduling. A kad_group holds one kad_ctx per listed device (a device may repeat: the
+ * members then share it, e.g. tests on one GPU) and one host thread per member, so every member's
+ * uploads, launches and copies are issued concurrently.
+ *   kad_group_snapshot_upload: H2D to member 0, then device to device to the others (xGMI peer copies);
+ *                              each member rebuilds its derived snapshot state on its own device.
+ *   kad_group_snapshot_update: the delta applied on every member.
+ *   kad_group_batch_upload   : the whole blob validated once; member i takes units
+ *                              [unit_lo[i], unit_lo[i+1]) (kad_batch_split) and H2Ds only the blob bytes
+ *                              those units read (their per-unit entries, their CSR data, the batch-wide
+ *                              tables) into a buffer of the blob's layout.
+ *   kad_group_schedule       : every member's pipeline, asynchronous on its stream.
+ *   kad_group_results_download: each member writes its units' status / count / flags at unit_lo[i] and
+ *                              its slots at slot_lo[i] = OUT_OFF[unit_lo[i]] of the ONE caller view sized
+ *                              for the whole batch — the same bytes as one kad_ctx over the whole batch.
+ * A kad_group is internally serialised (a mutex), like a kad_ctx. */
+typedef struct kad_group kad_group;
+int kad_group_create(const int* hip_devices, int n, kad_group** out);
+int kad_group_destroy(kad_group* group);
+const char* kad_group_last_error(kad_group* group);
+int kad_group_size(kad_group* group);
+int kad_group_snapshot_upload(kad_group* group, const void* blob, size_t nbytes);
+int kad_group_snapshot_update(kad_group* group, const void* delta, size_t nbytes);
+int kad_group_batch_upload(kad_group* group, const void* blob, size_t nbytes);
+int kad_group_schedule(kad_group* group, const kad_profile* profile);
+int kad_group_sync(kad_group* group);
+int kad_group_results_download(kad_group* group, const kad_result_view* out);
+/* All in one: upload batch, schedule on every member, download (blocking). */
+int kad_group_schedule_batch(kad_group* group, const kad_profile* profile, const void* batch_blob, size_t nbytes,
+                             const kad_result_view* out);
+/* The resident batch's split: unit_lo[n+1], slot_lo[n+1]. */
+int kad_group_ranges(kad_group* group, int64_t* unit_lo, int64_t* slot_lo);
+/* kad_path_counts summed over the members; kad_set_timing on every member. */
+int kad_group_path_counts(kad_group* group, int32_t* out);
+int kad_group_set_timing(kad_group* group, int on);
+/* Member i's kad_ctx, for per-member instrumentation only (kad_stage_timing, kad_path_counts): it
+ * schedules units [unit_lo[i], unit_lo[i+1]) of the group's batch; its own kad_results_download writes
+ * them at offset 0. */
+int kad_group_member(kad_group* group, int i, kad_ctx** out);
+/* Host only (no device): the split kad_group_batch_upload makes of a packed batch blob for n members —
+ * unit_lo[i] = W*i/n, slot_lo[i] = OUT_OFF[unit_lo[i]], i = 0..n. */
+int kad_batch_split(const void* batch_blob, size_t nbytes, int n, int64_t* unit_lo, int64_t* slot_lo);
 
 /* ---------------------------------------------------- stage entry points
  * The select and planner stages on caller-provided rows, for parity tests of

@@ -26,11 +26,13 @@ from .framework import Framework
 
 
 class CoalescingScheduler:
-    def __init__(self, scheduler=None, max_batch: int = 65536, max_wait_s: float = 0.002, device: int = 0):
+    def __init__(self, scheduler=None, max_batch: int = 65536, max_wait_s: float = 0.002, device: int = 0,
+                 devices=None):
+        """``devices``: run each gathered batch split over these GPUs (runtime.GroupContext)."""
         if scheduler is None:
             from .runtime import BatchScheduler
 
-            scheduler = BatchScheduler(device=device)
+            scheduler = BatchScheduler(device=device, devices=devices)
         self.scheduler = scheduler
         self.max_batch = max_batch
         self.max_wait_s = max_wait_s

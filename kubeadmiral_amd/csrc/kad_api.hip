@@ -72,6 +72,9 @@ struct kad_ctx {
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
   bool have_snapshot = false, have_batch = false, ran = false;
+  // the resident batch's units this ctx schedules: all of them, or a kad_group member's contiguous shard
+  // [unit_lo, unit_lo + unit_n) whose output slots are [slot_lo, slot_lo + slot_n) of the batch's
+  int64_t unit_lo = 0, unit_n = 0, slot_lo = 0, slot_n = 0;
   int inject_fault = 0;  // kad_debug_inject_fault: 1 = the next refresh_derived fails (tests)
   int plan_force_ws = 0;  // kad_debug_plan_force_workspace: kad_plan_rows through the workspace planner (tests)
   void* d_diff = nullptr;  // kad_result_diff: canonical object state + flags
@@ -82,7 +85,7 @@ struct kad_ctx {
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
   std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
   std::vector<uint64_t> h_ns;  // host shadow of the NoSchedule|NoExecute taint words [TW][C] (SnapDev::present_taints)
-  void* d_slices = nullptr;    // SnapDev::slices [128*TW + 64][nch], then SnapDev::taint_tab [2][8*TW][256][nch]
+  void* d_slices = nullptr;    // SnapDev::slices [128*TW + 64*GW][nch], then SnapDev::taint_tab [2][8*TW][256][nch]
   size_t slices_cap = 0;
   std::vector<int64_t> h_fit;  // SnapDev::fit_vals / fit_rows (host copy the upload reads from)
   void* d_fit = nullptr;
@@ -124,8 +127,10 @@ static int guarded(kad_ctx* c, F f) {
     return f();
   } catch (const std::bad_alloc&) {
     return fail(c, KAD_ENOMEM, "host allocation failed");
-  } catch (const std::exception& e) {
-    return fail(c, KAD_ENOMEM, std::string("host error: ") + e.what());
+  } catch (const std::exception& e) {  // e.g. std::system_error from a pool thread's creation
+    return fail(c, KAD_EHOST, std::string("host error: ") + e.what());
+  } catch (...) {
+    return fail(c, KAD_EHOST, "host error: unknown exception");
   }
 }
 
@@ -647,7 +652,7 @@ static int refresh_derived(kad_ctx* c) {
   }
   const size_t nch = (size_t)((C + 63) / 64);
   const size_t nc1 = nch ? nch : 1;
-  const size_t n_slices = ((size_t)128 * TW + 64) * nc1, n_tab = (size_t)2 * 8 * TW * 256 * nc1;
+  const size_t n_slices = ((size_t)128 * TW + (size_t)64 * c->sd.GW) * nc1, n_tab = (size_t)2 * 8 * TW * 256 * nc1;
   // the table is rebuilt whole on every upload / update: above TTAB_MAX_BYTES (C beyond ~32k clusters at
   // 4 taint words) the kernels test taints per cluster instead (unfolded path)
   if (c->sd.fold && (n_slices + n_tab) * 8 > TTAB_MAX_BYTES) c->sd.fold = 0;
@@ -666,33 +671,61 @@ static void invalidate_snapshot(kad_ctx* c) {
   c->ran = false;
 }
 
+static int snapshot_upload_locked(kad_ctx* c, const void* blob, size_t nbytes);
+
 int kad_snapshot_upload(kad_ctx* c, const void* blob, size_t nbytes) {
   return guarded(c, [&]() -> int {
     if (!c || !blob) return KAD_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    kad_snapshot_header h;
-    std::memcpy(&h, blob, sizeof(h) < nbytes ? sizeof(h) : nbytes);
-    if (int r = check_snapshot_header(c, h, nbytes)) return r;
-    // the resident snapshot, its derived state and any batch validated against it are about to be
-    // overwritten: nothing may run on them until every step below has succeeded
-    invalidate_snapshot(c);
-    HIPCHK(c, hipSetDevice(c->device));
-    if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
-    HIPCHK(c, hipMemcpyAsync(c->d_snap, blob, nbytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->snap_hdr = h;
-    if (int r = bind_snapshot(c, h)) return r;
-    c->h_res.assign((size_t)4 * h.n_clusters, 0);
-    {
-      for (int q = 0; q < 4; q++)
-        if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
-    }
-    c->h_ns.assign(at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE),
-                  at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + (size_t)h.n_taint_words * h.n_clusters);
-    if (int r = refresh_derived(c)) return r;
-    c->have_snapshot = true;
-    return KAD_OK;
+    return snapshot_upload_locked(c, blob, nbytes);
   });
+}
+
+static int snapshot_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
+  kad_snapshot_header h;
+  std::memcpy(&h, blob, sizeof(h) < nbytes ? sizeof(h) : nbytes);
+  if (int r = check_snapshot_header(c, h, nbytes)) return r;
+  // the resident snapshot, its derived state and any batch validated against it are about to be
+  // overwritten: nothing may run on them until every step below has succeeded
+  invalidate_snapshot(c);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_snap, blob, nbytes, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->snap_hdr = h;
+  if (int r = bind_snapshot(c, h)) return r;
+  c->h_res.assign((size_t)4 * h.n_clusters, 0);
+  {
+    for (int q = 0; q < 4; q++)
+      if (h.n_clusters) std::memcpy(c->h_res.data() + (size_t)q * h.n_clusters, at<int64_t>(blob, h.off, kResArrays[q]), (size_t)h.n_clusters * 8);
+  }
+  c->h_ns.assign(at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE),
+                at<uint64_t>(blob, h.off, KAD_S_TAINT_NSNE) + (size_t)h.n_taint_words * h.n_clusters);
+  if (int r = refresh_derived(c)) return r;
+  c->have_snapshot = true;
+  return KAD_OK;
+}
+
+// kad_group: member c takes the snapshot resident on member src (same vocabulary and host shadows) with
+// one device-to-device copy (xGMI between two GPUs) and rebuilds its derived state on its own device
+static int snapshot_from_peer_locked(kad_ctx* c, kad_ctx* src) {
+  if (!src->have_snapshot) return fail(c, KAD_ESTATE, "source member has no snapshot");
+  invalidate_snapshot(c);
+  const size_t nbytes = src->snap_hdr.total_bytes;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int r = grow(c, &c->d_snap, &c->snap_bytes, nbytes)) return r;
+  if (c->device == src->device)
+    HIPCHK(c, hipMemcpyAsync(c->d_snap, src->d_snap, nbytes, hipMemcpyDeviceToDevice, c->stream));
+  else
+    HIPCHK(c, hipMemcpyPeerAsync(c->d_snap, c->device, src->d_snap, src->device, nbytes, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->snap_hdr = src->snap_hdr;
+  if (int r = bind_snapshot(c, c->snap_hdr)) return r;
+  c->h_res = src->h_res;
+  c->h_ns = src->h_ns;
+  if (int r = refresh_derived(c)) return r;
+  c->have_snapshot = true;
+  return KAD_OK;
 }
 
 int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) {
@@ -724,78 +757,125 @@ int kad_snapshot_upload_device(kad_ctx* c, const void* dev_blob, size_t nbytes) 
   });
 }
 
+static int snapshot_update_locked(kad_ctx* c, const void* delta, size_t nbytes);
+
 int kad_snapshot_update(kad_ctx* c, const void* delta, size_t nbytes) {
   return guarded(c, [&]() -> int {
     if (!c || !delta) return KAD_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot uploaded");
-    kad_snapshot_delta_header h;
-    if (nbytes < sizeof(h)) return fail(c, KAD_EINVAL, "delta too small");
-    std::memcpy(&h, delta, sizeof(h));
-    const kad_snapshot_header& sh = c->snap_hdr;
-    if (h.magic != KAD_DELTA_MAGIC) return fail(c, KAD_EINVAL, "bad delta magic");
-    if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "delta ABI version mismatch");
-    if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "delta size mismatch");
-    if (h.n_clusters != sh.n_clusters || h.fingerprint != sh.fingerprint)
-      return fail(c, KAD_EINVAL, "delta was packed against a different snapshot vocabulary");
-    const int n = h.n_changed, C = sh.n_clusters;
-    if (n < 0 || n > C) return fail(c, KAD_EINVAL, "bad n_changed");
-    if (n == 0) return KAD_OK;
-    if (h.idx_off > nbytes || (h.idx_off & 3) || h.idx_off + (uint64_t)n * 4 > nbytes)
-      return fail(c, KAD_EINVAL, "bad delta index offset");
-    const int32_t* idx = reinterpret_cast<const int32_t*>(static_cast<const char*>(delta) + h.idx_off);
-    for (int j = 0; j < n; j++)
-      if (idx[j] < 0 || idx[j] >= C || (j && idx[j] <= idx[j - 1]))
-        return fail(c, KAD_EINVAL, "delta cluster indices must be strictly increasing snapshot positions");
-    DeltaDev d{};
-    d.n = n;
-    d.C = C;
-    d.start[0] = 0;
-    for (int a = 0; a < KAD_S_NARRAYS; a++) {
-      int64_t rows;
-      int esz;
-      snapshot_array_shape(sh, a, &rows, &esz);
-      const uint64_t len = (uint64_t)rows * n * esz;
-      if (h.off[a] > nbytes || (h.off[a] % esz) || h.off[a] + len > nbytes)
-        return fail(c, KAD_EINVAL, "bad delta array offset");
-      d.s_off[a] = sh.off[a];
-      d.d_off[a] = h.off[a];
-      d.esz[a] = esz;
-      d.start[a + 1] = d.start[a] + rows * n;
-    }
-    HIPCHK(c, hipSetDevice(c->device));
-    if (int r = grow(c, &c->d_delta, &c->delta_cap, nbytes)) return r;
-    HIPCHK(c, hipMemcpyAsync(c->d_delta, delta, nbytes, hipMemcpyHostToDevice, c->stream));
-    d.snap = static_cast<uint8_t*>(c->d_snap);
-    d.delta = static_cast<const uint8_t*>(c->d_delta);
-    d.idx = reinterpret_cast<const int32_t*>(d.delta + h.idx_off);
-    {
-      hipError_t e = launch_snapshot_delta(d, c->stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the caller's delta buffer is free on return
-      if (e != hipSuccess) {
-        invalidate_snapshot(c);  // the scatter may have run partway
-        return fail(c, KAD_EHIP, std::string("snapshot delta scatter: ") + hipGetErrorString(e));
-      }
-    }
-    {
-      for (int q = 0; q < 4; q++) {
-        const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
-        for (int j = 0; j < n; j++) c->h_res[(size_t)q * C + idx[j]] = v[j];
-      }
-      const uint64_t* ns = at<uint64_t>(delta, h.off, KAD_S_TAINT_NSNE);  // [TW][n_changed]
-      for (int t = 0; t < sh.n_taint_words; t++)
-        for (int j = 0; j < n; j++) c->h_ns[(size_t)t * C + idx[j]] = ns[(size_t)t * n + j];
-    }
-    if (int r = refresh_derived(c)) {
-      invalidate_snapshot(c);  // the scattered snapshot no longer matches its derived rows / tables
-      return r;
-    }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return KAD_OK;
+    return snapshot_update_locked(c, delta, nbytes);
   });
 }
 
-static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
+static int snapshot_update_locked(kad_ctx* c, const void* delta, size_t nbytes) {
+  if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot uploaded");
+  kad_snapshot_delta_header h;
+  if (nbytes < sizeof(h)) return fail(c, KAD_EINVAL, "delta too small");
+  std::memcpy(&h, delta, sizeof(h));
+  const kad_snapshot_header& sh = c->snap_hdr;
+  if (h.magic != KAD_DELTA_MAGIC) return fail(c, KAD_EINVAL, "bad delta magic");
+  if (h.abi_version != KAD_ABI_VERSION) return fail(c, KAD_EINVAL, "delta ABI version mismatch");
+  if (h.total_bytes != nbytes) return fail(c, KAD_EINVAL, "delta size mismatch");
+  if (h.n_clusters != sh.n_clusters || h.fingerprint != sh.fingerprint)
+    return fail(c, KAD_EINVAL, "delta was packed against a different snapshot vocabulary");
+  const int n = h.n_changed, C = sh.n_clusters;
+  if (n < 0 || n > C) return fail(c, KAD_EINVAL, "bad n_changed");
+  if (n == 0) return KAD_OK;
+  if (h.idx_off > nbytes || (h.idx_off & 3) || h.idx_off + (uint64_t)n * 4 > nbytes)
+    return fail(c, KAD_EINVAL, "bad delta index offset");
+  const int32_t* idx = reinterpret_cast<const int32_t*>(static_cast<const char*>(delta) + h.idx_off);
+  for (int j = 0; j < n; j++)
+    if (idx[j] < 0 || idx[j] >= C || (j && idx[j] <= idx[j - 1]))
+      return fail(c, KAD_EINVAL, "delta cluster indices must be strictly increasing snapshot positions");
+  DeltaDev d{};
+  d.n = n;
+  d.C = C;
+  d.start[0] = 0;
+  for (int a = 0; a < KAD_S_NARRAYS; a++) {
+    int64_t rows;
+    int esz;
+    snapshot_array_shape(sh, a, &rows, &esz);
+    const uint64_t len = (uint64_t)rows * n * esz;
+    if (h.off[a] > nbytes || (h.off[a] % esz) || h.off[a] + len > nbytes)
+      return fail(c, KAD_EINVAL, "bad delta array offset");
+    d.s_off[a] = sh.off[a];
+    d.d_off[a] = h.off[a];
+    d.esz[a] = esz;
+    d.start[a + 1] = d.start[a] + rows * n;
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int r = grow(c, &c->d_delta, &c->delta_cap, nbytes)) return r;
+  HIPCHK(c, hipMemcpyAsync(c->d_delta, delta, nbytes, hipMemcpyHostToDevice, c->stream));
+  d.snap = static_cast<uint8_t*>(c->d_snap);
+  d.delta = static_cast<const uint8_t*>(c->d_delta);
+  d.idx = reinterpret_cast<const int32_t*>(d.delta + h.idx_off);
+  {
+    hipError_t e = launch_snapshot_delta(d, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the caller's delta buffer is free on return
+    if (e != hipSuccess) {
+      invalidate_snapshot(c);  // the scatter may have run partway
+      return fail(c, KAD_EHIP, std::string("snapshot delta scatter: ") + hipGetErrorString(e));
+    }
+  }
+  {
+    for (int q = 0; q < 4; q++) {
+      const int64_t* v = at<int64_t>(delta, h.off, kResArrays[q]);
+      for (int j = 0; j < n; j++) c->h_res[(size_t)q * C + idx[j]] = v[j];
+    }
+    const uint64_t* ns = at<uint64_t>(delta, h.off, KAD_S_TAINT_NSNE);  // [TW][n_changed]
+    for (int t = 0; t < sh.n_taint_words; t++)
+      for (int j = 0; j < n; j++) c->h_ns[(size_t)t * C + idx[j]] = ns[(size_t)t * n + j];
+  }
+  if (int r = refresh_derived(c)) {
+    invalidate_snapshot(c);  // the scattered snapshot no longer matches its derived rows / tables
+    return r;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KAD_OK;
+}
+
+// The host-side batch array extents a shard [lo, hi) of units reads (kad_group members): per-unit arrays
+// [lo, hi) (offset arrays [lo, hi]), CSR data between its units' offsets, batch-wide tables whole. Each
+// entry: (array, first byte, bytes) relative to the array's offset.
+struct BlobRange {
+  int a;
+  uint64_t first, bytes;
+};
+static std::vector<BlobRange> shard_ranges(const void* blob, const kad_batch_header& h, int64_t lo, int64_t hi) {
+  std::vector<BlobRange> out;
+  const uint64_t n = (uint64_t)(hi - lo);
+  auto unit = [&](int a, int esz) { out.push_back({a, (uint64_t)lo * esz, n * esz}); };
+  auto offs = [&](int a, int esz) { out.push_back({a, (uint64_t)lo * esz, (n + 1) * esz}); };
+  auto csr = [&](int off_a, std::initializer_list<std::pair<int, int>> data) {
+    offs(off_a, 4);
+    const int32_t* o = at<int32_t>(blob, h.off, off_a);
+    for (auto [a, esz] : data) out.push_back({a, (uint64_t)o[lo] * esz, (uint64_t)(o[hi] - o[lo]) * esz});
+  };
+  const int pvb = (h.flags & KAD_BATCH_NARROW_PREFS) ? 4 : 8;
+  for (int a : {KAD_B_FLAGS, KAD_B_GVK, KAD_B_TOLSET}) unit(a, 4);
+  for (int a : {KAD_B_REQ_CPU, KAD_B_REQ_MEM, KAD_B_DESIRED, KAD_B_MAX_CLUSTERS}) unit(a, 8);
+  offs(KAD_B_OUT_OFF, 8);
+  csr(KAD_B_SREQ_OFF, {{KAD_B_SREQ_ID, 4}, {KAD_B_SREQ_VAL, 8}});
+  csr(KAD_B_FPROG_OFF, {{KAD_B_FPROG, 4}});
+  csr(KAD_B_SPROG_OFF, {{KAD_B_SPROG, 4}});
+  csr(KAD_B_PLACE_OFF, {{KAD_B_PLACE, 4}});
+  csr(KAD_B_CUR_OFF, {{KAD_B_CUR_ID, 4}, {KAD_B_CUR_REP, 8}});
+  csr(KAD_B_PREF_OFF, {{KAD_B_PREF_ID, 4}, {KAD_B_PREF_W, pvb}, {KAD_B_PREF_MIN, pvb}, {KAD_B_PREF_MAX, pvb},
+                       {KAD_B_PREF_CAP, pvb}, {KAD_B_PREF_FLAGS, 4}});
+  csr(KAD_B_KEY_OFF, {{KAD_B_KEY, 1}});
+  const uint64_t tol = (uint64_t)h.n_tolsets * (uint64_t)h.n_taint_words * 8;
+  out.push_back({KAD_B_TOL_ALL, 0, tol});
+  out.push_back({KAD_B_TOL_PNS, 0, tol});
+  out.push_back({KAD_B_REQ_OFF, 0, ((uint64_t)h.n_reqs + 1) * 4});
+  out.push_back({KAD_B_REQ, 0, (uint64_t)at<int32_t>(blob, h.off, KAD_B_REQ_OFF)[h.n_reqs] * 4});
+  return out;
+}
+
+// lo, hi: the units this ctx schedules (hi < 0: all); a shard copies only the blob bytes it reads
+// (shard_ranges) into a device buffer of the whole blob's layout, so every offset stays valid. validated:
+// the caller (kad_group_batch_upload) has run validate_batch on this blob already.
+static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int64_t lo = 0, int64_t hi = -1,
+                               bool validated = false) {
   // any failed upload leaves no batch resident (validation failed, or device buffers half-written)
   c->have_batch = false;
   c->ran = false;
@@ -818,27 +898,43 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
     fprintf(stderr, "[kad_upload] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_prev).count());
     t_prev = t;
   };
-  if (int r = validate_batch(c, blob, nbytes, h)) return r;
+  if (!validated)
+    if (int r = validate_batch(c, blob, nbytes, h)) return r;
   lap("validate");
+  if (hi < 0) hi = h.n_units;
+  if (lo < 0 || lo > hi || hi > h.n_units) return fail(c, KAD_EINVAL, "bad unit range");
+  const bool shard = lo > 0 || hi < h.n_units;
   HIPCHK(c, hipSetDevice(c->device));
   if (int r = grow(c, &c->d_batch, &c->batch_cap, nbytes)) return r;
-  HIPCHK(c, hipMemcpyAsync(c->d_batch, blob, nbytes, hipMemcpyHostToDevice, c->stream));
+  if (!shard) {
+    HIPCHK(c, hipMemcpyAsync(c->d_batch, blob, nbytes, hipMemcpyHostToDevice, c->stream));
+  } else {
+    char* d = static_cast<char*>(c->d_batch);
+    const char* hb = static_cast<const char*>(blob);
+    HIPCHK(c, hipMemcpyAsync(d, hb, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    for (const BlobRange& r : shard_ranges(blob, h, lo, hi))
+      if (r.bytes)
+        HIPCHK(c, hipMemcpyAsync(d + h.off[r.a] + r.first, hb + h.off[r.a] + r.first, r.bytes, hipMemcpyHostToDevice,
+                                 c->stream));
+  }
   lap("dma-issue");
-  const int W = h.n_units;
-  // rows that need the replica planner: Divide mode, DesiredReplicas > 0, not sticky
-  const uint32_t* fl = at<uint32_t>(blob, h.off, KAD_B_FLAGS);
-  const int64_t* des = at<int64_t>(blob, h.off, KAD_B_DESIRED);
+  const int W = (int)(hi - lo);
+  const int64_t* oo_h = at<int64_t>(blob, h.off, KAD_B_OUT_OFF);
+  const int64_t slot_lo = oo_h[lo], S = oo_h[hi] - oo_h[lo];
+  // rows that need the replica planner: Divide mode, DesiredReplicas > 0, not sticky (unit ids of the shard)
+  const uint32_t* fl = at<uint32_t>(blob, h.off, KAD_B_FLAGS) + lo;
+  const int64_t* des = at<int64_t>(blob, h.off, KAD_B_DESIRED) + lo;
   uint32_t flags_or = 0;
   // batch_defer: units the lean kernel would defer whatever the profile (prep_kernel's
   // REC_FULL reasons; wide affinity weights or negative requests can give
   // totals spanning >= 2^32)
   {
-    const int32_t* gv = at<int32_t>(blob, h.off, KAD_B_GVK);
-    const int32_t* so = at<int32_t>(blob, h.off, KAD_B_SREQ_OFF);
-    const int64_t* rc = at<int64_t>(blob, h.off, KAD_B_REQ_CPU);
-    const int64_t* rm = at<int64_t>(blob, h.off, KAD_B_REQ_MEM);
+    const int32_t* gv = at<int32_t>(blob, h.off, KAD_B_GVK) + lo;
+    const int32_t* so = at<int32_t>(blob, h.off, KAD_B_SREQ_OFF) + lo;
+    const int64_t* rc = at<int64_t>(blob, h.off, KAD_B_REQ_CPU) + lo;
+    const int64_t* rm = at<int64_t>(blob, h.off, KAD_B_REQ_MEM) + lo;
     c->batch_defer = first_bad(W, [&](int64_t w) {
-      return gv[w] >= 64 || so[w] < so[w + 1] || rc[w] < 0 || rm[w] < 0 || rc[w] >= (1ll << 46) ||
+      return (gv[w] >= 64 && !c->sd.fold) || so[w] < so[w + 1] || rc[w] < 0 || rm[w] < 0 || rc[w] >= (1ll << 46) ||
              rm[w] >= (1ll << 46) || (fl[w] & KAD_W_WIDE_SCORES);
     }) >= 0;
   }
@@ -896,7 +992,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
     HIPCHK(c, hipMalloc(&c->d_flags, wcap * 4));
     c->out_w_cap = wcap;
   }
-  const size_t slots = h.n_out_slots > 0 ? (size_t)h.n_out_slots : 1;
+  const size_t slots = S > 0 ? (size_t)S : 1;
   if (slots > scap || !c->d_cluster) {
     if (c->d_cluster) { (void)hipFree(c->d_cluster); (void)hipFree(c->d_replicas); }
     HIPCHK(c, hipMalloc(&c->d_cluster, slots * 4));
@@ -1015,6 +1111,10 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   lap("sync");
   c->batch_hdr = h;
+  c->unit_lo = lo;
+  c->unit_n = W;
+  c->slot_lo = slot_lo;
+  c->slot_n = S;
   const char* base = static_cast<const char*>(c->d_batch);
   BatchDev& b = c->bd;
   b.W = W;
@@ -1057,6 +1157,24 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes) {
   b.key_off = at<int32_t>(base, h.off, KAD_B_KEY_OFF);
   b.key = at<uint8_t>(base, h.off, KAD_B_KEY);
   b.out_off = at<int64_t>(base, h.off, KAD_B_OUT_OFF);
+  // a shard: every per-unit array starts at its first unit (CSR offsets and out_off keep their batch-wide
+  // values, so the data arrays and the output slots are indexed as in the whole batch; OutDev's slot
+  // arrays are shifted by slot_lo instead, out_dev)
+  b.flags += lo;
+  b.gvk += lo;
+  b.req_cpu += lo;
+  b.req_mem += lo;
+  b.desired += lo;
+  b.maxc += lo;
+  b.tolset += lo;
+  b.sreq_off += lo;
+  b.fprog_off += lo;
+  b.sprog_off += lo;
+  b.place_off += lo;
+  b.cur_off += lo;
+  b.pref_off += lo;
+  b.key_off += lo;
+  b.out_off += lo;
   b.NR = h.n_reqs;
   b.req_off = at<int32_t>(base, h.off, KAD_B_REQ_OFF);
   b.req = at<int32_t>(base, h.off, KAD_B_REQ);
@@ -1111,8 +1229,9 @@ static OutDev out_dev(kad_ctx* c) {
   o.status = c->d_status;
   o.count = c->d_count;
   o.flags = c->d_flags;
-  o.cluster = c->d_cluster;
-  o.replicas = c->d_replicas;
+  // the kernels write slot out_off[w] (batch-wide): a shard's buffer holds slots [slot_lo, slot_lo + slot_n)
+  o.cluster = reinterpret_cast<int32_t*>(reinterpret_cast<uintptr_t>(c->d_cluster) - 4 * (uintptr_t)c->slot_lo);
+  o.replicas = reinterpret_cast<int64_t*>(reinterpret_cast<uintptr_t>(c->d_replicas) - 8 * (uintptr_t)c->slot_lo);
   return o;
 }
 
@@ -1197,19 +1316,21 @@ int kad_last_timing(kad_ctx* c, float ms[3]) {
   return KAD_OK;
 }
 
-static int results_download_locked(kad_ctx* c, const kad_result_view* out) {
+// the ctx's units' results into out; at_offsets (kad_group): into the whole batch's view, at the shard's
+// unit and slot offsets
+static int results_download_locked(kad_ctx* c, const kad_result_view* out, bool at_offsets = false) {
   if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
   HIPCHK(c, hipSetDevice(c->device));
-  const size_t W = c->batch_hdr.n_units;
-  const size_t S = c->batch_hdr.n_out_slots;
+  const size_t W = (size_t)c->unit_n, S = (size_t)c->slot_n;
+  const size_t uo = at_offsets ? (size_t)c->unit_lo : 0, so = at_offsets ? (size_t)c->slot_lo : 0;
   if (W) {
-    HIPCHK(c, hipMemcpyAsync(out->status, c->d_status, W * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(out->count, c->d_count, W * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(out->flags, c->d_flags, W * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->status + uo, c->d_status, W * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->count + uo, c->d_count, W * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->flags + uo, c->d_flags, W * 4, hipMemcpyDeviceToHost, c->stream));
   }
   if (S) {
-    HIPCHK(c, hipMemcpyAsync(out->cluster, c->d_cluster, S * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(out->replicas, c->d_replicas, S * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->cluster + so, c->d_cluster, S * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out->replicas + so, c->d_replicas, S * 8, hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KAD_OK;
@@ -1376,15 +1497,21 @@ int kad_result_diff(kad_ctx* c, const kad_result_state* st, uint32_t* out) {
   });
 }
 
+static int path_counts_locked(kad_ctx* c, int32_t* out);
+
 int kad_path_counts(kad_ctx* c, int32_t* out) {
   if (!c || !out) return KAD_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
+  return path_counts_locked(c, out);
+}
+
+static int path_counts_locked(kad_ctx* c, int32_t* out) {
   if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
   int32_t h[4] = {0, 0, 0, 0};
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipMemcpyAsync(h, c->d_defer, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  out[0] = c->batch_hdr.n_units;
+  out[0] = (int32_t)c->unit_n;
   out[1] = h[0];  // defer_n: units the full kernel (schedule_kernel) took
   out[2] = c->bd.use_rows ? h[2] : 0;  // rows_n: units schedule_row_kernel took
   out[3] = (int32_t)c->plan_rows.size();  // Divide units handed to the planner
@@ -1656,6 +1783,266 @@ int kad_trigger_hashes(kad_ctx* c, int n, const int64_t* prefix_off, const uint8
     if (!r) r = trigger_download_locked(c, out_hash);
     return r;
   });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ multi-GPU group (kad_group_*)
+// One process, N GPUs (the reference's single scheduler process with --worker-count goroutines,
+// worker.go:132-134, calling Schedule at scheduler.go:507): units are independent given the read-only
+// snapshot (scheduler.go:246-309), so the batch splits into contiguous unit ranges, one per member
+// context, with no exchange while scheduling. Each member is a full kad_ctx on its device; a host pool
+// with one thread per member issues every member's uploads / launches / copies concurrently.
+struct kad_group {
+  std::vector<kad_ctx*> m;
+  kadpool::Pool* pool = nullptr;  // n - 1 workers + the calling thread: member i runs on thread i
+  std::mutex mu;
+  std::string err;
+  std::vector<int64_t> unit_lo, slot_lo;  // [n + 1] the resident batch's split (kad_batch_split)
+  bool have_batch = false, ran = false;
+};
+
+static int gfail(kad_group* g, int code, const std::string& msg) {
+  if (g) g->err = msg;
+  return code;
+}
+
+// f(i, member i) on every member concurrently; the first failure (lowest member) is the group's error
+template <class F>
+static int each_member(kad_group* g, F f) {
+  const int n = (int)g->m.size();
+  std::vector<int> rc((size_t)n, 0);
+  try {
+    g->pool->run(n, [&](int i) {
+      kad_ctx* c = g->m[(size_t)i];
+      rc[(size_t)i] = guarded(c, [&]() -> int {
+        std::lock_guard<std::mutex> lk(c->mu);
+        return f(i, c);
+      });
+    });
+  } catch (const std::exception& e) {
+    return gfail(g, KAD_EHOST, std::string("host error: ") + e.what());
+  }
+  for (int i = 0; i < n; i++)
+    if (rc[(size_t)i]) return gfail(g, rc[(size_t)i], "member " + std::to_string(i) + ": " + g->m[(size_t)i]->err);
+  return KAD_OK;
+}
+
+template <class F>
+static int gguarded(kad_group* g, F f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return gfail(g, KAD_ENOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return gfail(g, KAD_EHOST, std::string("host error: ") + e.what());
+  } catch (...) {
+    return gfail(g, KAD_EHOST, "host error: unknown exception");
+  }
+}
+
+static void split_ranges(const int64_t* out_off, int64_t W, int n, int64_t* unit_lo, int64_t* slot_lo) {
+  for (int i = 0; i <= n; i++) {
+    unit_lo[i] = W * i / n;
+    slot_lo[i] = out_off[unit_lo[i]];
+  }
+}
+
+extern "C" {
+
+int kad_batch_split(const void* blob, size_t nbytes, int n, int64_t* unit_lo, int64_t* slot_lo) {
+  if (!blob || n < 1 || !unit_lo || !slot_lo || nbytes < sizeof(kad_batch_header)) return KAD_EINVAL;
+  kad_batch_header h;
+  std::memcpy(&h, blob, sizeof(h));
+  if (h.magic != KAD_BATCH_MAGIC || h.abi_version != KAD_ABI_VERSION || h.total_bytes != nbytes || h.n_units < 0)
+    return KAD_EINVAL;
+  const uint64_t o = h.off[KAD_B_OUT_OFF], len = ((uint64_t)h.n_units + 1) * 8;
+  if (o > nbytes || (o & 7) || len > nbytes - o) return KAD_EINVAL;
+  const int64_t* oo = at<int64_t>(blob, h.off, KAD_B_OUT_OFF);
+  for (int64_t w = 0; w < h.n_units; w++)
+    if (oo[w + 1] < oo[w]) return KAD_EINVAL;
+  split_ranges(oo, h.n_units, n, unit_lo, slot_lo);
+  return KAD_OK;
+}
+
+int kad_group_create(const int* hip_devices, int n, kad_group** out) {
+  if (!out || !hip_devices || n < 1 || n > 64) return KAD_EINVAL;
+  *out = nullptr;
+  auto* g = new (std::nothrow) kad_group();
+  if (!g) return KAD_ENOMEM;
+  for (int i = 0; i < n; i++) {
+    kad_ctx* c = nullptr;
+    if (int r = kad_ctx_create(hip_devices[i], &c)) {
+      kad_group_destroy(g);
+      return r;
+    }
+    g->m.push_back(c);
+  }
+  // direct peer access for the snapshot copies from member 0 (hipMemcpyPeerAsync works without it, staged)
+  for (int i = 1; i < n; i++) {
+    const int d = hip_devices[i], d0 = hip_devices[0];
+    int can = 0;
+    if (d != d0 && hipDeviceCanAccessPeer(&can, d, d0) == hipSuccess && can && hipSetDevice(d) == hipSuccess) {
+      const hipError_t e = hipDeviceEnablePeerAccess(d0, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    }
+  }
+  try {
+    g->pool = new kadpool::Pool(n - 1);
+  } catch (...) {
+    kad_group_destroy(g);
+    return KAD_EHOST;
+  }
+  *out = g;
+  return KAD_OK;
+}
+
+int kad_group_destroy(kad_group* g) {
+  if (!g) return KAD_OK;
+  delete g->pool;  // joins its threads: nothing of the group runs after this
+  for (kad_ctx* c : g->m) kad_ctx_destroy(c);
+  delete g;
+  return KAD_OK;
+}
+
+const char* kad_group_last_error(kad_group* g) { return g ? g->err.c_str() : "null group"; }
+
+int kad_group_size(kad_group* g) { return g ? (int)g->m.size() : KAD_EINVAL; }
+
+int kad_group_member(kad_group* g, int i, kad_ctx** out) {
+  if (!g || !out || i < 0 || i >= (int)g->m.size()) return KAD_EINVAL;
+  *out = g->m[(size_t)i];
+  return KAD_OK;
+}
+
+int kad_group_snapshot_upload(kad_group* g, const void* blob, size_t nbytes) {
+  return gguarded(g, [&]() -> int {
+    if (!g || !blob) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->have_batch = g->ran = false;
+    for (kad_ctx* c : g->m) {  // a failure below must leave no member with a usable old state
+      std::lock_guard<std::mutex> l2(c->mu);
+      invalidate_snapshot(c);
+    }
+    kad_ctx* c0 = g->m[0];
+    {
+      std::lock_guard<std::mutex> l0(c0->mu);
+      if (int r = guarded(c0, [&] { return snapshot_upload_locked(c0, blob, nbytes); }))
+        return gfail(g, r, "member 0: " + c0->err);
+    }
+    return each_member(g, [&](int i, kad_ctx* c) { return i == 0 ? KAD_OK : snapshot_from_peer_locked(c, c0); });
+  });
+}
+
+int kad_group_snapshot_update(kad_group* g, const void* delta, size_t nbytes) {
+  return gguarded(g, [&]() -> int {
+    if (!g || !delta) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    const int r = each_member(g, [&](int, kad_ctx* c) { return snapshot_update_locked(c, delta, nbytes); });
+    if (r) g->have_batch = g->ran = false;  // some member dropped its snapshot (and batch)
+    return r;
+  });
+}
+
+int kad_group_batch_upload(kad_group* g, const void* blob, size_t nbytes) {
+  return gguarded(g, [&]() -> int {
+    if (!g || !blob) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->have_batch = g->ran = false;
+    const int n = (int)g->m.size();
+    kad_ctx* c0 = g->m[0];
+    kad_batch_header h;
+    {
+      // one validation of the whole blob (member 0's snapshot: every member holds the same one)
+      std::lock_guard<std::mutex> l0(c0->mu);
+      if (!c0->have_snapshot) return gfail(g, KAD_ESTATE, "no snapshot uploaded");
+      if (nbytes < sizeof(h)) return gfail(g, KAD_EINVAL, "batch too small");
+      std::memcpy(&h, blob, sizeof(h));
+      if (h.magic != KAD_BATCH_MAGIC || h.abi_version != KAD_ABI_VERSION || h.total_bytes != nbytes)
+        return gfail(g, KAD_EINVAL, "bad batch header");
+      if (int r = guarded(c0, [&] { return validate_batch(c0, blob, nbytes, h); })) return gfail(g, r, c0->err);
+    }
+    g->unit_lo.assign((size_t)n + 1, 0);
+    g->slot_lo.assign((size_t)n + 1, 0);
+    split_ranges(at<int64_t>(blob, h.off, KAD_B_OUT_OFF), h.n_units, n, g->unit_lo.data(), g->slot_lo.data());
+    if (int r = each_member(g, [&](int i, kad_ctx* c) {
+          return batch_upload_locked(c, blob, nbytes, g->unit_lo[(size_t)i], g->unit_lo[(size_t)i + 1], true);
+        }))
+      return r;
+    g->have_batch = true;
+    return KAD_OK;
+  });
+}
+
+int kad_group_schedule(kad_group* g, const kad_profile* p) {
+  return gguarded(g, [&]() -> int {
+    if (!g) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->have_batch) return gfail(g, KAD_ESTATE, "snapshot and batch must be uploaded first");
+    if (int r = each_member(g, [&](int, kad_ctx* c) { return schedule_locked(c, p, nullptr, nullptr); })) return r;
+    g->ran = true;
+    return KAD_OK;
+  });
+}
+
+int kad_group_sync(kad_group* g) {
+  return gguarded(g, [&]() -> int {
+    if (!g) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    return each_member(g, [&](int, kad_ctx* c) -> int {
+      HIPCHK(c, hipSetDevice(c->device));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      return KAD_OK;
+    });
+  });
+}
+
+int kad_group_results_download(kad_group* g, const kad_result_view* out) {
+  return gguarded(g, [&]() -> int {
+    if (!g || !out) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->ran) return gfail(g, KAD_ESTATE, "nothing ran");
+    return each_member(g, [&](int, kad_ctx* c) { return results_download_locked(c, out, true); });
+  });
+}
+
+int kad_group_schedule_batch(kad_group* g, const kad_profile* p, const void* blob, size_t nbytes,
+                             const kad_result_view* out) {
+  if (!g || !p || !blob || !out) return KAD_EINVAL;
+  if (int r = kad_group_batch_upload(g, blob, nbytes)) return r;
+  if (int r = kad_group_schedule(g, p)) return r;
+  return kad_group_results_download(g, out);
+}
+
+int kad_group_ranges(kad_group* g, int64_t* unit_lo, int64_t* slot_lo) {
+  if (!g || !unit_lo || !slot_lo) return KAD_EINVAL;
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (!g->have_batch) return gfail(g, KAD_ESTATE, "no batch uploaded");
+  std::copy(g->unit_lo.begin(), g->unit_lo.end(), unit_lo);
+  std::copy(g->slot_lo.begin(), g->slot_lo.end(), slot_lo);
+  return KAD_OK;
+}
+
+int kad_group_path_counts(kad_group* g, int32_t* out) {
+  return gguarded(g, [&]() -> int {
+    if (!g || !out) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->ran) return gfail(g, KAD_ESTATE, "nothing ran");
+    std::vector<int32_t> per(4 * g->m.size(), 0);
+    if (int r = each_member(g, [&](int i, kad_ctx* c) { return path_counts_locked(c, per.data() + 4 * (size_t)i); }))
+      return r;
+    for (int k = 0; k < 4; k++) {
+      out[k] = 0;
+      for (size_t i = 0; i < g->m.size(); i++) out[k] += per[4 * i + (size_t)k];
+    }
+    return KAD_OK;
+  });
+}
+
+int kad_group_set_timing(kad_group* g, int on) {
+  if (!g) return KAD_EINVAL;
+  for (kad_ctx* c : g->m) kad_set_timing(c, on);
+  return KAD_OK;
 }
 
 }  // extern "C"

@@ -26,7 +26,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libkad.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "kad_sched.h")
 
-KAD_ERRORS = {-1: "KAD_EINVAL", -2: "KAD_EHIP", -3: "KAD_ENOMEM", -4: "KAD_ESTATE", -5: "KAD_EUNSUPPORTED"}
+KAD_ERRORS = {-1: "KAD_EINVAL", -2: "KAD_EHIP", -3: "KAD_ENOMEM", -4: "KAD_ESTATE", -5: "KAD_EUNSUPPORTED",
+              -6: "KAD_EHOST"}
 
 
 class KadError(RuntimeError):
@@ -101,6 +102,23 @@ def load_library(path: str = LIB_PATH):
     L.kad_trigger_hashes.argtypes = [P, I, P, P, P, SZ, P]
     L.kad_host_alloc.argtypes = [SZ, ctypes.POINTER(P)]
     L.kad_host_free.argtypes = [P]
+    L.kad_group_create.argtypes = [P, I, ctypes.POINTER(P)]
+    L.kad_group_destroy.argtypes = [P]
+    L.kad_group_last_error.argtypes = [P]
+    L.kad_group_last_error.restype = ctypes.c_char_p
+    L.kad_group_size.argtypes = [P]
+    L.kad_group_snapshot_upload.argtypes = [P, P, SZ]
+    L.kad_group_snapshot_update.argtypes = [P, P, SZ]
+    L.kad_group_batch_upload.argtypes = [P, P, SZ]
+    L.kad_group_schedule.argtypes = [P, P]
+    L.kad_group_sync.argtypes = [P]
+    L.kad_group_results_download.argtypes = [P, P]
+    L.kad_group_schedule_batch.argtypes = [P, P, P, SZ, P]
+    L.kad_group_ranges.argtypes = [P, P, P]
+    L.kad_group_path_counts.argtypes = [P, P]
+    L.kad_group_set_timing.argtypes = [P, I]
+    L.kad_group_member.argtypes = [P, I, ctypes.POINTER(P)]
+    L.kad_batch_split.argtypes = [P, SZ, I, P, P]
     _lib = L
     return L
 
@@ -371,6 +389,124 @@ class Context:
         return out[:self._trig_n]
 
 
+def batch_split(batch, n: int):
+    """kad_batch_split (host only): the contiguous unit ranges a kad_group of n members gives its members,
+    and their first output slots: (unit_lo[n+1], slot_lo[n+1])."""
+    L = load_library()
+    ulo = np.zeros(n + 1, np.int64)
+    slo = np.zeros(n + 1, np.int64)
+    rc = L.kad_batch_split(_p(batch.blob), batch.blob.nbytes, n, _p(ulo), _p(slo))
+    if rc != 0:
+        raise KadError(rc, "kad_batch_split: malformed batch blob or n < 1")
+    return ulo, slo
+
+
+class GroupContext:
+    """A kad_group: one process scheduling each batch over several GPUs (contiguous unit ranges, one
+    kad_ctx per device), results in one view as from a single Context. Same interface as :class:`Context`
+    for what :class:`BatchScheduler` uses (upload_snapshot, update_snapshot, upload_batch, schedule, sync,
+    download, run, path_counts), so a BatchScheduler / CoalescingScheduler drives N GPUs unchanged."""
+
+    def __init__(self, devices: Sequence[int]):
+        self.devices = list(devices)
+        self.L = load_library()
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        rc = self.L.kad_group_create(arr, len(self.devices), ctypes.byref(h))
+        if rc != 0:
+            raise KadError(rc, f"kad_group_create(devices={self.devices}) failed (no GPU?)")
+        self.h = h
+        self.snap: Optional[Snapshot] = None
+        self.batch: Optional[Batch] = None
+
+    @property
+    def device(self):
+        return self.devices[0]
+
+    def close(self):
+        if self.h:
+            self.L.kad_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise KadError(rc, self.L.kad_group_last_error(self.h).decode())
+
+    def upload_snapshot(self, snap: Snapshot):
+        self._chk(self.L.kad_group_snapshot_upload(self.h, _p(snap.blob), snap.blob.nbytes))
+        self.snap = snap
+
+    def update_snapshot(self, delta: SnapshotDelta):
+        self._chk(self.L.kad_group_snapshot_update(self.h, _p(delta.blob), delta.blob.nbytes))
+
+    def upload_batch(self, batch: Batch):
+        chk = getattr(batch, "check_current", None)
+        if chk is not None:
+            chk()
+        self._chk(self.L.kad_group_batch_upload(self.h, _p(batch.blob), batch.blob.nbytes))
+        self.batch = batch
+
+    def schedule(self, fwk: Framework):
+        prof = fwk.to_c()
+        self._chk(self.L.kad_group_schedule(self.h, ctypes.byref(prof)))
+
+    def sync(self):
+        self._chk(self.L.kad_group_sync(self.h))
+
+    def set_timing(self, on: bool):
+        self._chk(self.L.kad_group_set_timing(self.h, 1 if on else 0))
+
+    def ranges(self):
+        n = len(self.devices)
+        ulo = np.zeros(n + 1, np.int64)
+        slo = np.zeros(n + 1, np.int64)
+        self._chk(self.L.kad_group_ranges(self.h, _p(ulo), _p(slo)))
+        return ulo, slo
+
+    def path_counts(self) -> dict:
+        out = (ctypes.c_int32 * 4)()
+        self._chk(self.L.kad_group_path_counts(self.h, out))
+        return {"units": out[0], "full_kernel": out[1], "row_kernel": out[2], "planner_rows": out[3]}
+
+    def member_stage_timing(self, i: int) -> dict:
+        """kad_stage_timing of member i (timing on)."""
+        c = ctypes.c_void_p()
+        self._chk(self.L.kad_group_member(self.h, i, ctypes.byref(c)))
+        ms = (ctypes.c_float * 7)()
+        rc = self.L.kad_stage_timing(c, ms, 7)
+        if rc != 0:
+            raise KadError(rc, self.L.kad_last_error(c).decode())
+        return {k: float(v) for k, v in zip(Context.STAGES, ms)}
+
+    def download(self, out: Optional[BatchResult] = None) -> BatchResult:
+        res = BatchResult.empty(self.batch) if out is None else out
+        v = ResultView(res.status.ctypes.data, res.count.ctypes.data, res.flags.ctypes.data, res.cluster.ctypes.data,
+                       res.replicas.ctypes.data)
+        self._chk(self.L.kad_group_results_download(self.h, ctypes.byref(v)))
+        return res
+
+    def schedule_batch(self, fwk: Framework, batch: Batch) -> BatchResult:
+        res = BatchResult.empty(batch)
+        v = ResultView(res.status.ctypes.data, res.count.ctypes.data, res.flags.ctypes.data, res.cluster.ctypes.data,
+                       res.replicas.ctypes.data)
+        prof = fwk.to_c()
+        self._chk(self.L.kad_group_schedule_batch(self.h, ctypes.byref(prof), _p(batch.blob), batch.blob.nbytes,
+                                                  ctypes.byref(v)))
+        self.batch = batch
+        return res
+
+    def run(self, fwk: Framework, batch: Batch) -> BatchResult:
+        self.upload_batch(batch)
+        self.schedule(fwk)
+        return self.download()
+
+
 class TriggerHasher:
     """Scheduler.computeSchedulingTriggerHash for a batch of objects (schedulingtriggers.go:106-147).
 
@@ -414,8 +550,12 @@ class BatchScheduler:
     re-upload on the next call.
     """
 
-    def __init__(self, ctx: Optional[Context] = None, device: int = 0):
-        self.ctx = ctx if ctx is not None else Context(device)
+    def __init__(self, ctx: Optional[Context] = None, device: int = 0, devices: Optional[Sequence[int]] = None):
+        """``devices``: schedule every batch over these GPUs (a :class:`GroupContext`, one process), else one
+        Context on ``device``."""
+        if ctx is None:
+            ctx = GroupContext(devices) if devices is not None else Context(device)
+        self.ctx = ctx
         self.full_uploads = 0   # snapshot (re)packs + uploads
         self.delta_updates = 0  # in-place kad_snapshot_update calls
 
