@@ -201,13 +201,32 @@ def roofline_for(stage: str, kernel: str, t_ms: float, compulsory: float, pmc, p
             "pmc": os.path.relpath(pmc_path, ROOT) if pmc is not None else why_not}
 
 
+def host_cpus():
+    """(CPUs this process may run on = len(sched_getaffinity), os.cpu_count(), the cgroup's CPU limit or None):
+    the CPU baseline runs one worker thread per CPU it may use and reports all three (on the GPU box the
+    machine's count is many times the box's share)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    return usable, os.cpu_count(), quota
+
+
 def cpu_baseline(snap, batch, fwk, C, target_s):
     """The C restatement timed on the host (kind "port") over the first n units, n sized for ~target_s of
-    work. Returns (line, oracle result of units [0, n), n) — the result doubles as the parity check of
-    the GPU rows (verify_rows)."""
+    work, one worker thread per CPU the process may use (host_cpus). Returns (line, oracle result of units
+    [0, n), n) — the result doubles as the parity check of the GPU rows (verify_rows)."""
     from oracle import ref
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, n_machine, quota = host_cpus()
     n = min(batch.W, 2000)
     t0 = time.perf_counter()
     want = ref.schedule(snap, batch, fwk, 0, n, threads)
@@ -225,8 +244,10 @@ def cpu_baseline(snap, batch, fwk, C, target_s):
             ref.schedule(snap, batch, fwk, 0, n, threads)
         dt = time.perf_counter() - t0
     line = {"value": reps * n * C / dt, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "cpu_count": n_machine, "cgroup_cpu_limit": quota,
             "sample": f"{reps} pass(es) over units [0, {n}) of {batch.W} x {C} clusters, oracle/kad_ref.c "
-                      f"(C restatement of the Go reference, one unit per worker thread), {dt:.2f}s wall"}
+                      f"(C restatement of the Go reference, one unit per worker thread, {threads} threads = the "
+                      f"CPUs this process may use; machine {n_machine}, cgroup limit {quota}), {dt:.2f}s wall"}
     return line, want, n
 
 
@@ -243,6 +264,10 @@ def verify_rows(snap, batch, fwk, res, want=None, n_want=0, max_units=200_000):
         wins = [(0, n_want, want)]
         if n_want < W <= max_units:  # a time-bounded CPU pass stopped short: the remaining units too
             wins.append((n_want, W, None))
+        elif n_want < W:  # ... of a large batch: 16 windows spread over the rest, so the tail is sampled too
+            rest = W - n_want
+            span = max(1, min(rest // 16, max_units // 16))
+            wins += [(n_want + rest * i // 16, min(W, n_want + rest * i // 16 + span), None) for i in range(16)]
     elif W <= max_units:
         wins = [(0, W, None)]
     else:
@@ -877,7 +902,7 @@ def bench_trigger(args, cfg, rank, world, local, dist):
         if world == 1 and not args.no_cpu_baseline:
             from oracle import ref
 
-            threads = min(16, os.cpu_count() or 1)
+            threads, n_machine, quota = host_cpus()
             n = min(W, 64)
             t0 = time.perf_counter()
             ref.trigger_hashes(prefixes[:n], suffix, threads)
@@ -887,6 +912,7 @@ def bench_trigger(args, cfg, rank, world, local, dist):
             ref.trigger_hashes(prefixes[:n], suffix, threads)
             dt = time.perf_counter() - t0
             out["cpu_baseline"] = {"value": n / dt, "unit": "objects/s", "cores": threads, "kind": "port",
+                                   "cpu_count": n_machine, "cgroup_cpu_limit": quota,
                                    "sample": f"first {n} of {W} objects, oracle/kad_trigger_ref.c (each object's "
                                              f"bytes folded end to end, as schedulingtriggers.go:141-145; JSON "
                                              f"building not timed), {dt:.2f}s wall"}

@@ -66,7 +66,9 @@ typedef struct kad_units kad_units;
  * ClusterPropagationPolicies (no namespace), keyed by (namespace, name) as the
  * informer caches are. `policy_of` NULL: each object's policy is found through
  * its labels (MatchedPolicyKey); else policy_of[i] is object i's policy index
- * (-1: none — a caller that did the lookup itself). `threads` <= 0: every
+ * (-1: none — a caller that did the lookup itself; any other value outside
+ * [0, policies->n) is KAD_EINVAL). Every kad_strs must have offsets starting
+ * at 0 and never decreasing (else KAD_EINVAL). `threads` <= 0: every
  * worker of the library's pool.
  * Returns KAD_OK with *out set (free with kad_units_free) — per-object failures
  * are statuses, not errors — or KAD_EINVAL / KAD_ENOMEM. */

@@ -799,6 +799,8 @@ def trigger_prefixes(type_config, objects: Sequence, policies: Sequence, policy_
     po = None
     if policy_of is not None:
         po = np.ascontiguousarray(policy_of, I32)
+        if len(po) != n:
+            raise ValueError("policy_of: one entry per object")
         keep.append(po)
     h = P()
     rc = L.kad_trigger_prefixes(ctypes.byref(KadTypeConfig(

@@ -889,8 +889,8 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
   if (h.snapshot_fingerprint != c->snap_hdr.fingerprint || h.n_clusters != c->snap_hdr.n_clusters ||
       h.n_taint_words != c->snap_hdr.n_taint_words)
     return fail(c, KAD_EINVAL, "batch was packed against a different snapshot");
-  // KAD_UPLOAD_TIMING: host-side laps of the upload on stderr (measurement only)
-  static const bool tm = getenv("KAD_UPLOAD_TIMING") != nullptr;
+  // KAD_UPLOAD_TIMING: host-side laps of the upload on stderr (measurement builds only: tuning_env)
+  static const bool tm = tuning_env("KAD_UPLOAD_TIMING", 0) != 0;
   auto t_prev = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
     if (!tm) return;

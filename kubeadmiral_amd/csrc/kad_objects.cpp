@@ -936,8 +936,8 @@ struct Builder {
       return d.str((uint32_t)v);
     };
     // MatchedPolicyKey (scheduler/util.go:37-49) and the informer lookup (scheduler.go:359-372)
-    if (forced >= -1) {
-      if (forced < 0 || forced >= (int32_t)pols.size()) {
+    if (forced >= -1) {  // the caller's index, range-checked on entry (policy_of_ok)
+      if (forced < 0) {
         u.status = KAD_OBJ_NO_POLICY;
         return;
       }
@@ -1904,10 +1904,32 @@ void merge(kad_units& R, const kad_type_config& tc, std::vector<Unit>& units) {
 
 }  // namespace
 
+// A caller's kad_strs, checked once on entry (as the packer's validate_columns does): n >= 0, offsets from 0 and
+// never decreasing, data present when any string is non-empty — a decreasing offset would otherwise become a
+// huge string length and an out-of-bounds read. A null `s` is valid where the argument is optional.
+static bool strs_ok(const kad_strs* s) {
+  if (!s) return true;
+  if (s->n < 0) return false;
+  if (s->n == 0) return !s->off || s->off[0] == 0;
+  if (!s->off || s->off[0] != 0) return false;
+  for (int32_t i = 0; i < s->n; ++i)
+    if (s->off[i + 1] < s->off[i]) return false;
+  return s->off[s->n] == 0 || s->bytes;
+}
+
+// policy_of[i]: -1 (no policy: the object is scheduled to no clusters) or an index into `policies`. Anything
+// else is a caller bug (a stale or off-by-one index) that must not silently unschedule the object everywhere.
+static bool policy_of_ok(const int32_t* policy_of, int n, int np) {
+  if (!policy_of) return true;
+  for (int i = 0; i < n; ++i)
+    if (policy_of[i] < -1 || policy_of[i] >= np) return false;
+  return true;
+}
+
 extern "C" int kad_units_from_objects(const kad_type_config* tc, const kad_strs* objects, const kad_strs* policies,
                                       const int32_t* policy_of, int threads, kad_units** out) {
-  if (!tc || !objects || !out || objects->n < 0 || (objects->n > 0 && (!objects->off || !objects->bytes)) ||
-      (policies && policies->n > 0 && (!policies->off || !policies->bytes)))
+  if (!tc || !objects || !out || !strs_ok(objects) || !strs_ok(policies) ||
+      !policy_of_ok(policy_of, objects->n, policies ? policies->n : 0))
     return KAD_EINVAL;
   *out = nullptr;
   try {
@@ -2059,13 +2081,13 @@ extern "C" int kad_apply_results(const kad_type_config* tc, const kad_strs* obje
                                  const int32_t* res_off, const int32_t* res_cluster, const int64_t* res_replicas,
                                  const uint8_t* follower, const int64_t* threshold_ns, const kad_strs* trigger,
                                  const uint8_t* ann_only, int threads, kad_applied** out) {
-  if (!tc || !objects || !cluster_names || !res_off || !out || objects->n < 0 ||
-      (objects->n > 0 && (!objects->off || !objects->bytes)) || cluster_names->n < 0 ||
-      (cluster_names->n > 0 && (!cluster_names->off || !cluster_names->bytes)))
+  if (!tc || !objects || !cluster_names || !res_off || !out || !strs_ok(objects) || !strs_ok(cluster_names) ||
+      !strs_ok(trigger))
     return KAD_EINVAL;
   *out = nullptr;
   const int n = objects->n;
-  if (trigger && (trigger->n != n || (n > 0 && (!trigger->off || !trigger->bytes)))) return KAD_EINVAL;
+  if (trigger && trigger->n != n) return KAD_EINVAL;
+  if (res_off[0] != 0) return KAD_EINVAL;
   if (n > 0 && res_off[n] > 0 && (!res_cluster || !res_replicas)) return KAD_EINVAL;
   for (int i = 0; i < n; ++i)
     if (res_off[i] < 0 || res_off[i + 1] < res_off[i]) return KAD_EINVAL;
@@ -2229,7 +2251,7 @@ void trigger_one(const kad_type_config& tc, const std::vector<Policy>& pols,
   };
   // MatchedPolicyKey + lookup (scheduler.go:359-372), as Builder::build
   if (forced >= -1) {
-    o.policy = forced >= 0 && forced < (int32_t)pols.size() ? forced : -1;
+    o.policy = forced >= 0 ? forced : -1;  // range-checked on entry (policy_of_ok)
   } else {
     std::optional<std::string> key;
     const int64_t pl = labels >= 0 ? get(d, (uint32_t)labels, POLICY_LABEL) : -1;
@@ -2316,8 +2338,8 @@ void trigger_one(const kad_type_config& tc, const std::vector<Policy>& pols,
 
 extern "C" int kad_trigger_prefixes(const kad_type_config* tc, const kad_strs* objects, const kad_strs* policies,
                                     const int32_t* policy_of, int threads, kad_trigger_objs** out) {
-  if (!tc || !objects || !out || objects->n < 0 || (objects->n > 0 && (!objects->off || !objects->bytes)) ||
-      (policies && policies->n > 0 && (!policies->off || !policies->bytes)))
+  if (!tc || !objects || !out || !strs_ok(objects) || !strs_ok(policies) ||
+      !policy_of_ok(policy_of, objects->n, policies ? policies->n : 0))
     return KAD_EINVAL;
   *out = nullptr;
   try {

@@ -622,7 +622,11 @@ static int pack_batch_impl(kad_packer* P, const kad_profile* prof, const kad_su_
   if (W < 0) return P->fail(KAD_EINVAL, "n_units < 0");
   const Strs S{su->str.off, su->str.bytes, su->str.n};
   const int C = P->C, TW = P->TW;
-  static const bool tm = getenv("KAD_PACK_TIMING") != nullptr;
+#if defined(KAD_PHASE_PROF) || defined(KAD_TUNING)
+  static const bool tm = getenv("KAD_PACK_TIMING") != nullptr;  // measurement builds only
+#else
+  constexpr bool tm = false;
+#endif
   auto t_prev = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
     if (!tm) return;

@@ -17,6 +17,12 @@ import numpy as np  # noqa: E402
 import bench  # noqa: E402
 from kubeadmiral_amd import columns as CO  # noqa: E402
 from kubeadmiral_amd import pack, synth  # noqa: E402
+from kubeadmiral_amd import build as kbuild, runtime  # noqa: E402
+
+# the packer / upload laps (KAD_PACK_TIMING / KAD_UPLOAD_TIMING) are compiled into measurement builds only
+TUNE_LIB = os.path.join(kbuild.HERE, "libkad_tune.so")
+kbuild.build(extra=["-DKAD_TUNING"], out=TUNE_LIB)
+runtime.load_library(TUNE_LIB)
 from kubeadmiral_amd.results import BatchResult  # noqa: E402
 from kubeadmiral_amd.runtime import Context  # noqa: E402
 

@@ -5,7 +5,11 @@
 """
 import sys, time, os; sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 import bench
-from kubeadmiral_amd import columns, synth
+from kubeadmiral_amd import build as kbuild, columns, runtime, synth
+# the packer's phase laps (KAD_PACK_TIMING=1) are compiled into measurement builds only
+TUNE_LIB = os.path.join(kbuild.HERE, "libkad_tune.so")
+kbuild.build(extra=["-DKAD_TUNING"], out=TUNE_LIB)
+runtime.load_library(TUNE_LIB)
 from kubeadmiral_amd.pack import Snapshot
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c4"
 W0, C = synth.SIZES[cfg]

@@ -157,6 +157,18 @@ def test_verify_rows_reports_mismatches(fake):
     assert p["windows"] == 16 and p["units_checked"] == 16 * (1000 // 16)
     p = bench.verify_rows(snap, nb, fwk, res, max_units=10_000)
     assert p["mismatches"] == 1 and p["first_mismatch"] == w
+    # a CPU pass that covered [0, 500) of a batch larger than max_units: the rest is sampled by 16 windows,
+    # the last of which reaches the batch's tail
+    from oracle import ref
+    want = ref.schedule(snap, nb, fwk, 0, 500, 4)
+    p = bench.verify_rows(snap, nb, fwk, res, want=want, n_want=500, max_units=1600)
+    assert p["windows"] == 17 and p["units_checked"] > 500 + 16 * 90
+    tail = nb.W - 1
+    while res.count[tail] == 0:
+        tail -= 1
+    res.cluster[nb.out_off[tail]] += 1
+    p2 = bench.verify_rows(snap, nb, fwk, res, want=want, n_want=500, max_units=nb.W * 16)
+    assert p2["mismatches"] >= 1
 
 
 def test_stale_pmc_is_not_used(fake, tmp_path, monkeypatch):

@@ -616,3 +616,39 @@ def test_apply_with_trigger_annotation_matches_python():
         else:
             assert a.texts[i] == json.dumps(obj, separators=(",", ":")).encode(), i
     assert kinds == {(False, False), (False, True), (True, False), (True, True)}
+
+
+def test_entry_points_refuse_bad_policy_index_and_offsets():
+    """a policy index outside [-1, n_policies) is a caller bug, refused with KAD_EINVAL instead of
+    read as 'no policy' (which would unschedule the object everywhere); a kad_strs whose offsets do not start
+    at 0 or decrease is refused before any string is read; a short policy_of raises on the Python side."""
+    import ctypes
+
+    import numpy as np
+
+    from kubeadmiral_amd.runtime import load_library
+    rng = random.Random(5)
+    policies = [_policy(rng, f"p{i}", True) for i in range(3)]
+    objs = [_object(rng, policies) for _ in range(4)]
+    ftc = O.FederatedTypeConfig("apps", "v1", "Deployment", "deployments", "Namespaced", "spec.replicas")
+    K.units_from_objects(ftc, objs, policies, policy_of=[0, -1, 2, 1])  # in range: fine
+    for bad in ([0, 3, 1, 1], [0, -2, 1, 1]):
+        with pytest.raises(RuntimeError):
+            K.units_from_objects(ftc, objs, policies, policy_of=bad)
+        with pytest.raises(RuntimeError):
+            K.trigger_prefixes(ftc, objs, policies, policy_of=bad)
+    with pytest.raises(ValueError):
+        K.trigger_prefixes(ftc, objs, policies, policy_of=[0, 1])
+    # malformed kad_strs straight through the C ABI
+    L = load_library()
+    P = ctypes.c_void_p
+    L.kad_units_from_objects.argtypes = [P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
+    L.kad_trigger_prefixes.argtypes = [P, P, P, P, ctypes.c_int, ctypes.POINTER(P)]
+    tc = K.KadTypeConfig(b"apps", b"v1", b"Deployment", b"deployments", 1, b"spec.replicas")
+    data = np.frombuffer(b'{"a":1}{"b":2}', np.uint8).copy()
+    for off in ([0, 7, 3], [1, 7, 14]):
+        o = np.array(off, np.int64)
+        s = K.KadStrs(2, o.ctypes.data, data.ctypes.data)
+        h = P()
+        assert L.kad_units_from_objects(ctypes.byref(tc), ctypes.byref(s), None, None, 1, ctypes.byref(h)) == -1
+        assert L.kad_trigger_prefixes(ctypes.byref(tc), ctypes.byref(s), None, None, 1, ctypes.byref(h)) == -1
