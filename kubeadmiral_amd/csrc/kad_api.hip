@@ -93,6 +93,7 @@ struct kad_ctx {
   void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
   size_t delta_cap = 0;
   bool batch_defer = false;    // some unit uses a feature the lean kernel defers
+  bool batch_many_terms = false;  // some unit has more than ROW_MAX_TERMS preferred terms (the row path defers it)
   // scheduling-trigger hashes (kad_trigger_*)
   void* t_suffix = nullptr;
   size_t t_suffix_cap = 0;
@@ -937,6 +938,9 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
       return (gv[w] >= 64 && !c->sd.fold) || so[w] < so[w + 1] || rc[w] < 0 || rm[w] < 0 || rc[w] >= (1ll << 46) ||
              rm[w] >= (1ll << 46) || (fl[w] & KAD_W_WIDE_SCORES);
     }) >= 0;
+    const int32_t* spo = at<int32_t>(blob, h.off, KAD_B_SPROG_OFF) + lo;
+    const int32_t* sp = at<int32_t>(blob, h.off, KAD_B_SPROG);
+    c->batch_many_terms = first_bad(W, [&](int64_t w) { return sp[spo[w]] > ROW_MAX_TERMS; }) >= 0;
   }
   {
     // plan rows in unit order: per-piece counts, then each piece writes at its prefix
@@ -1246,14 +1250,23 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   o.dbg_feas = dbg_feas;
   o.dbg_total = dbg_total;
   const bool tm = c->timing;
-  c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total || wide_path(c->sd);
   // long feasible lists go to schedule_row_kernel when every filter is in the static words
   const bool no_rows = tuning_env("KAD_NO_ROWS", 0) != 0;  // (read per launch: tuning builds only)
   c->bd.use_rows = !no_rows && c->sd.clean && c->sd.fold && c->sd.fitfold && row_kernel_fits(c->sd.C);
   const bool rows_after = tuning_env("KAD_ROWS_AFTER", 0) != 0;
   const int per = prep_lanes_per_unit(c->sd.C);
-  c->bd.early_rows = c->bd.use_rows && !rows_after && wide_path(c->sd) && (per & (per - 1)) == 0 && per <= 64 &&
+  const bool wide = wide_path(c->sd);
+  c->bd.early_rows = c->bd.use_rows && !rows_after && wide && (per & (per - 1)) == 0 && per <= 64 &&
                      !dbg_feas && !dbg_total;
+  // can any unit reach the defer list (schedule_kernel)? The wide kernel with early routing (every filter in
+  // the static words, long lists routed by prep) defers only the units batch_defer names; the row path also
+  // those with more preferred terms than it holds. Otherwise as before: the lean kernel's own reasons, and
+  // on the wide path without early routing, lists past WIDE_P.
+  const bool rows_defer = c->batch_many_terms && (p->score_mask & (1u << KAD_PL_CLUSTER_AFFINITY));
+  if (wide)
+    c->bd.may_defer = c->batch_defer || dbg_feas || dbg_total || !c->bd.early_rows || rows_defer;
+  else
+    c->bd.may_defer = c->batch_defer || c->snap_negative || c->sd.TW > 1 || dbg_feas || dbg_total;
   if (c->bd.use_rows) {
     if (int r = grow(c, &c->d_rowslab, &c->rowslab_cap, (size_t)ROW_MAX_BLOCKS * row_slab_bytes(c->sd.C))) return r;
     c->bd.row_slabs = static_cast<char*>(c->d_rowslab);

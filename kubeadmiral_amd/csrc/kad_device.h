@@ -137,6 +137,7 @@ static_assert(sizeof(UnitRec) == 64, "UnitRec is one 64-B line");
 constexpr uint32_t REC_DESIRED_POS = 1u << 31;  // DesiredReplicas != nil && *DesiredReplicas > 0
 constexpr uint32_t REC_FULL = 1u << 30;         // scheduled by schedule_kernel (features the lean kernel omits)
 constexpr uint32_t REC_ROW = 1u << 29;          // routed to schedule_row_kernel by prep_kernel (BatchDev::early_rows)
+constexpr int ROW_MAX_TERMS = 8;                // schedule_row_kernel: preferred terms held as per-chunk words
 constexpr int WIDE_Q = 8;                       // schedule_wide_kernel: positions per lane
 constexpr int WIDE_P = WIDE_Q * 64;             //   and per wave (longer feasible lists: schedule_row_kernel)
 

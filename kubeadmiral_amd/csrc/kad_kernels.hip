@@ -1977,6 +1977,13 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 // outside the exact-f64 range go to the defer list (schedule_kernel).
 constexpr int WIDE_MAX_NCH = 16;
 constexpr int WIDE_THREADS = 1024;
+// the row path's body (defined with schedule_row_kernel below), run by the wide kernel's opening phase
+template <int SM, int NT, class ArgsOf>
+__device__ __forceinline__ void row_units(ArgsOf args, char* smem, int rexp);
+// the wide kernel's row phase as a separate (not inlined) function: its register demand stays out of the
+// unit loop's allocation
+template <int SM>
+__device__ __attribute__((noinline)) void wide_rows(char* smem, const __attribute__((address_space(4))) struct WideArgs* a);
 
 struct WideLayout {
   size_t key, idx, pid, posl, posr, bytes;
@@ -2009,6 +2016,7 @@ struct WideArgs {
   ProfDev p;
   int waves_per_block;
   int cache_ne, cache_pn;
+  int rows_inline;  // the units prep_kernel routed to rows run in this kernel's opening phase (row_units)
   int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default; results differ from
             // the reference): bit 0 skips the pdqsort replay (ties taken by position), bit 1 ends each unit
             // after the filters, bit 2 after the scores (no selection), bit 3 skips the output pass
@@ -2063,6 +2071,18 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
   constexpr int P = WIDE_P;
   static_assert(XN <= NCH, "exact chunk count within the template bound");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // the units prep_kernel routed to the row path (more than P feasible clusters, BatchDev::early_rows):
+  // the first blocks take them, one unit per block at a time, before their own work queue — in the LDS
+  // of the waves' regions (the cluster cache above is loaded afterwards); the queue's dynamic batches
+  // absorb the delay of these blocks' static first batches. First in the kernel, so that nothing of the
+  // unit loop is live across the row body (its register pressure does not spill the loop's values).
+  if (wargs()->rows_inline) {
+    const int rn = __hip_atomic_load(wargs()->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)blockIdx.x < rn) {
+      wide_rows<SM>(smem, wargs());  // (a callee cannot read the kernarg segment pointer itself: pass it)
+      __syncthreads();  // the row body's LDS reads are done before the waves' regions are reused
+    }
+  }
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int C, W, TWs;
@@ -2631,8 +2651,8 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
 // ROW_MAX_TERMS preferred terms go on to the defer list.
 constexpr int ROW_THREADS = 512;
 constexpr int ROW_WAVES = ROW_THREADS / 64;
+constexpr int ROW_MAX_WAVES = 16;  // the row body also runs on schedule_wide_kernel's 1024-thread blocks
 constexpr int ROW_MAX_C = 12288;
-constexpr int ROW_MAX_TERMS = 8;  // preferred terms held as per-chunk words (8 x nch x 8 B = Cp bytes)
 constexpr int ROW_NREP = 2048;    // replays of up to this many positions keep their scratch in LDS
 constexpr int ROW_BLOCK_PART = 256;  // replay partitions of longer ranges run on every wave of the block
 #ifndef KAD_ROW_RU
@@ -2663,8 +2683,8 @@ __host__ __device__ inline RowKLayout rowk_layout(int C) {
   L.cnt = L.sw + 16 * nch;                //   unit's are prefetched); i32[2][nch + 1]: chunk counts →
                                           //   exclusive prefix (+ total)
   L.hist = (L.cnt + 8 * (nch + 1) + 15) & ~(size_t)15;  // u32[256]
-  L.red = L.hist + 4 * 256;               // i32[4][ROW_WAVES] per-wave partials, i32[24] broadcasts
-  L.bytes = L.red + 4 * (4 * ROW_WAVES + 24);
+  L.red = L.hist + 4 * 256;               // i32[4][ROW_MAX_WAVES] per-wave partials, i32[24] broadcasts
+  L.bytes = L.red + 4 * (4 * ROW_MAX_WAVES + 24);
   return L;
 }
 size_t row_kernel_lds(int C) { return rowk_layout(C).bytes; }
@@ -2686,25 +2706,37 @@ __device__ __forceinline__ RArgs rargs() {
   return (RArgs)opq((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
 }
 
-// block-wide reductions of one i32 per thread: wave partials in red[ROW_WAVES], every thread reads all
-__device__ __forceinline__ int row_block_max(int v, int* red) {
+// block-wide reductions of one i32 per thread: wave partials in red[nw], every thread reads all (NW > 0: the
+// wave count as a constant)
+template <int NW>
+__device__ __forceinline__ int row_block_max(int v, int* red, int nw) {
   const int r = wave_max_u_i32(v);
   if (lane_id() == 0) red[threadIdx.x >> 6] = r;
   __syncthreads();
   int m = red[0];
+  if constexpr (NW > 0) {
 #pragma unroll
-  for (int i = 1; i < ROW_WAVES; ++i) m = red[i] > m ? red[i] : m;
+    for (int i = 1; i < NW; ++i) m = red[i] > m ? red[i] : m;
+  } else {
+    for (int i = 1; i < nw; ++i) m = red[i] > m ? red[i] : m;
+  }
   __syncthreads();
   return m;
 }
-__device__ __forceinline__ int row_block_min(int v, int* red) { return -row_block_max(-v, red); }
-__device__ __forceinline__ int row_block_sum(int v, int* red) {
+template <int NW>
+__device__ __forceinline__ int row_block_min(int v, int* red, int nw) { return -row_block_max<NW>(-v, red, nw); }
+template <int NW>
+__device__ __forceinline__ int row_block_sum(int v, int* red, int nw) {
   const int r = wave_sum_u_i32(v);
   if (lane_id() == 0) red[threadIdx.x >> 6] = r;
   __syncthreads();
   int m = 0;
+  if constexpr (NW > 0) {
 #pragma unroll
-  for (int i = 0; i < ROW_WAVES; ++i) m += red[i];
+    for (int i = 0; i < NW; ++i) m += red[i];
+  } else {
+    for (int i = 0; i < nw; ++i) m += red[i];
+  }
   __syncthreads();
   return m;
 }
@@ -2723,17 +2755,23 @@ __device__ __forceinline__ void row_exclusive_scan(int* cnt, int m, int by = 0) 
   if (lane == 0) cnt[m] = carry;
 }
 
-// SM >= 0: specialised for that score-plugin mask (as schedule_wide_kernel)
-template <int SM = -1>
-__global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel(RowArgs args) {
-  (void)args;  // read through rargs()
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// The row path over BatchDev::rows, for one workgroup: schedule_row_kernel's body (NT = ROW_THREADS) and
+// schedule_wide_kernel's opening phase (NT = 0: the wide block's blockDim.x threads, up to ROW_MAX_WAVES
+// waves) — the wide kernel's blocks take the units prep_kernel routed to rows before their own work
+// queue, so no second stream, fork or join is needed. `args` returns the kernel's arguments (SnapDev s,
+// BatchDev b, OutDev o, ProfDev p in the constant address space); smem: row_kernel_lds(C) bytes of LDS.
+// SM >= 0: specialised for that score-plugin mask (as schedule_wide_kernel).
+template <int SM, int NT, class ArgsOf>
+__device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg) {
+  constexpr int NW = NT / 64;
+  const int NTH = NT > 0 ? NT : (int)blockDim.x;
+  const int NWV = NT > 0 ? NW : NTH >> 6;
   const int tid = threadIdx.x, lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   int C, TW;
   uint32_t fm, sm;
   {
-    RArgs a = rargs();
+    auto a = rargs();
     C = a->s.C;
     TW = a->s.TW;
     fm = a->p.filter_mask;
@@ -2749,16 +2787,17 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
   uint16_t* posr_l = (uint16_t*)(smem + L.posr);
   uint64_t* termw = (uint64_t*)(smem + L.x);  // preferred-term words (scoring and normalisation only)
   uint16_t* pid_g;  // the block's global slab (replays longer than ROW_NREP)
-  pid_g = (uint16_t*)(rargs()->slabs + (size_t)blockIdx.x * row_slab_bytes(C));
+  pid_g = (uint16_t*)(rargs()->b.row_slabs + (size_t)blockIdx.x * row_slab_bytes(C));
   uint64_t* const swl0 = (uint64_t*)(smem + L.sw);
   int32_t* const cnt0 = (int32_t*)(smem + L.cnt);
   uint32_t* hist = (uint32_t*)(smem + L.hist);
   int32_t* red = (int32_t*)(smem + L.red);
-  int32_t* bc = red + 4 * ROW_WAVES;  // broadcasts
+  int32_t* bc = red + 4 * ROW_MAX_WAVES;  // broadcasts
 #if defined(KAD_PHASE_PROF) || defined(KAD_TUNING)
-  const int rexp = rargs()->exp;
+  const int rexp = rexp_arg;
 #else
   constexpr int rexp = 0;
+  (void)rexp_arg;
 #endif
   const bool s_res =
       (sm & (BIT(KAD_PL_LEAST_ALLOCATED) | BIT(KAD_PL_MOST_ALLOCATED) | BIT(KAD_PL_BALANCED_ALLOCATION))) && !(rexp & 1);
@@ -2779,7 +2818,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
   if (tid == 0) bc[20] = -2;
   int par = 0;  // the current unit's buffers
   auto next_unit = [&]() -> int {  // thread 64 only
-    RArgs a = rargs();
+    auto a = rargs();
     const int rn = __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int nx = ticket < rn ? a->b.rows[ticket] : -1;
     if (ticket < rn) ticket = atomicAdd(a->b.rows_head, 1);
@@ -2821,7 +2860,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     uint64_t* const swl = swl0 + (size_t)par * nch;
     int32_t* const cnt = cnt0 + (size_t)par * (nch + 1);
     bool did_pf = false;  // wave 1 prefetched the next unit during this one (uniform)
-    RArgs a = rargs();
+    auto a = rargs();
     const UnitRec* rec = a->b.rec + w;
     const uint32_t fc = ldc(&rec->flags);
     const int64_t rqc = ldc(&rec->req_cpu), rqm = ldc(&rec->req_mem);
@@ -2838,7 +2877,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     const int64_t mc = ldc(&rec->maxc), ooff = ldc(&rec->out_off);
     auto status = [&](int32_t st) {
       if (tid == 0) {
-        RArgs ao = rargs();
+        auto ao = rargs();
         ao->o.status[w] = st;
         ao->o.count[w] = 0;
         ao->o.flags[w] = 0;
@@ -2847,7 +2886,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
 
     // ---------------- compaction of the static words (every filter folded by prep_kernel)
     if (!pre) {
-      for (int ch = tid; ch < nch; ch += ROW_THREADS) {
+      for (int ch = tid; ch < nch; ch += NTH) {
         const uint64_t m = ldg(a->b.sw, (uint32_t)(w * nch + ch));
         swl[ch] = m;
         cnt[ch] = popc64(m);
@@ -2857,7 +2896,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     }
     __syncthreads();
     const int n = __builtin_amdgcn_readfirstlane(cnt[nch]);
-    for (int ch = wv; ch < nch; ch += ROW_WAVES) {
+    for (int ch = wv; ch < nch; ch += NWV) {
       const uint64_t m = swl[ch];
       if (lane_on(m)) idx[cnt[ch] + mbcnt(m)] = (uint16_t)(ch * WAVE + lane);
     }
@@ -2924,7 +2963,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     };
     if (s_aff) {
       __syncthreads();  // tdesc
-      for (int x = tid; x < n_terms * nch; x += ROW_THREADS) {
+      for (int x = tid; x < n_terms * nch; x += NTH) {
         const int t = x / nch, ch = x - t * nch;
         const int ne = tdesc[t], io = tdesc[ROW_MAX_TERMS + t];
         uint64_t m = ~0ull;
@@ -2945,15 +2984,15 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     // ROW_RU positions per trip: every gather of all of them is issued before any is used (the phase is
     // latency-bound: its resource, taint and affinity parts cost cycles in proportion to their load chains)
     constexpr int RU = ROW_RU;
-    for (int j0 = tid; j0 < n; j0 += RU * ROW_THREADS) {
-      RArgs as = rargs();
+    for (int j0 = tid; j0 < n; j0 += RU * NTH) {
+      auto as = rargs();
       double4 r4[RU];
       float2 iv[RU];
       uint64_t pn[RU][TFOLD_MAX_TW];
       uint32_t cs[RU];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
-        const int j = j0 + u * ROW_THREADS;
+        const int j = j0 + u * NTH;
         cs[u] = idx[j < n ? j : j0];
       }
 #pragma unroll
@@ -2977,7 +3016,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
       }
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
-        const int j = j0 + u * ROW_THREADS;
+        const int j = j0 + u * NTH;
         if (j >= n) break;
         const uint32_t c = cs[u];
         int x = 0;
@@ -3010,15 +3049,15 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
     }
     KAD_PT(t1b);
     KAD_PADD(7, t1b - t1a);
-    if (s_tt) ttmax = row_block_max(ttmax, red);
-    if (s_aff) amax = row_block_max(amax, red);
+    if (s_tt) ttmax = row_block_max<NW>(ttmax, red, NWV);
+    if (s_aff) amax = row_block_max<NW>(amax, red, NWV);
     __syncthreads();
     KAD_PT(t2);
     KAD_PADD(2, t2 - t1);
 
     // ---------------- DefaultNormalizeScore + totals, stored order-preserving as u32 (total ^ 2^31)
     int mn = INT32_MAX, mx = INT32_MIN;
-    for (int j = tid; j < n; j += ROW_THREADS) {
+    for (int j = tid; j < n; j += NTH) {
       const uint32_t x = key[j];
       int t = (int)(x & 0x3FFu);
       if (s_tt) t += ttmax == 0 ? 100 : 100 - (int)small_quot(100 * (int)((x >> 10) & 0x1FFu), ttmax);
@@ -3031,8 +3070,8 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
       mn = t < mn ? t : mn;
       mx = t > mx ? t : mx;
     }
-    mn = row_block_min(mn, red);
-    mx = row_block_max(mx, red);
+    mn = row_block_min<NW>(mn, red, NWV);
+    mx = row_block_max<NW>(mx, red, NWV);
     KAD_PT(t3);
     KAD_PADD(3, t3 - t2);
 
@@ -3052,7 +3091,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
         for (int shift = ((bits + 7) / 8 - 1) * 8; shift >= 0; shift -= 8) {
           if (tid < 256) hist[tid] = 0;
           __syncthreads();
-          for (int j = tid; j < n; j += ROW_THREADS) {
+          for (int j = tid; j < n; j += NTH) {
             const uint32_t d = key[j] - base;
             if ((d & pmask) == prefix) atomicAdd(&hist[(d >> shift) & 255u], 1u);
           }
@@ -3088,13 +3127,13 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
       }
       Tk = base + prefix;
       int g = 0, e = 0;
-      for (int j = tid; j < n; j += ROW_THREADS) {
+      for (int j = tid; j < n; j += NTH) {
         const uint32_t t = key[j];
         g += t > Tk;
         e += t == Tk;
       }
-      g = row_block_sum(g, red);
-      e = row_block_sum(e, red);
+      g = row_block_sum<NW>(g, red, NWV);
+      e = row_block_sum<NW>(e, red, NWV);
       KAD_PT(t4);
       KAD_PADD(4, t4 - t3);
       if (k - g != e) {  // ties straddle the cut: Go's pdqsort decides which tied clusters stay (n > 256)
@@ -3108,7 +3147,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
         inv = posl;
         // packed replay (key - min << 16 | position: every C5 row, n <= C < 2^16) unless the totals span 2^16
         const bool packed = (uint32_t)mx - (uint32_t)mn < 65536u;
-        for (int j = tid; j < n; j += ROW_THREADS) {
+        for (int j = tid; j < n; j += NTH) {
           if (packed)
             key[j] = (((key[j] ^ 0x80000000u) - (uint32_t)mn) << 16) | (uint32_t)j;
           else
@@ -3122,12 +3161,12 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
         did_pf = true;  // wave 1 prefetches the next unit while wave 0 finishes the replay alone
         if (packed && in_lds) {
           PdqWaveP<> pw{key, posl, posr, xs_b, xs_c};
-          const auto st = pw.select_block(n, k, ROW_BLOCK_PART, ROW_WAVES, wv, red);
+          const auto st = pw.select_block(n, k, ROW_BLOCK_PART, NWV, wv, red);
           if (wv == 0) pw.select_from(st, k);
           else if (wv == 1) prefetch();
         } else if (packed) {  // elements stay in LDS; stopper scratch in the slab (workgroup fences order both)
           PdqWaveP<true> pw{key, posl, posr, xs_b, xs_c};
-          const auto st = pw.select_block(n, k, ROW_BLOCK_PART, ROW_WAVES, wv, red);
+          const auto st = pw.select_block(n, k, ROW_BLOCK_PART, NWV, wv, red);
           if (wv == 0) pw.select_from(st, k);
           else if (wv == 1) prefetch();
         } else if (wv == 1) {
@@ -3142,7 +3181,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
           }
         }
         __syncthreads();
-        for (int r = tid; r < n; r += ROW_THREADS) inv[packed ? (key[r] & 0xFFFFu) : pid[r]] = (uint16_t)r;
+        for (int r = tid; r < n; r += NTH) inv[packed ? (key[r] & 0xFFFFu) : pid[r]] = (uint16_t)r;
         __syncthreads();
         KAD_PT(t5);
         KAD_PADD(5, t5 - t4);
@@ -3163,7 +3202,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
         if (mode == 1) return key[p] >= Tk;
         return inv[p] < k;
       };
-      for (int q = wv; q < nq; q += ROW_WAVES) {
+      for (int q = wv; q < nq; q += NWV) {
         const uint64_t m = ballot(selected(q * WAVE + lane));
         if (lane == 0) cnt[q] = popc64(m);
       }
@@ -3171,10 +3210,10 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
       row_exclusive_scan(cnt, nq);
       __syncthreads();
       total = __builtin_amdgcn_readfirstlane(cnt[nq]);
-      RArgs ao = rargs();
+      auto ao = rargs();
       int32_t* oc = ao->o.cluster + ooff;
       int64_t* orp = ao->o.replicas + ooff;
-      for (int q = wv; q < nq; q += ROW_WAVES) {
+      for (int q = wv; q < nq; q += NWV) {
         const int p = q * WAVE + lane;
         const bool s = selected(p);
         const uint64_t m = ballot(s);
@@ -3186,7 +3225,7 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
       }
     }
     if (tid == 0) {
-      RArgs ao = rargs();
+      auto ao = rargs();
       ao->o.status[w] = KAD_ST_OK;
       ao->o.count[w] = total;  // Divide without replicas plugin: empty map
       ao->o.flags[w] = rflags;
@@ -3201,6 +3240,23 @@ __global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel
   }
 #endif
   KAD_PFLUSH_ROW;
+}
+
+template <int SM>
+__device__ __attribute__((noinline)) void wide_rows(char* smem, WArgs a) {
+  row_units<SM, 0>([a] { return a; }, smem, 0);
+}
+
+template <int SM = -1>
+__global__ __launch_bounds__(ROW_THREADS, KAD_ROW_MINW) void schedule_row_kernel(RowArgs args) {
+  (void)args;  // read through rargs()
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#if defined(KAD_PHASE_PROF) || defined(KAD_TUNING)
+  const int rexp = rargs()->exp;
+#else
+  constexpr int rexp = 0;
+#endif
+  row_units<SM, ROW_THREADS>([] { return rargs(); }, smem, rexp);
 }
 
 // ============================================================ plan kernel
@@ -3900,8 +3956,13 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const long need = ((long)b.W + wpb - 1) / wpb;
     if (grid > need) grid = need;
     static const int exp = tuning_env("KAD_WIDE_EXPERIMENT", 0);
-    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, exp};
-    const bool beside = b.early_rows && b.use_rows && side && fork && join;
+    // the routed long units inside the wide kernel (its opening phase) when the row body's LDS fits below
+    // the cluster cache; else the row kernel beside it on a second stream
+    const int no_inline = tuning_env("KAD_ROWS_NO_INLINE", 0);  // (read per launch: tuning builds only)
+    const bool inline_rows = b.early_rows && b.use_rows && !no_inline && wpb >= 2 &&
+                             row_kernel_lds(s.C) <= (size_t)wpb * per_wave;
+    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, inline_rows ? 1 : 0, exp};
+    const bool beside = !inline_rows && b.early_rows && b.use_rows && side && fork && join;
     if (beside) {  // the row kernel on the side stream, from the end of prep_kernel, beside the wide kernel
       if (hipError_t e = hipEventRecord(fork, st)) return e;
       if (hipError_t e = hipStreamWaitEvent(side, fork, 0)) return e;
@@ -3916,12 +3977,15 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
       // anything later on st (the next batch upload) can overwrite what it reads
       const hipError_t j = hipStreamWaitEvent(st, join, 0);
       if (e == hipSuccess) e = j;
-    } else if (e == hipSuccess) {
+    } else if (e == hipSuccess && !inline_rows) {
       e = launch_rows(s, b, o, p, st);
     }
     if (e != hipSuccess) return e;
     if (hipError_t e2 = rec(after_rows)) return e2;
-    // feasible lists longer than WIDE_P positions can come from any unit: the defer pass always runs
+    // the defer pass only when some unit can reach the defer list (BatchDev::may_defer, host-checked:
+    // REC_FULL units, requests or affinity weights outside the exact path, rows with more preferred terms
+    // than ROW_MAX_TERMS, or units past WIDE_P without early routing)
+    if (!b.may_defer) return hipSuccess;
     return launch_defer_pass(s, b, o, p, gscr, scr_bytes, st);
   }
   if (fast_path(s.C)) {
