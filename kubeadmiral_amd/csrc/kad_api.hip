@@ -41,6 +41,8 @@ struct kad_ctx {
   std::vector<int32_t> plan_rows;
   int32_t* d_plan_rows = nullptr;
   size_t plan_rows_cap = 0;
+  void* d_plan_hdr = nullptr;  // PlanRowHdr per planner row (plan_hdr_kernel at upload)
+  size_t plan_hdr_cap = 0;
   // outputs
   int32_t *d_status = nullptr, *d_count = nullptr, *d_cluster = nullptr;
   uint32_t* d_flags = nullptr;
@@ -443,7 +445,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (c->side) (void)hipStreamSynchronize(c->side);  // the row kernel may run there: drain it before any free
-  for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
+  for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, c->d_plan_hdr, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
                   (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab, c->d_vrows, c->d_rescols,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs, c->d_diff})
     if (p) (void)hipFree(p);
@@ -1198,6 +1200,10 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
   b.defer = b.defer_n + 4;
   b.rows = b.defer + W;
   b.wq = static_cast<uint32_t*>(c->d_wq);
+  // the planner rows' unit-level operands in one line per row (plan_kernel), gathered on the device
+  if (int r = grow(c, &c->d_plan_hdr, &c->plan_hdr_cap, c->plan_rows.size() * sizeof(PlanRowHdr))) return r;
+  HIPCHK(c, launch_plan_hdr(b, c->d_plan_rows, (int)c->plan_rows.size(), static_cast<PlanRowHdr*>(c->d_plan_hdr),
+                            c->stream));
   c->have_batch = true;
   c->ran = false;
   return KAD_OK;
@@ -1287,7 +1293,8 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
                             tm ? c->ev[6] : nullptr, c->side, c->fork_ev, c->join_ev));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())
-    HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, c->d_plan_rows, (int)c->plan_rows.size(), c->batch_hdr.max_row_slots,
+    HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, static_cast<const PlanRowHdr*>(c->d_plan_hdr), (int)c->plan_rows.size(),
+                          c->batch_hdr.max_row_slots,
                           c->d_scratch, c->scratch_bytes, c->stream));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   c->ran = true;

@@ -235,7 +235,24 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
                            void* global_scratch, size_t scratch_bytes, hipStream_t st, hipEvent_t after_main = nullptr,
                            hipEvent_t after_rows = nullptr, hipStream_t side = nullptr, hipEvent_t fork = nullptr,
                            hipEvent_t join = nullptr);
-hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,
+// One planner row's unit-level operands, gathered once per batch upload (plan_hdr_kernel) from the batch's
+// per-unit arrays so that plan_kernel reads one 64-B line per row (its lanes 0..15 hold the dwords) instead
+// of ten scattered per-unit loads one dependent step before everything else.
+struct PlanRowHdr {
+  int32_t w;          // unit
+  uint32_t flags;     // KAD_W_*
+  int64_t off;        // OUT_OFF[w]
+  int32_t slots;      // OUT_OFF[w + 1] - OUT_OFF[w] (the unit's slot bound)
+  int32_t p0, p1;     // PREF_OFF[w], PREF_OFF[w + 1]
+  int32_t c0, c1;     // CUR_OFF[w], CUR_OFF[w + 1]
+  int32_t k0, k1;     // KEY_OFF[w], KEY_OFF[w + 1]
+  int32_t pad;
+  int64_t desired;    // *DesiredReplicas
+  int64_t pad2;
+};
+static_assert(sizeof(PlanRowHdr) == 64, "one line per planner row");
+hipError_t launch_plan_hdr(const BatchDev& b, const int32_t* rows, int n_rows, PlanRowHdr* out, hipStream_t st);
+hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const PlanRowHdr* rows,
                        int n_rows, int kmax, void* global_scratch, size_t scratch_bytes, hipStream_t st);
 hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,
                               uint32_t pflags, int kmax, int32_t* out_count, int32_t* out_sel, int32_t* out_status,

@@ -977,7 +977,10 @@ __device__ __forceinline__ int2 fit_ranks(const SnapDev& s, const int64_t (*fenc
 #define KAD_PREP_CPL 4
 #endif
 constexpr int PREP_CPL = KAD_PREP_CPL;                 // chunks per lane
-__global__ __launch_bounds__(256) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
+#ifndef KAD_PREP_MINW
+#define KAD_PREP_MINW 1
+#endif
+__global__ __launch_bounds__(256, KAD_PREP_MINW) void prep_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
   constexpr int CPL = PREP_CPL;
   __shared__ int32_t prog_words[256 * CPL];  // words CPL*l .. CPL*l+CPL-1 of its unit's filter program, per lane
   const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
@@ -3340,8 +3343,30 @@ __device__ __forceinline__ int find_sorted(const int32_t* a, int lo, int hi, int
 // LANES: rows of K <= 64 only, the planner in registers (8 waves / SIMD: <= 64 VGPRs); else rows of
 // K > 64 only, with the LDS / global-scratch workspace (GSCR). launch_plan runs the first and, when
 // some row may exceed 64 clusters, the second; each skips the other's rows.
+// PlanRowHdr of every planner row (once per batch upload): one lane per row
+__global__ __launch_bounds__(256) void plan_hdr_kernel(BatchDev b, const int32_t* rows, int n_rows, PlanRowHdr* out) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_rows) return;
+  const int w = rows[r];
+  PlanRowHdr h;
+  h.w = w;
+  h.flags = b.flags[w];
+  h.off = b.out_off[w];
+  h.slots = (int32_t)(b.out_off[w + 1] - b.out_off[w]);
+  h.p0 = b.pref_off[w];
+  h.p1 = b.pref_off[w + 1];
+  h.c0 = b.cur_off[w];
+  h.c1 = b.cur_off[w + 1];
+  h.k0 = b.key_off[w];
+  h.k1 = b.key_off[w + 1];
+  h.pad = 0;
+  h.desired = b.desired[w];
+  h.pad2 = 0;
+  out[r] = h;
+}
+
 template <bool GSCR, bool LANES>
-__global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, BatchDev b, OutDev o, const int32_t* rows,
+__global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, BatchDev b, OutDev o, const PlanRowHdr* rows,
                                                                  int n_rows, int kmax, char* gscratch, int wave_bytes,
                                                                  int r_stride, int tbl_cp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -3364,37 +3389,46 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
     wsync<GSCR>();
   }
   KAD_PACC;
-  int wn = gw < n_rows ? rows[gw] : 0;  // the next row's unit, loaded one row ahead
+  // the row's PlanRowHdr in lanes 0..15 (one 64-B line), loaded one row ahead
+  auto fetch_hdr = [&](int r) -> uint32_t {
+    return (r < n_rows && lane < 16) ? ldg((const uint32_t*)(rows + r), (uint32_t)lane) : 0u;
+  };
+  uint32_t hn = fetch_hdr(gw);
   for (int r = gw; r < n_rows; r += r_stride) {
     KAD_PT(t0);
-    const int w = wn;
-    if (r + r_stride < n_rows) wn = rows[r + r_stride];
-    // every per-unit scalar is loaded before the status test so the loads
-    // issue together (one memory round trip instead of three dependent ones;
-    // w < W, so each index is in bounds whatever the status)
+    const uint32_t hc = hn;
+    hn = fetch_hdr(r + r_stride);
+    auto hf = [&](int d) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)hc, d); };
+    const int w = (int)hf(0);
+    const uint32_t f = hf(1);
+    const int64_t off = (int64_t)(((uint64_t)hf(3) << 32) | hf(2));
+    const int slots = (int)hf(4);
+    const int p0 = (int)hf(5), p1 = (int)hf(6);
+    const int c0 = (int)hf(7), c1 = (int)hf(8);
+    const int ko0 = (int)hf(9), ko1 = (int)hf(10);
+    const int64_t desired = (int64_t)(((uint64_t)hf(13) << 32) | hf(12));
+    // everything this row reads next issues together (one memory round trip): the schedule stage's status,
+    // count and flags, the unit's slot ids (within its bound, whatever the count), key bytes, and (K <= 64)
+    // the preference / current-cluster ids for the lookup tables
     const int st = o.status[w];
     const int K = o.count[w];
-    const uint32_t f = b.flags[w];
-    const int64_t off = b.out_off[w];
-    const int p0 = b.pref_off[w], p1 = b.pref_off[w + 1];
-    const int c0 = b.cur_off[w], c1 = b.cur_off[w + 1];
-    const int ko0 = b.key_off[w], ko1 = b.key_off[w + 1];
-    const int64_t desired = b.desired[w];
     const uint32_t rflags0 = o.flags[w];
-    if (st != KAD_ST_OK || K <= 0 || (K <= WAVE) != LANES) continue;
     const uint8_t* key = b.key + ko0;
     const int klen = ko1 - ko0;
-    const int64_t total = (f & KAD_W_HAS_DESIRED) ? desired : 0;
     // su.Key() bytes in lanes (uniform): the FNV-1 continuation of every element
     // reads them with v_readlane instead of one dependent load per byte
     const uint32_t kb0 = lane < klen ? (uint32_t)key[lane] : 0u;
-    // rows of K <= 64: element `lane`'s cluster id and name hash are loaded before the lookup tables are
-    // filled, so those loads and the tables' index loads share one memory round trip
     int c_l = 0;
+    if (LANES && slots > 0) c_l = o.cluster[off + (lane < slots ? lane : 0)];  // (no slot: nothing to read)
+    if (st != KAD_ST_OK || K <= 0 || (K <= WAVE) != LANES) continue;
+    const int64_t total = (f & KAD_W_HAS_DESIRED) ? desired : 0;
+    // rows of K <= 64: element `lane`'s name hash (and cores) are loaded before the lookup tables are
+    // filled, so those loads and the tables' index loads share one memory round trip
     uint32_t h_l = 0;
     int64_t ac_l = 0, av_l = 0;  // cores for dynamic weights (rsp.go:183-272)
     if constexpr (LANES) {
-      c_l = o.cluster[off + (lane < K ? lane : 0)];
+      const int first_c = __builtin_amdgcn_readfirstlane(c_l);  // (every lane active: lane 0 holds element 0)
+      if (lane >= K) c_l = first_c;  // past K: element 0 (masked off later)
       h_l = s.name_fnv[c_l];
       if (f & KAD_W_DYNAMIC_WEIGHTS) {
         ac_l = s.alloc_cores[c_l];
@@ -4080,7 +4114,14 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
   return hipGetLastError();
 }
 
-hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const int32_t* rows,
+hipError_t launch_plan_hdr(const BatchDev& b, const int32_t* rows, int n_rows, PlanRowHdr* out, hipStream_t st) {
+  (void)hipGetLastError();
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(plan_hdr_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, st, b, rows, n_rows, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const PlanRowHdr* rows,
                        int n_rows, int kmax, void* gscr, size_t scr_bytes, hipStream_t st) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   (void)p;
