@@ -2694,8 +2694,11 @@ constexpr int ROW_BLOCK_PART = 256;  // replay partitions of longer ranges run o
 constexpr int ROW_RU = KAD_ROW_RU;
 static_assert(ROW_MAX_BLOCKS >= 1, "row kernel slabs");
 struct RowKLayout {
-  size_t key, idx, x, pid, posl, posr, sw, cnt, hist, red, bytes;
+  size_t key, idx, x, pid, posl, posr, sw, cnt, hist, red, pre, bytes;
 };
+// a unit's staged record and score program (u32[2][ROW_PRE_DW], the next unit's prefetched into the other
+// buffer): its UnitRec dwords, the program length, then its first ROW_PRE_PROG program words
+constexpr int ROW_PRE_PROG = 64, ROW_PRE_DW = 16 + 1 + ROW_PRE_PROG + 15;
 __host__ __device__ inline RowKLayout rowk_layout(int C) {
   const size_t Cp = (size_t)((C + 63) & ~63), nch = Cp / 64;
   RowKLayout L;
@@ -2711,7 +2714,8 @@ __host__ __device__ inline RowKLayout rowk_layout(int C) {
                                           //   exclusive prefix (+ total)
   L.hist = (L.cnt + 8 * (nch + 1) + 15) & ~(size_t)15;  // u32[256]
   L.red = L.hist + 4 * 256;               // i32[4][ROW_MAX_WAVES] per-wave partials, i32[24] broadcasts
-  L.bytes = L.red + 4 * (4 * ROW_MAX_WAVES + 24);
+  L.pre = L.red + 4 * (4 * ROW_MAX_WAVES + 24);  // u32[2][ROW_PRE_DW]: staged records + score programs
+  L.bytes = L.pre + 4 * 2 * ROW_PRE_DW;
   return L;
 }
 size_t row_kernel_lds(int C) { return rowk_layout(C).bytes; }
@@ -2836,19 +2840,42 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
   // also prefetches the next unit: its static words, chunk counts and their prefix into the other LDS
   // buffer (bc[20]: the prefetched unit, -1 the list is drained, -2 nothing prefetched); the list is
   // complete before this kernel starts (prep_kernel's early routing, or the lean kernel before it)
-  int ticket = 0;
-  if (tid == 64) ticket = atomicAdd(rargs()->b.rows_head, 1);
+  // thread 64 holds the list length (complete before this kernel starts), its ticket and the unit the ticket
+  // names, loaded one dequeue ahead: a dequeue returns a unit already in a register and only issues the next
+  // ticket's atomic and list load (waited for at the next dequeue, a unit later)
+  int ticket = 0, rn = 0, nxt_u = -1;
+  if (tid == 64) {
+    auto a = rargs();
+    rn = __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = atomicAdd(a->b.rows_head, 1);
+    nxt_u = ticket < rn ? a->b.rows[ticket] : -1;
+  }
 #ifdef KAD_PHASE_PROF
   const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
   unsigned long long rt_units = 0;
 #endif
   if (tid == 0) bc[20] = -2;
   int par = 0;  // the current unit's buffers
-  auto next_unit = [&]() -> int {  // thread 64 only
+  uint32_t* const pre0 = (uint32_t*)(smem + L.pre);
+  // one wave: unit u's UnitRec dwords (lanes 0-15), its score-program length and first ROW_PRE_PROG words into
+  // pr — the unit's scalars are then LDS reads, not a chain of scalar loads (record → program → each term)
+  auto stage_unit = [&](int u, uint32_t* pr) {
     auto a = rargs();
-    const int rn = __hip_atomic_load(a->b.rows_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int nx = ticket < rn ? a->b.rows[ticket] : -1;
-    if (ticket < rn) ticket = atomicAdd(a->b.rows_head, 1);
+    const uint32_t rd = lane < 16 ? ldg((const uint32_t*)(a->b.rec + u), (uint32_t)lane) : 0u;
+    const int so = ldg(a->b.sprog_off, (uint32_t)u), se = ldg(a->b.sprog_off, (uint32_t)u + 1u);
+    const int len = se - so;
+    const int32_t pw = lane < len ? ldg(a->b.sprog, (uint32_t)(so + lane)) : 0;
+    if (lane < 16) pr[lane] = rd;
+    if (lane == 0) pr[16] = (uint32_t)len;
+    pr[17 + lane] = (uint32_t)pw;
+  };
+  auto next_unit = [&]() -> int {  // thread 64 only
+    const int nx = nxt_u;
+    if (nx >= 0) {
+      auto a = rargs();
+      ticket = atomicAdd(a->b.rows_head, 1);
+      nxt_u = ticket < rn ? a->b.rows[ticket] : -1;
+    }
     return nx;
   };
   auto prefetch = [&]() {  // wave 1
@@ -2856,6 +2883,7 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
     wave_sync();
     const int nx = __builtin_amdgcn_readfirstlane(bc[20]);
     if (nx < 0) return;
+    stage_unit(nx, pre0 + (size_t)(par ^ 1) * ROW_PRE_DW);
     uint64_t* sw2 = swl0 + (size_t)(par ^ 1) * nch;
     int32_t* c2 = cnt0 + (size_t)(par ^ 1) * (nch + 1);
     const uint64_t* src = rargs()->b.sw + (size_t)nx * nch;
@@ -2886,13 +2914,31 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
     if (pre) par ^= 1;
     uint64_t* const swl = swl0 + (size_t)par * nch;
     int32_t* const cnt = cnt0 + (size_t)par * (nch + 1);
+    uint32_t* const pr = pre0 + (size_t)par * ROW_PRE_DW;
     bool did_pf = false;  // wave 1 prefetched the next unit during this one (uniform)
     auto a = rargs();
-    const UnitRec* rec = a->b.rec + w;
-    const uint32_t fc = ldc(&rec->flags);
-    const int64_t rqc = ldc(&rec->req_cpu), rqm = ldc(&rec->req_mem);
-    const int spo = ldc(&rec->sprog_off);
-    const bool many_terms = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && ldc(a->b.sprog + spo) > ROW_MAX_TERMS;
+    if (!pre) {  // not prefetched: record, program and static words now (the chunk counts' prefix below)
+      if (wv == 0) stage_unit(w, pr);
+      for (int ch = tid; ch < nch; ch += NTH) {
+        const uint64_t m = ldg(a->b.sw, (uint32_t)(w * nch + ch));
+        swl[ch] = m;
+        cnt[ch] = popc64(m);
+      }
+      __syncthreads();
+      row_exclusive_scan(cnt, nch);
+    }
+    __syncthreads();
+    auto prd = [&](int d) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)pr[d]); };
+    auto prd64 = [&](int d) -> int64_t { return (int64_t)(((uint64_t)prd(d + 1) << 32) | prd(d)); };
+    const uint32_t fc = prd(0);
+    const int64_t rqc = prd64(4), rqm = prd64(6);
+    const int spo = (int)prd(3);
+    const int plen = (int)prd(16);
+    // score program word i: staged in LDS (programs of up to ROW_PRE_PROG words, every bench unit's), else global
+    auto spw = [&](int i) -> int32_t {
+      return plen <= ROW_PRE_PROG ? (int32_t)prd(17 + i) : ldc(rargs()->b.sprog + spo + i);
+    };
+    const bool many_terms = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && plen > 0 && spw(0) > ROW_MAX_TERMS;
     if ((uint64_t)rqc >= (1ull << 46) || (uint64_t)rqm >= (1ull << 46) || (fc & KAD_W_WIDE_SCORES) || many_terms) {
       if (tid == 0) {  // outside the exact clean-f64 range: the full kernel
         const int slot = atomicAdd(a->b.defer_n, 1);
@@ -2900,8 +2946,8 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
       }
       continue;
     }
-    const int tsc = ldc(&rec->tolset);
-    const int64_t mc = ldc(&rec->maxc), ooff = ldc(&rec->out_off);
+    const int tsc = (int)prd(2);
+    const int64_t mc = prd64(8), ooff = prd64(10);
     auto status = [&](int32_t st) {
       if (tid == 0) {
         auto ao = rargs();
@@ -2912,20 +2958,30 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
     };
 
     // ---------------- compaction of the static words (every filter folded by prep_kernel)
-    if (!pre) {
-      for (int ch = tid; ch < nch; ch += NTH) {
-        const uint64_t m = ldg(a->b.sw, (uint32_t)(w * nch + ch));
-        swl[ch] = m;
-        cnt[ch] = popc64(m);
-      }
-      __syncthreads();
-      row_exclusive_scan(cnt, nch);
-    }
-    __syncthreads();
     const int n = __builtin_amdgcn_readfirstlane(cnt[nch]);
-    for (int ch = wv; ch < nch; ch += NWV) {
-      const uint64_t m = swl[ch];
-      if (lane_on(m)) idx[cnt[ch] + mbcnt(m)] = (uint16_t)(ch * WAVE + lane);
+    {
+      // four chunks per trip, their words and offsets read together; every lane stores (infeasible lanes
+      // into a dummy slot of the term-word region, unused until the term words below): no exec branch
+      // between the LDS reads of consecutive chunks
+      uint16_t* const dmy = (uint16_t*)(smem + L.x) + lane;
+      for (int ch0 = wv; ch0 < nch; ch0 += 4 * NWV) {
+        uint64_t mm[4];
+        int co[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int ch = ch0 + u * NWV;
+          const int cl = ch < nch ? ch : nch - 1;
+          const uint64_t m = swl[cl];
+          mm[u] = ch < nch ? m : 0ull;
+          co[u] = cnt[cl];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool on = lane_on(mm[u]);
+          uint16_t* const dst = on ? idx + co[u] + mbcnt(mm[u]) : dmy;
+          *dst = (uint16_t)((ch0 + u * NWV) * WAVE + lane);
+        }
+      }
     }
     KAD_PADD(0, 1);
     if (n == 0) {  // generic_scheduler.go:112-114
@@ -2951,7 +3007,7 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
 
     // ---------------- raw scores (RunScorePlugins, framework.go:139-181)
     const int32_t* sp = a->b.sprog + spo;
-    const int n_terms = ldc(sp);
+    const int n_terms = plen > 0 ? spw(0) : 0;
     const bool s_aff = (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && n_terms > 0 && !(rexp & 4);  // no terms: 0 everywhere
     // ClusterAffinity preferred terms (cluster_affinity.go:96-135) as per-chunk words in LDS (<= ROW_MAX_TERMS,
     // checked above): word (t, ch) = AND of the term's requirement rows — once per chunk instead of once per
@@ -2967,8 +3023,8 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
       for (int t = 0; t < ROW_MAX_TERMS; ++t) {
         wt[t] = 0;
         if (t < n_terms) {
-          wt[t] = ldc(sp + pc);
-          const int ne = ldc(sp + pc + 1);
+          wt[t] = spw(pc);
+          const int ne = spw(pc + 1);
           if (tid == 0) {
             tdesc[t] = ne;
             tdesc[ROW_MAX_TERMS + t] = pc + 2;
@@ -2994,8 +3050,20 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
         const int t = x / nch, ch = x - t * nch;
         const int ne = tdesc[t], io = tdesc[ROW_MAX_TERMS + t];
         uint64_t m = ~0ull;
-        for (int i = 0; i < ne; ++i)
-          m &= ldg(a->b.req_mask, (uint32_t)ldg(sp, (uint32_t)(io + i)) * (uint32_t)nch + (uint32_t)ch);
+        if (plen <= ROW_PRE_PROG && ne >= 1 && ne <= 4) {  // the rows' loads together (ids repeat past ne: AND is idempotent)
+          uint64_t r[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int id = (int)pr[17 + io + (i < ne ? i : ne - 1)];
+            r[i] = ldg(a->b.req_mask, (uint32_t)id * (uint32_t)nch + (uint32_t)ch);
+          }
+          m = r[0] & r[1] & r[2] & r[3];
+        } else {
+          for (int i = 0; i < ne; ++i) {
+            const int id = plen <= ROW_PRE_PROG ? (int)pr[17 + io + i] : ldg(sp, (uint32_t)(io + i));
+            m &= ldg(a->b.req_mask, (uint32_t)id * (uint32_t)nch + (uint32_t)ch);
+          }
+        }
         termw[x] = m;
       }
       __syncthreads();
@@ -3115,12 +3183,16 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
       int kk = k;
       if (span != 0) {
         const int bits = 32 - __builtin_clz(span);
-        for (int shift = ((bits + 7) / 8 - 1) * 8; shift >= 0; shift -= 8) {
+        // digits from the top: the first pass takes the span's top 8 bits (C5's totals span ~9 bits: 8-bit
+        // digits aligned at bit 8 put every position into 2 bins, thousands of LDS atomics on two words)
+        for (int hi = bits; hi > 0; hi -= 8) {
+          const int shift = hi > 8 ? hi - 8 : 0;
+          const uint32_t dmask = (1u << (hi - shift)) - 1u;
           if (tid < 256) hist[tid] = 0;
           __syncthreads();
           for (int j = tid; j < n; j += NTH) {
             const uint32_t d = key[j] - base;
-            if ((d & pmask) == prefix) atomicAdd(&hist[(d >> shift) & 255u], 1u);
+            if ((d & pmask) == prefix) atomicAdd(&hist[(d >> shift) & dmask], 1u);
           }
           __syncthreads();
           if (wv == 0) {  // lane l owns digits 255-4l .. 252-4l (descending)
@@ -3149,7 +3221,7 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
           const int digit = __builtin_amdgcn_readfirstlane(bc[1]), above = __builtin_amdgcn_readfirstlane(bc[2]);
           kk -= above;
           prefix |= (uint32_t)digit << shift;
-          pmask |= 255u << shift;
+          pmask |= dmask << shift;
         }
       }
       Tk = base + prefix;
