@@ -3527,6 +3527,11 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
     const uint32_t kb0 = lane < klen ? (uint32_t)key[lane] : 0u;
     int c_l = 0;
     if (LANES && slots > 0) c_l = o.cluster[off + (lane < slots ? lane : 0)];  // (no slot: nothing to read)
+    // the lookup tables' first 64 preference / current-cluster ids (uniform guards, clamped lanes: no
+    // exec branch), so that the name hashes and the preference columns below share the next round trip
+    int pid_l = 0, cid_l = 0;
+    if (use_tbl && p1 > p0) pid_l = b.pref_id[p0 + (p0 + lane < p1 ? lane : 0)];
+    if (use_tbl && c1 > c0) cid_l = b.cur_id[c0 + (c0 + lane < c1 ? lane : 0)];
     if (st != KAD_ST_OK || K <= 0 || (K <= WAVE) != LANES) continue;
     const int64_t total = (f & KAD_W_HAS_DESIRED) ? desired : 0;
     // rows of K <= 64: element `lane`'s name hash (and cores) are loaded before the lookup tables are
@@ -3550,8 +3555,10 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
         wsync<GSCR>();
         tag = 1;
       }
-      for (int j = p0 + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = (tag << 16) | (uint32_t)(j - p0 + 1);
-      for (int j = c0 + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = (tag << 16) | (uint32_t)(j - c0 + 1);
+      if (p0 + lane < p1) tbl_p[pid_l] = (tag << 16) | (uint32_t)(lane + 1);
+      if (c0 + lane < c1) tbl_c[cid_l] = (tag << 16) | (uint32_t)(lane + 1);
+      for (int j = p0 + WAVE + lane; j < p1; j += WAVE) tbl_p[b.pref_id[j]] = (tag << 16) | (uint32_t)(j - p0 + 1);
+      for (int j = c0 + WAVE + lane; j < c1; j += WAVE) tbl_c[b.cur_id[j]] = (tag << 16) | (uint32_t)(j - c0 + 1);
       wsync<GSCR>();
     }
     // element i: cluster id, hash, preference columns, current replicas
@@ -3564,15 +3571,6 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
         c = o.cluster[off + i];
         h = s.name_fnv[c];
       }
-      for (int k0 = 0; k0 < klen; k0 += WAVE) {
-        const uint32_t kb = k0 == 0 ? kb0 : (k0 + lane < klen ? (uint32_t)key[k0 + lane] : 0u);
-        const int m = klen - k0 < WAVE ? klen - k0 : WAVE;
-        for (int q = 0; q < m; ++q) {
-          h *= 16777619u;
-          h ^= (uint32_t)__builtin_amdgcn_readlane((int)kb, q);
-        }
-      }
-      e.hash = h;
       int pi, ci;
       if (use_tbl) {
         const uint32_t tp = tbl_p[c], tc = tbl_c[c];
@@ -3610,6 +3608,17 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
         }
       }
       e.cur = ci >= 0 ? b.cur_rep[ci] : 0;
+      // the FNV-1 continuation after the column loads are issued: the name hash's load and theirs share
+      // one round trip
+      for (int k0 = 0; k0 < klen; k0 += WAVE) {
+        const uint32_t kb = k0 == 0 ? kb0 : (k0 + lane < klen ? (uint32_t)key[k0 + lane] : 0u);
+        const int m = klen - k0 < WAVE ? klen - k0 : WAVE;
+        for (int q = 0; q < m; ++q) {
+          h *= 16777619u;
+          h ^= (uint32_t)__builtin_amdgcn_readlane((int)kb, q);
+        }
+      }
+      e.hash = h;
     };
     const bool avoid = f & KAD_W_AVOID_DISRUPTION;
     const bool keep = f & KAD_W_KEEP_UNSCHED;
