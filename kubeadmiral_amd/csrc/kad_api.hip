@@ -908,7 +908,9 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
   if (lo < 0 || lo > hi || hi > h.n_units) return fail(c, KAD_EINVAL, "bad unit range");
   const bool shard = lo > 0 || hi < h.n_units;
   HIPCHK(c, hipSetDevice(c->device));
-  if (int r = grow(c, &c->d_batch, &c->batch_cap, nbytes)) return r;
+  // 256 B of slack past the blob: the schedule kernels read a unit's score program as a 64-word window from
+  // its offset (affinity_score_pv), which may run past the last array
+  if (int r = grow(c, &c->d_batch, &c->batch_cap, nbytes + 256)) return r;
   if (!shard) {
     HIPCHK(c, hipMemcpyAsync(c->d_batch, blob, nbytes, hipMemcpyHostToDevice, c->stream));
   } else {

@@ -389,6 +389,38 @@ __device__ int64_t affinity_score(const uint64_t* rows, const int32_t* p, int nc
   return score;
 }
 
+// The same score with the unit's program words 0..63 in the lanes of `pv` (one vector load of the window at
+// the program's offset; the batch buffer has 256 B of slack past the blob, BatchDev): the program is parsed
+// with v_readlane, and each term's expression rows load together, four at a time (the AND of a term's rows
+// at c is the AND of their bits) — one memory round trip per term instead of a scalar load chain through
+// the program plus one load per expression. Words past 63 are read from memory (sp = the program).
+__device__ __forceinline__ int64_t affinity_score_pv(const uint64_t* rows, uint32_t pv, const int32_t* sp, int nch,
+                                                     int c) {
+  auto pw = [&](int i) -> int { return i < WAVE ? __builtin_amdgcn_readlane((int)pv, i) : ldc(sp + i); };
+  const int n_terms = pw(0);
+  int pc = 1;
+  int64_t score = 0;
+  const uint32_t ch = (uint32_t)(c >> 6);
+  const int bit = c & 63;
+  for (int t = 0; t < n_terms; t++) {
+    const int32_t wgt = pw(pc), ne = pw(pc + 1);
+    const int at = pc + 2;
+    pc += 2 + ne;
+    uint64_t all = ~0ull;
+    for (int i0 = 0; i0 < ne; i0 += 4) {
+      uint64_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = i0 + u < ne ? i0 + u : ne - 1;  // (repeats past ne: AND is idempotent)
+        r[u] = ldg(rows, (uint32_t)pw(at + i) * (uint32_t)nch + ch);
+      }
+      all &= r[0] & r[1] & r[2] & r[3];
+    }
+    if ((all >> bit) & 1) score = wadd(score, wgt);
+  }
+  return score;
+}
+
 // least_allocated.go:88-94 / most_allocated.go:90-97:
 //   capacity == 0 || requested > capacity ? 0 : (x * 100) / capacity
 // with x = capacity - requested (least) or requested (most). Fast path for
@@ -1469,6 +1501,16 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       dcw = (use_cur && ch < nch) ? ldg(a->b.cw, (uint32_t)(w * nch + ch)) : 0ull;
     };
     if constexpr (NCH == 0) load_words(0);
+    // (NCH == 0, every filter in the static words: the words of chunks 64..191 load in the same round trip)
+    uint64_t dsw1 = 0, dsw2 = 0;
+    if constexpr (NCH == 0) {
+      if (fold && fitf && f_sw && nch > WAVE) {
+        LArgs a = largs();
+        const int c1 = WAVE + lane, c2 = 2 * WAVE + lane;
+        dsw1 = ldg(a->b.sw, (uint32_t)(w * nch + (c1 < nch ? c1 : nch - 1)));
+        dsw2 = ldg(a->b.sw, (uint32_t)(w * nch + (c2 < nch ? c2 : nch - 1)));
+      }
+    }
 
     // ---------------- filters → compacted feasible list (findClustersThatFitWorkload, :152-169)
     int n = 0;
@@ -1507,7 +1549,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
         // every filter is in the static words: only the non-zero words of each 64-chunk group (one per
         // lane) are compacted — C5's median unit has 2 feasible clusters of 10 000
         for (int g = 0; g < nch; g += WAVE) {
-          if (g > 0) load_words(g);
+          if (g == WAVE) dsw = f_sw ? dsw1 : ~0ull;
+          else if (g == 2 * WAVE) dsw = f_sw ? dsw2 : ~0ull;
+          else if (g > 0) load_words(g);
           uint64_t nz = ballot(g + lane < nch && dsw != 0);
           while (nz) {
             const int l = __builtin_ctzll(nz);
@@ -1707,13 +1751,14 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
     if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {  // cluster_affinity.go:96-140 + DefaultNormalizeScore(100, false)
       LArgs a = largs();
       const int32_t* sp = a->b.sprog + spo;
-      if (ldc(sp) > 0) {  // units without preferred terms score 0 everywhere
+      const uint32_t pv = ldg((const uint32_t*)sp, (uint32_t)lane);  // program words 0..63 (slack past the blob)
+      if (__builtin_amdgcn_readfirstlane((int)pv) > 0) {  // units without preferred terms score 0 everywhere
         TT afs[Q];  // CL: |raw| <= sum |weight| <= 2^20 (wider units are deferred)
         TT amax = 0;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           afs[q] = 0;
-          if (q < nq && q * 64 + lane < n) afs[q] = (TT)affinity_score(a->b.req_mask, sp, nch, (int)cid[q]);
+          if (q < nq && q * 64 + lane < n) afs[q] = (TT)affinity_score_pv(a->b.req_mask, pv, sp, nch, (int)cid[q]);
           amax = afs[q] > amax ? afs[q] : amax;
         }
         if constexpr (CL) {
@@ -2403,13 +2448,14 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {  // cluster_affinity.go:96-140 + DefaultNormalizeScore(100, false)
         WArgs a = wargs();
         const int32_t* sp = a->b.sprog + spo;
-        if (ldc(sp) > 0) {
+        const uint32_t pv = ldg((const uint32_t*)sp, (uint32_t)lane);  // program words 0..63 (slack past the blob)
+        if (__builtin_amdgcn_readfirstlane((int)pv) > 0) {
           int afs[Q];  // |raw| <= sum |weight| <= 2^20 (wider units are deferred)
           int amax = 0;
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
             afs[q] = 0;
-            if (q < nq && q * 64 + lane < n) afs[q] = (int)affinity_score(a->b.req_mask, sp, nch, (int)cid[q]);
+            if (q < nq && q * 64 + lane < n) afs[q] = (int)affinity_score_pv(a->b.req_mask, pv, sp, nch, (int)cid[q]);
             amax = afs[q] > amax ? afs[q] : amax;
           }
           amax = wave_max_u_i32(amax);
