@@ -802,12 +802,12 @@ __global__ __launch_bounds__(256) void schedule_kernel(SchedArgs args) {
 // p(i): word i of the unit's filter program (prep_kernel stages the first words in LDS). The CPL
 // chunks ch0 .. ch0+CPL-1 are evaluated together (their row loads are independent); chunks past
 // nch read chunk nch-1 and are never stored.
-template <int CPL, class Prog>
+template <int CPL, class Prog, bool WAVE_ANY = false>
 __device__ __forceinline__ void affinity_words(const uint64_t* rows, Prog p, uint32_t nch, uint32_t ch0,
-                                               uint64_t (&out)[CPL]) {
+                                               uint64_t (&out)[CPL], uint32_t cst = 1) {
   uint32_t cc[CPL];
 #pragma unroll
-  for (int k = 0; k < CPL; k++) cc[k] = ch0 + k < nch ? ch0 + k : nch - 1;
+  for (int k = 0; k < CPL; k++) cc[k] = ch0 + k * cst < nch ? ch0 + k * cst : nch - 1;
   auto and_row = [&](uint64_t (&v)[CPL], int id) {
     uint64_t r[CPL];
 #pragma unroll
@@ -819,6 +819,7 @@ __device__ __forceinline__ void affinity_words(const uint64_t* rows, Prog p, uin
     uint64_t o = 0;
 #pragma unroll
     for (int k = 0; k < CPL; k++) o |= v[k];
+    if constexpr (WAVE_ANY) return ballot(o != 0) != 0;  // (one unit per wave: uniform control flow)
     return o != 0;
   };
   int pc = 0;
@@ -893,6 +894,39 @@ __device__ __forceinline__ void id_list_words(const int32_t* ids, int lo, int hi
       past |= v[u] >= end;
     }
     if (past) break;
+  }
+}
+
+// the words of chunks ch0 + k*cst (k < CPL) of the sorted cluster-id list ids[lo, hi): per chunk one lower
+// bound of its base, then the ids inside it four at a time (prep_wave_kernel's strided chunks)
+template <int CPL>
+__device__ __forceinline__ void id_list_words_strided(const int32_t* ids, int lo, int hi, uint32_t ch0, uint32_t cst,
+                                                      uint64_t (&out)[CPL]) {
+#pragma unroll
+  for (int k = 0; k < CPL; k++) {
+    out[k] = 0;
+    const int base = (int)(ch0 + k * cst) * WAVE, end = base + WAVE;
+    int a = lo, b = hi;
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (ids[mid] < base)
+        a = mid + 1;
+      else
+        b = mid;
+    }
+    for (int j = a; j < hi; j += 4) {
+      int v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[u] = j + u < hi ? ids[j + u] : INT32_MAX;
+      bool past = false;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int d = v[u] - base;
+        if (d >= 0 && d < WAVE) out[k] |= 1ull << d;
+        past |= v[u] >= end;
+      }
+      if (past) break;
+    }
   }
 }
 
@@ -1131,6 +1165,130 @@ __global__ __launch_bounds__(256, KAD_PREP_MINW) void prep_kernel(SnapDev s, Bat
             (uint64_t)rqm < (1ull << 46) && cnt > WIDE_P;
   }
   if (l == 0) {
+    UnitRec r;
+    r.flags = rflags | (route ? REC_ROW : 0u);
+    r.gvk = gvk;
+    r.tolset = tolset;
+    r.sprog_off = sprog;
+    r.req_cpu = rqc;
+    r.req_mem = rqm;
+    r.maxc = maxc;
+    r.out_off = oo;
+    r.tol0 = tol0;
+    r.tolp0 = tolp0;
+    b.rec[w] = r;
+    if (route) b.rows[atomicAdd(b.rows_n, 1)] = (int32_t)w;
+  }
+}
+
+// prep_wave_kernel<CW> — prep_kernel for wide snapshots (64 < ceil(C/64) <= 64*CW chunks, C5's 10 000
+// clusters): one unit per wave, lane l owning chunks l, l+64, ... (CW of them). prep_kernel's lanes pack
+// CPL consecutive chunks and ceil(nch/CPL) lanes per unit, so a wave holds parts of two or three units whose
+// filter programs diverge (every loop runs the longest unit's trips under exec masks) and a load
+// instruction reads every CPL-th word of a row; here the unit's program, tolerations and taint groups are
+// wave-uniform (scalar branches; the program words are v_readlane reads of one window load) and every row
+// load reads 64 consecutive words. Same outputs as prep_kernel.
+template <int CW>
+__global__ __launch_bounds__(256) void prep_wave_kernel(SnapDev s, BatchDev b, ProfDev p, int force_full) {
+  const uint32_t nch = (uint32_t)((s.C + 63) >> 6);
+  const int lane = lane_id();
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  if (g == 0) {
+    *b.defer_n = 0;
+    *b.work_n = 0;
+    if (!b.early_rows) {
+      *b.rows_n = 0;
+      *b.rows_head = 0;
+    }
+  }
+  if (g < (uint32_t)WQ_HEADS) b.wq[g * WQ_STRIDE] = 0u;
+  __shared__ int64_t fences[2][FIT_FENCES];
+  if (s.fitfold) {
+    const int S = s.fit_mp / FIT_FENCES;
+    const int64_t* fv0 = s.fit_vals[0];
+    const int64_t* fv1 = s.fit_vals[1];
+    for (int i = threadIdx.x; i < FIT_FENCES; i += 256) {
+      const int64_t a0 = fv0[(i + 1) * S - 1], a1 = fv1[(i + 1) * S - 1];
+      fences[0][i] = a0;
+      fences[1][i] = a1;
+    }
+  }
+  __syncthreads();
+  const int w = __builtin_amdgcn_readfirstlane((int)(g >> 6));
+  if (w >= b.W) return;
+  const uint32_t f = (uint32_t)ldc(b.flags + w);
+  const uint32_t fm = p.filter_mask;
+  const int32_t gvk = ldc(b.gvk + w), tolset = ldc(b.tolset + w), sprog = ldc(b.sprog_off + w);
+  const int64_t rqc = ldc(b.req_cpu + w), rqm = ldc(b.req_mem + w), maxc = ldc(b.maxc + w), desired = ldc(b.desired + w);
+  const int64_t oo = ldc(b.out_off + w);
+  const int32_t so0 = ldc(b.sreq_off + w), so1 = ldc(b.sreq_off + w + 1);
+  const int32_t fpo = ldc(b.fprog_off + w), plen = ldc(b.fprog_off + w + 1) - fpo;
+  const uint64_t tol0 = ldc(b.tol_all + (size_t)tolset * b.TW), tolp0 = ldc(b.tol_pns + (size_t)tolset * b.TW);
+  bool full = force_full != 0;
+  if ((fm & (1u << KAD_PL_API_RESOURCES)) && gvk >= 64 && !s.fold) full = true;
+  if ((fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO) && so0 < so1) full = true;
+  const uint32_t rflags = f | (((f & KAD_W_HAS_DESIRED) && desired > 0) ? REC_DESIRED_POS : 0u) | (full ? REC_FULL : 0u);
+  const bool act = !(f & KAD_W_STICKY);
+  int cnt = 0;
+  if (act) {
+    uint32_t cc[CW];
+#pragma unroll
+    for (int k = 0; k < CW; k++) cc[k] = (uint32_t)(lane + 64 * k) < nch ? (uint32_t)(lane + 64 * k) : nch - 1;
+    uint64_t m[CW];
+#pragma unroll
+    for (int k = 0; k < CW; k++) m[k] = ~0ull;
+    if (fm & (1u << KAD_PL_CLUSTER_AFFINITY)) {
+      // program words 0..63 in the lanes (one load; the batch buffer's slack covers a window past the blob)
+      const int32_t* gp = b.fprog + fpo;
+      const int32_t pv = ldg(gp, (uint32_t)lane);
+      auto word = [&](int i) -> int32_t { return i < WAVE ? __builtin_amdgcn_readlane(pv, i) : ldc(gp + i); };
+      affinity_words<CW, decltype(word), true>(b.req_mask, word, nch, (uint32_t)lane, m, 64u);
+    }
+    if (s.fitfold && (fm & (1u << KAD_PL_CLUSTER_RESOURCES_FIT)) && (f & KAD_W_FIT_NONZERO)) {
+      const int2 j = fit_ranks(s, fences, rqc, rqm);
+      const int jc = __builtin_amdgcn_readfirstlane(j.x), jm = __builtin_amdgcn_readfirstlane(j.y);
+#pragma unroll
+      for (int k = 0; k < CW; k++)
+        m[k] &= ldg(s.fit_rows[0], (uint32_t)jc * nch + cc[k]) & ldg(s.fit_rows[1], (uint32_t)jm * nch + cc[k]);
+    }
+    const bool place = (fm & (1u << KAD_PL_PLACEMENT_FILTER)) && (f & KAD_W_HAS_PLACEMENT);
+    const bool curw = (fm & (1u << KAD_PL_TAINT_TOLERATION)) && (f & KAD_W_HAS_CURRENT);
+    uint64_t cwv[CW];
+#pragma unroll
+    for (int k = 0; k < CW; k++) cwv[k] = 0;
+    if (place) {
+      uint64_t pw[CW];
+      id_list_words_strided<CW>(b.place, ldc(b.place_off + w), ldc(b.place_off + w + 1), (uint32_t)lane, 64u, pw);
+#pragma unroll
+      for (int k = 0; k < CW; k++) m[k] &= pw[k];
+    }
+    if (curw) id_list_words_strided<CW>(b.cur_id, ldc(b.cur_off + w), ldc(b.cur_off + w + 1), (uint32_t)lane, 64u, cwv);
+    if (s.fold) {
+      uint64_t tw[TFOLD_MAX_TW];
+      tw[0] = tol0;
+      for (int t = 1; t < s.TW && t < TFOLD_MAX_TW; t++) tw[t] = ldc(b.tol_all + (size_t)tolset * b.TW + t);
+      uint64_t fw[CW];
+      folded_words<CW>(s, fm, f, gvk, tw, cwv, nch, cc, fw);
+#pragma unroll
+      for (int k = 0; k < CW; k++) m[k] &= fw[k];
+    }
+#pragma unroll
+    for (int k = 0; k < CW; k++) {
+      const uint32_t ch = (uint32_t)(lane + 64 * k);
+      if (ch >= nch) break;
+      if (curw) b.cw[(size_t)w * nch + ch] = cwv[k];
+      if (ch == nch - 1 && (s.C & 63)) m[k] &= (1ull << (s.C & 63)) - 1;
+      b.sw[(size_t)w * nch + ch] = m[k];
+      cnt += popc64(m[k]);
+    }
+  }
+  bool route = false;
+  if (b.early_rows) {
+    cnt = wave_sum_i32(cnt);
+    route = act && !(rflags & REC_FULL) && !(f & KAD_W_WIDE_SCORES) && (uint64_t)rqc < (1ull << 46) &&
+            (uint64_t)rqm < (1ull << 46) && cnt > WIDE_P;
+  }
+  if (lane == 0) {
     UnitRec r;
     r.flags = rflags | (route ? REC_ROW : 0u);
     r.gvk = gvk;
@@ -2413,7 +2571,8 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         if (q >= nq) continue;
         const int p = q * 64 + lane;
         const bool v = p < n;
-        cid[q] = v ? idx[p] : 0u;
+        const uint32_t raw = idx[p];  // (p < 512 = P: inside the wave's region, no exec branch; past n discarded)
+        cid[q] = v ? raw : 0u;
         const uint32_t cq = cid[q];
         if (s_res) {
           // x = cap - req = available - request (exact); req > cap <=> x < 0 (score 0)
@@ -2639,7 +2798,8 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
             for (int q = 0; q < Q; ++q)
               if (q < nq) {
                 const int p = q * 64 + lane;
-                emit(q, p < n && inv[p] < k);
+                const uint32_t rk = inv[p];  // (p < P + 64: inside the region, no exec branch; past n discarded)
+                emit(q, p < n && rk < (uint32_t)k);
               }
           } else if (mode == 2) {  // every total > T, then the first `need` ties by position
             int eq_before = 0;
@@ -4034,6 +4194,16 @@ hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bo
   const int nch = (s.C + 63) >> 6;
   const long lanes = (long)b.W * (nch > 0 ? (nch + PREP_CPL - 1) / PREP_CPL : 1);
   const long grid = lanes > 0 ? (lanes + 255) / 256 : 1;  // one block at W = 0 still resets defer_n
+  // wide snapshots (more than 64 chunks, up to 256): one unit per wave
+  const int cw = (nch + 63) / 64;
+  if (nch > 64 && cw <= 4 && tuning_env("KAD_PREP_WAVE", 1)) {
+    const long wgrid = b.W > 0 ? ((long)b.W + 3) / 4 : 1;
+    const int ff = force_full ? 1 : 0;
+    if (cw == 2) hipLaunchKernelGGL(prep_wave_kernel<2>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
+    else if (cw == 3) hipLaunchKernelGGL(prep_wave_kernel<3>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
+    else hipLaunchKernelGGL(prep_wave_kernel<4>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(prep_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, p, force_full ? 1 : 0);
   return hipGetLastError();
 }
