@@ -2223,6 +2223,7 @@ struct WideArgs {
   int waves_per_block;
   int cache_ne, cache_pn;
   int rows_inline;  // the units prep_kernel routed to rows run in this kernel's opening phase (row_units)
+  int batch;        // units per work-queue batch (launch_schedule: by units per wave)
   int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default; results differ from
             // the reference): bit 0 skips the pdqsort replay (ties taken by position), bit 1 ends each unit
             // after the filters, bit 2 after the scores (no selection), bit 3 skips the output pass
@@ -2362,7 +2363,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
     recs = a->b.rec;
     sws = a->b.sw;
   }
-  WorkTicket tk = wq_start(nwaves);
+  WorkTicket tk = wq_start(nwaves, wargs()->batch);
 #ifdef KAD_PHASE_PROF
   const unsigned long long wt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz, device-wide
   unsigned long long wx_units = 0, wx_max = 0, wx_deq = wt_start, wx_str = 0;
@@ -4327,7 +4328,12 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const int no_inline = tuning_env("KAD_ROWS_NO_INLINE", 0);  // (read per launch: tuning builds only)
     const bool inline_rows = b.early_rows && b.use_rows && !no_inline && wpb >= 2 &&
                              row_kernel_lds(s.C) <= (size_t)wpb * per_wave;
-    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, inline_rows ? 1 : 0, exp};
+    // work-queue batch: 4 units, 3 when the waves take fewer than 64 units each (a 125k-unit shard: the last
+    // batches are the tail; at 1M units 3-unit batches cost more in dequeue atomics than they save:
+    // profiles/r05/ab_wide_batch_c3.txt)
+    const long upw = ((long)b.W + grid * wpb - 1) / (grid * wpb);
+    const int wbatch = upw < 64 ? 3 : WQ_BATCH;
+    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, inline_rows ? 1 : 0, wbatch, exp};
     const bool beside = !inline_rows && b.early_rows && b.use_rows && side && fork && join;
     if (beside) {  // the row kernel on the side stream, from the end of prep_kernel, beside the wide kernel
       if (hipError_t e = hipEventRecord(fork, st)) return e;
