@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -58,6 +59,8 @@ WORKLOAD_DESC = {
     "c3": "1M SchedulingUnits x 1k FederatedClusters (c2 generator), sharded over the GPUs",
     "c3r": "c3 with production-shaped snapshots: ~150 Kind-sorted discovery API resources per cluster "
            "(clusterstatus.go:221-266) and units over 8 workload kinds",
+    "c3p": "c3r with the live controller's inputs: ResourceRequest never set (schedulingtriggers.go:188-191) and "
+           "1.5 % of clusters with available < 0, 0.5 % with empty allocatable (federatedcluster/util.go:178-214)",
     "c4": "1M Divide SchedulingUnits x 512 clusters: weights, min/max replicas, capacity caps",
     "c5": "100k SchedulingUnits x 10k clusters: dense label affinity, many taints, API-resource gaps",
     "t1": "scheduling-trigger hashes: 1k federated Deployments x 16 joined clusters",
@@ -97,9 +100,11 @@ def make_clusters(cfg: str, C: int):
         return synth.gen_clusters(rng, C, n_keys=64, n_vals=16, n_int_keys=4, n_taints=256, taints_per=(4, 16),
                                   p_gvk=0.9, gvks=synth.GVKS)
     cl = synth.gen_clusters(rng, C)
-    if cfg == "c3r":  # C3's clusters with discovery-shaped API-resource lists (their own random stream)
+    if cfg in ("c3r", "c3p"):  # C3's clusters with discovery-shaped API-resource lists (their own random stream)
         for c, api in zip(cl, synth.discovery_api_resources(np.random.default_rng([synth.SEEDS[cfg], 0xA91]), C)):
             c.api_resource_types = api
+    if cfg == "c3p":  # over-committed and fully cordoned clusters (their own random stream)
+        synth.production_resources(cl, np.random.default_rng([synth.SEEDS[cfg], 0x9E5]))
     return cl
 
 
@@ -113,6 +118,11 @@ def make_columns(cfg: str, lo: int, hi: int, clusters):
         return synth.gen_units_c2_columns(rng, hi - lo, prefix=f"su{lo}")
     if cfg == "c3r":  # C3's units (same stream) over 8 workload kinds
         return synth.gen_units_c2_columns(rng, hi - lo, prefix=f"su{lo}", workloads=synth.C3R_WORKLOADS)
+    if cfg == "c3p":  # c3r's units as the live controller builds them: no ResourceRequest
+        cols = synth.gen_units_c2_columns(rng, hi - lo, prefix=f"su{lo}", workloads=synth.C3R_WORKLOADS)
+        cols["req_cpu"][:] = 0
+        cols["req_mem"][:] = 0
+        return cols
     if cfg == "c4":  # vectorised generators: 1M C4 units in seconds (the object generator takes minutes)
         return synth.gen_units_c4_columns(rng, hi - lo, [c.name for c in clusters], prefix=f"c4-{lo}")
     if cfg == "c5":
@@ -202,9 +212,10 @@ def roofline_for(stage: str, kernel: str, t_ms: float, compulsory: float, pmc, p
 
 
 def host_cpus():
-    """(CPUs this process may run on = len(sched_getaffinity), os.cpu_count(), the cgroup's CPU limit or None):
-    the CPU baseline runs one worker thread per CPU it may use and reports all three (on the GPU box the
-    machine's count is many times the box's share)."""
+    """(worker threads for the CPU baseline, os.cpu_count(), the cgroup's CPU limit or None): one thread per CPU
+    this process may both run on (len(sched_getaffinity)) and be given time on (ceil of the cgroup quota,
+    /sys/fs/cgroup/cpu.max) — on the GPU box the affinity mask names the machine's 256 threads while the
+    cgroup allows 16, and 256 threads under a 16-CPU quota are throttled, not faster. All three are reported."""
     try:
         usable = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -217,7 +228,8 @@ def host_cpus():
                 quota = int(q) / int(period)
     except (OSError, ValueError):
         pass
-    return usable, os.cpu_count(), quota
+    threads = usable if quota is None else max(1, min(usable, math.ceil(quota)))
+    return threads, os.cpu_count(), quota
 
 
 def cpu_baseline(snap, batch, fwk, C, target_s):
@@ -247,7 +259,8 @@ def cpu_baseline(snap, batch, fwk, C, target_s):
             "cpu_count": n_machine, "cgroup_cpu_limit": quota,
             "sample": f"{reps} pass(es) over units [0, {n}) of {batch.W} x {C} clusters, oracle/kad_ref.c "
                       f"(C restatement of the Go reference, one unit per worker thread, {threads} threads = the "
-                      f"CPUs this process may use; machine {n_machine}, cgroup limit {quota}), {dt:.2f}s wall"}
+                      f"CPUs this process may use within its cgroup limit {quota}; machine {n_machine}), "
+                      f"{dt:.2f}s wall"}
     return line, want, n
 
 
@@ -387,6 +400,9 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, cpu_second
     elapsed = time.perf_counter() - t0
     res = ctx.download()
     paths = ctx.path_counts()
+    sp = ctx.snapshot_paths()  # the main kernel and the snapshot's resource class (per-cluster clean)
+    paths["main"] = "wide" if sp["wide"] else "lean"
+    paths["resource_class"] = sp["resource_class"]
     # per-stage device time (HIP events on the context's stream), outside the timed region
     ctx.set_timing(True)
     st = []
@@ -930,7 +946,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the embedded C2/C4/C5 lines of the default run")
-    ap.add_argument("--extras", default="c3r,c2,c4,c5", help="configs embedded under `extra` in the default C3 run")
+    ap.add_argument("--extras", default="c3r,c3p,c2,c4,c5", help="configs embedded under `extra` in the default C3 run")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 shard-size sweep of the default run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pack -> upload -> schedule -> download timing")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),

@@ -351,6 +351,14 @@ int kad_stage_timing(kad_ctx* ctx, float* ms, int n);
  * [1] the full kernel (defer list), [2] the long-feasible-list kernel, [3] planner rows (Divide units).
  * Measurement only (bench.py's per-kernel byte models). No reference counterpart. */
 int kad_path_counts(kad_ctx* ctx, int32_t* out);
+/* How the resident snapshot is scheduled (no device work): out[0] its resource class (2 every cluster
+ * has 1 <= allocatable and used <= allocatable; 1 some cluster has allocatable 0 or available < 0 — the
+ * clusters federatedcluster/util.go:178-214 reports when cordoned / tainted nodes are left out of
+ * allocatable —, all below 2^46; 0 otherwise), [1] 1 if the exact-f64 fast path applies (class 2, or class
+ * 1 with the filter folded), [2] 1 if the main kernel is schedule_wide_kernel, [3] taint / API filters
+ * folded into the static words, [4] the fit threshold rows folded too. Returns KAD_ESTATE without a
+ * snapshot. Measurement / tests only. No reference counterpart. */
+int kad_snapshot_paths(kad_ctx* ctx, int32_t* out);
 int kad_results_download(kad_ctx* ctx, const kad_result_view* out);
 /* Page-locked host memory for the download's (or a batch blob's) buffers, reused across batches: the
  * copies then DMA straight into / out of it (no staging). kad_host_free(NULL) is a no-op. Caller-side

@@ -100,6 +100,17 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) 
         # only when the build fails
         sys.stderr.write(fails[0][1][-20000:])
         raise subprocess.CalledProcessError(1, fails[0][0])
+    # device functions called from kernels must not read the kernarg segment pointer (isa_check)
+    from . import isa_check
+
+    bad = []
+    for src in SOURCES:
+        if src.endswith(".hip"):
+            bad += isa_check.null_kernarg_loads(os.path.join(odir, src + ".o"))
+    if bad:
+        raise RuntimeError("device functions load through a null kernarg segment pointer (pass the kernel's "
+                           "argument pointer in instead): " + "; ".join(bad[:8]))
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", out + ".tmp"] + \
         [os.path.join(odir, f + ".o") for f in SOURCES]
     subprocess.run(link, check=True)

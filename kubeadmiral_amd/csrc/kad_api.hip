@@ -85,6 +85,7 @@ struct kad_ctx {
   // kad_schedule recorded them
   bool timing = false, timed = false;
   bool snap_negative = false;  // some allocatable / used cpu or memory < 0 or >= 2^46 (odd score ranges)
+  int clean_kind = 0;          // res_clean of the resident snapshot: 2 strict, 1 relaxed, 0 generic
   std::vector<int64_t> h_res;  // host shadow of alloc/used cpu/mem [4][C] (snap_negative after deltas)
   std::vector<uint64_t> h_ns;  // host shadow of the NoSchedule|NoExecute taint words [TW][C] (SnapDev::present_taints)
   void* d_slices = nullptr;    // SnapDev::slices [128*TW + 64*GW][nch], then SnapDev::taint_tab [2][8*TW][256][nch]
@@ -502,16 +503,28 @@ static bool res_negative(const std::vector<int64_t>& v) {
   for (int64_t x : v) neg |= x < 0 || x >= (1ll << 46);
   return neg;
 }
-// every cluster has 1 <= allocatable < 2^46 and 0 <= used <= allocatable for cpu and
-// memory: the lean kernel's exact-f64 resource path applies (SnapDev::clean)
+// The exact-f64 resource path (SnapDev::clean) per cluster and resource r in {cpu, memory}, allocatable a and
+// used u = allocatable - available:
+//   2 (strict)  every cluster has 1 <= a < 2^46 and 0 <= u <= a;
+//   1 (relaxed) every cluster has 0 <= a < 2^46 and 0 <= u < 2^46, some with a = 0 or u > a — what
+//     aggregateResources (federatedcluster/util.go:178-214) reports for a cluster whose cordoned / tainted
+//     nodes are left out of allocatable while their pods still count (:183-189, :199-210): available < 0,
+//     or allocatable 0 when every node is left out;
+//   0 otherwise (the generic int64 path: Go's wrap-around, used < 0 from Resource.Sub errors).
+// Relaxed clusters score through the same f64 expressions (SnapDev::clean), which are exact for them as
+// long as their Fit test does not read the cached operands: the folded filter (fit threshold rows, exact
+// int64 compares of available against the request) — refresh_derived enables them only then. Their score
+// operands: score_res (kad_device.h).
 static int res_clean(const std::vector<int64_t>& v) {
   const size_t C = v.size() / 4;
+  int strict = 1;
   for (size_t c = 0; c < C; c++)
     for (int r = 0; r < 2; r++) {
       const int64_t a = v[r * C + c], u = v[(2 + r) * C + c];
-      if (a < 1 || a >= (1ll << 46) || u < 0 || u > a) return 0;
+      if (a < 0 || a >= (1ll << 46) || u < 0 || u >= (1ll << 46)) return 0;
+      strict &= a >= 1 && u <= a;
     }
-  return 1;
+  return strict ? 2 : 1;
 }
 
 // rows and element size of snapshot array a (include/kad_sched.h, enum kad_snapshot_array)
@@ -555,6 +568,8 @@ static int build_fit_table(kad_ctx* c) {
   const int C = c->sd.C;
   c->sd.fitfold = 0;
   if (!c->sd.clean || C <= 0 || C > FITFOLD_MAX_C) return 0;
+  // (available may be negative on relaxed clusters: the rows compare exact int64 amounts, available >= request
+  // <=> allocatable >= request + (allocatable - available) of fit.go:89,98 without overflow below 2^46)
   const int nch = (C + 63) / 64;
   std::vector<int64_t> vals[2];
   std::vector<int> order(C);
@@ -633,8 +648,17 @@ static int refresh_derived(kad_ctx* c) {
   }
   if (int r = build_value_rows(c)) return r;
   c->snap_negative = res_negative(c->h_res);
-  c->sd.clean = res_clean(c->h_res);
   const int C = c->sd.C, TW = c->sd.TW;
+  {
+    // relaxed clusters (res_clean 1) take the fast path only with the filter folded: taint / API words
+    // (fold, decided below from the same sizes) and the fit threshold rows (build_fit_table: C <= FITFOLD_MAX_C)
+    const size_t nc1 = C > 0 ? (size_t)((C + 63) / 64) : 1;
+    const size_t fold_words = ((size_t)128 * TW + (size_t)64 * c->sd.GW) * nc1 + (size_t)2 * 8 * TW * 256 * nc1;
+    const bool can_fold = TW >= 1 && TW <= TFOLD_MAX_TW && fold_words * 8 <= TTAB_MAX_BYTES;
+    const int rc = res_clean(c->h_res);
+    c->clean_kind = rc;
+    c->sd.clean = rc == 2 || (rc == 1 && can_fold && C > 0 && C <= FITFOLD_MAX_C);
+  }
   c->sd.res4 = nullptr;
   c->sd.res_iv = nullptr;
   c->sd.pns4 = nullptr;
@@ -1377,8 +1401,10 @@ int kad_results_copy_device(kad_ctx* c, const kad_result_view* dev_out) {
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->ran) return fail(c, KAD_ESTATE, "nothing ran");
   HIPCHK(c, hipSetDevice(c->device));
-  const size_t W = c->batch_hdr.n_units;
-  const size_t S = c->batch_hdr.n_out_slots;
+  // this ctx's units and slots (a kad_group member holds a shard: unit_n / slot_n of it, its own result
+  // buffers from index 0)
+  const size_t W = (size_t)c->unit_n;
+  const size_t S = (size_t)c->slot_n;
   if (W) {
     HIPCHK(c, hipMemcpyAsync(dev_out->status, c->d_status, W * 4, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(dev_out->count, c->d_count, W * 4, hipMemcpyDeviceToDevice, c->stream));
@@ -1436,7 +1462,9 @@ int kad_result_diff(kad_ctx* c, const kad_result_state* st, uint32_t* out) {
     if (!c || !st || !out) return KAD_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->ran || !c->have_batch) return fail(c, KAD_ESTATE, "no scheduled batch resident");
-    const int W = c->batch_hdr.n_units, C = c->sd.C;
+    // this ctx's units (a kad_group member: its shard, whose out_off keeps the batch-wide slot numbers that
+    // out_dev's shifted slot arrays are indexed by)
+    const int W = (int)c->unit_n, C = c->sd.C;
     if (st->n_units != W) return fail(c, KAD_EINVAL, "state n_units differs from the resident batch");
     if (W == 0) return KAD_OK;
     if (!st->place_off || !st->place_has || !st->ovr_off) return fail(c, KAD_EINVAL, "null state array");
@@ -1501,8 +1529,9 @@ int kad_result_diff(kad_ctx* c, const kad_result_state* st, uint32_t* out) {
     dd.W = W;
     dd.status = c->d_status;
     dd.count = c->d_count;
-    dd.cluster = c->d_cluster;
-    dd.replicas = c->d_replicas;
+    const OutDev od = out_dev(c);
+    dd.cluster = od.cluster;
+    dd.replicas = od.replicas;
     dd.out_off = c->bd.out_off;
     dd.pl_off = reinterpret_cast<const int32_t*>(d + b_ploff);
     dd.pl_id = reinterpret_cast<const int32_t*>(d + b_plid);
@@ -1538,6 +1567,20 @@ static int path_counts_locked(kad_ctx* c, int32_t* out) {
   out[2] = c->bd.use_rows ? h[2] : 0;  // rows_n: units schedule_row_kernel took
   out[3] = (int32_t)c->plan_rows.size();  // Divide units handed to the planner
   return KAD_OK;
+}
+
+int kad_snapshot_paths(kad_ctx* c, int32_t* out) {
+  return guarded(c, [&]() -> int {
+    if (!c || !out) return KAD_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->have_snapshot) return fail(c, KAD_ESTATE, "no snapshot");
+    out[0] = c->clean_kind;
+    out[1] = c->sd.clean;
+    out[2] = wide_path(c->sd) ? 1 : 0;
+    out[3] = c->sd.fold;
+    out[4] = c->sd.fitfold;
+    return KAD_OK;
+  });
 }
 
 int kad_debug_inject_fault(kad_ctx* c, int where) {
@@ -1966,33 +2009,52 @@ int kad_group_snapshot_update(kad_group* g, const void* delta, size_t nbytes) {
   });
 }
 
+// the group's steps with g->mu held by the caller: kad_group_schedule_batch runs all three in one critical
+// section (as kad_schedule_batch does for a ctx), so concurrent callers cannot interleave and download each
+// other's batches
+static int group_batch_upload_locked(kad_group* g, const void* blob, size_t nbytes) {
+  g->have_batch = g->ran = false;
+  const int n = (int)g->m.size();
+  kad_ctx* c0 = g->m[0];
+  kad_batch_header h;
+  {
+    // one validation of the whole blob (member 0's snapshot: every member holds the same one)
+    std::lock_guard<std::mutex> l0(c0->mu);
+    if (!c0->have_snapshot) return gfail(g, KAD_ESTATE, "no snapshot uploaded");
+    if (nbytes < sizeof(h)) return gfail(g, KAD_EINVAL, "batch too small");
+    std::memcpy(&h, blob, sizeof(h));
+    if (h.magic != KAD_BATCH_MAGIC || h.abi_version != KAD_ABI_VERSION || h.total_bytes != nbytes)
+      return gfail(g, KAD_EINVAL, "bad batch header");
+    if (int r = guarded(c0, [&] { return validate_batch(c0, blob, nbytes, h); })) return gfail(g, r, c0->err);
+  }
+  g->unit_lo.assign((size_t)n + 1, 0);
+  g->slot_lo.assign((size_t)n + 1, 0);
+  split_ranges(at<int64_t>(blob, h.off, KAD_B_OUT_OFF), h.n_units, n, g->unit_lo.data(), g->slot_lo.data());
+  if (int r = each_member(g, [&](int i, kad_ctx* c) {
+        return batch_upload_locked(c, blob, nbytes, g->unit_lo[(size_t)i], g->unit_lo[(size_t)i + 1], true);
+      }))
+    return r;
+  g->have_batch = true;
+  return KAD_OK;
+}
+
+static int group_schedule_locked(kad_group* g, const kad_profile* p) {
+  if (!g->have_batch) return gfail(g, KAD_ESTATE, "snapshot and batch must be uploaded first");
+  if (int r = each_member(g, [&](int, kad_ctx* c) { return schedule_locked(c, p, nullptr, nullptr); })) return r;
+  g->ran = true;
+  return KAD_OK;
+}
+
+static int group_results_download_locked(kad_group* g, const kad_result_view* out) {
+  if (!g->ran) return gfail(g, KAD_ESTATE, "nothing ran");
+  return each_member(g, [&](int, kad_ctx* c) { return results_download_locked(c, out, true); });
+}
+
 int kad_group_batch_upload(kad_group* g, const void* blob, size_t nbytes) {
   return gguarded(g, [&]() -> int {
     if (!g || !blob) return KAD_EINVAL;
     std::lock_guard<std::mutex> lk(g->mu);
-    g->have_batch = g->ran = false;
-    const int n = (int)g->m.size();
-    kad_ctx* c0 = g->m[0];
-    kad_batch_header h;
-    {
-      // one validation of the whole blob (member 0's snapshot: every member holds the same one)
-      std::lock_guard<std::mutex> l0(c0->mu);
-      if (!c0->have_snapshot) return gfail(g, KAD_ESTATE, "no snapshot uploaded");
-      if (nbytes < sizeof(h)) return gfail(g, KAD_EINVAL, "batch too small");
-      std::memcpy(&h, blob, sizeof(h));
-      if (h.magic != KAD_BATCH_MAGIC || h.abi_version != KAD_ABI_VERSION || h.total_bytes != nbytes)
-        return gfail(g, KAD_EINVAL, "bad batch header");
-      if (int r = guarded(c0, [&] { return validate_batch(c0, blob, nbytes, h); })) return gfail(g, r, c0->err);
-    }
-    g->unit_lo.assign((size_t)n + 1, 0);
-    g->slot_lo.assign((size_t)n + 1, 0);
-    split_ranges(at<int64_t>(blob, h.off, KAD_B_OUT_OFF), h.n_units, n, g->unit_lo.data(), g->slot_lo.data());
-    if (int r = each_member(g, [&](int i, kad_ctx* c) {
-          return batch_upload_locked(c, blob, nbytes, g->unit_lo[(size_t)i], g->unit_lo[(size_t)i + 1], true);
-        }))
-      return r;
-    g->have_batch = true;
-    return KAD_OK;
+    return group_batch_upload_locked(g, blob, nbytes);
   });
 }
 
@@ -2000,10 +2062,7 @@ int kad_group_schedule(kad_group* g, const kad_profile* p) {
   return gguarded(g, [&]() -> int {
     if (!g) return KAD_EINVAL;
     std::lock_guard<std::mutex> lk(g->mu);
-    if (!g->have_batch) return gfail(g, KAD_ESTATE, "snapshot and batch must be uploaded first");
-    if (int r = each_member(g, [&](int, kad_ctx* c) { return schedule_locked(c, p, nullptr, nullptr); })) return r;
-    g->ran = true;
-    return KAD_OK;
+    return group_schedule_locked(g, p);
   });
 }
 
@@ -2023,17 +2082,20 @@ int kad_group_results_download(kad_group* g, const kad_result_view* out) {
   return gguarded(g, [&]() -> int {
     if (!g || !out) return KAD_EINVAL;
     std::lock_guard<std::mutex> lk(g->mu);
-    if (!g->ran) return gfail(g, KAD_ESTATE, "nothing ran");
-    return each_member(g, [&](int, kad_ctx* c) { return results_download_locked(c, out, true); });
+    return group_results_download_locked(g, out);
   });
 }
 
+// one critical section from upload to download (kad_schedule_batch's contract, per group)
 int kad_group_schedule_batch(kad_group* g, const kad_profile* p, const void* blob, size_t nbytes,
                              const kad_result_view* out) {
-  if (!g || !p || !blob || !out) return KAD_EINVAL;
-  if (int r = kad_group_batch_upload(g, blob, nbytes)) return r;
-  if (int r = kad_group_schedule(g, p)) return r;
-  return kad_group_results_download(g, out);
+  return gguarded(g, [&]() -> int {
+    if (!g || !p || !blob || !out) return KAD_EINVAL;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (int r = group_batch_upload_locked(g, blob, nbytes)) return r;
+    if (int r = group_schedule_locked(g, p)) return r;
+    return group_results_download_locked(g, out);
+  });
 }
 
 int kad_group_ranges(kad_group* g, int64_t* unit_lo, int64_t* slot_lo) {

@@ -27,7 +27,10 @@ constexpr size_t VR_MAX_BYTES = (size_t)256 << 20;  // prep_kernel's LDS copy of
 
 struct SnapDev {
   int C, GW, TW, K, S;
-  int clean;  // host: every cluster's cpu/mem fit the lean kernel's exact-f64 path (kad_api.hip res_clean)
+  // host: every cluster's cpu/mem score through the exact-f64 path (kad_api.hip res_clean): strict clusters
+  // (1 <= allocatable, used <= allocatable), or — with the filter folded (fold, fitfold) — relaxed ones with
+  // allocatable 0 or used > allocatable (their score operands: score_res)
+  int clean;
   // TW <= TFOLD_MAX_TW: prep_kernel folds TaintToleration's and APIResources' filters into each unit's
   // static filter words from per-id cluster bitmask slices ([128*TW + 64*GW][nch]: rows t < 64*TW the
   // NoSchedule|NoExecute taint id t, rows 64*TW + t the NoExecute taint id t, rows 128*TW + g GVK id g of
@@ -68,6 +71,20 @@ struct SnapDev {
   // one 32-B gather per feasible position instead of TW 8-B ones from the [TW][C] array
   const ulonglong4* pns4;
 };
+
+// The exact-f64 score operands (cap, available = allocatable - used) of one resource of a clean cluster.
+// Least / Most / Balanced read them as x = available - request, exact in f64 (< 2^47): Least
+// floor(100 x / cap) when x >= 0 else 0 (least_allocated.go:88-96: requested > capacity => 0), Most
+// floor(100 (cap - x) / cap) when x >= 0 else 0, Balanced (cap - x) / cap = requested / capacity
+// (balanced_allocation.go:84-88). used > allocatable (available < 0) needs nothing: x < 0 scores 0 in
+// Least / Most and the fraction is > 1 (Balanced 0), as in Go. allocatable 0 scores 0 everywhere in Go
+// (capacity == 0 => 0, fractionOfCapacity => 1): (cap, available) = (1, -1) gives exactly that (x < 0,
+// fraction 2 + request >= 1) without a zero divisor. Fit never reads these (the relaxed clusters run only
+// with the fit threshold rows, SnapDev::fitfold), so the substitute amount changes no filter.
+__host__ __device__ inline void score_res(int64_t alloc, int64_t used, double& cap, double& avail) {
+  cap = alloc == 0 ? 1.0 : (double)alloc;
+  avail = alloc == 0 ? -1.0 : (double)(alloc - used);
+}
 
 struct BatchDev {
   int W, NT, TW;

@@ -278,9 +278,11 @@ __global__ __launch_bounds__(256) void req_row_kernel(SnapDev s, BatchDev b, int
 __global__ __launch_bounds__(256) void res_cols_kernel(SnapDev s, double4* r4, float2* iv, ulonglong4* p4) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= s.C) return;
-  const int64_t ac = s.alloc_cpu[c], uc = s.used_cpu[c], am = s.alloc_mem[c], um = s.used_mem[c];
-  r4[c] = make_double4((double)(ac - uc), (double)(am - um), (double)ac, (double)am);
-  iv[c] = make_float2((float)(100.0 / (double)ac), (float)(100.0 / (double)am));
+  double capc, avc, capm, avm;
+  score_res(s.alloc_cpu[c], s.used_cpu[c], capc, avc);
+  score_res(s.alloc_mem[c], s.used_mem[c], capm, avm);
+  r4[c] = make_double4(avc, avm, capc, capm);
+  iv[c] = make_float2((float)(100.0 / capc), (float)(100.0 / capm));
   if (p4) {
     const int TW = s.TW;
     p4[c] = make_ulonglong4(TW > 0 ? s.pns[c] : 0ull, TW > 1 ? s.pns[(size_t)s.C + c] : 0ull,
@@ -1552,11 +1554,14 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
       const int64_t ac = in ? ldg(a->s.alloc_cpu, cl) : 1, uc = in ? ldg(a->s.used_cpu, cl) : 0;
       const int64_t am = in ? ldg(a->s.alloc_mem, cl) : 1, um = in ? ldg(a->s.used_mem, cl) : 0;
       if (clean) {
-        c_ac[c] = __builtin_bit_cast(int64_t, (double)ac);
-        c_uc[c] = __builtin_bit_cast(int64_t, (double)(ac - uc));
-        c_am[c] = __builtin_bit_cast(int64_t, (double)am);
-        c_um[c] = __builtin_bit_cast(int64_t, (double)(am - um));
-        c_iv[c] = make_float2((float)(100.0 / (double)ac), (float)(100.0 / (double)am));
+        double capc, avc, capm, avm;  // (relaxed clusters: only with the fit rows, MODE 3 below)
+        score_res(ac, uc, capc, avc);
+        score_res(am, um, capm, avm);
+        c_ac[c] = __builtin_bit_cast(int64_t, capc);
+        c_uc[c] = __builtin_bit_cast(int64_t, avc);
+        c_am[c] = __builtin_bit_cast(int64_t, capm);
+        c_um[c] = __builtin_bit_cast(int64_t, avm);
+        c_iv[c] = make_float2((float)(100.0 / capc), (float)(100.0 / capm));
       } else {
         c_ac[c] = in ? ac : 0;
         c_uc[c] = uc;
@@ -2344,9 +2349,12 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       const uint32_t cl = in ? (uint32_t)c : 0u;
       const int64_t ac = in ? ldg(a->s.alloc_cpu, cl) : 1, uc = in ? ldg(a->s.used_cpu, cl) : 0;
       const int64_t am = in ? ldg(a->s.alloc_mem, cl) : 1, um = in ? ldg(a->s.used_mem, cl) : 0;
-      c_av[c] = make_double2((double)(ac - uc), (double)(am - um));
-      c_cap[c] = make_double2((double)ac, (double)am);
-      c_iv[c] = make_float2((float)(100.0 / (double)ac), (float)(100.0 / (double)am));
+      double capc, avc, capm, avm;
+      score_res(ac, uc, capc, avc);
+      score_res(am, um, capm, avm);
+      c_av[c] = make_double2(avc, avm);
+      c_cap[c] = make_double2(capc, capm);
+      c_iv[c] = make_float2((float)(100.0 / capc), (float)(100.0 / capm));
       c_tg[c] = make_ulonglong2(in ? ldg(a->s.nsne, cl) : 0ull, in ? ldg(a->s.gvk, cl) : 0ull);
       if (c_ne) c_ne[c] = in ? ldg(a->s.ne, cl) : 0;
       if (c_pn) c_pn[c] = in ? ldg(a->s.pns, cl) : 0;
@@ -3395,7 +3403,7 @@ __device__ __forceinline__ void row_units(ArgsOf rargs, char* smem, int rexp_arg
         for (int hi = bits; hi > 0; hi -= 8) {
           const int shift = hi > 8 ? hi - 8 : 0;
           const uint32_t dmask = (1u << (hi - shift)) - 1u;
-          if (tid < 256) hist[tid] = 0;
+          for (int i = tid; i < 256; i += NTH) hist[i] = 0;  // (NTH >= 256 on every caller; any NTH is correct)
           __syncthreads();
           for (int j = tid; j < n; j += NTH) {
             const uint32_t d = key[j] - base;
@@ -4326,6 +4334,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     // the routed long units inside the wide kernel (its opening phase) when the row body's LDS fits below
     // the cluster cache; else the row kernel beside it on a second stream
     const int no_inline = tuning_env("KAD_ROWS_NO_INLINE", 0);  // (read per launch: tuning builds only)
+    // (the row body needs >= 2 waves: wave 1 dequeues and prefetches while wave 0 replays)
     const bool inline_rows = b.early_rows && b.use_rows && !no_inline && wpb >= 2 &&
                              row_kernel_lds(s.C) <= (size_t)wpb * per_wave;
     // work-queue batch: 4 units, 3 when the waves take fewer than 64 units each (a 125k-unit shard: the last

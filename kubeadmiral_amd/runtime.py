@@ -87,6 +87,8 @@ def load_library(path: str = LIB_PATH):
     L.kad_results_copy_device.argtypes = [P, P]
     L.kad_stage_timing.argtypes = [P, P, I]
     L.kad_path_counts.argtypes = [P, P]
+    if hasattr(L, "kad_snapshot_paths"):  # (absent from libraries of older revisions: A/B runs)
+        L.kad_snapshot_paths.argtypes = [P, P]
     L.kad_result_diff.argtypes = [P, P, P]
     L.kad_schedule_batch.argtypes = [P, P, P, SZ, P]
     L.kad_select_rows.argtypes = [P, I, P, P, P, U32, P, P, P]
@@ -102,6 +104,17 @@ def load_library(path: str = LIB_PATH):
     L.kad_trigger_hashes.argtypes = [P, I, P, P, P, SZ, P]
     L.kad_host_alloc.argtypes = [SZ, ctypes.POINTER(P)]
     L.kad_host_free.argtypes = [P]
+    _bind_group(L, P, I, SZ)
+    _lib = L
+    return L
+
+
+def _bind_group(L, P, I, SZ):
+    """The kad_group_* entry points (ABI 3). A library built from an older revision for a same-box A/B run
+    (scripts/build_old.sh) may lack them: its Context still works, GroupContext raises on first use.
+    tests/test_abi.py checks that the product library exports every declared symbol."""
+    if not hasattr(L, "kad_group_create"):
+        return
     L.kad_group_create.argtypes = [P, I, ctypes.POINTER(P)]
     L.kad_group_destroy.argtypes = [P]
     L.kad_group_last_error.argtypes = [P]
@@ -119,8 +132,6 @@ def load_library(path: str = LIB_PATH):
     L.kad_group_set_timing.argtypes = [P, I]
     L.kad_group_member.argtypes = [P, I, ctypes.POINTER(P)]
     L.kad_batch_split.argtypes = [P, SZ, I, P, P]
-    _lib = L
-    return L
 
 
 class _HostBlock:
@@ -260,6 +271,13 @@ class Context:
         out = (ctypes.c_int32 * 4)()
         self._chk(self.L.kad_path_counts(self.h, out))
         return {"units": out[0], "full_kernel": out[1], "row_kernel": out[2], "planner_rows": out[3]}
+
+    def snapshot_paths(self) -> dict:
+        """kad_snapshot_paths: the resident snapshot's resource class and the kernel path it takes."""
+        out = (ctypes.c_int32 * 5)()
+        self._chk(self.L.kad_snapshot_paths(self.h, out))
+        return {"resource_class": {2: "strict", 1: "relaxed", 0: "generic"}[out[0]], "exact_f64": bool(out[1]),
+                "wide": bool(out[2]), "fold": bool(out[3]), "fitfold": bool(out[4])}
 
     def copy_results_device(self, status_ptr: int, count_ptr: int, flags_ptr: int, cluster_ptr: int,
                             replicas_ptr: int):
@@ -401,6 +419,13 @@ def batch_split(batch, n: int):
     return ulo, slo
 
 
+class _MemberContext(Context):
+    """A kad_group member's kad_ctx, owned by the group (GroupContext.member)."""
+
+    def close(self):
+        self.h = None
+
+
 class GroupContext:
     """A kad_group: one process scheduling each batch over several GPUs (contiguous unit ranges, one
     kad_ctx per device), results in one view as from a single Context. Same interface as :class:`Context`
@@ -441,6 +466,16 @@ class GroupContext:
     def upload_snapshot(self, snap: Snapshot):
         self._chk(self.L.kad_group_snapshot_upload(self.h, _p(snap.blob), snap.blob.nbytes))
         self.snap = snap
+
+    def member(self, i: int) -> "Context":
+        """kad_group_member: member i's kad_ctx (its shard of the resident batch) as a Context that the group
+        owns (closing it does nothing). Its per-ctx calls — copy_results_device, result_diff, path_counts,
+        stage_timing — cover the member's units."""
+        c = ctypes.c_void_p()
+        self._chk(self.L.kad_group_member(self.h, i, ctypes.byref(c)))
+        m = _MemberContext.__new__(_MemberContext)
+        m.device, m.L, m.h, m.snap, m.batch = self.devices[i], self.L, c, self.snap, None
+        return m
 
     def update_snapshot(self, delta: SnapshotDelta):
         self._chk(self.L.kad_group_snapshot_update(self.h, _p(delta.blob), delta.blob.nbytes))

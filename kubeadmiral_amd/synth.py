@@ -33,9 +33,38 @@ GVKS = [("apps", "v1", "Deployment"), ("apps", "v1", "StatefulSet"), ("apps", "v
         ("batch", "v1", "Job"), ("", "v1", "ConfigMap"), ("", "v1", "Service"), ("batch", "v1", "CronJob"),
         ("networking.k8s.io", "v1", "Ingress")]
 
-SEEDS = {"c1": 0xC1, "c2": 0xC2, "c3": 0xC3, "c4": 0xC4, "c5": 0xC5, "c3r": 0xC3}
+SEEDS = {"c1": 0xC1, "c2": 0xC2, "c3": 0xC3, "c4": 0xC4, "c5": 0xC5, "c3r": 0xC3, "c3p": 0xC3}
 SIZES = {"c1": (1000, 16), "c2": (100_000, 256), "c3": (1_000_000, 1000), "c4": (1_000_000, 512),
-         "c5": (100_000, 10_000), "c3r": (1_000_000, 1000)}
+         "c5": (100_000, 10_000), "c3r": (1_000_000, 1000), "c3p": (1_000_000, 1000)}
+
+
+def production_resources(clusters, rng: np.random.Generator, p_over: float = 0.015, p_empty: float = 0.005):
+    """``clusters`` (in place) with the resource shapes aggregateResources
+    (pkg/controllers/federatedcluster/util.go:178-214) reports for real member clusters: nodes that are
+    Unschedulable, NotReady or carry a NoSchedule / NoExecute taint (isNodeSchedulable, :114-131) are left out
+    of allocatable, while every non-terminal pod's requests are still subtracted from available (:199-210) —
+    * a fraction ``p_over`` of clusters whose pods on left-out nodes push cpu and / or memory available
+      below 0 (used = allocatable - available above allocatable by up to 30 %);
+    * a fraction ``p_empty`` whose every node is left out: empty Allocatable and Available lists
+      (allocatable 0, used 0 — pods subtract only from resources present, :203-207).
+    Returns the indices of the two groups."""
+    C = len(clusters)
+    u = rng.random(C)
+    over = np.nonzero(u < p_over)[0]
+    empty = np.nonzero((u >= p_over) & (u < p_over + p_empty))[0]
+    for c in over:
+        cl = clusters[int(c)]
+        which = int(rng.integers(1, 4))  # 1 cpu, 2 memory, 3 both
+        if which & 1 and "cpu" in (cl.allocatable or {}):
+            ac = k8s.milli_value(k8s.quantity(cl.allocatable["cpu"]))
+            cl.available = dict(cl.available or {}, cpu=f"{-int(ac * rng.uniform(0.001, 0.3))}m")
+        if which & 2 and "memory" in (cl.allocatable or {}):
+            am = k8s.value(k8s.quantity(cl.allocatable["memory"]))
+            cl.available = dict(cl.available or {}, memory=str(-int(am * rng.uniform(0.001, 0.3))))
+    for c in empty:
+        clusters[int(c)].allocatable = {}
+        clusters[int(c)].available = {}
+    return over, empty
 
 # ------------------------------------------------------- production-shaped API-resource lists
 # What a member cluster's discovery returns (kube 1.26 built-ins and commonly installed operators' CRDs), as
@@ -133,7 +162,7 @@ def discovery_api_resources(rng: np.random.Generator, C: int, n_extra_crds: int 
 
 def profile_for(config: str) -> F.Framework:
     """The plugin set each config is quoted on (BASELINE.json configs)."""
-    if config in ("c2", "c3", "c3r"):
+    if config in ("c2", "c3", "c3r", "c3p"):
         return F.Framework(F.EnabledPlugins(
             [F.APIResources, F.TaintToleration, F.ClusterResourcesFit, F.ClusterAffinity],
             [F.ClusterResourcesLeastAllocated], [F.MaxCluster], [F.ClusterCapacityWeight]))
@@ -314,11 +343,15 @@ def make_config(config: str, scale: float = 1.0, seed: Optional[int] = None, W: 
     if config in ("c2", "c3"):
         cl = gen_clusters(rng, C)
         return cl, gen_units_c2(rng, W), profile_for(config)
-    if config == "c3r":
+    if config in ("c3r", "c3p"):
         cl = gen_clusters(rng, C)
         for c, api in zip(cl, discovery_api_resources(np.random.default_rng([SEEDS[config], 0xA91]), C)):
             c.api_resource_types = api
         units = gen_units_c2(rng, W)
+        if config == "c3p":  # over-committed / cordoned clusters, no ResourceRequest (bench.make_clusters)
+            production_resources(cl, np.random.default_rng([SEEDS[config], 0x9E5]))
+            for su in units:
+                su.resource_request = T.Resource()
         r2 = np.random.default_rng([SEEDS[config], 0x6E7])
         gv = [g for g, _ in C3R_WORKLOADS]
         share = np.array([p for _, p in C3R_WORKLOADS])

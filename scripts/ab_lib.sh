@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two builds of libkad.so on the same box: bench lines alternating between the product library and
-# kubeadmiral_amd/libkad_old.so (runtime.LIB_PATH patched before the first load).
+# ablibs/libkad_old.so (runtime.LIB_PATH patched before the first load).
 #   scripts/ab_lib.sh TAG "c3 c2" [rounds]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -13,7 +13,7 @@ import os, runpy, sys
 lib, cfg = sys.argv[1], sys.argv[2]
 from kubeadmiral_amd import runtime
 if lib == "old":
-    runtime.LIB_PATH = os.path.join(os.path.dirname(runtime.__file__), "libkad_old.so")
+    runtime.LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(runtime.__file__)), "ablibs", "libkad_old.so")
 sys.argv = ["bench.py", "--config", cfg, "--steps", "20", "--warmup", "3", "--no-cpu-baseline", "--no-extra",
             "--no-sweep", "--no-e2e"]
 runpy.run_path("bench.py", run_name="__main__")

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box counter A/B of kubeadmiral_amd/libkad_old.so vs the product library: one rocprofv3 --pmc pass per
+# Same-box counter A/B of ablibs/libkad_old.so vs the product library: one rocprofv3 --pmc pass per
 # (lib, counter set) over scripts/step_ab.py, then the per-dispatch average of each counter for the kernels
 # matching REGEX.   scripts/ab_pmc.sh TAG CFG UNITS REGEX "FETCH_SIZE" ["WRITE_SIZE" ...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 tag=$1; cfg=$2; units=$3; rx=$4; shift 4
 mkdir -p gpurun_out
 for lib in old new; do
-  L=kubeadmiral_amd/libkad.so; [ $lib = old ] && L=kubeadmiral_amd/libkad_old.so
+  L=kubeadmiral_amd/libkad.so; [ $lib = old ] && L=ablibs/libkad_old.so
   i=0
   for set in "$@"; do
     i=$((i + 1))

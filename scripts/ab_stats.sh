@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box kernel-time A/B of several builds (kubeadmiral_amd/libkad_<name>.so, "new" = libkad.so): one
+# Same-box kernel-time A/B of several builds (ablibs/libkad_<name>.so, "new" = libkad.so): one
 # rocprofv3 --kernel-trace --stats run of scripts/step_ab.py per lib, then each kernel's average duration.
 #   scripts/ab_stats.sh TAG CFG UNITS "old new px1" [steps]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 tag=$1; cfg=$2; units=$3; libs=$4; steps=${5:-10}
 mkdir -p gpurun_out
 for lib in $libs; do
-  L=kubeadmiral_amd/libkad_$lib.so; [ $lib = new ] && L=kubeadmiral_amd/libkad.so
+  L=ablibs/libkad_$lib.so; [ $lib = new ] && L=kubeadmiral_amd/libkad.so
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_$lib -o run -- python \
     scripts/step_ab.py --config $cfg --units $units --lib $L --rounds 1 --steps $steps > gpurun_out/${tag}_$lib.log 2>&1 \
     || { echo "stats run $lib failed"; tail -5 gpurun_out/${tag}_$lib.log; exit 1; }

@@ -4,13 +4,13 @@
 set -e
 name=$1; flags=$2
 repo=$(cd "$(dirname "$0")/.." && pwd)
-d=$(mktemp -d)
+d=$(mktemp -d); mkdir -p "$repo/ablibs"
 cd "$repo/kubeadmiral_amd/csrc"
 for f in kad_kernels.hip kad_trigger.hip kad_delta.hip kad_diff.hip kad_api.hip kad_pack.cpp kad_objects.cpp; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -w -pthread $flags \
     -I"$repo/include" -c $f -o "$d/$f.o" &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o "$repo/kubeadmiral_amd/libkad_$name.so" "$d"/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o "$repo/ablibs/libkad_$name.so" "$d"/*.o
 rm -rf "$d"
-echo "$repo/kubeadmiral_amd/libkad_$name.so ($flags)"
+echo "$repo/ablibs/libkad_$name.so ($flags)"

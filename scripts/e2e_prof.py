@@ -20,7 +20,7 @@ from kubeadmiral_amd import pack, synth  # noqa: E402
 from kubeadmiral_amd import build as kbuild, runtime  # noqa: E402
 
 # the packer / upload laps (KAD_PACK_TIMING / KAD_UPLOAD_TIMING) are compiled into measurement builds only
-TUNE_LIB = os.path.join(kbuild.HERE, "libkad_tune.so")
+TUNE_LIB = os.path.join(os.path.dirname(kbuild.HERE), "ablibs", "libkad_tune.so")
 kbuild.build(extra=["-DKAD_TUNING"], out=TUNE_LIB)
 runtime.load_library(TUNE_LIB)
 from kubeadmiral_amd.results import BatchResult  # noqa: E402

@@ -7,7 +7,7 @@ import sys, time, os; sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/roo
 import bench
 from kubeadmiral_amd import build as kbuild, columns, runtime, synth
 # the packer's phase laps (KAD_PACK_TIMING=1) are compiled into measurement builds only
-TUNE_LIB = os.path.join(kbuild.HERE, "libkad_tune.so")
+TUNE_LIB = os.path.join(os.path.dirname(kbuild.HERE), "ablibs", "libkad_tune.so")
 kbuild.build(extra=["-DKAD_TUNING"], out=TUNE_LIB)
 runtime.load_library(TUNE_LIB)
 from kubeadmiral_amd.pack import Snapshot

@@ -3,7 +3,7 @@
 
     python scripts/phase_prof.py [--config c2] [--units N] [--build]
 
-Builds kubeadmiral_amd/libkad_prof.so with -DKAD_PHASE_PROF (s_memtime at the
+Builds ablibs/libkad_prof.so with -DKAD_PHASE_PROF (s_memtime at the
 phase boundaries of each SchedulingUnit, summed with atomics), runs a few
 launches of the config and prints mean cycles per unit per phase. The
 instrumentation perturbs timing (s_memtime ≈ +11 % wave cycles); the
@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 from kubeadmiral_amd import build as kbuild  # noqa: E402
 
-PROF_LIB = os.environ.get("KAD_PROF_LIB", os.path.join(kbuild.HERE, "libkad_prof.so"))
+PROF_LIB = os.environ.get("KAD_PROF_LIB", os.path.join(os.path.dirname(kbuild.HERE), "ablibs", "libkad_prof.so"))
 NAMES = ["A_filter", "B_score", "C_normalize", "D_select", "E_output", "n_straddle", "n_select", "sum_feasible",
          "D_select_straddle", "row_units", "lean_A_filter", "lean_B_score", "lean_D_select", "lean_E_output",
          "lean_n_straddle", "lean_D_select_straddle", "plan_P0_setup", "plan_P1_weights", "plan_P2_plan",

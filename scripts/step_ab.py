@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Step-time A/B of tuning knobs (a -DKAD_TUNING build, libkad_tune.so: scripts/wide_exp.py --build) on one
+"""Step-time A/B of tuning knobs (a -DKAD_TUNING build, ablibs/libkad_tune.so: scripts/wide_exp.py --build) on one
 workload, variants alternating within one process so that box-to-box spread cancels.
 
     python scripts/step_ab.py --config c3 --units 125000 --variants "base;KAD_ROWS_AFTER=1" [--rounds 3]
@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--variants", default="base")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--lib", default=os.path.join(ROOT, "kubeadmiral_amd", "libkad_tune.so"))
+    ap.add_argument("--lib", default=os.path.join(ROOT, "ablibs", "libkad_tune.so"))
     a = ap.parse_args()
     import torch  # noqa: F401
 

@@ -3,7 +3,7 @@
 realtime start (100 MHz), duration, feasible count, straddle flag and global wave, saved as .npz for
 offline analysis of the kernel's tail (which units run last, how long, on which waves).
 
-    python scripts/unit_trace.py --build                      # CPU side: libkad_prof.so
+    python scripts/unit_trace.py --build                      # CPU side: ablibs/libkad_prof.so
     python scripts/unit_trace.py --units 125000 --out gpurun_out/utrace_125k.npz
 """
 import argparse
@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 
 from kubeadmiral_amd import build as kbuild  # noqa: E402
 
-PROF_LIB = os.environ.get("KAD_PROF_LIB", os.path.join(kbuild.HERE, "libkad_prof.so"))
+PROF_LIB = os.environ.get("KAD_PROF_LIB", os.path.join(os.path.dirname(kbuild.HERE), "ablibs", "libkad_prof.so"))
 
 
 def main():

@@ -3,7 +3,7 @@
 of its time and of its instruction counts each phase costs. Results differ from the reference under any
 bit; the product library ignores the variable.
 
-    python scripts/wide_exp.py --build                  # builds kubeadmiral_amd/libkad_tune.so (CPU ok)
+    python scripts/wide_exp.py --build                  # builds ablibs/libkad_tune.so (CPU ok)
     KAD_WIDE_EXPERIMENT=<bits> python scripts/wide_exp.py [--config c3] [--units N]
 bits: 1 no pdqsort replay, 2 stop after the filters, 4 no selection, 8 no output pass."""
 import argparse
@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 from kubeadmiral_amd import build as kbuild  # noqa: E402
 
-TUNE_LIB = os.path.join(kbuild.HERE, "libkad_tune.so")
+TUNE_LIB = os.path.join(os.path.dirname(kbuild.HERE), "ablibs", "libkad_tune.so")
 
 
 def main():

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Wide-kernel phase costs on the GPU box: per KAD_WIDE_EXPERIMENT variant, the stage times and one SQ
-# instruction-count pass (rocprofv3 --pmc, counters only). Needs kubeadmiral_amd/libkad_tune.so
+# instruction-count pass (rocprofv3 --pmc, counters only). Needs ablibs/libkad_tune.so
 # (python scripts/wide_exp.py --build, on the CPU side).   scripts/wide_exp.sh [cfg] [units] [bits...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -52,6 +52,9 @@ class FakeContext:
     def path_counts(self):
         return {"units": self.batch.W, "full_kernel": 3, "row_kernel": 5, "planner_rows": 0}
 
+    def snapshot_paths(self):
+        return {"resource_class": "strict", "exact_f64": True, "wide": True, "fold": True, "fitfold": True}
+
     def set_timing(self, on):
         pass
 

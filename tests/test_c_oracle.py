@@ -5,8 +5,10 @@ program compilation, resource conversion) and the C oracle that the GPU
 parity tests and the CPU baseline use at sizes the Python oracle cannot reach.
 """
 
+import numpy as np
 import pytest
 
+from kubeadmiral_amd import framework as F
 from kubeadmiral_amd import pack, synth
 from kubeadmiral_amd import types as T
 from kubeadmiral_amd.results import to_schedule_result
@@ -85,6 +87,19 @@ def test_c_oracle_matches_python_oracle_c3r_small():
     assert snap.GW >= 3
     assert sum(snap.gvk_id[(su.group, su.version, su.kind)] >= 64 for su in units) > 50
     assert not compare(clusters, units, fwk)
+
+
+def test_c_oracle_matches_python_oracle_relaxed_resources():
+    """c3p's cluster shapes (available < 0, empty allocatable: federatedcluster/util.go:178-214) with zero and
+    non-zero requests: the C restatement equals the object-level oracle (fit.go's int64 compare, the
+    capacity == 0 branches of least/most_allocated.go and fractionOfCapacity)."""
+    clusters, units, fwk = synth.make_config("c3p", W=200, C=200)
+    rng = np.random.default_rng(3)
+    synth.production_resources(clusters, rng, p_over=0.3, p_empty=0.15)
+    for su in units[::2]:
+        su.resource_request = T.Resource(int(rng.integers(0, 64_001)), int(rng.integers(0, 1 << 38)))
+    for f in (fwk, F.Framework(F.default_enabled_plugins())):
+        assert not compare(clusters, units, f)
 
 
 def test_c_oracle_matches_python_oracle_c1():

@@ -96,3 +96,19 @@ def test_c3_full_properties(full_c3):
     res2 = ctx.download()
     for a in ("status", "count", "flags", "cluster", "replicas"):
         assert np.array_equal(getattr(res2, a), getattr(res, a)), a
+
+
+def test_c3p_full_equals_c_oracle():
+    """c3p at full size: c3r's snapshots with over-committed (available < 0) and fully cordoned (empty
+    allocatable) clusters, units without ResourceRequest (the live controller's, schedulingtriggers.go:188-191).
+    The relaxed snapshot stays on the exact-f64 fast path: the wide kernel, no unit on the full kernel, and
+    every row equals the C oracle's."""
+    ctx, snap, nb, cols, fwk, res = _full("c3p")
+    try:
+        paths = ctx.snapshot_paths()
+        assert paths == {"resource_class": "relaxed", "exact_f64": True, "wide": True, "fold": True,
+                         "fitfold": True}, paths
+        assert ctx.path_counts()["full_kernel"] == 0
+        assert_same(res, c_oracle(snap, nb, fwk), "c3p 1M x 1000")
+    finally:
+        ctx.close()

@@ -127,3 +127,110 @@ def test_batch_scheduler_and_coalescer_on_a_group():
     for w, su in enumerate(units):
         a, b = res[w], to_schedule_result(want, w, su, snap.names)
         assert type(a) is type(b) and (getattr(a, "suggested_clusters", None) == getattr(b, "suggested_clusters", None))
+
+
+def _slice_state(st, lo, hi):
+    """The kad_result_state arrays of units [lo, hi)."""
+    po, oo = st["place_off"], st["ovr_off"]
+    return {"place_off": (po[lo:hi + 1] - po[lo]).astype(np.int32), "place_cluster": st["place_cluster"][po[lo]:po[hi]],
+            "place_has": st["place_has"][lo:hi], "ovr_off": (oo[lo:hi + 1] - oo[lo]).astype(np.int32),
+            "ovr_cluster": st["ovr_cluster"][oo[lo]:oo[hi]], "ovr_value": st["ovr_value"][oo[lo]:oo[hi]],
+            "ovr_kind": st["ovr_kind"][oo[lo]:oo[hi]]}
+
+
+def test_group_member_copy_and_diff(single, group):
+    """A member ctx's kad_results_copy_device and kad_result_diff cover its shard (they read the
+    whole batch's sizes from shard-sized buffers before): equal to the group's download and to the single
+    context's diff over the same units."""
+    import torch
+    clusters, units = synth.gen_fuzz(8500, W=150, C=60)
+    fwk = synth.fuzz_framework(2)
+    snap, batch, got, want = _both(single, group, clusters, units, fwk)
+    rng = np.random.default_rng(8500)
+    W, C = batch.W, snap.C
+    cnt = want.count.astype(np.int64)
+    place, p_off, o_id, o_val, o_off = [], [0], [], [], [0]
+    for w in range(W):
+        sel = want.cluster[batch.out_off[w]:batch.out_off[w] + cnt[w]].tolist()
+        r = rng.random()
+        ids = sel if r < 0.4 else (sel[:-1] if r < 0.6 else rng.integers(-1, C, int(rng.integers(0, 5))).tolist())
+        place += ids
+        p_off.append(len(place))
+        for cid in (sel[:2] if rng.random() < 0.5 else []):
+            o_id.append(cid)
+            o_val.append(int(rng.integers(0, 4)))
+        o_off.append(len(o_id))
+    state = {"place_off": np.asarray(p_off, np.int32), "place_cluster": np.asarray(place, np.int32),
+             "place_has": (rng.random(W) < 0.9).astype(np.uint8), "ovr_off": np.asarray(o_off, np.int32),
+             "ovr_cluster": np.asarray(o_id, np.int32), "ovr_value": np.asarray(o_val, np.int64),
+             "ovr_kind": np.zeros(len(o_id), np.uint8)}
+    full = single.result_diff(state)
+    ulo, slo = group.ranges()
+    for i in range(len(group.devices)):
+        m = group.member(i)
+        lo, hi, s0, s1 = int(ulo[i]), int(ulo[i + 1]), int(slo[i]), int(slo[i + 1])
+        assert np.array_equal(m.result_diff(_slice_state(state, lo, hi)), full[lo:hi]), i
+        dev = f"cuda:{group.devices[i]}"
+        t = [torch.full((max(1, n),), -7, dtype=dt, device=dev) for n, dt in
+             ((hi - lo, torch.int32), (hi - lo, torch.int32), (hi - lo, torch.int32), (s1 - s0, torch.int32),
+              (s1 - s0, torch.int64))]
+        m.copy_results_device(*(x.data_ptr() for x in t))
+        torch.cuda.synchronize()
+        for x, ref, n in zip(t, (got.status[lo:hi], got.count[lo:hi], got.flags[lo:hi], got.cluster[s0:s1],
+                                 got.replicas[s0:s1]), (hi - lo,) * 3 + (s1 - s0,) * 2):
+            assert np.array_equal(x.cpu().numpy()[:n].view(np.asarray(ref).dtype) if n else x.cpu().numpy()[:0],
+                                  np.asarray(ref)[:n]), i
+            if n < x.numel():  # nothing past the member's own results
+                assert (x.cpu().numpy()[n:] == -7).all()
+
+
+def test_group_schedule_batch_concurrent_callers(single, group):
+    """kad_group_schedule_batch holds the group lock from upload to download: two threads with
+    batches of different sizes never download each other's batch."""
+    import threading
+    clusters, units = synth.gen_fuzz(8600, W=400, C=50)
+    fwk = synth.fuzz_framework(1)
+    snap = pack.Snapshot(clusters)
+    b_small, b_big = pack.Batch(snap, fwk, units[:97]), pack.Batch(snap, fwk, units)
+    single.upload_snapshot(snap)
+    w_small, w_big = single.run(fwk, b_small), single.run(fwk, b_big)
+    group.upload_snapshot(snap)
+    errs = []
+
+    def worker(b, want):
+        try:
+            for _ in range(12):
+                _same_arrays(group.schedule_batch(fwk, b), want, b, "concurrent schedule_batch")
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=a) for a in ((b_small, w_small), (b_big, w_big))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs[0]
+
+
+def test_group_across_devices_equals_single():
+    """Members on distinct GPUs (peer access, hipMemcpyPeerAsync snapshot copies, per-device streams): skipped
+    on a one-GPU box — runs on a multi-GPU node."""
+    from kubeadmiral_amd import runtime
+    import torch
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("one GPU: the cross-device path needs >= 2")
+    clusters, units, fwk = synth.make_config("c3r", W=40_000)
+    snap = pack.Snapshot(clusters)
+    batch = pack.Batch(snap, fwk, units)
+    c = runtime.Context(0)
+    g = runtime.GroupContext(list(range(min(n, 8))))
+    try:
+        c.upload_snapshot(snap)
+        want = c.run(fwk, batch)
+        g.upload_snapshot(snap)
+        _same_arrays(g.run(fwk, batch), want, batch, f"group over {min(n, 8)} devices")
+        assert_same(want, c_oracle(snap, batch, fwk), "single vs oracle")
+    finally:
+        g.close()
+        c.close()

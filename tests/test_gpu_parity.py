@@ -582,3 +582,29 @@ def test_fuzz_clean_snapshot_gpu_equals_c_oracle(ctx, seed):
     snap, batch, res = run(ctx, clusters, units, fwk)
     assert snapshot_is_clean(snap), "fixture must exercise the clean path"
     assert_same(res, c_oracle(snap, batch, fwk), f"clean fuzz seed {seed} C={C}")
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_fuzz_relaxed_snapshot_gpu_equals_c_oracle(ctx, seed):
+    """Per-cluster clean (kad_api.hip res_clean class 1): some clusters with available < 0 (used >
+    allocatable) and some with empty allocatable — the shapes aggregateResources reports
+    (federatedcluster/util.go:178-214) — on the exact-f64 fast path of every kernel that has one: the lean
+    kernel's clean instantiations (C <= 256), the wide kernel (C = 400..1000) and the row kernel's score
+    columns (C = 1500, 3000: lean NCH = 0 + schedule_row_kernel). Requests zero and non-zero, every fuzz
+    profile; the snapshot must stay on the fast path (snapshot_paths exact_f64)."""
+    rng = np.random.default_rng(9500 + seed)
+    C = [16, 64, 200, 256, 400, 700, 1000, 1500, 3000][seed % 9]
+    W = 90 if C <= 1000 else 60
+    clusters, units = synth.gen_fuzz(9500 + seed, W=W, C=C)
+    synth.production_resources(clusters, rng, p_over=0.2, p_empty=0.1)
+    cls = clusters[:2]  # at least one of each kind
+    cls[0].allocatable, cls[0].available = {}, {}
+    cls[1].available = dict(cls[1].available, cpu="-5", memory="-1Gi")
+    for su in units[: W // 3]:  # zero requests: Fit returns early (fit.go:82-87), scores see request 0
+        su.resource_request = T.Resource()
+    fwk = synth.fuzz_framework(seed) if seed % 3 else F.Framework(F.default_enabled_plugins())
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    paths = ctx.snapshot_paths()
+    assert paths["resource_class"] == "relaxed", paths
+    assert paths["exact_f64"] == (paths["fold"] and paths["fitfold"]), paths
+    assert_same(res, c_oracle(snap, batch, fwk), f"relaxed fuzz seed {seed} C={C}")
