@@ -443,6 +443,96 @@ def bench_schedule(args, cfg, rank, world, local, dist, W_total=None, cpu_second
     return out
 
 
+def bench_group(args, cfg, devices, dist, rank):
+    """--gpus N in one process (the default --mode group): the product's multi-GPU path, kad_group_* behind the
+    C ABI (include/kad_sched.h) — the path a Go controller links, one scheduler process calling Schedule from
+    its workers (worker.go:132-134, scheduler.go:507). One snapshot upload copied device to device, the whole
+    batch split into N contiguous unit ranges, the members' pipelines issued concurrently from a host pool.
+    The timed step is kad_group_schedule over all N devices (K back to back) between two kad_group_sync. Under
+    torch.distributed.run (the driver's SCALE launch) rank 0 drives all N devices and the other ranks only
+    join the barriers around the timed region; the max over ranks is rank 0's time."""
+    import torch  # noqa: F401  (HIP runtime initialised by torch before libkad.so)
+
+    from kubeadmiral_amd import columns as CO
+    from kubeadmiral_amd import pack, synth
+    from kubeadmiral_amd.runtime import GroupContext
+
+    N = len(devices)
+    W0, C = synth.SIZES[cfg]
+    W_total = args.units if args.units is not None else W0
+    fwk = synth.profile_for(cfg)
+    g = snap = batch = stats0 = None
+    if rank == 0:
+        t0 = time.perf_counter()
+        clusters = make_clusters(cfg, C)
+        snap = pack.Snapshot(clusters)
+        cols = make_columns(cfg, 0, W_total, clusters)
+        batch = CO.NativePacker(snap).pack(fwk, cols)
+        stats0 = (cols, batch)
+        log(f"[group] {cfg}: {W_total} units x {C} clusters over devices {devices}: generated + packed in "
+            f"{time.perf_counter() - t0:.1f}s, batch {batch.blob.nbytes / 1e6:.1f} MB")
+        g = GroupContext(devices)
+        t0 = time.perf_counter()
+        g.upload_snapshot(snap)
+        g.upload_batch(batch)
+        upload_ms = (time.perf_counter() - t0) * 1e3
+        for _ in range(args.warmup):
+            g.schedule(fwk)
+            g.sync()
+    if dist is not None:
+        dist.barrier()
+    if g is not None:
+        g.sync()
+    t0 = time.perf_counter()
+    if g is not None:
+        for _ in range(args.steps):
+            g.schedule(fwk)
+        g.sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / max(1, args.steps) * 1e3
+    if dist is not None:  # max over ranks (rank 0 did the work; the others waited at the barriers)
+        import torch
+
+        t = torch.tensor([ms if rank == 0 else 0.0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t[0])
+    if rank != 0:
+        return None
+    t1 = time.perf_counter()
+    res = g.download()
+    d2h_ms = (time.perf_counter() - t1) * 1e3
+    paths = g.path_counts()
+    sp = g.member(0).snapshot_paths()
+    paths["main"] = "wide" if sp["wide"] else "lean"
+    paths["resource_class"] = sp["resource_class"]
+    # per-member stage times (timing on, outside the timed region): the slowest member per stage
+    g.set_timing(True)
+    per = []
+    for _ in range(max(3, min(args.steps, 10))):
+        g.schedule(fwk)
+        g.sync()
+        per.append([g.member_stage_timing(i) for i in range(N)])
+    g.set_timing(False)
+    from kubeadmiral_amd.runtime import Context
+
+    stage = {k: float(np.mean([max(m[k] for m in run) for run in per])) for k in Context.STAGES}
+    member_main = [float(np.mean([run[i]["total"] for run in per])) for i in range(N)]
+    ulo, _ = g.ranges()
+    out = schedule_line(args, cfg, N, W_total, C, batch, snap, fwk, res, stage, ms, stats0, paths)
+    out["config"]["parallelism"] = f"dp{N} (kad_group: one process, {N} devices)"
+    out["config"]["rccl_world_size"] = None
+    out["config"]["units_per_gpu"] = int(np.max(np.diff(ulo)))
+    out["group"] = {"devices": list(devices), "member_total_ms": member_main, "upload_ms": upload_ms,
+                    "download_ms": d2h_ms, "mode": "group"}
+    out["parity"] = verify_rows(snap, batch, fwk, res)
+    if out["parity"]["mismatches"]:
+        log(f"[group] {cfg}: PARITY FAILURE {out['parity']}")
+    g.close()
+    return out
+
+
 def stage_bytes_model(stage, W, C, nch, batch, snap, out_bytes, paths, n_distinct_reqs, divide_slots):
     """Compulsory HBM bytes of one launch of each stage's kernels (inputs read once, outputs written once):
     * req_mask: every distinct requirement's row words written + the label columns read once;
@@ -584,6 +674,9 @@ def compact_line(out: dict, headline: bool = True) -> dict:
         line["end_to_end"] = {"decisions_per_s": e["decisions_per_s"],
                               "seq_ms": {k[:-3]: s[k] for k in ("pack_ms", "h2d_ms", "schedule_ms", "d2h_ms")},
                               "blob_mb": s["blob_mb"], "pipelined_decisions_per_s": e["pipelined"]["decisions_per_s"]}
+    if out.get("group"):
+        gr = out["group"]
+        line["group"] = {"devices": gr["devices"], "member_total_ms": gr["member_total_ms"], "mode": gr["mode"]}
     if out.get("allgather"):
         a = out["allgather"]
         line["allgather"] = {"ms": a["ms"], "gbs": a["gbs"], "backend": a["backend"], "verified": a["verified"]}
@@ -952,8 +1045,17 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse the multi-rank path with host-tensor transfers (e.g. ranks sharing one GPU)")
     ap.add_argument("--share-gpu", action="store_true", help="every rank uses device 0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--mode", default="group", choices=("group", "ranks"),
+                    help="--gpus N > 1: group = one process over N devices through kad_group_* (the C ABI's "
+                         "multi-GPU path, default); ranks = one torch.distributed rank per GPU, snapshot and "
+                         "shards over RCCL, placements all-gathered")
+    ap.add_argument("--group-devices", default=None,
+                    help="group mode: comma-separated HIP device ids (default 0..N-1; e.g. 0,0,0,0 rehearses "
+                         "four members on a one-GPU box)")
     args = ap.parse_args()
 
+    if args.mode == "group" and args.gpus > 1 and not args.config.startswith("t"):
+        sys.exit(main_group(args))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch(args))
     rank = int(os.environ.get("RANK", "0"))
@@ -1001,6 +1103,38 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main_group(args) -> int:
+    """--mode group: this process (or rank 0 of a torch.distributed launch) drives all N devices."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world not in (1, args.gpus):
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    import torch  # noqa: F401
+
+    dist = None
+    if world > 1:  # launched one rank per GPU (the driver's SCALE run): a CPU process group for the barriers
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    devices = ([int(x) for x in args.group_devices.split(",")] if args.group_devices
+               else list(range(args.gpus)))
+    if len(devices) != args.gpus:
+        raise SystemExit(f"--group-devices names {len(devices)} devices, --gpus {args.gpus}")
+    from kubeadmiral_amd import build
+
+    if rank == 0:
+        build.build()
+    if dist is not None:
+        dist.barrier()
+    out = bench_group(args, args.config, devices, dist, rank)
+    if rank == 0 and out is not None:
+        emit(out, args.config)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

@@ -2188,6 +2188,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 // outside the exact-f64 range go to the defer list (schedule_kernel).
 constexpr int WIDE_MAX_NCH = 16;
 constexpr int WIDE_THREADS = 1024;
+#ifndef KAD_WIDE_C8
+#define KAD_WIDE_C8 0  // compaction at exactly 8 chunks: 0 chunk loop, 1 8-cluster lane pieces, 2 16-cluster pieces
+#endif
 // the row path's body (defined with schedule_row_kernel below), run by the wide kernel's opening phase
 template <int SM, int NT, class ArgsOf>
 __device__ __forceinline__ void row_units(ArgsOf args, char* smem, int rexp);
@@ -2456,24 +2459,31 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       auto filter_chunks = [&](auto mode_t) {
         constexpr int MODE = decltype(mode_t)::value;
         constexpr bool FAST = MODE >= 1, FOLD = MODE >= 2, FITF = MODE == 3;
-        if constexpr (FITF) {
-          // the static words are the whole filter: compact them with each lane owning 16 clusters instead of
-          // a chunk loop (per chunk two readlanes, a 64-bit rank and a store — ~9 VALU + 4 SALU, 16 chunks at
-          // C3). Lane L takes clusters 16L .. 16L+15 (bits 16(L&1).. of the dword in lane 16 + L/2 of `cur`),
-          // its first position is the wave's exclusive prefix of the piece popcounts (cluster order), and
-          // the lanes write their set bits one per trip — as many trips as the densest piece holds
+        // exactly 8 chunks (C4's instantiation): KAD_WIDE_C8 0 keeps the unrolled chunk loop below, 1 gives
+        // each lane 8 clusters (all 64 lanes hold bits), 2 the 16-cluster pieces of the general case (half the
+        // lanes idle at 512 clusters; 5a66d20 took C4's wide kernel 665 -> 688 us: profiles/r06/bisect_c4.txt)
+        constexpr int C8 = KAD_WIDE_C8;
+        constexpr bool PIECES = FITF && !(XN == 8 && C8 == 0);
+        if constexpr (PIECES) {
+          // the static words are the whole filter: compact them with each lane owning B = 16 (8) clusters
+          // instead of a chunk loop (per chunk two readlanes, a 64-bit rank and a store — ~9 VALU + 4 SALU, 16
+          // chunks at C3). Lane L takes clusters B·L .. B·L+B-1 (its B bits of the dword in lane 16 + L·B/32 of
+          // `cur`), its first position is the wave's exclusive prefix of the piece popcounts (cluster order),
+          // and the lanes write their set bits one per trip — as many trips as the densest piece holds
           // (C3: ~6); lanes out of bits write their dummy slot P + lane (no exec-mask branch)
-          const uint32_t dw = (uint32_t)__builtin_amdgcn_ds_bpermute((16 + (lane >> 1)) << 2, (int)cur);
-          uint32_t x = (dw >> ((lane & 1) << 4)) & 0xFFFFu;
+          constexpr bool B8 = XN == 8 && C8 == 1;
+          constexpr int B = B8 ? 8 : 16;
+          const uint32_t dw = (uint32_t)__builtin_amdgcn_ds_bpermute((16 + (B8 ? lane >> 2 : lane >> 1)) << 2, (int)cur);
+          uint32_t x = B8 ? (dw >> ((lane & 3) << 3)) & 0xFFu : (dw >> ((lane & 1) << 4)) & 0xFFFFu;
           const int c = __builtin_popcount(x);
           const int incl = wave_incl_sum_i32(c);
           n = __builtin_amdgcn_readlane(incl, 63);
           if (n > P) return;  // (positions past P are never written: the unit goes to rows / defer)
           int pos = incl - c;
-          const int base = 16 * lane;
+          const int base = B * lane;
           while (ballot(x != 0)) {
             const bool on = x != 0;
-            const int bit = __builtin_ctz(x | 0x10000u);
+            const int bit = __builtin_ctz(x | (1u << B));
             idx[on ? pos : P + lane] = (uint16_t)(base + bit);
             pos += on ? 1 : 0;
             x &= x - 1u;
@@ -2613,11 +2623,14 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         for (int q = 0; q < Q; ++q)
           if (q < nq) t[q] += ttmax == 0 ? 100 : 100 - (int)small_quot(100 * ttv[q], ttmax);
       }
-      if (sm & BIT(KAD_PL_CLUSTER_AFFINITY)) {  // cluster_affinity.go:96-140 + DefaultNormalizeScore(100, false)
+      // units without preferred terms (C4's) score 0 everywhere: one scalar load of the term count decides
+      // before the 64-word window's vector load (2ef3455 loaded the window for every unit: C4's wide kernel
+      // 688 -> 728 us, profiles/r06/bisect_c4.txt)
+      if ((sm & BIT(KAD_PL_CLUSTER_AFFINITY)) && ldc(wargs()->b.sprog + spo) > 0) {  // cluster_affinity.go:96-140
         WArgs a = wargs();
         const int32_t* sp = a->b.sprog + spo;
         const uint32_t pv = ldg((const uint32_t*)sp, (uint32_t)lane);  // program words 0..63 (slack past the blob)
-        if (__builtin_amdgcn_readfirstlane((int)pv) > 0) {
+        {
           int afs[Q];  // |raw| <= sum |weight| <= 2^20 (wider units are deferred)
           int amax = 0;
 #pragma unroll
