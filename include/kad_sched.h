@@ -514,7 +514,8 @@ int kad_debug_phase_counters(uint64_t* out, int reset);
 int kad_debug_inject_fault(kad_ctx* ctx, int where);
 
 /* Tests only: on = 1 sends every row of kad_plan_rows through the LDS-workspace planner (the path of rows
- * with more than 64 clusters), so the golden planner cases cover both planners; 0 restores the default
+ * with more than 64 clusters), so the golden planner cases cover both planners; on = 2 runs rows two per
+ * wave where both hold at most 32 clusters (plan_pair_kernel's half-wave planner); 0 restores the default
  * choice by row length. Not part of the reference. */
 int kad_debug_plan_force_workspace(kad_ctx* ctx, int on);
 

@@ -42,6 +42,8 @@ struct kad_ctx {
   int32_t* d_plan_rows = nullptr;
   size_t plan_rows_cap = 0;
   void* d_plan_hdr = nullptr;  // PlanRowHdr per planner row (plan_hdr_kernel at upload)
+  void* d_plan_big = nullptr;  // i32[rows + 1]: plan_pair_kernel's list of rows for the 64-lane planner + its length
+  size_t plan_big_cap = 0;
   size_t plan_hdr_cap = 0;
   // outputs
   int32_t *d_status = nullptr, *d_count = nullptr, *d_cluster = nullptr;
@@ -446,7 +448,7 @@ int kad_ctx_destroy(kad_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (c->side) (void)hipStreamSynchronize(c->side);  // the row kernel may run there: drain it before any free
-  for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, c->d_plan_hdr, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
+  for (void* p : {c->d_snap, c->d_batch, (void*)c->d_plan_rows, c->d_plan_hdr, c->d_plan_big, (void*)c->d_req_mask, (void*)c->d_status, (void*)c->d_count,
                   (void*)c->d_cluster, (void*)c->d_flags, (void*)c->d_replicas, c->d_scratch, c->d_rec, c->d_delta, c->d_sw, c->d_cw, c->d_defer, c->d_wq, c->d_slices, c->d_fit, c->d_reqseg, c->d_rowslab, c->d_vrows, c->d_rescols,
                   c->t_suffix, c->t_prefix, c->t_work, c->t_tabs, c->d_diff})
     if (p) (void)hipFree(p);
@@ -1228,6 +1230,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
   b.wq = static_cast<uint32_t*>(c->d_wq);
   // the planner rows' unit-level operands in one line per row (plan_kernel), gathered on the device
   if (int r = grow(c, &c->d_plan_hdr, &c->plan_hdr_cap, c->plan_rows.size() * sizeof(PlanRowHdr))) return r;
+  if (int r = grow(c, &c->d_plan_big, &c->plan_big_cap, (c->plan_rows.size() + 1) * sizeof(int32_t))) return r;
   HIPCHK(c, launch_plan_hdr(b, c->d_plan_rows, (int)c->plan_rows.size(), static_cast<PlanRowHdr*>(c->d_plan_hdr),
                             c->stream));
   c->have_batch = true;
@@ -1320,8 +1323,9 @@ static int schedule_locked(kad_ctx* c, const kad_profile* p, uint8_t* dbg_feas, 
   if (tm) HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   if (p->replicas_plugin == KAD_PL_CLUSTER_CAPACITY_WEIGHT && !c->plan_rows.empty())
     HIPCHK(c, launch_plan(c->sd, c->bd, o, pd, static_cast<const PlanRowHdr*>(c->d_plan_hdr), (int)c->plan_rows.size(),
-                          c->batch_hdr.max_row_slots,
-                          c->d_scratch, c->scratch_bytes, c->stream));
+                          c->batch_hdr.max_row_slots, c->d_scratch, c->scratch_bytes, c->stream,
+                          static_cast<int32_t*>(c->d_plan_big),
+                          static_cast<int32_t*>(c->d_plan_big) + c->plan_rows.size()));
   if (tm) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   c->ran = true;
   c->timed = tm;
@@ -1591,9 +1595,9 @@ int kad_debug_inject_fault(kad_ctx* c, int where) {
 }
 
 int kad_debug_plan_force_workspace(kad_ctx* c, int on) {
-  if (!c) return KAD_EINVAL;
+  if (!c || on < 0 || on > 2) return KAD_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
-  c->plan_force_ws = on != 0;
+  c->plan_force_ws = on;
   return KAD_OK;
 }
 

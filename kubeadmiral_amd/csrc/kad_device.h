@@ -18,7 +18,10 @@ constexpr int TFOLD_MAX_TW = 4;
 constexpr size_t TTAB_MAX_BYTES = (size_t)128 << 20;
 // unit work queue of the schedule kernels: WQ_HEADS counters, one 128-B line apart (BatchDev::wq)
 constexpr int WQ_HEADS = 64, WQ_STRIDE = 32;
-constexpr int FIT_FENCES = 256;
+#ifndef KAD_FIT_FENCES
+#define KAD_FIT_FENCES 256
+#endif
+constexpr int FIT_FENCES = KAD_FIT_FENCES;  // prep's LDS copy of every (fit_mp / FIT_FENCES)-th fit value
 constexpr int REQ_SEG_G = 8;  // chunks per req_mask_kernel wave (kad_kernels.hip REQ_G)
 // SnapDev::vrows: label value ids below VR_SLOTS get a cluster row; requirements naming at most
 // VR_MAX_VALS such values are ORs of rows (req_row_kernel)
@@ -269,8 +272,11 @@ struct PlanRowHdr {
 };
 static_assert(sizeof(PlanRowHdr) == 64, "one line per planner row");
 hipError_t launch_plan_hdr(const BatchDev& b, const int32_t* rows, int n_rows, PlanRowHdr* out, hipStream_t st);
+// big / big_n: device list of planner rows (n_rows + 1 ints) for plan_pair_kernel's rows of 32 < K <= 64 (null:
+// one row per wave throughout)
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const PlanRowHdr* rows,
-                       int n_rows, int kmax, void* global_scratch, size_t scratch_bytes, hipStream_t st);
+                       int n_rows, int kmax, void* global_scratch, size_t scratch_bytes, hipStream_t st,
+                       int32_t* big = nullptr, int32_t* big_n = nullptr);
 hipError_t launch_select_rows(int n_rows, const int32_t* row_off, const int64_t* scores, const int64_t* maxc,
                               uint32_t pflags, int kmax, int32_t* out_count, int32_t* out_sel, int32_t* out_status,
                               void* global_scratch, size_t scratch_bytes, hipStream_t st);

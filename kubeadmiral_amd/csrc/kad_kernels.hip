@@ -2188,6 +2188,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
 // outside the exact-f64 range go to the defer list (schedule_kernel).
 constexpr int WIDE_MAX_NCH = 16;
 constexpr int WIDE_THREADS = 1024;
+#ifndef KAD_DUMMY_STRIDE
+#define KAD_DUMMY_STRIDE 1  // u16 dummy slots of the wide kernel's compaction: P + stride * lane (<= 2: inside idx / pid)
+#endif
 #ifndef KAD_WIDE_C8
 #define KAD_WIDE_C8 0  // compaction at exactly 8 chunks: 0 chunk loop, 1 8-cluster lane pieces, 2 16-cluster pieces
 #endif
@@ -2484,7 +2487,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           while (ballot(x != 0)) {
             const bool on = x != 0;
             const int bit = __builtin_ctz(x | (1u << B));
-            idx[on ? pos : P + lane] = (uint16_t)(base + bit);
+            idx[on ? pos : P + KAD_DUMMY_STRIDE * lane] = (uint16_t)(base + bit);
             pos += on ? 1 : 0;
             x &= x - 1u;
           }
@@ -3692,7 +3695,11 @@ __global__ __launch_bounds__(256) void plan_hdr_kernel(BatchDev b, const int32_t
 template <bool GSCR, bool LANES>
 __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, BatchDev b, OutDev o, const PlanRowHdr* rows,
                                                                  int n_rows, int kmax, char* gscratch, int wave_bytes,
-                                                                 int r_stride, int tbl_cp) {
+                                                                 int r_stride, int tbl_cp, const int32_t* list = nullptr,
+                                                                 const int32_t* list_n = nullptr) {
+  // list (LANES only): the rows plan_pair_kernel left to the 64-lane planner (32 < K <= 64): row list[i] for
+  // i < *list_n instead of row i
+  if (list) n_rows = __hip_atomic_load(list_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id_h();
   const int gw = blockIdx.x;
@@ -3726,7 +3733,9 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
   }
   // the row's PlanRowHdr in lanes 0..15 (one 64-B line), loaded one row ahead
   auto fetch_hdr = [&](int r) -> uint32_t {
-    return (r < r_hi && lane < 16) ? ldg((const uint32_t*)(rows + r), (uint32_t)lane) : 0u;
+    if (r >= r_hi) return 0u;
+    const int rr = list ? ldc(list + r) : r;
+    return lane < 16 ? ldg((const uint32_t*)(rows + rr), (uint32_t)lane) : 0u;
   };
   uint32_t hn = fetch_hdr(r_lo);
   for (int r = r_lo; r < r_hi; r += r_st) {
@@ -4027,6 +4036,206 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
   KAD_PFLUSH_PLAN;
 }
 
+// plan_pair_kernel — rows of K <= 32, two per wave (kad_plan.h plan_row_pair): row A (the wave's r-th row) in
+// lanes 0-31, row B (the next row of its range) in lanes 32-63; C4's rows hold 15 selected clusters on
+// average, so the 64-lane planner (one row per wave) left three quarters of its lanes idle. The same steps as
+// plan_kernel<false, true> per segment: the row's header line, the schedule stage's status / count / flags,
+// the slot ids, key bytes and preference / current-cluster ids in one round trip; name hashes and cores; the
+// lookup tables (u16 per segment: (tag << 10) | (index + 1), rows of more than 1022 ids search the sorted
+// lists instead); the preference columns; the FNV-1 continuation; dynamic weights; the plan. Rows with
+// 32 < K <= 64 go to `big` (plan_kernel<false, true> runs them next); K > 64 rows are the workspace planner's.
+#ifndef KAD_PAIR_MINW
+#define KAD_PAIR_MINW 8  // waves per SIMD plan_pair_kernel's VGPR budget is sized for (8: 64 VGPRs)
+#endif
+__global__ __launch_bounds__(64, KAD_PAIR_MINW) void plan_pair_kernel(SnapDev s, BatchDev b, OutDev o, const PlanRowHdr* rows,
+                                                          int n_rows, int r_stride, int tbl_cp, int32_t* big,
+                                                          int32_t* big_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = lane_id_h();
+  const int sl = lane & 31;
+  const bool hi = lane >= 32;
+  const int gw = blockIdx.x;
+  uint16_t* const tbl = (uint16_t*)smem;  // [kind: pref, cur][segment][tbl_cp]
+  uint16_t* const tbl_p = tbl + (hi ? tbl_cp : 0);
+  uint16_t* const tbl_c = tbl + 2 * (size_t)tbl_cp + (hi ? tbl_cp : 0);
+  uint64_t* const kbuf = (uint64_t*)(smem + (size_t)tbl_cp * 8);
+  const bool use_tbl = tbl_cp > 0;
+  constexpr int TAG_MAX = 63, IDX_MAX = 1022;
+  uint32_t tag = 0;
+  auto clear_tables = [&]() {
+    for (int i = lane; i < 2 * tbl_cp; i += WAVE) ((uint32_t*)tbl)[i] = 0u;  // 4 tables of tbl_cp u16
+    wave_sync();
+  };
+  if (use_tbl) clear_tables();
+  int r_lo = gw, r_hi = n_rows, r_st = r_stride;
+  if ((r_stride & 7) == 0 && r_stride >= 8) {  // XCD-contiguous ranges (plan_kernel)
+    const int x = gw & 7;
+    r_lo = (int)((int64_t)n_rows * x / 8) + (gw >> 3);
+    r_hi = (int)((int64_t)n_rows * (x + 1) / 8);
+    r_st = r_stride >> 3;
+  }
+  for (int r = r_lo; r < r_hi; r += 2 * r_st) {
+    const int rr = hi ? r + r_st : r;  // this segment's row
+    const bool has = rr < r_hi;
+    const uint32_t hc = (has && sl < 16) ? ldg((const uint32_t*)(rows + rr), (uint32_t)sl) : 0u;
+    auto hf = [&](int d) -> uint32_t { return (uint32_t)seg_read32((int)hc, d); };
+    const int w = has ? (int)hf(0) : 0;
+    const uint32_t f = hf(1);
+    const int64_t off = (int64_t)(((uint64_t)hf(3) << 32) | hf(2));
+    const int p0 = (int)hf(5), p1 = (int)hf(6);
+    const int c0 = (int)hf(7), c1 = (int)hf(8);
+    const int ko0 = (int)hf(9), ko1 = (int)hf(10);
+    const int64_t desired = (int64_t)(((uint64_t)hf(13) << 32) | hf(12));
+    // the schedule stage's outputs, the slot ids, key bytes and the first 32 preference / current ids together
+    const int st = has ? o.status[w] : -1;
+    const int Kr = has ? o.count[w] : 0;
+    const uint32_t rflags0 = has ? o.flags[w] : 0u;
+    const int klen = ko1 - ko0;
+    const bool ok = st == KAD_ST_OK && Kr > 0;
+    const bool pok = ok && Kr <= 32;
+    const int K = pok ? Kr : 0;
+    const uint8_t* key = b.key + ko0;
+    const uint32_t kb0 = (pok && sl < klen) ? (uint32_t)key[sl] : 0u;
+    int c_l = pok ? o.cluster[off + (sl < K ? sl : 0)] : 0;
+    const bool tbl_row = use_tbl && p1 - p0 <= IDX_MAX && c1 - c0 <= IDX_MAX;
+    int pid_l = 0, cid_l = 0;
+    if (pok && tbl_row && p1 > p0) pid_l = b.pref_id[p0 + (p0 + sl < p1 ? sl : 0)];
+    if (pok && tbl_row && c1 > c0) cid_l = b.cur_id[c0 + (c0 + sl < c1 ? sl : 0)];
+    if (ok && Kr > 32 && Kr <= WAVE && sl == 0) big[atomicAdd(big_n, 1)] = rr;  // the 64-lane planner's
+    if (!ballot(pok)) continue;
+    const int64_t total = (f & KAD_W_HAS_DESIRED) ? desired : 0;
+    const bool dyn = f & KAD_W_DYNAMIC_WEIGHTS;
+    const uint32_t h_l = s.name_fnv[c_l];
+    int64_t ac_l = 0, av_l = 0;
+    if (ballot(pok && dyn)) {
+      ac_l = s.alloc_cores[c_l];
+      av_l = s.avail_cores[c_l];
+    }
+    if (use_tbl) {
+      if (++tag > TAG_MAX) {  // wrapped: no stale entry may carry a live tag
+        clear_tables();
+        tag = 1;
+      }
+      const uint16_t tg = (uint16_t)(tag << 10);
+      if (pok && tbl_row) {
+        if (p0 + sl < p1) tbl_p[pid_l] = (uint16_t)(tg | (sl + 1));
+        if (c0 + sl < c1) tbl_c[cid_l] = (uint16_t)(tg | (sl + 1));
+        for (int j = p0 + 32 + sl; j < p1; j += 32) tbl_p[b.pref_id[j]] = (uint16_t)(tg | (j - p0 + 1));
+        for (int j = c0 + 32 + sl; j < c1; j += 32) tbl_c[b.cur_id[j]] = (uint16_t)(tg | (j - c0 + 1));
+      }
+      wave_sync();
+    }
+    // element sl of this segment's row (lanes past K: element 0, masked off below)
+    const bool v = sl < K;
+    const int c = c_l;
+    PlanLane e;
+    {
+      int pi, ci;
+      if (pok && tbl_row) {
+        const uint32_t tp = tbl_p[c], tcc = tbl_c[c];
+        pi = (tp >> 10) == tag ? p0 + (int)(tp & 1023u) - 1 : -1;
+        ci = (tcc >> 10) == tag ? c0 + (int)(tcc & 1023u) - 1 : -1;
+      } else if (pok) {
+        pi = find_sorted(b.pref_id, p0, p1, c);
+        ci = find_sorted(b.cur_id, c0, c1, c);
+      } else {
+        pi = ci = -1;
+      }
+      e.fl = 0;
+      e.w = e.mn = e.mx = e.cap = 0;
+      if (pi >= 0) {
+        const uint32_t pf = b.pref_fl[pi];
+        int64_t pw, pmx, pcp;
+        if (b.pref_narrow) {
+          pw = b.pref_w32[pi];
+          pmx = b.pref_max32[pi];
+          pcp = b.pref_cap32[pi];
+          e.mn = b.pref_min32[pi];
+        } else {
+          pw = b.pref_w[pi];
+          pmx = b.pref_max[pi];
+          pcp = b.pref_cap[pi];
+          e.mn = b.pref_min[pi];
+        }
+        if (pf & KAD_PREF_HAS_WEIGHT) e.w = pw;
+        if (pf & KAD_PREF_HAS_MAX) {
+          e.fl |= EF_HAS_MAX;
+          e.mx = pmx;
+        }
+        if (pf & KAD_PREF_HAS_CAP) {
+          e.fl |= EF_HAS_CAP;
+          e.cap = pcp;
+        }
+      }
+      e.cur = ci >= 0 ? b.cur_rep[ci] : 0;
+      // FNV-1 continuation with su.Key() (planner.go:185-195): the segment's key bytes by readlane
+      uint32_t h = h_l;
+      const int kmax = wave_max_u_i32(pok ? klen : 0);
+      for (int k0 = 0; k0 < kmax; k0 += 32) {
+        const uint32_t kb = k0 == 0 ? kb0 : ((pok && k0 + sl < klen) ? (uint32_t)key[k0 + sl] : 0u);
+        const int m = kmax - k0 < 32 ? kmax - k0 : 32;
+        for (int q = 0; q < m; ++q) {
+          const uint32_t byte = (uint32_t)seg_read32((int)kb, q);
+          if (k0 + q < klen) h = (h * 16777619u) ^ byte;
+        }
+      }
+      e.hash = h;
+    }
+    if (use_tbl) wave_sync();  // the next pair's table writes follow these reads
+    if (!v) e = PlanLane{0, 0, 0, 0, 0, 0u, 0u};
+    uint32_t rflags = rflags0;
+    if (ballot(pok && dyn)) {
+      // CalcWeightLimit (rsp.go:183-213) + AvailableToPercentage (rsp.go:215-272), per segment
+      const int64_t ac = v ? ac_l : 0, av = v ? av_l : 0;
+      const double sum = seg_sum_f64(v ? (double)ac : 0.0);
+      const double suma = seg_sum_f64((v && av > 0) ? (double)av : 0.0);
+      int64_t wdyn;
+      uint32_t tf = 0;
+      // (segment-uniform branches: a segment's reductions read only its own lanes, so the two segments may
+      // take different ones)
+      if (suma == 0) {
+        wdyn = v ? go_f2i(round(1000.0 / (double)(K > 0 ? K : 1))) : 0;
+      } else {
+        const int64_t lim = sum == 0 ? go_f2i(round(1000.0 / (double)(K > 0 ? K : 1)))
+                                     : go_f2i(round((double)ac / sum * 1000.0 * 1.4));
+        const double avd = av < 0 ? 0.0 : (double)av;
+        int64_t wt = go_f2i(round(avd / suma * 1000.0));
+        if (wt > lim) wt = lim;
+        const int64_t sumtmp = seg_sum_i64(v ? wt : 0);
+        wt = go_f2i(round((double)wt / (double)sumtmp * 1000.0));
+        const int64_t other = seg_sum_i64(v ? wt : 0);
+        const int64_t maxw = seg_max_i64(v ? wt : 0);
+        wdyn = v ? wt : 0;
+        const uint32_t tm = seg_ballot(v && wt == maxw);
+        if (maxw > 0) {  // remainder → first strict maximum (lowest cluster id among ties)
+          const int first = (int)__builtin_ctz(tm | 0x80000000u);
+          if (__builtin_popcount(tm) > 1) tf = KAD_RF_REMAINDER_TIE;
+          if (sl == first) wdyn = wadd(wdyn, wsub(1000, other));
+        }
+      }
+      if (dyn) {
+        e.w = wdyn;
+        rflags |= tf;
+      }
+    }
+    PlanOut po;
+    rflags |= plan_row_pair(e, K, total, (f & KAD_W_AVOID_DISRUPTION) != 0, (f & KAD_W_KEEP_UNSCHED) != 0, po, kbuf);
+    // result = plan + overflow, zeros dropped (rsp.go:162-179), ascending cluster id
+    const int64_t res = v ? wadd(po.plan, (po.ofl & EF_HAS_OVER) ? po.over : 0) : 0;
+    const bool nz = v && res != 0;
+    const uint32_t m = seg_ballot(nz);
+    if (nz) {
+      const int64_t at = off + seg_mbcnt(m);
+      o.cluster[at] = c;
+      o.replicas[at] = res;
+    }
+    if (pok && sl == 0) {
+      o.count[w] = __builtin_popcount(m);
+      o.flags[w] = rflags;
+    }
+  }
+}
+
 // ============================================= stand-alone stage entry points
 template <bool GSCR>
 __global__ __launch_bounds__(64) void select_rows_kernel(int n_rows, const int32_t* row_off, const int64_t* scores,
@@ -4088,10 +4297,12 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = lane_id();
   char* region = GSCR ? gscratch + (size_t)blockIdx.x * wave_bytes : smem;
-  for (int r = blockIdx.x; r < R.n_rows; r += r_stride) {
+  // one row with the whole wave: the register planner for K <= 64 (plan_kernel's path), else (or with
+  // force_ws == 1) the LDS-workspace planner
+  auto one_row = [&](int r) {
     const int a = R.row_off[r], K = R.row_off[r + 1] - a;
-    if (K <= 0) continue;
-    if (K <= WAVE && !force_ws) {  // the register planner (plan_kernel's path for K <= 64)
+    if (K <= 0) return;
+    if (K <= WAVE && force_ws != 1) {
       const bool v = lane < K;
       PlanLane e{0, 0, 0, 0, 0, 0u, 0u};
       if (v) {
@@ -4109,7 +4320,7 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
         R.out_plan[a + lane] = po.plan;
         R.out_overflow[a + lane] = (po.ofl & EF_HAS_OVER) ? po.over : -1;
       }
-      continue;
+      return;
     }
     PlanWs ws = plan_ws(region, K);
     for (int i = lane; i < K; i += WAVE) {
@@ -4129,7 +4340,43 @@ __global__ __launch_bounds__(64) void plan_rows_kernel(PlanRowsDev R, char* gscr
       R.out_overflow[a + i] = (ws.ofl[i] & EF_HAS_OVER) ? ws.over[i] : -1;
     }
     wsync<GSCR>();
+  };
+  if (force_ws == 2 && !GSCR) {  // rows r, r + 1 together in the two half-waves when both hold <= 32 elements (plan_row_pair)
+    uint64_t* kbuf = (uint64_t*)region;
+    const int sl = lane & 31;
+    for (int r = 2 * (int)blockIdx.x; r < R.n_rows; r += 2 * r_stride) {
+      const int KA = R.row_off[r + 1] - R.row_off[r];
+      const int KB = r + 1 < R.n_rows ? R.row_off[r + 2] - R.row_off[r + 1] : 0;
+      if (KA > 32 || KB > 32) {
+        one_row(r);
+        if (r + 1 < R.n_rows) one_row(r + 1);
+        continue;
+      }
+      const int rr = lane >= 32 ? r + 1 : r;
+      const int K = lane >= 32 ? KB : KA;
+      const int a = rr < R.n_rows ? R.row_off[rr] : 0;
+      const bool v = sl < K;
+      PlanLane e{0, 0, 0, 0, 0, 0u, 0u};
+      if (v) {
+        e.hash = R.hash[a + sl];
+        e.w = R.weight[a + sl];
+        e.mn = R.min_r[a + sl];
+        e.mx = R.max_r[a + sl];
+        e.cap = R.cap[a + sl];
+        e.cur = R.current[a + sl];
+        e.fl = R.elem_flags[a + sl] & (EF_HAS_MAX | EF_HAS_CAP);
+      }
+      const uint32_t rf = K > 0 ? R.row_flags[rr] : 0u;
+      PlanOut po;
+      plan_row_pair(e, K, K > 0 ? R.total[rr] : 0, rf & 1, (rf >> 1) & 1, po, kbuf);
+      if (v) {
+        R.out_plan[a + sl] = po.plan;
+        R.out_overflow[a + sl] = (po.ofl & EF_HAS_OVER) ? po.over : -1;
+      }
+    }
+    return;
   }
+  for (int r = blockIdx.x; r < R.n_rows; r += r_stride) one_row(r);
 }
 
 // ================================================================ launchers
@@ -4482,7 +4729,7 @@ hipError_t launch_plan_hdr(const BatchDev& b, const int32_t* rows, int n_rows, P
 }
 
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const PlanRowHdr* rows,
-                       int n_rows, int kmax, void* gscr, size_t scr_bytes, hipStream_t st) {
+                       int n_rows, int kmax, void* gscr, size_t scr_bytes, hipStream_t st, int32_t* big, int32_t* big_n) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   (void)p;
   if (n_rows == 0 || kmax <= 0) return hipSuccess;
@@ -4494,13 +4741,27 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
     long grid = (long)n_cus() * per_cu;
     return (int)(grid > n_rows ? n_rows : grid);
   };
-  // rows of K <= 64: the register planner, lookup tables only in LDS (8 B per cluster)
+  // rows of K <= 64: the register planners, lookup tables only in LDS. Two rows per wave for K <= 32
+  // (plan_pair_kernel: u16 tables, 8 B per cluster for the two segments), then the rows of 32 < K <= 64 it
+  // listed, one per wave (plan_kernel<false, true>: u32 tables, 8 B per cluster)
   {
     const int tbl_cp = cp <= 1024 ? cp : 0;
     const size_t lds = (size_t)tbl_cp * 8 + 64 * 8;  // tables + sort keys
-    const int grid = persistent((const void*)plan_kernel<false, true>, lds);
-    hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows, kmax,
-                       (char*)nullptr, 0, grid, tbl_cp);
+    static const int pairs = tuning_env("KAD_PLAN_PAIRS", 1);
+    if (pairs && big) {
+      if (hipError_t e = hipMemsetAsync(big_n, 0, sizeof(int32_t), st)) return e;
+      const int grid = persistent((const void*)plan_pair_kernel, lds);
+      hipLaunchKernelGGL(plan_pair_kernel, dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows, grid, tbl_cp,
+                         big, big_n);
+      if (hipError_t e = hipGetLastError()) return e;
+      const int grid2 = persistent((const void*)plan_kernel<false, true>, lds);
+      hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid2), dim3(64), lds, st, s, b, o, rows, n_rows,
+                         kmax, (char*)nullptr, 0, grid2, tbl_cp, (const int32_t*)big, (const int32_t*)big_n);
+    } else {
+      const int grid = persistent((const void*)plan_kernel<false, true>, lds);
+      hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows,
+                         kmax, (char*)nullptr, 0, grid, tbl_cp, (const int32_t*)nullptr, (const int32_t*)nullptr);
+    }
     if (hipError_t e = hipGetLastError()) return e;
   }
   if (kmax <= WAVE) return hipSuccess;

@@ -771,4 +771,420 @@ __device__ __forceinline__ uint32_t plan_row_lanes(const PlanLane& e, int K, int
   return rflags;
 }
 
+// ------------------------------------------------ two rows per wave (rows of K <= 32)
+// C4's rows hold 15 selected clusters on average (97 % at most 32), so the 64-lane planner leaves three
+// quarters of each wave idle. plan_pair_kernel runs two rows per wave: row A in lanes 0-31, row B in lanes
+// 32-63 (a "segment" each). What is row-uniform in the 64-lane planner is segment-uniform here (a VGPR
+// holding one value per segment); scans and reductions stop at the segment boundary (no row_bcast31 step);
+// the loops run until both segments are done, a finished segment's lanes frozen; the narrow / wide choice
+// is made for the two rows together (both paths give identical results). Element i of a row is in
+// segment lane i.
+__device__ __forceinline__ int seg_lane() { return lane_id_h() & 31; }
+__device__ __forceinline__ bool seg_hi() { return lane_id_h() >= 32; }
+// lane l of this lane's segment
+__device__ __forceinline__ int seg_read32(int v, int l) {
+  const int a = __builtin_amdgcn_readlane(v, l), b = __builtin_amdgcn_readlane(v, 32 + l);
+  return seg_hi() ? b : a;
+}
+__device__ __forceinline__ int64_t seg_read64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)seg_read32((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)seg_read32((int)(uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// this segment's 32 bits of a wave ballot
+__device__ __forceinline__ uint32_t seg_bits(uint64_t b) { return seg_hi() ? (uint32_t)(b >> 32) : (uint32_t)b; }
+__device__ __forceinline__ uint32_t seg_ballot(bool p) { return seg_bits(ballot(p)); }
+__device__ __forceinline__ int seg_mbcnt(uint32_t sb) { return __builtin_popcount(sb & ((1u << seg_lane()) - 1u)); }
+// segment reductions: row_shr 1/2/4/8 within 16-lane rows, then row_bcast15 into rows 1 and 3 (row mask 0xa)
+// — lanes 31 and 63 hold their segment's result; every lane active
+#define KAD_SEG_STEPS(OP, ID)          \
+  v = OP(v, dpp32<0x111, 0xf>(ID, v)); \
+  v = OP(v, dpp32<0x112, 0xf>(ID, v)); \
+  v = OP(v, dpp32<0x114, 0xf>(ID, v)); \
+  v = OP(v, dpp32<0x118, 0xf>(ID, v)); \
+  v = OP(v, dpp32<0x142, 0xa>(ID, v)); \
+  return seg_read32(v, 31)
+__device__ __forceinline__ int seg_sum_i32(int v) { KAD_SEG_STEPS(iadd_, 0); }
+__device__ __forceinline__ int seg_max_i32(int v) { KAD_SEG_STEPS(imax_, INT32_MIN); }
+#undef KAD_SEG_STEPS
+__device__ __forceinline__ int64_t seg_sum_i64(int64_t v) {  // wrapping (Go int64)
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x111, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x112, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x114, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x118, 0xf>(0, v));
+  v = (int64_t)((uint64_t)v + (uint64_t)dpp64<0x142, 0xa>(0, v));
+  return seg_read64(v, 31);
+}
+__device__ __forceinline__ int64_t seg_max_i64(int64_t v) {  // signed: high words, then the low words under them
+  const int hi = (int)(v >> 32);
+  const int mh = seg_max_i32(hi);
+  const uint32_t lo = hi == mh ? (uint32_t)v : 0u;
+  const uint32_t ml = (uint32_t)seg_max_i32((int)(lo ^ 0x80000000u)) ^ 0x80000000u;
+  return (int64_t)(((uint64_t)(uint32_t)mh << 32) | ml);
+}
+__device__ __forceinline__ double seg_sum_f64(double v) {  // exact for integer-valued sums < 2^53
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+// inclusive clamp scan within each segment; lanes without a source combine with the identity (0, -inf)
+__device__ __forceinline__ Clamp seg_scan_clamp(Clamp v) {
+  v = clamp_compose(dpp_clamp<0x111, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x112, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x114, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x118, 0xf>(v), v);
+  v = clamp_compose(dpp_clamp<0x142, 0xa>(v), v);
+  return v;
+}
+// exclusive value: the inclusive scan one lane up; each segment's lane 0 gets the identity
+__device__ __forceinline__ Clamp seg_shr1_clamp(Clamp v) {
+  Clamp o = wave_shr1_clamp(v);
+  if (seg_lane() == 0) o = Clamp{0, NEG_INF};
+  return o;
+}
+__device__ __forceinline__ Clamp seg_last_clamp(Clamp v) { return Clamp{seg_read64(v.s, 31), seg_read64(v.t, 31)}; }
+// the 32-bit scan of desired_plan_lanes32 per segment (both rows narrow: see desired_narrow)
+__device__ __forceinline__ bool pair_clamp_narrow(Clamp f, int64_t R) {
+  return !ballot(R < 0 || R >= (1ll << 24) || f.s <= -(1ll << 24) || f.s >= (1ll << 24));
+}
+#define KAD_CLAMP32_STEP(CTRL, RM)                                        \
+  {                                                                       \
+    const int ps = dpp32<CTRL, RM>(0, s), pt = dpp32<CTRL, RM>(NEG32, t); \
+    const int at = pt == NEG32 ? NEG32 : pt - s;                          \
+    t = at > t ? at : t;                                                  \
+    s = ps + s;                                                           \
+  }
+__device__ __forceinline__ Clamp seg_scan_clamp_n(Clamp v, bool narrow) {
+  if (!narrow) return seg_scan_clamp(v);
+  int s = (int)v.s, t = v.t == NEG_INF ? NEG32 : (int)v.t;
+  KAD_CLAMP32_STEP(0x111, 0xf)
+  KAD_CLAMP32_STEP(0x112, 0xf)
+  KAD_CLAMP32_STEP(0x114, 0xf)
+  KAD_CLAMP32_STEP(0x118, 0xf)
+  KAD_CLAMP32_STEP(0x142, 0xa)
+  return Clamp{(int64_t)s, t == NEG32 ? NEG_INF : (int64_t)t};
+}
+#undef KAD_CLAMP32_STEP
+
+// lane_sort_rank per segment: the rank among the segment's listed lanes by (weight desc, hash asc, element
+// asc); unlisted lanes get m + their order among the segment's unlisted lanes. kbuf: 64 u64 of the wave's
+// LDS, segment s compacts its keys into kbuf[32 s ..]. *tie: per segment.
+__device__ __forceinline__ int pair_sort_rank(bool in, int64_t we, uint32_t he, bool* tie, uint64_t* kbuf) {
+  const int lane = lane_id_h(), sl = seg_lane();
+  const uint64_t lmw = ballot(in);
+  const uint32_t lm = seg_bits(lmw);
+  const int m = __builtin_popcount(lm);
+  const int mmax = __builtin_popcount((uint32_t)lmw) > __builtin_popcount((uint32_t)(lmw >> 32))
+                       ? __builtin_popcount((uint32_t)lmw) : __builtin_popcount((uint32_t)(lmw >> 32));
+  int rank = 0;
+  bool t = false;
+  if (!ballot(in && (we < 0 || we >= (1 << 25)))) {
+    const uint64_t ke = ((uint64_t)(uint32_t)((1 << 25) - 1 - (int)(in ? we : 0)) << 38) | ((uint64_t)he << 6) | (uint64_t)lane;
+    uint64_t* kb = kbuf + (lane & 32);
+    if (in) kb[seg_mbcnt(lm)] = ke;
+    wave_sync();
+#pragma unroll 4
+    for (int i = 0; i < mmax; ++i) rank += (i < m && kb[i] < ke) ? 1 : 0;
+    wave_sync();  // the buffer is reused by the next sort
+    const int rk = in ? rank : m + seg_mbcnt(~lm);
+    const int64_t sk = lane_perm64((lane & 32) + rk, (int64_t)(ke >> 6));
+    const int64_t pk = dpp64<0x138, 0xf>(-1, sk);  // the previous sorted lane's key (wave_shr:1)
+    *tie = seg_ballot(sl > 0 && sl < m && sk == pk) != 0;
+    return rk;
+  }
+  for (uint64_t r = lmw; r; r &= r - 1) {
+    const int j = __builtin_ctzll(r);
+    const int64_t wf = readlane64(we, j);
+    const uint32_t hf = (uint32_t)__builtin_amdgcn_readlane((int)he, j);
+    if ((j & 32) == (lane & 32)) {
+      rank += wf > we || (wf == we && (hf < he || (hf == he && j < lane)));
+      t |= (j != lane && wf == we && hf == he);
+    }
+  }
+  *tie = seg_ballot(in && t) != 0;
+  return in ? rank : m + seg_mbcnt(~lm);
+}
+
+// getDesiredPlan (planner.go:211-304) of two rows on sorted segment lanes (desired_plan_lanes per segment):
+// m, total, keep segment-uniform. Returns each segment's R.
+__device__ __forceinline__ int64_t desired_plan_pair(int m, int64_t wt, int64_t mxv, int64_t Mn, bool hc, int64_t cap,
+                                                     int64_t total, bool keep, int64_t& plan, int64_t& over,
+                                                     uint32_t& ofl) {
+  const bool v = seg_lane() < m;
+  int64_t R = total;
+  {
+    const int64_t U = hc ? cap : I64_MAX;
+    Clamp f;
+    if (!v)
+      f = {0, NEG_INF};
+    else if (Mn >= 0)
+      f = {Mn < U ? Mn : U, 0};
+    else
+      f = {Mn, NEG_INF};
+    const Clamp inc = seg_scan_clamp_n(f, pair_clamp_narrow(f, R));
+    const int64_t Ri = clamp_apply(seg_shr1_clamp(inc), R);
+    int64_t mt = Mn < Ri ? Mn : Ri;
+    ofl = v ? EF_HAS_PLAN : 0u;
+    over = 0;
+    if (v && hc && cap < mt) {
+      over = mt - cap;
+      ofl |= EF_HAS_OVER;
+      mt = cap;
+    }
+    plan = v ? mt : 0;
+    R = clamp_apply(seg_last_clamp(inc), R);
+  }
+  bool active = v;
+  bool modified = true;
+  bool go = true;  // this segment still iterates (segment-uniform)
+  int rounds = 0;
+  for (;;) {
+    go = go && modified && R > 0 && rounds < 4 * m + 64;
+    if (!ballot(go)) break;
+    rounds++;
+    const int64_t wsum = seg_sum_i64((go && active) ? wt : 0);
+    go = go && wsum > 0;
+    if (!ballot(go)) break;
+    const bool act = go && active;
+    const int64_t D = R;
+    const int64_t start = plan;
+    const double inv = 1.0 / (double)(wsum > 0 ? wsum : 1);
+    const int64_t ee = act ? ceil_extra_inv(D, wt, wsum, inv) : 0;
+    const bool hm = act && mxv != I64_MAX;
+    const bool hcap = act && hc;
+    int64_t U = I64_MAX;
+    if (hm) U = mxv;
+    if (hcap && cap < U) U = cap;
+    const int64_t V = U == I64_MAX ? I64_MAX : wsub(U, start);
+    const int64_t mm = ee < V ? ee : V;
+    const Clamp f = !act ? Clamp{0, NEG_INF} : (mm >= 0 ? Clamp{mm, 0} : Clamp{mm, NEG_INF});
+    const Clamp inc = seg_scan_clamp_n(f, pair_clamp_narrow(f, go ? R : 0));
+    const int64_t Ri = clamp_apply(seg_shr1_clamp(inc), R);
+    bool full = false, mod = false;
+    if (act) {
+      const int64_t extra = ee < Ri ? ee : Ri;
+      int64_t t = wadd(start, extra);
+      if (hm && t > mxv) {
+        t = mxv;
+        full = true;
+      }
+      if (hcap && t > cap) {
+        over = wadd((ofl & EF_HAS_OVER) ? over : 0, wsub(t, cap));
+        ofl |= EF_HAS_OVER;
+        t = cap;
+        full = true;
+      }
+      plan = t;
+      mod = t > start;
+    }
+    if (go) {
+      active = active && !full;
+      R = clamp_apply(seg_last_clamp(inc), R);
+    }
+    modified = seg_ballot(mod) != 0;
+  }
+  if (!keep && v && (ofl & EF_HAS_OVER)) {
+    const int64_t x = over < R ? over : R;
+    if (x > 0) {
+      over = x;
+    } else {
+      over = 0;
+      ofl &= ~EF_HAS_OVER;
+    }
+  }
+  return R;
+}
+
+// desired_plan_lanes32 per segment (both rows narrow, desired_narrow's bounds)
+__device__ __forceinline__ int64_t desired_plan_pair32(int m, int wt, int mxv, int Mn, bool hc, int cap, int total,
+                                                       bool keep, int64_t& plan64, int64_t& over64, uint32_t& ofl) {
+  constexpr int NONE = INT32_MAX;
+  const bool v = seg_lane() < m;
+  auto scan = [](int s, int t) {
+#define KAD_C32(CTRL, RM)                                                        \
+  {                                                                              \
+    const int pt = __builtin_amdgcn_update_dpp(NEG30, t, CTRL, RM, 0xf, false); \
+    const int at = pt - s;                                                       \
+    t = at > t ? at : t;                                                         \
+    s += __builtin_amdgcn_update_dpp(0, s, CTRL, RM, 0xf, true);                 \
+  }
+    KAD_C32(0x111, 0xf)
+    KAD_C32(0x112, 0xf)
+    KAD_C32(0x114, 0xf)
+    KAD_C32(0x118, 0xf)
+    KAD_C32(0x142, 0xa)
+#undef KAD_C32
+    return make_int2(s, t);
+  };
+  auto apply = [](int s, int t, int R) { const int x = R - s; return x > t ? x : t; };
+  auto excl = [](int2 inc) {  // one lane up; each segment's lane 0 gets the identity
+    int es = dpp32<0x138, 0xf>(0, inc.x), et = dpp32<0x138, 0xf>(NEG30, inc.y);
+    if (seg_lane() == 0) {
+      es = 0;
+      et = NEG30;
+    }
+    return make_int2(es, et);
+  };
+  int R = total;
+  int plan, over = 0;
+  {
+    const int U = hc ? cap : NONE;
+    const int fs = v ? (Mn < U ? Mn : U) : 0, ft = v ? 0 : NEG30;
+    const int2 inc = scan(fs, ft);
+    const int2 ex = excl(inc);
+    const int Ri = apply(ex.x, ex.y, R);
+    int mt = Mn < Ri ? Mn : Ri;
+    ofl = v ? EF_HAS_PLAN : 0u;
+    if (v && hc && cap < mt) {
+      over = mt - cap;
+      ofl |= EF_HAS_OVER;
+      mt = cap;
+    }
+    plan = v ? mt : 0;
+    R = apply(seg_read32(inc.x, 31), seg_read32(inc.y, 31), R);
+  }
+  bool active = v;
+  bool modified = true;
+  bool go = true;
+  int rounds = 0;
+  for (;;) {
+    go = go && modified && R > 0 && rounds < 4 * m + 64;
+    if (!ballot(go)) break;
+    rounds++;
+    const int wsum = seg_sum_i32((go && active) ? wt : 0);
+    go = go && wsum > 0;
+    if (!ballot(go)) break;
+    const bool act = go && active;
+    const int D = R;
+    const int start = plan;
+    const double sd = (double)(wsum > 0 ? wsum : 1), inv = 1.0 / sd;
+    int ee = 0;
+    if (act) {  // ceil((D·w + wsum − 1) / wsum), exact
+      const double nd = (double)D * (double)wt + (double)(wsum - 1);
+      int q = (int)(nd * inv);
+      double r = nd - (double)q * sd;
+      q += (r >= sd) - (r < 0.0);
+      r = nd - (double)q * sd;
+      q += (r >= sd) - (r < 0.0);
+      ee = q;
+    }
+    const bool hm = act && mxv != NONE;
+    const bool hcap = act && hc;
+    int U = NONE;
+    if (hm) U = mxv;
+    if (hcap && cap < U) U = cap;
+    const int V = U == NONE ? NONE : U - start;
+    const int mm = ee < V ? ee : V;
+    const int fs = act ? mm : 0, ft = (act && mm >= 0) ? 0 : NEG30;
+    const int2 inc = scan(fs, ft);
+    const int2 ex = excl(inc);
+    const int Ri = apply(ex.x, ex.y, R);
+    bool full = false, mod = false;
+    if (act) {
+      const int extra = ee < Ri ? ee : Ri;
+      int t = start + extra;
+      if (hm && t > mxv) {
+        t = mxv;
+        full = true;
+      }
+      if (hcap && t > cap) {
+        over = ((ofl & EF_HAS_OVER) ? over : 0) + (t - cap);
+        ofl |= EF_HAS_OVER;
+        t = cap;
+        full = true;
+      }
+      plan = t;
+      mod = t > start;
+    }
+    if (go) {
+      active = active && !full;
+      R = apply(seg_read32(inc.x, 31), seg_read32(inc.y, 31), R);
+    }
+    modified = seg_ballot(mod) != 0;
+  }
+  if (!keep && v && (ofl & EF_HAS_OVER)) {
+    const int x = over < R ? over : R;
+    if (x > 0) {
+      over = x;
+    } else {
+      over = 0;
+      ofl &= ~EF_HAS_OVER;
+    }
+  }
+  plan64 = plan;
+  over64 = over;
+  return R;
+}
+__device__ __forceinline__ int64_t desired_plan_pair_any(int m, int64_t wt, int64_t mxv, int64_t Mn, bool hc,
+                                                         int64_t cap, int64_t total, bool keep, int64_t& plan,
+                                                         int64_t& over, uint32_t& ofl) {
+  // desired_narrow's bounds for both rows together (one path for the wave; both give the same results)
+  const bool v = seg_lane() < m;
+  if (!ballot(total < 0 || total >= (1 << 24) ||
+              (v && (wt < 0 || wt >= (1 << 20) || Mn < 0 || Mn >= (1 << 18) ||
+                     (mxv != I64_MAX && (mxv < 0 || mxv >= (1 << 24) || Mn > mxv)) ||
+                     (hc && (cap < 0 || cap >= (1 << 24)))))))
+    return desired_plan_pair32(m, (int)wt, mxv == I64_MAX ? INT32_MAX : (int)mxv, (int)Mn, hc, (int)cap, (int)total,
+                               keep, plan, over, ofl);
+  return desired_plan_pair(m, wt, mxv, Mn, hc, cap, total, keep, plan, over, ofl);
+}
+
+// planner.Plan (planner.go:83-177) of two rows of K <= 32 (segment-uniform K, total, avoid, keep): element i
+// of each row in its segment lane i. Returns each segment's KAD_RF_HASH_TIE.
+__device__ __forceinline__ uint32_t plan_row_pair(const PlanLane& e, int K, int64_t total, bool avoid, bool keep,
+                                                  PlanOut& out, uint64_t* kbuf) {
+  const int base = lane_id_h() & 32;
+  const bool v = seg_lane() < K;
+  uint32_t rflags = 0;
+  const bool hmax = v && (e.fl & EF_HAS_MAX), hcap = v && (e.fl & EF_HAS_CAP);
+  const int64_t mx2 = hmax ? e.mx : I64_MAX;
+  bool tie;
+  const int rank = base + pair_sort_rank(v, e.w, e.hash, &tie, kbuf);
+  if (tie) rflags |= KAD_RF_HASH_TIE;
+  if (!avoid) keep = true;
+  const int64_t s_w = lane_perm64(rank, e.w), s_mx = lane_perm64(rank, mx2), s_mn = lane_perm64(rank, e.mn);
+  const int64_t s_cap = lane_perm64(rank, e.cap);
+  const bool s_hc = lane_perm32(rank, hcap ? 1 : 0) != 0;
+  int64_t p_s, o_s;
+  uint32_t f_s;
+  desired_plan_pair_any(K, s_w, s_mx, s_mn, s_hc, s_cap, total, keep, p_s, o_s, f_s);
+  int64_t plan = lane_bperm64(rank, p_s);
+  out.over = lane_bperm64(rank, o_s);
+  out.ofl = (uint32_t)lane_bperm32(rank, (int)f_s);
+  if (ballot(avoid)) {
+    // currentPlan, capped by capacity (planner.go:134-146), per segment that avoids disruption
+    int64_t adj = v ? e.cur : 0;
+    if (hcap && e.cap < adj) adj = e.cap;
+    const int64_t cur_total = seg_sum_i64(adj), des_total = seg_sum_i64(v ? plan : 0);
+    const bool scale = avoid && cur_total != des_total;
+    const bool up = cur_total < des_total;
+    const int64_t count = up ? des_total - cur_total : cur_total - des_total;
+    const bool sel = scale && v && (up ? plan > adj : plan < adj);
+    const int64_t w2 = up ? plan - adj : adj - plan;
+    const int64_t m2 = up ? (hmax ? e.mx - adj : I64_MAX) : adj;
+    const int m = __builtin_popcount(seg_ballot(sel));
+    int64_t plan2 = 0;
+    uint32_t ofl2 = 0;
+    if (ballot(m > 0)) {
+      bool tie2;
+      const int r2 = base + pair_sort_rank(sel, w2, e.hash, &tie2, kbuf);
+      if (tie2) rflags |= KAD_RF_HASH_TIE;
+      int64_t p2s, o2s;
+      uint32_t f2s;
+      // scale plan: no capacity, no minimums, keepUnschedulable = false (its overflow is discarded)
+      desired_plan_pair_any(m, lane_perm64(r2, w2), lane_perm64(r2, m2), 0, false, 0, count, false, p2s, o2s, f2s);
+      plan2 = lane_bperm64(r2, p2s);
+      const uint32_t f2 = (uint32_t)lane_bperm32(r2, (int)f2s);
+      ofl2 = sel ? f2 : 0u;
+    }
+    if (avoid) {
+      int64_t pa = adj;
+      if (ofl2 & EF_HAS_PLAN) pa = up ? wadd(adj, plan2) : wsub(adj, plan2);
+      plan = pa;
+    }
+  }
+  out.plan = plan;
+  return rflags;
+}
+
 }  // namespace kad

@@ -213,9 +213,10 @@ class Context:
         rebuild."""
         self._chk(self.L.kad_debug_inject_fault(self.h, where))
 
-    def plan_force_workspace(self, on: bool):
-        """kad_debug_plan_force_workspace (tests): plan_rows through the LDS-workspace planner."""
-        self._chk(self.L.kad_debug_plan_force_workspace(self.h, int(bool(on))))
+    def plan_force_workspace(self, on):
+        """kad_debug_plan_force_workspace (tests): plan_rows through the LDS-workspace planner (True / 1), the
+        half-wave pair planner (2), or the default choice by row length (False / 0)."""
+        self._chk(self.L.kad_debug_plan_force_workspace(self.h, int(on)))
 
     def update_snapshot(self, delta: SnapshotDelta):
         """kad_snapshot_update: patch the resident snapshot; the resident batch stays valid."""

@@ -106,14 +106,15 @@ def _gpu_plan(ctx, rsp, replicas, clusters, existing, est, avoid, keep):
             {n: v for (n, _), v in zip(prefs, over) if v is not None})
 
 
-@pytest.mark.parametrize("path", ["lanes", "ws"])
+@pytest.mark.parametrize("path", ["lanes", "ws", "pairs"])
 @pytest.mark.parametrize("c", PLANNER, ids=[f"{case_id(c)}-a{int(c['avoidDisruption'])}k{int(c['keepUnschedulableReplicas'])}"
                                             for c in PLANNER])
 def test_golden_planner_on_gpu(ctx, c, path, monkeypatch):
-    """planner_test.go's cases through kad_plan_rows: the register planner (rows of K <= 64, plan_row_lanes)
-    and the LDS-workspace planner (kad_debug_plan_force_workspace, the path of rows with K > 64)."""
+    """planner_test.go's cases through kad_plan_rows: the register planner (rows of K <= 64, plan_row_lanes),
+    the LDS-workspace planner (kad_debug_plan_force_workspace 1, the path of rows with K > 64) and the
+    half-wave pair planner (2: plan_row_pair, plan_pair_kernel's path for rows of K <= 32)."""
     from test_oracle_golden import run_planner_case
-    ctx.plan_force_workspace(path == "ws")
+    ctx.plan_force_workspace({"lanes": 0, "ws": 1, "pairs": 2}[path])
     try:
         converged, plan, over = run_planner_case(
             c, lambda rsp, r, cl, ex, est, key, av, kp: _gpu_plan(ctx, rsp, r, cl, ex, est, av, kp))
@@ -151,6 +152,39 @@ def test_plan_rows_lanes_equal_workspace(ctx, seed, monkeypatch):
     finally:
         ctx.plan_force_workspace(False)
     assert lanes == ws
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_plan_rows_pairs_equal_lanes(ctx, seed):
+    """The half-wave pair planner (two rows of K <= 32 per wave, plan_row_pair) against the 64-lane register
+    planner on random rows: K 1..40 (pairs with one row past 32 fall back to one row per wave), tie-heavy
+    hashes, weights up to 2^26 on some rows (the non-kbuf rank path), totals past 2^24 on some rows (the
+    int64 desired-plan path beside a narrow row), minimums / maximums / capacities / current replicas,
+    avoid / keep both ways."""
+    rng = np.random.default_rng(700 + seed)
+    rows = []
+    for _ in range(400):
+        K = int(rng.integers(1, 41)) if rng.random() < 0.9 else int(rng.integers(1, 9))
+        hs = rng.integers(0, 4 if rng.random() < 0.3 else 1 << 32, K)
+        wide_w = rng.random() < 0.05
+        elems = []
+        for i in range(K):
+            elems.append({"hash": int(hs[i]),
+                          "weight": int(rng.integers(0, (1 << 26) if wide_w else (5 if rng.random() < 0.4 else 1000))),
+                          "min": int(rng.integers(0, 6)) if rng.random() < 0.3 else 0,
+                          "max": int(rng.integers(0, 200)) if rng.random() < 0.3 else None,
+                          "cap": int(rng.integers(0, 300)) if rng.random() < 0.25 else None,
+                          "current": int(rng.integers(0, 400)) if rng.random() < 0.5 else 0})
+        total = int(rng.integers(0, 20_000)) if rng.random() < 0.95 else int(rng.integers(1 << 24, 1 << 30))
+        rows.append({"elems": elems, "total": total, "avoid": bool(rng.random() < 0.5),
+                     "keep": bool(rng.random() < 0.5)})
+    lanes = ctx.plan_rows(rows)
+    ctx.plan_force_workspace(2)
+    try:
+        pairs = ctx.plan_rows(rows)
+    finally:
+        ctx.plan_force_workspace(0)
+    assert pairs == lanes
 
 
 @pytest.mark.parametrize("c", RSP, ids=[case_id(c) for c in RSP])
