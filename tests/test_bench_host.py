@@ -239,3 +239,67 @@ def test_two_ranks_gloo_line_and_gather_verification(tmp_path):
     assert line["n_gpus"] == 2 and line["config"]["units_total"] == 900 and line["config"]["units_per_gpu"] == 450
     assert line["allgather"]["backend"] == "gloo"
     assert line["allgather"]["verified"] and "2 ranks" in line["allgather"]["verified"]
+
+
+class FakeGroup:
+    """runtime.GroupContext's surface as bench_group uses it: the members' shards of one batch, results
+    from the C oracle over the whole batch."""
+
+    def __init__(self, devices):
+        self.devices = list(devices)
+        self.ctx = FakeContext()
+        self.timing = False
+
+    def upload_snapshot(self, snap):
+        self.ctx.upload_snapshot(snap)
+
+    def upload_batch(self, batch):
+        self.ctx.upload_batch(batch)
+
+    def schedule(self, fwk):
+        self.ctx.schedule(fwk)
+
+    def sync(self):
+        pass
+
+    def download(self, out=None):
+        return self.ctx.download()
+
+    def path_counts(self):
+        return self.ctx.path_counts()
+
+    def member(self, i):
+        return self.ctx
+
+    def set_timing(self, on):
+        self.timing = on
+
+    def member_stage_timing(self, i):
+        st = self.ctx.stage_timing()
+        return {k: v * (1 + 0.1 * i) for k, v in st.items()}  # member i a little slower
+
+    def ranges(self):
+        W = self.ctx.batch.W
+        n = len(self.devices)
+        ulo = np.array([W * i // n for i in range(n + 1)], np.int64)
+        return ulo, np.asarray(self.ctx.batch.out_off)[ulo]
+
+    def close(self):
+        pass
+
+
+def test_group_mode_line(fake, monkeypatch):
+    """bench_group (--gpus N, the default group mode): the contract fields, whole-batch parity, per-member
+    stage times (the slowest member per stage), the group summary in the printed line."""
+    monkeypatch.setattr(runtime, "GroupContext", FakeGroup)
+    out = bench.bench_group(_args(gpus=4), "c3", [0, 1, 2, 3], None, 0)
+    json.dumps(out)
+    assert out["n_gpus"] == 4 and out["scaling"] == "strong" and out["value"] > 0
+    assert out["config"]["units_total"] == 3000 and out["config"]["units_per_gpu"] == 750
+    assert "kad_group" in out["config"]["parallelism"] and out["config"]["rccl_world_size"] is None
+    assert out["parity"]["mismatches"] == 0 and out["parity"]["units_checked"] == 3000
+    assert out["config"]["stage_ms"]["main"] == pytest.approx(0.2 * 1.3)  # member 3's
+    assert len(out["group"]["member_total_ms"]) == 4
+    line = bench.compact_line(out)
+    assert line["group"]["devices"] == [0, 1, 2, 3] and line["group"]["mode"] == "group"
+    assert out["cpu_baseline"] is None  # the CPU baseline is the N = 1 line's
