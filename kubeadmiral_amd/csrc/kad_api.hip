@@ -973,7 +973,10 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
     c->batch_many_terms = first_bad(W, [&](int64_t w) { return sp[spo[w]] > ROW_MAX_TERMS; }) >= 0;
   }
   {
-    // plan rows in unit order: per-piece counts, then each piece writes at its prefix
+    // plan rows in unit order: per-piece counts, then each piece writes at its prefix. (Grouping them by path
+    // class — dynamic weights × avoid disruption — so that plan_pair_kernel's pairs share their passes made the
+    // pair kernel 11 % slower: neighbouring rows then lie ~4 units apart and share fewer lines of the per-unit
+    // columns; profiles/r06/ab_c4_planner_occupancy_classes.txt)
     constexpr int PIECES = 16;
     int64_t cnt[PIECES + 1] = {};
     uint32_t ors[PIECES] = {};

@@ -1044,6 +1044,9 @@ __device__ __forceinline__ int2 fit_ranks(const SnapDev& s, const int64_t (*fenc
 #ifndef KAD_PREP_CPL
 #define KAD_PREP_CPL 4
 #endif
+#ifndef KAD_PREP_GRID_CAP
+#define KAD_PREP_GRID_CAP 0  // prep grids: 0 = the resident block count (persistent), > 0 that many, < 0 one block per 256 lanes
+#endif
 constexpr int PREP_CPL = KAD_PREP_CPL;                 // chunks per lane
 #ifndef KAD_PREP_MINW
 #define KAD_PREP_MINW 1
@@ -1063,26 +1066,33 @@ __global__ __launch_bounds__(256, KAD_PREP_MINW) void prep_kernel(SnapDev s, Bat
     }
   }
   if (g < (uint32_t)WQ_HEADS) b.wq[g * WQ_STRIDE] = 0u;  // the schedule kernels' work heads
-  const bool live = g < (uint32_t)b.W * per;
+  __shared__ int64_t fences[2][FIT_FENCES];  // SnapDev::fitfold: every S-th fit value per resource
+  if (s.fitfold) {  // once per block (read after the first barrier below)
+    const int S = s.fit_mp / FIT_FENCES;
+    for (int i = threadIdx.x; i < 2 * FIT_FENCES; i += 256)
+      fences[i / FIT_FENCES][i % FIT_FENCES] = s.fit_vals[i / FIT_FENCES][(i % FIT_FENCES + 1) * S - 1];
+  }
+  // persistent blocks (launch_prep: at most the resident count) stride over the batch's lanes: one block per
+  // 64 units (C3: 15 625 blocks of ~3.5 us waves) was bound by work-group dispatch, ~4 resident waves per CU
+  // of the 20 the registers allow (round-5 PMC: 518M wave-cycles over a 456k-cycle kernel)
+  const uint32_t total = (uint32_t)b.W * per;
+  for (uint32_t base = blockIdx.x * 256u; base < total; base += gridDim.x * 256u) {  // (block-uniform trips)
+  const uint32_t g = base + threadIdx.x;
+  const bool live = g < total;
   const uint32_t w = live ? g / per : 0u, l = g - w * per, ch0 = l * CPL;
   // the unit's lanes load its program words 0 .. CPL*per-1 with coalesced
   // loads into LDS: the interpreter's word → row chain then runs on LDS
   // reads, not on dependent global loads
   const int32_t fpo = live ? b.fprog_off[w] : 0;
   const int32_t plen = live ? b.fprog_off[w + 1] - fpo : 0;
+  __syncthreads();  // the previous trip's program-word reads are done (a unit's lanes may span two waves)
 #pragma unroll
   for (int k = 0; k < CPL; k++) {
     const int i = (int)ch0 + k;
     prog_words[threadIdx.x * CPL + k] = i < plen ? b.fprog[fpo + i] : 0;
   }
-  __shared__ int64_t fences[2][FIT_FENCES];  // SnapDev::fitfold: every S-th fit value per resource
-  if (s.fitfold) {
-    const int S = s.fit_mp / FIT_FENCES;
-    for (int i = threadIdx.x; i < 2 * FIT_FENCES; i += 256)
-      fences[i / FIT_FENCES][i % FIT_FENCES] = s.fit_vals[i / FIT_FENCES][(i % FIT_FENCES + 1) * S - 1];
-  }
   __syncthreads();
-  if (!live) return;
+  if (!live) continue;
   // every per-unit load is issued up front by every lane (the lanes of a
   // unit share its cache lines), so the record lane's chain and the affinity
   // chain below overlap instead of running one after the other
@@ -1181,6 +1191,7 @@ __global__ __launch_bounds__(256, KAD_PREP_MINW) void prep_kernel(SnapDev s, Bat
     b.rec[w] = r;
     if (route) b.rows[atomicAdd(b.rows_n, 1)] = (int32_t)w;
   }
+  }  // the block's trips
 }
 
 // prep_wave_kernel<CW> — prep_kernel for wide snapshots (64 < ceil(C/64) <= 64*CW chunks, C5's 10 000
@@ -1216,8 +1227,9 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(SnapDev s, BatchDev b, P
     }
   }
   __syncthreads();
-  const int w = __builtin_amdgcn_readfirstlane((int)(g >> 6));
-  if (w >= b.W) return;
+  // persistent waves (launch_prep): wave v of the grid takes units v, v + waves, ... (no barrier inside)
+  const int n_waves = (int)gridDim.x * 4;
+  for (int w = __builtin_amdgcn_readfirstlane((int)(g >> 6)); w < b.W; w += n_waves) {
   const uint32_t f = (uint32_t)ldc(b.flags + w);
   const uint32_t fm = p.filter_mask;
   const int32_t gvk = ldc(b.gvk + w), tolset = ldc(b.tolset + w), sprog = ldc(b.sprog_off + w);
@@ -1305,6 +1317,7 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(SnapDev s, BatchDev b, P
     b.rec[w] = r;
     if (route) b.rows[atomicAdd(b.rows_n, 1)] = (int32_t)w;
   }
+  }  // the wave's units
 }
 
 int prep_lanes_per_unit(int C) {
@@ -2191,6 +2204,9 @@ constexpr int WIDE_THREADS = 1024;
 #ifndef KAD_DUMMY_STRIDE
 #define KAD_DUMMY_STRIDE 1  // u16 dummy slots of the wide kernel's compaction: P + stride * lane (<= 2: inside idx / pid)
 #endif
+#ifndef KAD_WIDE_ZS
+#define KAD_WIDE_ZS 1  // the wide kernel's per-cluster zero-request resource scores (c_zs)
+#endif
 #ifndef KAD_WIDE_C8
 #define KAD_WIDE_C8 0  // compaction at exactly 8 chunks: 0 chunk loop, 1 8-cluster lane pieces, 2 16-cluster pieces
 #endif
@@ -2221,9 +2237,9 @@ __host__ __device__ inline WideLayout wide_layout() {
 static_assert(2 * 64 * WIDE_MAX_NCH <= 6 * WIDE_P, "idx overflow past P must stay in the wave's region");
 // block-shared cluster cache: av (f64 x2), tg (u64 x2: NS|NE taints, GVK word),
 // cap (f64 x2), iv (f32 x2), [ne u64], [pn u64]
-__host__ __device__ inline size_t wide_cache_bytes(int C, int cache_ne, int cache_pn) {
+__host__ __device__ inline size_t wide_cache_bytes(int C, int cache_ne, int cache_pn, int cache_zs = 0) {
   const size_t Cp = (size_t)((C + 63) & ~63);
-  return Cp * (16 + 16 + 16 + 8 + 8 * cache_ne + 8 * cache_pn);
+  return Cp * (16 + 16 + 16 + 8 + 8 * cache_ne + 8 * cache_pn + 4 * cache_zs);
 }
 
 struct WideArgs {
@@ -2233,6 +2249,7 @@ struct WideArgs {
   ProfDev p;
   int waves_per_block;
   int cache_ne, cache_pn;
+  int cache_zs;     // the resource scores of a zero request per cluster (c_zs, below)
   int rows_inline;  // the units prep_kernel routed to rows run in this kernel's opening phase (row_units)
   int batch;        // units per work-queue batch (launch_schedule: by units per wave)
   int exp;  // measurement-only variants (KAD_WIDE_EXPERIMENT, never set by default; results differ from
@@ -2331,6 +2348,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
   float2* c_iv = (float2*)(cache + (size_t)48 * Cp);
   uint64_t* c_ne = nullptr;
   uint64_t* c_pn = nullptr;
+  // the sum of the profile's resource scores for a ZERO request per cluster: the live controller never sets
+  // ResourceRequest (schedulingtriggers.go:188-191), so Least / Most / Balanced are per-cluster constants
+  // there — one LDS read per position instead of the exact-f64 quotients
+  int32_t* c_zs = nullptr;
   {
     WArgs a = wargs();
     size_t o = (size_t)56 * Cp;
@@ -2338,7 +2359,11 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       c_ne = (uint64_t*)(cache + o);
       o += (size_t)8 * Cp;
     }
-    if (a->cache_pn) c_pn = (uint64_t*)(cache + o);
+    if (a->cache_pn) {
+      c_pn = (uint64_t*)(cache + o);
+      o += (size_t)8 * Cp;
+    }
+    if (a->cache_zs) c_zs = (int32_t*)(cache + o);
   }
   const bool f_taint = fm & BIT(KAD_PL_TAINT_TOLERATION), f_api = fm & BIT(KAD_PL_API_RESOURCES);
   const bool fold = wargs()->s.fold;  // taint + API filters in the static words (prep_kernel)
@@ -2360,10 +2385,21 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
       score_res(am, um, capm, avm);
       c_av[c] = make_double2(avc, avm);
       c_cap[c] = make_double2(capc, capm);
-      c_iv[c] = make_float2((float)(100.0 / capc), (float)(100.0 / capm));
+      const float ivc = (float)(100.0 / capc), ivm = (float)(100.0 / capm);
+      c_iv[c] = make_float2(ivc, ivm);
       c_tg[c] = make_ulonglong2(in ? ldg(a->s.nsne, cl) : 0ull, in ? ldg(a->s.gvk, cl) : 0ull);
       if (c_ne) c_ne[c] = in ? ldg(a->s.ne, cl) : 0;
       if (c_pn) c_pn[c] = in ? ldg(a->s.pns, cl) : 0;
+      if (c_zs) {  // the score expressions below with request 0: x = available
+        const double xcp = fmax(avc, 0.0), xmp = fmax(avm, 0.0);
+        const int okc = -(int)(avc >= 0.0), okm = -(int)(avm >= 0.0);
+        int x = 0;
+        if (sm & BIT(KAD_PL_LEAST_ALLOCATED)) x += (quot100(xcp, capc, ivc) + quot100(xmp, capm, ivm)) >> 1;
+        if (sm & BIT(KAD_PL_MOST_ALLOCATED))
+          x += ((quot100(capc - xcp, capc, ivc) & okc) + (quot100(capm - xmp, capm, ivm) & okm)) >> 1;
+        if (sm & BIT(KAD_PL_BALANCED_ALLOCATION)) x += (int)balanced_d((capc - avc) / capc, (capm - avm) / capm);
+        c_zs[c] = x;
+      }
     }
     __syncthreads();
   }
@@ -2443,6 +2479,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         break;
       }
       const double rqcd = (double)rqc, rqmd = (double)rqm;  // exact: 0 <= request < 2^46
+      const bool zreq = c_zs != nullptr && (rqc | rqm) == 0;  // the per-cluster constants apply
       const int spo = (int)fld(3);
       const int64_t mc = fld64(8), ooff = fld64(10);
       const uint64_t tolp0 = (uint64_t)fld64(14);
@@ -2596,7 +2633,9 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         const uint32_t raw = idx[p];  // (p < 512 = P: inside the wave's region, no exec branch; past n discarded)
         cid[q] = v ? raw : 0u;
         const uint32_t cq = cid[q];
-        if (s_res) {
+        if (s_res && zreq) {
+          t[q] = c_zs[cq];
+        } else if (s_res) {
           // x = cap - req = available - request (exact); req > cap <=> x < 0 (score 0)
           const double2 cap = c_cap[cq], av = c_av[cq];
           const double xc = av.x - rqcd, xm = av.y - rqmd;
@@ -4045,7 +4084,8 @@ __global__ __launch_bounds__(64, LANES ? 8 : 1) void plan_kernel(SnapDev s, Batc
 // lists instead); the preference columns; the FNV-1 continuation; dynamic weights; the plan. Rows with
 // 32 < K <= 64 go to `big` (plan_kernel<false, true> runs them next); K > 64 rows are the workspace planner's.
 #ifndef KAD_PAIR_MINW
-#define KAD_PAIR_MINW 8  // waves per SIMD plan_pair_kernel's VGPR budget is sized for (8: 64 VGPRs)
+#define KAD_PAIR_MINW 6  // waves per SIMD plan_pair_kernel's VGPR budget is sized for (6: 80 VGPRs; 8 spills, 5 / 7
+                         // slower: profiles/r06/ab_c4_pair_planner.txt, ab_c4_planner_occupancy_classes.txt)
 #endif
 __global__ __launch_bounds__(64, KAD_PAIR_MINW) void plan_pair_kernel(SnapDev s, BatchDev b, OutDev o, const PlanRowHdr* rows,
                                                           int n_rows, int r_stride, int tbl_cp, int32_t* big,
@@ -4458,21 +4498,35 @@ hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st) {
   return hipGetLastError();
 }
 
+static int n_cus();
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
   const long lanes = (long)b.W * (nch > 0 ? (nch + PREP_CPL - 1) / PREP_CPL : 1);
-  const long grid = lanes > 0 ? (lanes + 255) / 256 : 1;  // one block at W = 0 still resets defer_n
+  long grid = lanes > 0 ? (lanes + 255) / 256 : 1;  // one block at W = 0 still resets defer_n
+  // persistent: at most the resident block count (the kernels stride over the rest)
+  auto resident = [&](const void* fn) -> long {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 4;
+    return KAD_PREP_GRID_CAP > 0 ? (long)KAD_PREP_GRID_CAP : (KAD_PREP_GRID_CAP < 0 ? (1L << 30) : (long)n_cus() * per_cu);
+  };
   // wide snapshots (more than 64 chunks, up to 256): one unit per wave
   const int cw = (nch + 63) / 64;
   if (nch > 64 && cw <= 4 && tuning_env("KAD_PREP_WAVE", 1)) {
-    const long wgrid = b.W > 0 ? ((long)b.W + 3) / 4 : 1;
+    long wgrid = b.W > 0 ? ((long)b.W + 3) / 4 : 1;
+    const void* fw = cw == 2 ? (const void*)prep_wave_kernel<2> : cw == 3 ? (const void*)prep_wave_kernel<3>
+                                                                         : (const void*)prep_wave_kernel<4>;
+    // (not persistent: C5's one-unit-per-wave prep is L2-miss bound and took 587 -> 729 us with the resident
+    // grid, profiles/r06/ab_c5_prep_persistent.txt)
+    if (KAD_PREP_GRID_CAP > 0 && wgrid > resident(fw)) wgrid = resident(fw);
     const int ff = force_full ? 1 : 0;
     if (cw == 2) hipLaunchKernelGGL(prep_wave_kernel<2>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
     else if (cw == 3) hipLaunchKernelGGL(prep_wave_kernel<3>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
     else hipLaunchKernelGGL(prep_wave_kernel<4>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
     return hipGetLastError();
   }
+  const long rp = resident((const void*)prep_kernel);
+  if (grid > rp) grid = rp;
   hipLaunchKernelGGL(prep_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, p, force_full ? 1 : 0);
   return hipGetLastError();
 }
@@ -4560,9 +4614,14 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
   if (use_wide(s)) {
     const int cache_ne = (p.filter_mask & (1u << KAD_PL_TAINT_TOLERATION)) && (b.flags_or & KAD_W_HAS_CURRENT);
     const int cache_pn = (p.score_mask >> KAD_PL_TAINT_TOLERATION) & 1;
-    const size_t cache = wide_cache_bytes(s.C, cache_ne, cache_pn);
     const size_t per_wave = wide_layout().bytes;
     const size_t lds_max = 160 * 1024;
+    const bool s_res = p.score_mask & ((1u << KAD_PL_LEAST_ALLOCATED) | (1u << KAD_PL_MOST_ALLOCATED) |
+                                       (1u << KAD_PL_BALANCED_ALLOCATION));
+    // the zero-request score column when it costs no wave (LDS beside the 16 wave regions)
+    const int cache_zs =
+        (KAD_WIDE_ZS && s_res && wide_cache_bytes(s.C, cache_ne, cache_pn, 1) + (size_t)(WIDE_THREADS / 64) * per_wave <= lds_max) ? 1 : 0;
+    const size_t cache = wide_cache_bytes(s.C, cache_ne, cache_pn, cache_zs);
     int wpb = (int)((lds_max - cache) / per_wave);
     wpb = wpb > WIDE_THREADS / 64 ? WIDE_THREADS / 64 : wpb;
     if (wpb < 1) return hipErrorInvalidValue;
@@ -4602,7 +4661,7 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     // profiles/r05/ab_wide_batch_c3.txt)
     const long upw = ((long)b.W + grid * wpb - 1) / (grid * wpb);
     const int wbatch = upw < 64 ? 3 : WQ_BATCH;
-    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, inline_rows ? 1 : 0, wbatch, exp};
+    const WideArgs A{s, b, o, p, wpb, cache_ne, cache_pn, cache_zs, inline_rows ? 1 : 0, wbatch, exp};
     const bool beside = !inline_rows && b.early_rows && b.use_rows && side && fork && join;
     if (beside) {  // the row kernel on the side stream, from the end of prep_kernel, beside the wide kernel
       if (hipError_t e = hipEventRecord(fork, st)) return e;

@@ -10,7 +10,7 @@ cd "$d/kubeadmiral_amd/csrc"
 for f in kad_kernels.hip kad_trigger.hip kad_delta.hip kad_diff.hip kad_api.hip kad_pack.cpp kad_objects.cpp; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -w -pthread -c $f -o "$d/$f.o" &
 done
-wait
+for j in $(jobs -p); do wait $j || { echo "compile failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -pthread -o "$repo/ablibs/libkad_$name.so" "$d"/*.o
 rm -rf "$d"
 echo "$repo/ablibs/libkad_$name.so ($rev)"

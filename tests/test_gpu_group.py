@@ -234,3 +234,41 @@ def test_group_across_devices_equals_single():
     finally:
         g.close()
         c.close()
+
+
+def test_group_eight_members_full_c3_equals_single():
+    """C3 at full size (1M units x 1000 clusters, the bench's own batch) over an 8-member group — every member
+    on device 0, as the box has one GPU — bit-exact with a single context over the whole batch: the split
+    the driver's 8-GPU run uses (125 000 units per member), each member's opening phase and work queue on its
+    shard, the results at their offsets."""
+    import os
+    import sys
+    import torch  # noqa: F401
+    from kubeadmiral_amd import columns as CO
+    from kubeadmiral_amd import runtime
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    W, C = synth.SIZES["c3"]
+    clusters = bench.make_clusters("c3", C)
+    snap = pack.Snapshot(clusters)
+    fwk = synth.profile_for("c3")
+    nb = CO.NativePacker(snap).pack(fwk, bench.make_columns("c3", 0, W, clusters))
+    c = runtime.Context(0)
+    g = runtime.GroupContext([0] * 8)
+    try:
+        c.upload_snapshot(snap)
+        c.upload_batch(nb)
+        c.schedule(fwk)
+        want = c.download()
+        g.upload_snapshot(snap)
+        g.upload_batch(nb)
+        g.schedule(fwk)
+        got = g.download()
+        ulo, _ = g.ranges()
+        assert list(np.diff(ulo)) == [125_000] * 8
+        _same_arrays(got, want, nb, "c3 1M over 8 members")
+        assert g.path_counts()["units"] == W
+    finally:
+        g.close()
+        c.close()
