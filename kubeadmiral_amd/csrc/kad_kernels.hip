@@ -4525,8 +4525,12 @@ hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bo
     else hipLaunchKernelGGL(prep_wave_kernel<4>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
     return hipGetLastError();
   }
+  // persistent at 4+ lanes per unit (C3's 16 chunks: 202 -> 187 us); at fewer lanes per unit each lane carries
+  // more of its unit (C4: placement lists over 8 chunks in 2 lanes) and the resident grid measured slower (225 ->
+  // 238 us, profiles/r06/ab_c4_planner_occupancy_classes.txt): one block per 256 lanes there
+  const long per_unit = nch > 0 ? (nch + PREP_CPL - 1) / PREP_CPL : 1;
   const long rp = resident((const void*)prep_kernel);
-  if (grid > rp) grid = rp;
+  if ((per_unit >= 4 || KAD_PREP_GRID_CAP > 0) && grid > rp) grid = rp;
   hipLaunchKernelGGL(prep_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, p, force_full ? 1 : 0);
   return hipGetLastError();
 }
