@@ -2008,9 +2008,9 @@ __global__ __launch_bounds__(256, 6) void schedule_lean_kernel(LeanArgs args) {
           wave_sync();
 #pragma unroll
           for (int q = 0; q < Q; ++q)
-            if (q < nq) {  // exec-free: lanes past n add 0 to bin 127
+            if (q < nq) {  // exec-free: lanes past n add 0 to bin `lane` (not all to one bin)
               const bool vq = lane_on(vm[q]);
-              atomicAdd(hist + (vq ? 127 - (t32[q] - mn32) : 127), vq ? 1u : 0u);
+              atomicAdd(hist + (vq ? 127 - (t32[q] - mn32) : lane), vq ? 1u : 0u);
             }
           wave_sync();
           const uint2 hh = *(const uint2*)(hist + 2 * lane);  // bins 127-2l, 126-2l
@@ -2728,9 +2728,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
           wave_sync();
 #pragma unroll
           for (int q = 0; q < Q; ++q)
-            if (q < nq) {  // exec-free: lanes past n add 0 to bin 127
+            if (q < nq) {  // exec-free: lanes past n add 0 to bin `lane` (one shared bin: 26M of C3's 78M
+              // LDS bank-conflict cycles, 0.5 % of the kernel; profiles/r06/ab_c3_lds_conflicts.txt)
               const bool vq = q * 64 + lane < n;
-              atomicAdd(hist + (vq ? 127 - (t[q] - mn32) : 127), vq ? 1u : 0u);
+              atomicAdd(hist + (vq ? 127 - (t[q] - mn32) : lane), vq ? 1u : 0u);
             }
           wave_sync();
           const uint2 hh = *(const uint2*)(hist + 2 * lane);  // bins 127-2l, 126-2l
