@@ -98,6 +98,7 @@ struct kad_ctx {
   void* d_delta = nullptr;     // kad_snapshot_update: resident delta blob
   size_t delta_cap = 0;
   bool batch_defer = false;    // some unit uses a feature the lean kernel defers
+  bool batch_zero_req = false;  // no unit has a ResourceRequest (BatchDev::zero_req)
   bool batch_many_terms = false;  // some unit has more than ROW_MAX_TERMS preferred terms (the row path defers it)
   // scheduling-trigger hashes (kad_trigger_*)
   void* t_suffix = nullptr;
@@ -968,6 +969,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
       return (gv[w] >= 64 && !c->sd.fold) || so[w] < so[w + 1] || rc[w] < 0 || rm[w] < 0 || rc[w] >= (1ll << 46) ||
              rm[w] >= (1ll << 46) || (fl[w] & KAD_W_WIDE_SCORES);
     }) >= 0;
+    c->batch_zero_req = first_bad(W, [&](int64_t w) { return rc[w] != 0 || rm[w] != 0; }) < 0;
     const int32_t* spo = at<int32_t>(blob, h.off, KAD_B_SPROG_OFF) + lo;
     const int32_t* sp = at<int32_t>(blob, h.off, KAD_B_SPROG);
     c->batch_many_terms = first_bad(W, [&](int64_t w) { return sp[spo[w]] > ROW_MAX_TERMS; }) >= 0;
@@ -1156,6 +1158,7 @@ static int batch_upload_locked(kad_ctx* c, const void* blob, size_t nbytes, int6
   BatchDev& b = c->bd;
   b.W = W;
   b.flags_or = flags_or;
+  b.zero_req = c->batch_zero_req ? 1 : 0;
   b.NT = h.n_tolsets;
   b.TW = h.n_taint_words;
   b.flags = at<uint32_t>(base, h.off, KAD_B_FLAGS);

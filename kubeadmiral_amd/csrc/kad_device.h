@@ -93,6 +93,7 @@ struct BatchDev {
   int W, NT, TW;
   uint32_t flags_or;        // OR of every unit's KAD_W_* flags (host, at upload)
   int may_defer;            // host: some unit may reach the lean kernel's defer list (else that pass is skipped)
+  int zero_req;             // host: no unit of the batch has a ResourceRequest (the live controller's batches)
   const uint32_t* flags;
   const int32_t *gvk, *tolset;
   const int64_t *req_cpu, *req_mem, *desired, *maxc;

@@ -1227,9 +1227,10 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(SnapDev s, BatchDev b, P
     }
   }
   __syncthreads();
-  // persistent waves (launch_prep): wave v of the grid takes units v, v + waves, ... (no barrier inside)
-  const int n_waves = (int)gridDim.x * 4;
-  for (int w = __builtin_amdgcn_readfirstlane((int)(g >> 6)); w < b.W; w += n_waves) {
+  // one unit per wave, grid = units / 4 (a unit loop here, even at one trip per wave, took C5's prep
+  // 540 -> 588 us: profiles/r06/bisect_c5_prep.txt)
+  const int w = __builtin_amdgcn_readfirstlane((int)(g >> 6));
+  if (w >= b.W) return;
   const uint32_t f = (uint32_t)ldc(b.flags + w);
   const uint32_t fm = p.filter_mask;
   const int32_t gvk = ldc(b.gvk + w), tolset = ldc(b.tolset + w), sprog = ldc(b.sprog_off + w);
@@ -1317,7 +1318,6 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(SnapDev s, BatchDev b, P
     b.rec[w] = r;
     if (route) b.rows[atomicAdd(b.rows_n, 1)] = (int32_t)w;
   }
-  }  // the wave's units
 }
 
 int prep_lanes_per_unit(int C) {
@@ -2299,7 +2299,10 @@ __device__ __forceinline__ void wide_row_or_defer(int w) {
 // XN > 0: the kernel is specialised for exactly XN chunks; SM >= 0: for the score-plugin mask SM (the
 // profile's plugins as compile-time constants: every runtime plugin test of the hot loops folds away, and
 // with it the 64-bit condition masks the compiler otherwise keeps live — and spills — across the loop)
-template <int NCH, int XN, int SM>
+// ZR: every unit of the batch has a zero ResourceRequest (BatchDev::zero_req): the resource scores are the
+// per-cluster column c_zs. (A per-unit test inside the one instantiation cost C3's units, which all carry
+// requests, 31 us of 1.13 ms for the zero-request units' 24 us: profiles/r06/ab_c3_zero_request_kernel.txt)
+template <int NCH, int XN, int SM, bool ZR = false>
 __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs args) {
   (void)args;  // read through wargs()
   constexpr int Q = WIDE_Q;
@@ -2479,7 +2482,6 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         break;
       }
       const double rqcd = (double)rqc, rqmd = (double)rqm;  // exact: 0 <= request < 2^46
-      const bool zreq = c_zs != nullptr && (rqc | rqm) == 0;  // the per-cluster constants apply
       const int spo = (int)fld(3);
       const int64_t mc = fld64(8), ooff = fld64(10);
       const uint64_t tolp0 = (uint64_t)fld64(14);
@@ -2633,7 +2635,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 4) void schedule_wide_kernel(WideArgs
         const uint32_t raw = idx[p];  // (p < 512 = P: inside the wave's region, no exec branch; past n discarded)
         cid[q] = v ? raw : 0u;
         const uint32_t cq = cid[q];
-        if (s_res && zreq) {
+        if (ZR) {  // (s_res: ZR launches only with a resource score in the profile)
           t[q] = c_zs[cq];
         } else if (s_res) {
           // x = cap - req = available - request (exact); req > cap <=> x < 0 (score 0)
@@ -4514,12 +4516,9 @@ hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bo
   // wide snapshots (more than 64 chunks, up to 256): one unit per wave
   const int cw = (nch + 63) / 64;
   if (nch > 64 && cw <= 4 && tuning_env("KAD_PREP_WAVE", 1)) {
-    long wgrid = b.W > 0 ? ((long)b.W + 3) / 4 : 1;
-    const void* fw = cw == 2 ? (const void*)prep_wave_kernel<2> : cw == 3 ? (const void*)prep_wave_kernel<3>
-                                                                         : (const void*)prep_wave_kernel<4>;
     // (not persistent: C5's one-unit-per-wave prep is L2-miss bound and took 587 -> 729 us with the resident
     // grid, profiles/r06/ab_c5_prep_persistent.txt)
-    if (KAD_PREP_GRID_CAP > 0 && wgrid > resident(fw)) wgrid = resident(fw);
+    const long wgrid = b.W > 0 ? ((long)b.W + 3) / 4 : 1;
     const int ff = force_full ? 1 : 0;
     if (cw == 2) hipLaunchKernelGGL(prep_wave_kernel<2>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
     else if (cw == 3) hipLaunchKernelGGL(prep_wave_kernel<3>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
@@ -4623,9 +4622,11 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     const size_t lds_max = 160 * 1024;
     const bool s_res = p.score_mask & ((1u << KAD_PL_LEAST_ALLOCATED) | (1u << KAD_PL_MOST_ALLOCATED) |
                                        (1u << KAD_PL_BALANCED_ALLOCATION));
-    // the zero-request score column when it costs no wave (LDS beside the 16 wave regions)
-    const int cache_zs =
-        (KAD_WIDE_ZS && s_res && wide_cache_bytes(s.C, cache_ne, cache_pn, 1) + (size_t)(WIDE_THREADS / 64) * per_wave <= lds_max) ? 1 : 0;
+    // zero-request batches: the resource-score column, when it costs no wave (LDS beside the 16 wave regions)
+    const int cache_zs = (KAD_WIDE_ZS && s_res && b.zero_req &&
+                          wide_cache_bytes(s.C, cache_ne, cache_pn, 1) + (size_t)(WIDE_THREADS / 64) * per_wave <= lds_max)
+                             ? 1
+                             : 0;
     const size_t cache = wide_cache_bytes(s.C, cache_ne, cache_pn, cache_zs);
     int wpb = (int)((lds_max - cache) / per_wave);
     wpb = wpb > WIDE_THREADS / 64 ? WIDE_THREADS / 64 : wpb;
@@ -4637,17 +4638,23 @@ hipError_t launch_schedule(const SnapDev& s, const BatchDev& b, const OutDev& o,
     constexpr int SM_LEAST = 1 << KAD_PL_LEAST_ALLOCATED;
     constexpr int SM_DEFAULT = (1 << KAD_PL_TAINT_TOLERATION) | (1 << KAD_PL_BALANCED_ALLOCATION) |
                                (1 << KAD_PL_LEAST_ALLOCATED) | (1 << KAD_PL_CLUSTER_AFFINITY);
-    const void* fn = (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1>;
+    const bool zr = cache_zs != 0;
+    const void* fn = zr ? (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1, true>
+                        : (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1>;
     const bool folded = s.fold && s.fitfold;  // the LeastAllocated specialisation compiles the folded filter only
     if (folded && nch == 16 && p.score_mask == (uint32_t)SM_LEAST)
-      fn = (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>;
+      fn = zr ? (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST, true>
+              : (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>;
     else if (nch == 8 && p.score_mask == (uint32_t)SM_DEFAULT)
-      fn = (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT>;
+      fn = zr ? (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT, true> : (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT>;
     static bool attr = false;
     if (!attr) {
       for (const void* f : {(const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1>,
                             (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST>,
-                            (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT>})
+                            (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT>,
+                            (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, -1, true>,
+                            (const void*)schedule_wide_kernel<WIDE_MAX_NCH, 0, SM_LEAST, true>,
+                            (const void*)schedule_wide_kernel<8, 8, SM_DEFAULT, true>})
         if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max)) return e;
       attr = true;
     }

@@ -642,3 +642,28 @@ def test_fuzz_relaxed_snapshot_gpu_equals_c_oracle(ctx, seed):
     assert paths["resource_class"] == "relaxed", paths
     assert paths["exact_f64"] == (paths["fold"] and paths["fitfold"]), paths
     assert_same(res, c_oracle(snap, batch, fwk), f"relaxed fuzz seed {seed} C={C}")
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_zero_request_batches_gpu_equals_c_oracle(ctx, seed):
+    """Batches in which no unit has a ResourceRequest (BatchDev::zero_req, what the live controller sends:
+    schedulingtriggers.go:188-191) take the wide kernel's zero-request instantiation (the resource scores
+    from the per-cluster column c_zs): C3's profile at 1 000 clusters (the LeastAllocated specialisation),
+    the default set at 512 (the 8-chunk specialisation) and fuzz profiles at 400 / 700 (the generic one),
+    on clean and relaxed snapshots (clusters over-committed or with empty allocatable)."""
+    rng = np.random.default_rng(9700 + seed)
+    C = [1000, 512, 400, 700][seed % 4]
+    clusters, units = synth.gen_fuzz(9700 + seed, W=120, C=C)
+    if seed % 2:
+        synth.production_resources(clusters, rng, p_over=0.2, p_empty=0.1)
+        clusters[0].allocatable, clusters[0].available = {}, {}
+    for su in units:
+        su.resource_request = T.Resource()
+    if C == 1000:
+        fwk = synth.profile_for("c3")
+    elif C == 512:
+        fwk = F.Framework(F.default_enabled_plugins())
+    else:
+        fwk = synth.fuzz_framework(seed)
+    snap, batch, res = run(ctx, clusters, units, fwk)
+    assert_same(res, c_oracle(snap, batch, fwk), f"zero-request seed {seed} C={C} {ctx.snapshot_paths()}")
