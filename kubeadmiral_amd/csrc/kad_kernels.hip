@@ -1044,9 +1044,6 @@ __device__ __forceinline__ int2 fit_ranks(const SnapDev& s, const int64_t (*fenc
 #ifndef KAD_PREP_CPL
 #define KAD_PREP_CPL 4
 #endif
-#ifndef KAD_PREP_GRID_CAP
-#define KAD_PREP_GRID_CAP 0  // prep grids: 0 = the resident block count (persistent), > 0 that many, < 0 one block per 256 lanes
-#endif
 constexpr int PREP_CPL = KAD_PREP_CPL;                 // chunks per lane
 #ifndef KAD_PREP_MINW
 #define KAD_PREP_MINW 1
@@ -1066,33 +1063,28 @@ __global__ __launch_bounds__(256, KAD_PREP_MINW) void prep_kernel(SnapDev s, Bat
     }
   }
   if (g < (uint32_t)WQ_HEADS) b.wq[g * WQ_STRIDE] = 0u;  // the schedule kernels' work heads
-  __shared__ int64_t fences[2][FIT_FENCES];  // SnapDev::fitfold: every S-th fit value per resource
-  if (s.fitfold) {  // once per block (read after the first barrier below)
-    const int S = s.fit_mp / FIT_FENCES;
-    for (int i = threadIdx.x; i < 2 * FIT_FENCES; i += 256)
-      fences[i / FIT_FENCES][i % FIT_FENCES] = s.fit_vals[i / FIT_FENCES][(i % FIT_FENCES + 1) * S - 1];
-  }
-  // persistent blocks (launch_prep: at most the resident count) stride over the batch's lanes: one block per
-  // 64 units (C3: 15 625 blocks of ~3.5 us waves) was bound by work-group dispatch, ~4 resident waves per CU
-  // of the 20 the registers allow (round-5 PMC: 518M wave-cycles over a 456k-cycle kernel)
-  const uint32_t total = (uint32_t)b.W * per;
-  for (uint32_t base = blockIdx.x * 256u; base < total; base += gridDim.x * 256u) {  // (block-uniform trips)
-  const uint32_t g = base + threadIdx.x;
-  const bool live = g < total;
+  // one block per 256 lanes (a persistent grid striding over the batch measured equal at C3, 188 vs 187 us,
+  // and its loop cost C4's 2-lane units 17 us: profiles/r06/ab_c3_prep_persistent.txt)
+  const bool live = g < (uint32_t)b.W * per;
   const uint32_t w = live ? g / per : 0u, l = g - w * per, ch0 = l * CPL;
   // the unit's lanes load its program words 0 .. CPL*per-1 with coalesced
   // loads into LDS: the interpreter's word → row chain then runs on LDS
   // reads, not on dependent global loads
   const int32_t fpo = live ? b.fprog_off[w] : 0;
   const int32_t plen = live ? b.fprog_off[w + 1] - fpo : 0;
-  __syncthreads();  // the previous trip's program-word reads are done (a unit's lanes may span two waves)
 #pragma unroll
   for (int k = 0; k < CPL; k++) {
     const int i = (int)ch0 + k;
     prog_words[threadIdx.x * CPL + k] = i < plen ? b.fprog[fpo + i] : 0;
   }
+  __shared__ int64_t fences[2][FIT_FENCES];  // SnapDev::fitfold: every S-th fit value per resource
+  if (s.fitfold) {
+    const int S = s.fit_mp / FIT_FENCES;
+    for (int i = threadIdx.x; i < 2 * FIT_FENCES; i += 256)
+      fences[i / FIT_FENCES][i % FIT_FENCES] = s.fit_vals[i / FIT_FENCES][(i % FIT_FENCES + 1) * S - 1];
+  }
   __syncthreads();
-  if (!live) continue;
+  if (!live) return;
   // every per-unit load is issued up front by every lane (the lanes of a
   // unit share its cache lines), so the record lane's chain and the affinity
   // chain below overlap instead of running one after the other
@@ -1191,7 +1183,6 @@ __global__ __launch_bounds__(256, KAD_PREP_MINW) void prep_kernel(SnapDev s, Bat
     b.rec[w] = r;
     if (route) b.rows[atomicAdd(b.rows_n, 1)] = (int32_t)w;
   }
-  }  // the block's trips
 }
 
 // prep_wave_kernel<CW> — prep_kernel for wide snapshots (64 < ceil(C/64) <= 64*CW chunks, C5's 10 000
@@ -4501,18 +4492,11 @@ hipError_t launch_slices(const SnapDev& s, uint64_t* slices, hipStream_t st) {
   return hipGetLastError();
 }
 
-static int n_cus();
 hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bool force_full, hipStream_t st) {
   (void)hipGetLastError();
   const int nch = (s.C + 63) >> 6;
   const long lanes = (long)b.W * (nch > 0 ? (nch + PREP_CPL - 1) / PREP_CPL : 1);
-  long grid = lanes > 0 ? (lanes + 255) / 256 : 1;  // one block at W = 0 still resets defer_n
-  // persistent: at most the resident block count (the kernels stride over the rest)
-  auto resident = [&](const void* fn) -> long {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 4;
-    return KAD_PREP_GRID_CAP > 0 ? (long)KAD_PREP_GRID_CAP : (KAD_PREP_GRID_CAP < 0 ? (1L << 30) : (long)n_cus() * per_cu);
-  };
+  const long grid = lanes > 0 ? (lanes + 255) / 256 : 1;  // one block at W = 0 still resets defer_n
   // wide snapshots (more than 64 chunks, up to 256): one unit per wave
   const int cw = (nch + 63) / 64;
   if (nch > 64 && cw <= 4 && tuning_env("KAD_PREP_WAVE", 1)) {
@@ -4525,12 +4509,6 @@ hipError_t launch_prep(const SnapDev& s, const BatchDev& b, const ProfDev& p, bo
     else hipLaunchKernelGGL(prep_wave_kernel<4>, dim3((unsigned)wgrid), dim3(256), 0, st, s, b, p, ff);
     return hipGetLastError();
   }
-  // persistent at 4+ lanes per unit (C3's 16 chunks: 202 -> 187 us); at fewer lanes per unit each lane carries
-  // more of its unit (C4: placement lists over 8 chunks in 2 lanes) and the resident grid measured slower (225 ->
-  // 238 us, profiles/r06/ab_c4_planner_occupancy_classes.txt): one block per 256 lanes there
-  const long per_unit = nch > 0 ? (nch + PREP_CPL - 1) / PREP_CPL : 1;
-  const long rp = resident((const void*)prep_kernel);
-  if ((per_unit >= 4 || KAD_PREP_GRID_CAP > 0) && grid > rp) grid = rp;
   hipLaunchKernelGGL(prep_kernel, dim3((unsigned)grid), dim3(256), 0, st, s, b, p, force_full ? 1 : 0);
   return hipGetLastError();
 }
