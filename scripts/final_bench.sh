@@ -20,8 +20,9 @@ python - "$tag" <<'PY'
 import json, sys
 d = json.loads(open(f"gpurun_out/{sys.argv[1]}_bench.json").read().strip().splitlines()[-1])
 def show(d, n):
-    r = d["roofline"]
-    print(n, "%.4g" % d["value"], round(d["ms_per_step"], 4), r["bound"], round(r["frac"], 4), r["pmc"])
+    r = d.get("roofline") or {}
+    print(n, "%.4g" % d["value"], round(d["ms_per_step"], 4), r.get("bound"), r.get("frac"), r.get("pmc"),
+          "parity_mismatches", d.get("parity_mismatches", (d.get("parity") or {}).get("mismatches")))
 show(d, "c3")
 for k, v in d.get("extra", {}).items():
     show(v, k)
