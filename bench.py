@@ -165,7 +165,8 @@ def load_pmc(cfg: str, W: int, C: int):
 # stage (kad_stage_timing) → the kernels it launches (rocprofv3 names contain these)
 STAGE_KERNELS = {"req_mask": ("req_row_kernel", "req_mask_kernel"), "prep": ("prep_kernel",),
                  "main": ("schedule_wide_kernel", "schedule_lean_kernel"), "rows": ("schedule_row_kernel",),
-                 "defer": ("schedule_kernel<",), "planner": ("plan_kernel",)}
+                 "defer": ("schedule_kernel<",),
+                 "planner": ("plan_hdr_kernel", "plan_pair_kernel", "plan_kernel")}
 
 
 def pmc_kernel_sum(pmc, stage: str, main_name: str = None):

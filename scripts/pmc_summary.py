@@ -25,7 +25,7 @@ from kubeadmiral_amd.build import source_hash  # noqa: E402
 STAGE = ("req_mask_kernel", "req_row_kernel", "prep_kernel", "schedule_lean_kernel", "schedule_wide_kernel",
          "schedule_row_kernel", "schedule_kernel")
 # the step's kernels (bench.py picks its roofline kernel among them by live HIP-event time)
-STEP = STAGE + ("plan_kernel",)
+STEP = STAGE + ("plan_hdr_kernel", "plan_pair_kernel", "plan_kernel")
 
 ap = argparse.ArgumentParser()
 ap.add_argument("out")
