@@ -534,12 +534,37 @@ def bench_group(args, cfg, devices, dist, rank):
     return out
 
 
+def score_term_rows(batch) -> int:
+    """Distinct requirement ids in the batch's score programs (ClusterAffinity preferred terms): the rows the
+    row kernel's (term, chunk) word pass reads. Program layout: n_terms, then per term weight, n_expr, ids."""
+    from kubeadmiral_amd import pack
+
+    h = pack.header_of(batch.blob, pack.BatchHeader)
+    W = int(h.n_units)
+    off = pack.array_of(batch.blob, h, pack.B_SPROG_OFF, np.int32, W + 1)
+    prog = pack.array_of(batch.blob, h, pack.B_SPROG, np.int32, int(off[W]))
+    ids = set()
+    for w in range(W):
+        i, e = int(off[w]), int(off[w + 1])
+        if i >= e:
+            continue
+        nt, pc = int(prog[i]), i + 1
+        for _ in range(nt):
+            ne = int(prog[pc + 1])
+            ids.update(prog[pc + 2:pc + 2 + ne].tolist())
+            pc += 2 + ne
+    return len(ids)
+
+
 def stage_bytes_model(stage, W, C, nch, batch, snap, out_bytes, paths, n_distinct_reqs, divide_slots):
     """Compulsory HBM bytes of one launch of each stage's kernels (inputs read once, outputs written once):
     * req_mask: every distinct requirement's row words written + the label columns read once;
     * prep: the batch blob read once + UnitRec (64 B) and static filter words (8 B x chunks) per unit written;
     * main: UnitRec + static words per unit, 56 B per cached cluster, 12 B per unit + 12 B per placement out;
-    * rows / defer: UnitRec + static words per unit the kernel takes, its cached cluster columns;
+    * rows: UnitRec + static words per unit the kernel takes, its cluster columns (72 B: f64 resources, f32
+      inverses, 32-B PreferNoSchedule words), and its units' share of the distinct preferred-term requirement
+      rows (8 B x chunks each; the share assumes the routed units hold a proportional part of them);
+    * defer: UnitRec + static words per unit the kernel takes, its cached cluster columns;
     * planner: SURVEY §8(d) B_plan = 48 B per (Divide unit, selected cluster)."""
     K = snap.K if hasattr(snap, "K") else 0
     if stage == "req_mask":
@@ -549,7 +574,9 @@ def stage_bytes_model(stage, W, C, nch, batch, snap, out_bytes, paths, n_distinc
     if stage == "main":
         return (64.0 + 8 * nch) * W + 56.0 * C + out_bytes
     if stage == "rows":
-        return (64.0 + 8 * nch) * paths["row_kernel"] + 56.0 * C
+        R = paths["row_kernel"]
+        terms = 8.0 * nch * score_term_rows(batch) * (R / max(1, W)) if R else 0.0
+        return (64.0 + 8 * nch) * R + 72.0 * C + terms
     if stage == "defer":
         return (64.0 + 8 * nch) * paths["full_kernel"] + 56.0 * C
     if stage == "planner":
