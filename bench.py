@@ -859,32 +859,40 @@ def end_to_end(ctx, snap, fwk, cols, res, C, packer_for, chunks=4, packs=2):
     ctx2 = Context(ctx.device)
     ctx2.upload_snapshot(packer_for)
     ctxs = (ctx, ctx2)
-    packers = [packer] + [CO.NativePacker(packer_for) for _ in range(packs)]
     bounds = [W * i // chunks for i in range(chunks + 1)]
     parts = [cols.slice(bounds[i], bounds[i + 1]) for i in range(chunks)]
     bufs = None
     pipe = None
-    with ThreadPoolExecutor(max_workers=packs) as pool:
-        for rep in range(2):  # first pass warms the packers / contexts and sizes the result buffers
-            outs = []
-            t0 = time.perf_counter()
-            futs = {i: pool.submit(packers[i % len(packers)].pack, fwk, parts[i], 0, False)
-                    for i in range(min(packs, chunks))}
-            for i in range(chunks):
-                nbi = futs.pop(i).result()
-                if i + packs < chunks:
-                    j = i + packs
-                    futs[j] = pool.submit(packers[j % len(packers)].pack, fwk, parts[j], 0, False)
-                c = ctxs[i % 2]
-                c.upload_batch(nbi)
-                c.schedule(fwk)
-                r = c.download(out=bufs[i] if bufs else None)
-                r.out_off = np.array(r.out_off)  # a view into the packer's buffer, which chunk i + packs + 1 reuses
-                outs.append(r)
-            tot = time.perf_counter() - t0
-            pipe = {"chunks": chunks, "packs_in_flight": packs, "total_ms": tot * 1e3, "decisions_per_s": W * C / tot}
-            if bufs is None:
-                bufs = [BatchResult.pinned(len(r.status), len(r.cluster)) for r in outs]
+    tried = {}
+    # one pack in flight (it takes the library's whole host pool) and two (one pack's narrow phases beside the
+    # other's parallel ones): which wins depends on the host — on the round-5/6 boxes two in flight lost to the
+    # sequential pass — so both run and the faster is reported
+    for npk in sorted({1, packs}):
+        packers = [packer] + [CO.NativePacker(packer_for) for _ in range(npk)]
+        with ThreadPoolExecutor(max_workers=npk) as pool:
+            for rep in range(2):  # first pass warms the packers / contexts and sizes the result buffers
+                outs = []
+                t0 = time.perf_counter()
+                futs = {i: pool.submit(packers[i % len(packers)].pack, fwk, parts[i], 0, False)
+                        for i in range(min(npk, chunks))}
+                for i in range(chunks):
+                    nbi = futs.pop(i).result()
+                    if i + npk < chunks:
+                        j = i + npk
+                        futs[j] = pool.submit(packers[j % len(packers)].pack, fwk, parts[j], 0, False)
+                    c = ctxs[i % 2]
+                    c.upload_batch(nbi)
+                    c.schedule(fwk)
+                    r = c.download(out=bufs[i] if bufs else None)
+                    r.out_off = np.array(r.out_off)  # a view into the packer's buffer, which chunk i + npk + 1 reuses
+                    outs.append(r)
+                tot = time.perf_counter() - t0
+                if bufs is None:
+                    bufs = [BatchResult.pinned(len(r.status), len(r.cluster)) for r in outs]
+        tried[npk] = tot * 1e3
+        if pipe is None or tot * 1e3 < pipe["total_ms"]:
+            pipe = {"chunks": chunks, "packs_in_flight": npk, "total_ms": tot * 1e3, "decisions_per_s": W * C / tot}
+    pipe["total_ms_by_packs_in_flight"] = tried
     ctx2.close()
     # every chunk's rows equal the timed run's rows of the same units
     for i, r in enumerate(outs):

@@ -303,3 +303,30 @@ def test_group_mode_line(fake, monkeypatch):
     line = bench.compact_line(out)
     assert line["group"]["devices"] == [0, 1, 2, 3] and line["group"]["mode"] == "group"
     assert out["cpu_baseline"] is None  # the CPU baseline is the N = 1 line's
+
+
+def test_score_term_rows_counts_distinct_preferred_ids():
+    """The rows stage's compulsory model reads each distinct preferred-term requirement row once: the parser
+    walks every unit's score program (n_terms, then weight, n_expr, ids per term) and matches a direct count."""
+    from kubeadmiral_amd import pack
+
+    clusters, units, fwk = synth.make_config("c5", W=120, C=300)
+    snap = pack.pack_snapshot(clusters)
+    batch = pack.pack_batch(snap, fwk, units)
+    h = pack.header_of(batch.blob, pack.BatchHeader)
+    off = pack.array_of(batch.blob, h, pack.B_SPROG_OFF, np.int32, batch.W + 1)
+    prog = pack.array_of(batch.blob, h, pack.B_SPROG, np.int32, int(off[-1]))
+    want = set()
+    for w in range(batch.W):
+        p = prog[off[w]:off[w + 1]].tolist()
+        if not p:
+            continue
+        i = 1
+        for _ in range(p[0]):
+            want.update(p[i + 2:i + 2 + p[i + 1]])
+            i += 2 + p[i + 1]
+        assert i == len(p), "score program layout"
+    assert want and bench.score_term_rows(batch) == len(want)
+    nch = (300 + 63) // 64
+    b = bench.stage_bytes_model("rows", batch.W, 300, nch, batch, snap, 0, {"row_kernel": batch.W}, 0, 0)
+    assert b == (64.0 + 8 * nch) * batch.W + 72.0 * 300 + 8.0 * nch * len(want)
