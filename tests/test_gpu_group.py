@@ -64,7 +64,7 @@ def test_group_fuzz_equals_single(single, group, seed):
     assert group.path_counts()["units"] == batch.W
 
 
-@pytest.mark.parametrize("cfg,W", [("c2", 30_000), ("c4", 30_000), ("c3r", 20_000), ("c5", 600)])
+@pytest.mark.parametrize("cfg,W", [("c2", 30_000), ("c4", 30_000), ("c3r", 20_000), ("c3p", 20_000), ("c5", 600)])
 def test_group_configs_equal_single_and_oracle(single, group, cfg, W):
     clusters, units, fwk = synth.make_config(cfg, W=W)
     snap, batch, got, want = _both(single, group, clusters, units, fwk)

@@ -644,13 +644,14 @@ def test_fuzz_relaxed_snapshot_gpu_equals_c_oracle(ctx, seed):
     assert_same(res, c_oracle(snap, batch, fwk), f"relaxed fuzz seed {seed} C={C}")
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(16))
 def test_zero_request_batches_gpu_equals_c_oracle(ctx, seed):
     """Batches in which no unit has a ResourceRequest (BatchDev::zero_req, what the live controller sends:
     schedulingtriggers.go:188-191) take the wide kernel's zero-request instantiation (the resource scores
     from the per-cluster column c_zs): C3's profile at 1 000 clusters (the LeastAllocated specialisation),
     the default set at 512 (the 8-chunk specialisation) and fuzz profiles at 400 / 700 (the generic one),
-    on clean and relaxed snapshots (clusters over-committed or with empty allocatable)."""
+    on clean and relaxed snapshots (clusters over-committed or with empty allocatable); seeds 12-15 give one
+    unit a request, so the same batch shape takes the exact-f64 instantiation."""
     rng = np.random.default_rng(9700 + seed)
     C = [1000, 512, 400, 700][seed % 4]
     clusters, units = synth.gen_fuzz(9700 + seed, W=120, C=C)
@@ -659,6 +660,8 @@ def test_zero_request_batches_gpu_equals_c_oracle(ctx, seed):
         clusters[0].allocatable, clusters[0].available = {}, {}
     for su in units:
         su.resource_request = T.Resource()
+    if seed >= 12:  # one unit with a request: the batch is not zero-request, every unit takes the exact path
+        units[len(units) // 2].resource_request = T.Resource(250, 1 << 30)
     if C == 1000:
         fwk = synth.profile_for("c3")
     elif C == 512:
