@@ -69,7 +69,17 @@ def main():
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = x
-    print(json.dumps({"config": a.config, "units": batch.W, "ms": {v: [round(x, 4) for x in xs] for v, xs in res.items()},
+    # a digest of the results (every unit's status / count / flags and its counted slots): equal across
+    # libraries that schedule identically (a cross-library A/B's parity check)
+    import hashlib
+
+    st, cn = np.asarray(ref.status), np.asarray(ref.count)
+    oo = np.asarray(ref.out_off)[: len(cn)]
+    idx = np.repeat(oo, cn) + (np.arange(int(cn.sum())) - np.repeat(np.cumsum(cn) - cn, cn))
+    h = hashlib.sha1()
+    for x in (st, cn, np.asarray(ref.flags), np.asarray(ref.cluster)[idx], np.asarray(ref.replicas)[idx]):
+        h.update(np.ascontiguousarray(x).tobytes())
+    print(json.dumps({"config": a.config, "units": batch.W, "digest": h.hexdigest()[:16], "ms": {v: [round(x, 4) for x in xs] for v, xs in res.items()},
                       "mean": {v: round(float(np.mean(xs)), 4) for v, xs in res.items()},
                       "min": {v: round(float(np.min(xs)), 4) for v, xs in res.items()}}), flush=True)
 
