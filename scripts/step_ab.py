@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--variants", default="base")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--stages", action="store_true", help="also report mean per-stage times per variant")
     ap.add_argument("--lib", default=os.path.join(ROOT, "ablibs", "libkad_tune.so"))
     a = ap.parse_args()
     import torch  # noqa: F401
@@ -45,6 +46,7 @@ def main():
     ctx.upload_batch(batch)
     variants = [v.strip() for v in a.variants.split(";") if v.strip()]
     res = {v: [] for v in variants}
+    stg = {}
     ref = None
     for r in range(a.rounds):
         for v in variants:
@@ -59,6 +61,13 @@ def main():
                 ctx.schedule(fwk)
             ctx.sync()
             res[v].append((time.perf_counter() - t0) / a.steps * 1e3)
+            if a.stages:  # per-stage HIP-event times of 3 more steps (timing on, outside the timed loop)
+                ctx.set_timing(True)
+                for _ in range(3):
+                    ctx.schedule(fwk)
+                    ctx.sync()
+                    stg.setdefault(v, []).append(ctx.stage_timing())
+                ctx.set_timing(False)
             out = ctx.download()
             if v == "base" and ref is None:
                 ref = out
@@ -81,7 +90,9 @@ def main():
         h.update(np.ascontiguousarray(x).tobytes())
     print(json.dumps({"config": a.config, "units": batch.W, "digest": h.hexdigest()[:16], "ms": {v: [round(x, 4) for x in xs] for v, xs in res.items()},
                       "mean": {v: round(float(np.mean(xs)), 4) for v, xs in res.items()},
-                      "min": {v: round(float(np.min(xs)), 4) for v, xs in res.items()}}), flush=True)
+                      "min": {v: round(float(np.min(xs)), 4) for v, xs in res.items()},
+                      "stages": {v: {k: round(float(np.mean([d[k] for d in ds])), 4) for k in ds[0]} for v, ds in stg.items()}}),
+          flush=True)
 
 
 if __name__ == "__main__":
