@@ -48,9 +48,28 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+STAMP = LIB + ".sha256"  # SHA-256 of every input libkad.so was linked from (written by build())
+
+
+def inputs_hash() -> str:
+    """SHA-256 over every source and header libkad.so is compiled from (names and contents)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in _inputs():
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
 def up_to_date() -> bool:
+    """libkad.so was built from exactly the current sources: its stamp holds their content hash (robust to
+    copies and checkouts that reset modification times); a library without a stamp falls back to mtimes."""
     if not os.path.exists(LIB):
         return False
+    if os.path.exists(STAMP):
+        with open(STAMP) as f:
+            return f.read().strip() == inputs_hash()
     t = os.path.getmtime(LIB)
     return all(os.path.getmtime(p) <= t for p in _inputs())
 
@@ -70,7 +89,10 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) 
     build), and only the objects older than their source or any header are rebuilt; then one link."""
     from concurrent.futures import ThreadPoolExecutor
 
+    stamp = inputs_hash()  # of the sources as compiled below (an edit during the build leaves the stamp stale)
     if out == LIB and not force and up_to_date():
+        if not os.path.exists(STAMP):  # up to date by modification times (a library from before stamps)
+            _write_stamp(stamp)
         return LIB
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
              "-Wno-unused-function", "-pthread"] + list(extra)
@@ -114,8 +136,18 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = LIB) 
     link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", out + ".tmp"] + \
         [os.path.join(odir, f + ".o") for f in SOURCES]
     subprocess.run(link, check=True)
+    if out == LIB and os.path.exists(STAMP):
+        os.remove(STAMP)  # (no stamp while the library is being replaced)
     os.replace(out + ".tmp", out)
+    if out == LIB:
+        _write_stamp(stamp)
     return out
+
+
+def _write_stamp(h: str) -> None:
+    with open(STAMP + ".tmp", "w") as f:
+        f.write(h + "\n")
+    os.replace(STAMP + ".tmp", STAMP)
 
 
 if __name__ == "__main__":
