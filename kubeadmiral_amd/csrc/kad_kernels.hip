@@ -4777,19 +4777,25 @@ hipError_t launch_plan_hdr(const BatchDev& b, const int32_t* rows, int n_rows, P
   return hipGetLastError();
 }
 
+constexpr int PLAN_OVERSUB = 8;  // register planners' grid over the resident block count (launch_plan)
 hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, const ProfDev& p, const PlanRowHdr* rows,
                        int n_rows, int kmax, void* gscr, size_t scr_bytes, hipStream_t st, int32_t* big, int32_t* big_n) {
   (void)hipGetLastError();  // clear any stale error so the check below is this launch's
   (void)p;
   if (n_rows == 0 || kmax <= 0) return hipSuccess;
   const int cp = (s.C + 63) & ~63;
-  // persistent grid: the resident block count, rows round-robin (r += grid)
-  auto persistent = [&](const void* fn, size_t lds) {
+  // grid: `over` times the resident block count, rows round-robin (r += grid). The register planners take
+  // PLAN_OVERSUB = 8: each wave's rows are an eighth of a persistent wave's, and the hardware starts the next
+  // waves as earlier ones finish — with a fixed stride per resident wave, the waves whose rows held the most
+  // rounds set the kernel's end (C4: planner 1.463 -> 1.276 ms, step 2.29 -> 2.10 ms; 16x equal, 32x / 64x
+  // slower: profiles/r06/ab_c4_plan_grid.txt)
+  auto persistent = [&](const void* fn, size_t lds, int over = 1) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess || per_cu < 1) per_cu = 8;
-    long grid = (long)n_cus() * per_cu;
+    long grid = (long)n_cus() * per_cu * over;
     return (int)(grid > n_rows ? n_rows : grid);
   };
+  static const int over = tuning_env("KAD_PLAN_GRID_MULT", PLAN_OVERSUB);
   // rows of K <= 64: the register planners, lookup tables only in LDS. Two rows per wave for K <= 32
   // (plan_pair_kernel: u16 tables, 8 B per cluster for the two segments), then the rows of 32 < K <= 64 it
   // listed, one per wave (plan_kernel<false, true>: u32 tables, 8 B per cluster)
@@ -4799,15 +4805,15 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
     static const int pairs = tuning_env("KAD_PLAN_PAIRS", 1);
     if (pairs && big) {
       if (hipError_t e = hipMemsetAsync(big_n, 0, sizeof(int32_t), st)) return e;
-      const int grid = persistent((const void*)plan_pair_kernel, lds);
+      const int grid = persistent((const void*)plan_pair_kernel, lds, over);
       hipLaunchKernelGGL(plan_pair_kernel, dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows, grid, tbl_cp,
                          big, big_n);
       if (hipError_t e = hipGetLastError()) return e;
-      const int grid2 = persistent((const void*)plan_kernel<false, true>, lds);
+      const int grid2 = persistent((const void*)plan_kernel<false, true>, lds, over);
       hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid2), dim3(64), lds, st, s, b, o, rows, n_rows,
                          kmax, (char*)nullptr, 0, grid2, tbl_cp, (const int32_t*)big, (const int32_t*)big_n);
     } else {
-      const int grid = persistent((const void*)plan_kernel<false, true>, lds);
+      const int grid = persistent((const void*)plan_kernel<false, true>, lds, over);
       hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows,
                          kmax, (char*)nullptr, 0, grid, tbl_cp, (const int32_t*)nullptr, (const int32_t*)nullptr);
     }
