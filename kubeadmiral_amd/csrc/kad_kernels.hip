@@ -4784,15 +4784,18 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
   (void)p;
   if (n_rows == 0 || kmax <= 0) return hipSuccess;
   const int cp = (s.C + 63) & ~63;
-  // grid: `over` times the resident block count, rows round-robin (r += grid). The register planners take
-  // PLAN_OVERSUB = 8: each wave's rows are an eighth of a persistent wave's, and the hardware starts the next
-  // waves as earlier ones finish — with a fixed stride per resident wave, the waves whose rows held the most
-  // rounds set the kernel's end (C4: planner 1.463 -> 1.276 ms, step 2.29 -> 2.10 ms; 16x equal, 32x / 64x
-  // slower: profiles/r06/ab_c4_plan_grid.txt)
+  // grid: `over` times the resident block count, rows round-robin (r += grid). The pair planner takes up to
+  // PLAN_OVERSUB = 8 (at least 16 rows per wave): each wave's rows are an eighth of a persistent wave's, and the
+  // hardware starts the next waves as earlier ones finish — with a fixed stride per resident wave, the waves
+  // whose rows held the most rounds set the kernel's end (C4: planner 1.463 -> 1.276 ms, step 2.29 -> 2.10 ms;
+  // 16x equal, 32x / 64x slower: profiles/r06/ab_c4_plan_grid.txt). Small row sets (C5's) and the list kernel
+  // (its rows are known on the device only) keep the resident grid: extra waves there only start and exit.
   auto persistent = [&](const void* fn, size_t lds, int over = 1) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess || per_cu < 1) per_cu = 8;
-    long grid = (long)n_cus() * per_cu * over;
+    const long res = (long)n_cus() * per_cu;
+    long grid = res * over;
+    if (over > 1 && grid > n_rows / 16) grid = n_rows / 16 > res ? n_rows / 16 : res;
     return (int)(grid > n_rows ? n_rows : grid);
   };
   static const int over = tuning_env("KAD_PLAN_GRID_MULT", PLAN_OVERSUB);
@@ -4809,7 +4812,7 @@ hipError_t launch_plan(const SnapDev& s, const BatchDev& b, const OutDev& o, con
       hipLaunchKernelGGL(plan_pair_kernel, dim3((unsigned)grid), dim3(64), lds, st, s, b, o, rows, n_rows, grid, tbl_cp,
                          big, big_n);
       if (hipError_t e = hipGetLastError()) return e;
-      const int grid2 = persistent((const void*)plan_kernel<false, true>, lds, over);
+      const int grid2 = persistent((const void*)plan_kernel<false, true>, lds);
       hipLaunchKernelGGL((plan_kernel<false, true>), dim3((unsigned)grid2), dim3(64), lds, st, s, b, o, rows, n_rows,
                          kmax, (char*)nullptr, 0, grid2, tbl_cp, (const int32_t*)big, (const int32_t*)big_n);
     } else {
